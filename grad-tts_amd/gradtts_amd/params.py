@@ -1,0 +1,179 @@
+"""Parameter inventory of the Grad-TTS score U-Net and a deterministic synthetic-weight generator.
+
+The inventory enumerates the ``state_dict`` keys (and shapes) that the reference
+``GradLogPEstimator2d`` registers, so checkpoints saved by the reference
+(``train.py:174-175``) load into this package unchanged:
+
+* ``spk_mlp.{0,2}``              -- ``model/diffusion.py:139-141`` (only if n_spks > 1 or n_spks == -1)
+* ``mlp.{0,2}``                  -- ``model/diffusion.py:143-144``
+* ``downs.{i}.{0,1,2,3}``        -- ``model/diffusion.py:146-158``
+* ``mid_block1/mid_attn/mid_block2`` -- ``model/diffusion.py:160-163``
+* ``ups.{i}.{0,1,2,3}``          -- ``model/diffusion.py:165-170``
+* ``final_block``, ``final_conv`` -- ``model/diffusion.py:171-172``
+
+No trained checkpoint exists in this environment, so tests and the
+benchmark use :func:`synthetic_state_dict`: a framework-free numpy PCG64 stream that
+reproduces bit-identically on every host with the same numpy.
+"""
+from __future__ import annotations
+
+import hashlib
+from collections import OrderedDict
+
+import numpy as np
+
+DIM_MULTS = (1, 2, 4)
+HEADS = 4
+DIM_HEAD = 32
+GROUPS = 8
+
+
+def level_dims(dim: int, n_spks: int):
+    """Channel plan ``dims`` of ``model/diffusion.py:146``."""
+    cin = 2 + (1 if n_spks > 1 else 0)
+    return [cin] + [dim * m for m in DIM_MULTS]
+
+
+def uses_spk_mlp(n_spks: int) -> bool:
+    """``model/diffusion.py:139``: the speaker MLP exists for n_spks > 1 or n_spks == -1."""
+    return n_spks > 1 or n_spks == -1
+
+
+def _resnet(prefix, din, dout, dim, out):
+    out[prefix + "mlp.1.weight"] = (dout, dim)
+    out[prefix + "mlp.1.bias"] = (dout,)
+    out[prefix + "block1.block.0.weight"] = (dout, din, 3, 3)
+    out[prefix + "block1.block.0.bias"] = (dout,)
+    out[prefix + "block1.block.1.weight"] = (dout,)
+    out[prefix + "block1.block.1.bias"] = (dout,)
+    out[prefix + "block2.block.0.weight"] = (dout, dout, 3, 3)
+    out[prefix + "block2.block.0.bias"] = (dout,)
+    out[prefix + "block2.block.1.weight"] = (dout,)
+    out[prefix + "block2.block.1.bias"] = (dout,)
+    if din != dout:
+        out[prefix + "res_conv.weight"] = (dout, din, 1, 1)
+        out[prefix + "res_conv.bias"] = (dout,)
+
+
+def _attn(prefix, c, out):
+    hidden = HEADS * DIM_HEAD
+    out[prefix + "fn.g"] = (1,)
+    out[prefix + "fn.fn.to_qkv.weight"] = (3 * hidden, c, 1, 1)
+    out[prefix + "fn.fn.to_out.weight"] = (c, hidden, 1, 1)
+    out[prefix + "fn.fn.to_out.bias"] = (c,)
+
+
+def estimator_param_shapes(dim: int = 64, n_spks: int = 1, spk_emb_dim: int = 64,
+                           n_feats: int = 80) -> "OrderedDict[str, tuple]":
+    """Ordered ``{key: shape}`` of ``GradLogPEstimator2d.state_dict()`` (registration order)."""
+    out: "OrderedDict[str, tuple]" = OrderedDict()
+    if uses_spk_mlp(n_spks):
+        out["spk_mlp.0.weight"] = (spk_emb_dim * 4, spk_emb_dim)
+        out["spk_mlp.0.bias"] = (spk_emb_dim * 4,)
+        out["spk_mlp.2.weight"] = (n_feats, spk_emb_dim * 4)
+        out["spk_mlp.2.bias"] = (n_feats,)
+    out["mlp.0.weight"] = (dim * 4, dim)
+    out["mlp.0.bias"] = (dim * 4,)
+    out["mlp.2.weight"] = (dim, dim * 4)
+    out["mlp.2.bias"] = (dim,)
+    dims = level_dims(dim, n_spks)
+    in_out = list(zip(dims[:-1], dims[1:]))
+    for i, (din, dout) in enumerate(in_out):
+        p = f"downs.{i}."
+        _resnet(p + "0.", din, dout, dim, out)
+        _resnet(p + "1.", dout, dout, dim, out)
+        _attn(p + "2.", dout, out)
+        if i < len(in_out) - 1:
+            out[p + "3.conv.weight"] = (dout, dout, 3, 3)
+            out[p + "3.conv.bias"] = (dout,)
+    # `downs` and `ups` ModuleLists are registered before the mid blocks (diffusion.py:147-148),
+    # so the up path precedes mid_* in state_dict order.
+    for i, (din, dout) in enumerate(reversed(in_out[1:])):
+        p = f"ups.{i}."
+        _resnet(p + "0.", dout * 2, din, dim, out)
+        _resnet(p + "1.", din, din, dim, out)
+        _attn(p + "2.", din, out)
+        out[p + "3.conv.weight"] = (din, din, 4, 4)   # ConvTranspose2d: [in, out, kH, kW]
+        out[p + "3.conv.bias"] = (din,)
+    mid = dims[-1]
+    _resnet("mid_block1.", mid, mid, dim, out)
+    _attn("mid_attn.", mid, out)
+    _resnet("mid_block2.", mid, mid, dim, out)
+    out["final_block.block.0.weight"] = (dim, dim, 3, 3)
+    out["final_block.block.0.bias"] = (dim,)
+    out["final_block.block.1.weight"] = (dim,)
+    out["final_block.block.1.bias"] = (dim,)
+    out["final_conv.weight"] = (1, dim, 1, 1)
+    out["final_conv.bias"] = (1,)
+    return out
+
+
+def _fan_in(shape):
+    return int(shape[1] * int(np.prod(shape[2:]))) if len(shape) > 1 else int(shape[0])
+
+
+def synthetic_state_dict(seed: int = 0, dim: int = 64, n_spks: int = 1, spk_emb_dim: int = 64,
+                         n_feats: int = 80, rezero_g: float = 0.02) -> "OrderedDict[str, np.ndarray]":
+    """Deterministic synthetic weights (float32) for the estimator.
+
+    * conv / linear weights and their biases ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in)) (torch's default bound);
+    * GroupNorm affine: weight = 1 + 0.1*U(-1,1), bias = 0.1*U(-1,1) (exercises the affine path);
+    * Rezero ``g`` = ``rezero_g`` (0.02: attention is active and N<=1000 stays finite).
+
+    Keys are visited in registration order with one PCG64 stream seeded by ``seed``.
+    """
+    rng = np.random.default_rng(seed)
+    shapes = estimator_param_shapes(dim, n_spks, spk_emb_dim, n_feats)
+    out: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    last_fan = 1
+    for key, shape in shapes.items():
+        if key.endswith(".g"):
+            arr = np.full(shape, rezero_g, dtype=np.float64)
+        elif ".block.1." in key:  # GroupNorm affine (Block: Sequential(conv, GN, Mish))
+            u = rng.uniform(-1.0, 1.0, size=shape)
+            arr = (1.0 + 0.1 * u) if key.endswith("weight") else 0.1 * u
+        elif key.endswith("weight"):
+            last_fan = _fan_in(shape)
+            b = 1.0 / np.sqrt(last_fan)
+            arr = rng.uniform(-b, b, size=shape)
+        else:  # bias of the preceding weight
+            b = 1.0 / np.sqrt(last_fan)
+            arr = rng.uniform(-b, b, size=shape)
+        out[key] = np.ascontiguousarray(arr.astype(np.float32))
+    return out
+
+
+def state_dict_sha256(sd) -> str:
+    h = hashlib.sha256()
+    for k, v in sd.items():
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(np.asarray(v, dtype=np.float32)).tobytes())
+    return h.hexdigest()
+
+
+def synthetic_inputs(seed: int, B: int, T: int, n_feats: int = 80, lengths=None, spk_emb_dim: int = 64,
+                     temperature: float = 1.0):
+    """Synthetic decoder inputs: mu ~ N(0,1), z = mu + N(0,1)/temperature, mask from lengths."""
+    rng = np.random.default_rng(seed)
+    mu = rng.standard_normal((B, n_feats, T)).astype(np.float32)
+    z = (mu + rng.standard_normal((B, n_feats, T)).astype(np.float32) / np.float32(temperature)).astype(np.float32)
+    if lengths is None:
+        lengths = [T] * B
+    mask = np.zeros((B, 1, T), dtype=np.float32)
+    for b, L in enumerate(lengths):
+        mask[b, 0, :L] = 1.0
+    spk = rng.standard_normal((B, spk_emb_dim)).astype(np.float32)
+    return mu, z, mask, spk
+
+
+def fix_len_compatibility(length: int, num_downsamplings_in_unet: int = 2) -> int:
+    """Round a frame count up to a multiple of 4 (``model/utils.py:13-17``)."""
+    m = 2 ** num_downsamplings_in_unet
+    return ((int(length) + m - 1) // m) * m
+
+
+def estimator_flops(B: int, T: int, n_spks: int = 1) -> int:
+    """Algorithmic FLOPs of one estimator call (measured with torch flop_counter)."""
+    if n_spks > 1:
+        return B * (134_256_640 * T + 368_640)
+    return B * (134_154_240 * T + 294_912)

@@ -1,0 +1,142 @@
+"""ORACLE (test infrastructure only) -- CPU restatement of the Grad-TTS reverse-diffusion decoder.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import this
+module, and only as the checker / the timed CPU baseline. The product path
+(``grad-tts_amd/gradtts_amd``) never calls into ``oracle/``.
+
+This is a functional (module-free) restatement of ``/root/reference/model/diffusion.py`` in plain
+torch CPU ops over a ``{state_dict key: tensor}`` dict. Each function cites the reference lines it
+follows. It is pinned against golden vectors generated from the real reference
+(``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``; test ``tests/test_oracle_golden.py``).
+
+dtype: float32 by default (parity gate fp32 max|d| <= 1e-4 * max|ref|), float64 for the
+tolerance envelope.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+HEADS, DIM_HEAD, GROUPS = 4, 32, 8
+
+
+def mish(x):
+    """``Mish`` diffusion.py:16-18: x * tanh(softplus(x)) (softplus beta=1, threshold=20)."""
+    return x * torch.tanh(F.softplus(x))
+
+
+def sinusoidal_pos_emb(t, dim, scale):
+    """``SinusoidalPosEmb`` diffusion.py:113-125."""
+    half = dim // 2
+    emb = math.log(10000) / (half - 1)
+    emb = torch.exp(torch.arange(half, dtype=torch.float32) * -emb).to(t.dtype)
+    emb = scale * t.unsqueeze(1) * emb.unsqueeze(0)
+    return torch.cat((emb.sin(), emb.cos()), dim=-1)
+
+
+def linear(p, key, x):
+    return F.linear(x, p[key + ".weight"], p[key + ".bias"])
+
+
+def block(p, key, x, mask):
+    """``Block`` diffusion.py:49-58: Mish(GN8(conv3x3(x*mask))) * mask."""
+    y = F.conv2d(x * mask, p[key + ".block.0.weight"], p[key + ".block.0.bias"], padding=1)
+    y = F.group_norm(y, GROUPS, p[key + ".block.1.weight"], p[key + ".block.1.bias"], eps=1e-5)
+    return mish(y) * mask
+
+
+def resnet_block(p, key, x, mask, t_emb):
+    """``ResnetBlock`` diffusion.py:61-79."""
+    h = block(p, key + ".block1", x, mask)
+    tb = F.linear(mish(t_emb), p[key + ".mlp.1.weight"], p[key + ".mlp.1.bias"])
+    h = h + tb.unsqueeze(-1).unsqueeze(-1)
+    h = block(p, key + ".block2", h, mask)
+    if (key + ".res_conv.weight") in p:
+        res = F.conv2d(x * mask, p[key + ".res_conv.weight"], p[key + ".res_conv.bias"])
+    else:
+        res = x * mask
+    return h + res
+
+
+def linear_attention(p, key, x):
+    """``Residual(Rezero(LinearAttention))`` diffusion.py:39-46, 82-110."""
+    b, c, hh, ww = x.shape
+    qkv = F.conv2d(x, p[key + ".fn.fn.to_qkv.weight"])
+    qkv = qkv.reshape(b, 3, HEADS, DIM_HEAD, hh * ww)
+    q, k, v = qkv[:, 0], qkv[:, 1], qkv[:, 2]
+    k = k.softmax(dim=-1)
+    context = torch.einsum("bhdn,bhen->bhde", k, v)
+    out = torch.einsum("bhde,bhdn->bhen", context, q)
+    out = out.reshape(b, HEADS * DIM_HEAD, hh, ww)
+    out = F.conv2d(out, p[key + ".fn.fn.to_out.weight"], p[key + ".fn.fn.to_out.bias"])
+    return out * p[key + ".fn.g"] + x
+
+
+def estimator(p, x, mask, mu, t, spk=None, n_spks=1, pe_scale=1000.0, dim=64):
+    """``GradLogPEstimator2d.forward`` diffusion.py:174-216. x, mu: [B,80,T]; mask [B,1,T]; t [B]."""
+    s = None
+    if spk is not None:
+        s = F.linear(mish(linear(p, "spk_mlp.0", spk)), p["spk_mlp.2.weight"], p["spk_mlp.2.bias"])
+    t_emb = sinusoidal_pos_emb(t, dim, pe_scale)
+    t_emb = F.linear(mish(linear(p, "mlp.0", t_emb)), p["mlp.2.weight"], p["mlp.2.bias"])
+    if n_spks < 2:
+        h = torch.stack([mu, x], 1)
+    else:
+        h = torch.stack([mu, x, s.unsqueeze(-1).repeat(1, 1, x.shape[-1])], 1)
+    mask = mask.unsqueeze(1)
+    hiddens, masks = [], [mask]
+    n_levels = 3
+    for i in range(n_levels):
+        m = masks[-1]
+        h = resnet_block(p, f"downs.{i}.0", h, m, t_emb)
+        h = resnet_block(p, f"downs.{i}.1", h, m, t_emb)
+        h = linear_attention(p, f"downs.{i}.2", h)
+        hiddens.append(h)
+        if i < n_levels - 1:   # Downsample (diffusion.py:30-36) on x*mask
+            h = F.conv2d(h * m, p[f"downs.{i}.3.conv.weight"], p[f"downs.{i}.3.conv.bias"], stride=2, padding=1)
+        else:                  # Identity(x*mask)
+            h = h * m
+        masks.append(m[:, :, :, ::2])
+    masks = masks[:-1]
+    m = masks[-1]
+    h = resnet_block(p, "mid_block1", h, m, t_emb)
+    h = linear_attention(p, "mid_attn", h)
+    h = resnet_block(p, "mid_block2", h, m, t_emb)
+    for i in range(n_levels - 1):
+        m = masks.pop()
+        h = torch.cat((h, hiddens.pop()), dim=1)
+        h = resnet_block(p, f"ups.{i}.0", h, m, t_emb)
+        h = resnet_block(p, f"ups.{i}.1", h, m, t_emb)
+        h = linear_attention(p, f"ups.{i}.2", h)
+        h = F.conv_transpose2d(h * m, p[f"ups.{i}.3.conv.weight"], p[f"ups.{i}.3.conv.bias"], stride=2, padding=1)
+    h = block(p, "final_block", h, mask)
+    out = F.conv2d(h * mask, p["final_conv.weight"], p["final_conv.bias"])
+    return (out * mask).squeeze(1)
+
+
+def get_noise(t, beta_init, beta_term, cumulative=False):
+    """``get_noise`` diffusion.py:219-224."""
+    if cumulative:
+        return beta_init * t + 0.5 * (beta_term - beta_init) * (t ** 2)
+    return beta_init + (beta_term - beta_init) * t
+
+
+@torch.no_grad()
+def reverse_diffusion(p, z, mask, mu, n_timesteps, spk=None, n_spks=1, beta_min=0.05, beta_max=20.0,
+                      pe_scale=1000.0, dim=64):
+    """``Diffusion.reverse_diffusion`` diffusion.py:254-268 (deterministic Euler; ``stoc`` is ignored there)."""
+    h = 1.0 / n_timesteps
+    xt = z * mask
+    for i in range(n_timesteps):
+        t = (1.0 - (i + 0.5) * h) * torch.ones(z.shape[0], dtype=z.dtype)
+        noise_t = get_noise(t.unsqueeze(-1).unsqueeze(-1), beta_min, beta_max)
+        dxt = 0.5 * (mu - xt - estimator(p, xt, mask, mu, t, spk, n_spks, pe_scale, dim))
+        dxt = dxt * noise_t * h
+        xt = (xt - dxt) * mask
+    return xt
+
+
+def to_torch_params(sd, dtype=torch.float32):
+    return {k: torch.as_tensor(v).to(dtype) for k, v in sd.items()}
