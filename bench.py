@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark: mel-frames/s of the N-step reverse-diffusion decoder on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--frames 512] [--n-timesteps 50]
+                    [--dtype bf16|fp32] [--n-spks 1] [--no-cpu-baseline]
+
+A "step" is one complete ``Diffusion.reverse_diffusion`` call (n_timesteps Euler steps of the U-Net)
+over one batch of synthetic utterances already resident in HBM, followed by the RCCL all_gather of
+the mel outputs when N > 1. Default workload = BASELINE config 2: LJSpeech single speaker, batch 32
+per GPU, T = 512 frames, N = 50, bf16 compute. With N GPUs every rank decodes its own batch of 32
+(weak scaling: the 8-GPU run is config 4, 256 utterances), ``value`` = all frames / max-rank time.
+
+Printed (rank 0, one JSON line): the driver contract fields plus
+  roofline      the dominant kernel's achieved algorithmic TFLOP/s vs the bf16 dense MFMA peak,
+                measured live with HIP events around every launch during the timed steps;
+  cpu_baseline  the oracle CPU restatement (oracle/decoder.py, "port") timed on this host for a bounded
+                sample (one Euler step of a smaller batch at the same T), projected to mel-frames/s.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "grad-tts_amd"))
+
+from gradtts_amd import _lib  # noqa: E402
+from gradtts_amd.diffusion import Diffusion  # noqa: E402
+from gradtts_amd.params import estimator_flops, synthetic_inputs, synthetic_state_dict  # noqa: E402
+
+PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}   # dense MFMA peaks (MI355X_MICROARCH.md)
+HBM_PEAK = 8.0e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
+    ap.add_argument("--frames", type=int, default=512)
+    ap.add_argument("--n-timesteps", type=int, default=50)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--n-spks", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-batch", type=int, default=4)
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if one exists."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, sd):
+    """Oracle restatement on the host cores, one Euler step of a bounded sample at the bench T."""
+    from oracle import decoder as odec
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    Bs = args.cpu_sample_batch
+    mu, z, mask, spk = synthetic_inputs(99, Bs, args.frames)
+    p = odec.to_torch_params(sd)
+    spk_t = torch.from_numpy(spk) if args.n_spks > 1 else None
+    with torch.no_grad():
+        odec.estimator(p, torch.from_numpy(z[:1]), torch.from_numpy(mask[:1]), torch.from_numpy(mu[:1]),
+                       torch.tensor([0.5]), spk_t[:1] if spk_t is not None else None, n_spks=args.n_spks)   # warm-up
+        t0 = time.perf_counter()
+        odec.reverse_diffusion(p, torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu), 1, spk_t,
+                               n_spks=args.n_spks)
+        dt = time.perf_counter() - t0
+    frames_per_s = Bs * args.frames / (dt * args.n_timesteps)
+    return {"value": frames_per_s, "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/decoder.py (torch CPU fp32), 1 of {args.n_timesteps} Euler steps, B={Bs}, "
+                      f"T={args.frames}: {dt:.2f} s, projected x{args.n_timesteps}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    B, T, N = args.batch, args.frames, args.n_timesteps
+    dec = Diffusion(80, 64, args.n_spks, 64, 0.05, 20, 1000, compute_dtype=cdt)
+    sd = synthetic_state_dict(seed=0, n_spks=args.n_spks)
+    dec.estimator.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    dec = dec.to(dev)
+    mu, z, mask, spk = synthetic_inputs(1234 + rank, B, T)
+    mu, z, mask = (torch.from_numpy(a).to(dev) for a in (mu, z, mask))
+    spk = torch.from_numpy(spk).to(dev) if args.n_spks > 1 else None
+    gathered = torch.empty((world * B, 80, T), dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        y = dec(z, mask, mu, N, False, spk)
+        if world > 1:
+            torch.distributed.all_gather_into_tensor(gathered, y)
+        return y
+
+    L = _lib.lib()
+    handle = dec.estimator._native(dec.beta_min, dec.beta_max)
+    buf = ctypes.create_string_buffer(1 << 20)
+    L.gt_decoder_profile_enable(handle, 1)    # warm-up runs profiled too, so the event pool is allocated
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(L.gt_decoder_profile_read(handle, buf, len(buf)), "gt_decoder_profile_read")
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    L.gt_decoder_profile_enable(handle, 0)
+    _lib.check(L.gt_decoder_profile_read(handle, buf, len(buf)), "gt_decoder_profile_read")
+    prof = json.loads(buf.value.decode())
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(y).all(), "non-finite decoder output"
+
+    if rank == 0:
+        sec = elapsed / args.steps
+        frames = world * B * T
+        value = frames / sec
+        flop_step = N * estimator_flops(B, T, args.n_spks)
+        conv = [p for p in prof if p["kernel"].startswith("conv_kernel")]
+        dom = max(conv, key=lambda p: p["ms"])
+        avg_s = dom["ms"] / dom["launches"] / 1e3
+        achieved = dom["flop"] / dom["launches"] / avg_s
+        total_kernel_ms = sum(p["ms"] for p in prof)
+        out = {
+            "metric": "mel-frames/sec (reverse-diffusion, 80-mel, N=50) at 1/2/4/8 MI355X; RTF",
+            "value": value, "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": sec * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic: mu~N(0,1), z=mu+N(0,1), full-length masks; random-init weights (seed 0), no checkpoint",
+            "config": {"workload": f"LJSpeech single-speaker batch={B}/GPU, T={T} frames, n_timesteps={N}, "
+                                   f"{args.dtype} (BASELINE config 2; N GPUs = config 4 weak-scaled)",
+                       "global_batch": world * B, "seq_len": T, "n_timesteps": N, "n_spks": args.n_spks,
+                       "parallelism": f"dp{world} utterance shards, RCCL all_gather of mels" if world > 1 else "dp1"},
+            "rtf": sec * 22050 / (frames * 256),     # inference.py:91 formula
+            "frame_steps_per_s": value * N,
+            "path_tflops": flop_step * world / sec / 1e12,
+            "path_mfma_frac": flop_step / sec / PEAK[args.dtype],
+            "roofline": {"bound": "mfma", "kernel": dom["kernel"], "launches_per_step": dom["launches"] / args.steps,
+                         "achieved": achieved / 1e12, "peak": PEAK[args.dtype] / 1e12, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK[args.dtype], "avg_launch_us": avg_s * 1e6,
+                         "flop_per_launch": dom["flop"] / dom["launches"],
+                         "traffic": pmc_traffic(dom["kernel"]),
+                         "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"]},
+            "kernel_time_share": {p["kernel"]: round(p["ms"] / total_kernel_ms, 4) for p in
+                                  sorted(prof, key=lambda p: -p["ms"])[:8]},
+            "kernel_busy_frac": total_kernel_ms / args.steps / 1e3 / sec,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, sd)
+        print(json.dumps(out))
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

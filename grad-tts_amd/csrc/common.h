@@ -1,0 +1,112 @@
+// Shared device helpers for the gfx950 (CDNA4) Grad-TTS decoder kernels.
+//
+// Activation storage type `A` is either float (fp32 parity path) or __bf16 (throughput path).
+// Every 3x3 / 1x1 / transposed convolution of the score U-Net is an implicit GEMM on MFMA:
+//   bf16 : v_mfma_f32_32x32x16_bf16   (one instruction per 16-channel k-step)
+//   fp32 : v_mfma_f32_32x32x2_f32     (exact f32, eight instructions per 16-channel k-step)
+// Both flavours read their operand fragments as "8 contiguous channels at byte offset 8*h*sizeof(A)"
+// (h = lane >> 5); for fp32 the 16-channel step is split so that the k index of sub-step s, half h is
+// channel 8h+s on BOTH operands (the k order inside a step is free as long as A and B agree).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define GT_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- numerics
+// Mish (model/diffusion.py:16-18) = x * tanh(softplus(x)); torch softplus returns x for x > 20.
+// tanh(log1p(e^x)) = n / (n + 2) with n = e^x (e^x + 2): one exp + one divide.
+GT_DEV float mishf(float x) {
+  if (x > 20.f) return x;  // softplus(x) = x and tanh(x) == 1.0f in fp32 for x > 20
+  float e = __expf(x);
+  float n = e * (e + 2.f);
+  return x * __fdividef(n, n + 2.f);
+}
+
+// ---------------------------------------------------------------- storage
+template <class A> struct Act;
+template <> struct Act<float> {
+  static constexpr int kItemCh = 4;  // channels per 16-byte item
+  GT_DEV static float to_f(float v) { return v; }
+  GT_DEV static float from_f(float v) { return v; }
+};
+template <> struct Act<bf16> {
+  static constexpr int kItemCh = 8;
+  GT_DEV static float to_f(bf16 v) { return (float)v; }
+  GT_DEV static bf16 from_f(float v) { return (bf16)v; }
+};
+
+// 16-byte item <-> float[kItemCh]
+GT_DEV void item_to_f(const uint4& u, float* f, float) {
+  f[0] = __uint_as_float(u.x); f[1] = __uint_as_float(u.y); f[2] = __uint_as_float(u.z); f[3] = __uint_as_float(u.w);
+}
+GT_DEV uint4 f_to_item(const float* f, float) {
+  return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+}
+GT_DEV void item_to_f(const uint4& u, float* f, bf16) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+GT_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  bf16 a = (bf16)lo, b = (bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+GT_DEV uint4 f_to_item(const float* f, bf16) {
+  return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
+}
+
+// ---------------------------------------------------------------- MFMA traits
+template <class A> struct Mma;
+template <> struct Mma<bf16> {
+  typedef bf16x8 frag;
+  GT_DEV static frag load(const char* p) { return *reinterpret_cast<const frag*>(p); }
+  GT_DEV static void mma(const frag& a, const frag& b, f32x16& c) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  struct frag { f32x4 lo, hi; };
+  GT_DEV static frag load(const char* p) {
+    frag f;
+    f.lo = *reinterpret_cast<const f32x4*>(p);
+    f.hi = *reinterpret_cast<const f32x4*>(p + 16);
+    return f;
+  }
+  GT_DEV static void mma(const frag& a, const frag& b, f32x16& c) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.lo[s], b.lo[s], c, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.hi[s], b.hi[s], c, 0, 0, 0);
+  }
+};
+
+// Row (within a 32x32 accumulator block) held by register j of lane half h (CDNA4 C/D map:
+// col = lane & 31, row = (j & 3) + 8 * (j >> 2) + 4 * h).
+GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
+
+// ---------------------------------------------------------------- GroupNorm statistics
+// stats[(b * 8 + g) * 2 + {0,1}] = {sum, sum of squares} over (C/8) x F x T (all grid positions,
+// padded frames included: model/diffusion.py:52-54 normalises over the whole padded tensor).
+GT_DEV void gn_scale_shift(const double* stats, int b, int C, int c, long count, const float* gamma,
+                           const float* beta, float& scale, float& shift) {
+  const int g = c / (C / 8);
+  const double s = stats[(b * 8 + g) * 2 + 0];
+  const double q = stats[(b * 8 + g) * 2 + 1];
+  const double mean = s / (double)count;
+  double var = q / (double)count - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + 1e-5));
+  scale = gamma[c] * rstd;
+  shift = beta[c] - (float)mean * scale;
+}
+
+GT_DEV float mask_at(const float* mask, int T0, int b, int t, int lvl) { return mask[(long)b * T0 + ((long)t << lvl)]; }

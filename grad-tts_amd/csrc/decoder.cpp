@@ -1,0 +1,722 @@
+// Host side of the C ABI (include/gradtts.h): parameter registry, one-time weight packing into the
+// kernels' device layouts, workspace layout and the launch sequence of one U-Net evaluation.
+//
+// Launch sequence of GradLogPEstimator2d.forward (model/diffusion.py:174-216), per Euler step:
+//   down level l (l = 0,1,2):  ResnetBlock x2 -> LinearAttention -> Downsample (l < 2)
+//   mid:                       ResnetBlock -> LinearAttention -> ResnetBlock
+//   up level l (l = 2,1):      concat skip (read in place) -> ResnetBlock x2 -> LinearAttention -> Upsample
+//   final_block conv + fused {GN, Mish, final_conv, Euler update}
+// ResnetBlock = conv3(+GN sums) -> conv3 with GN/Mish/time-bias fused in its load (+GN sums)
+//             -> res_conv 1x1 with the block output fused in its epilogue (or an elementwise kernel)
+// LinearAttention = attn_kv (k/v GEMM + online softmax + context) -> merge -> M_b build -> 1x1 apply
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gradtts.h"
+#include "kernels.h"
+
+using namespace gt;
+
+namespace {
+
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct Shape { std::string name; std::vector<int64_t> dims; int64_t numel() const { int64_t n = 1; for (auto d : dims) n *= d; return n; } };
+
+void add_resnet(std::vector<Shape>& v, const std::string& p, int din, int dout, int dim) {
+  v.push_back({p + "mlp.1.weight", {dout, dim}});
+  v.push_back({p + "mlp.1.bias", {dout}});
+  v.push_back({p + "block1.block.0.weight", {dout, din, 3, 3}});
+  v.push_back({p + "block1.block.0.bias", {dout}});
+  v.push_back({p + "block1.block.1.weight", {dout}});
+  v.push_back({p + "block1.block.1.bias", {dout}});
+  v.push_back({p + "block2.block.0.weight", {dout, dout, 3, 3}});
+  v.push_back({p + "block2.block.0.bias", {dout}});
+  v.push_back({p + "block2.block.1.weight", {dout}});
+  v.push_back({p + "block2.block.1.bias", {dout}});
+  if (din != dout) {
+    v.push_back({p + "res_conv.weight", {dout, din, 1, 1}});
+    v.push_back({p + "res_conv.bias", {dout}});
+  }
+}
+void add_attn(std::vector<Shape>& v, const std::string& p, int c) {
+  v.push_back({p + "fn.g", {1}});
+  v.push_back({p + "fn.fn.to_qkv.weight", {384, c, 1, 1}});
+  v.push_back({p + "fn.fn.to_out.weight", {c, 128, 1, 1}});
+  v.push_back({p + "fn.fn.to_out.bias", {c}});
+}
+
+// GradLogPEstimator2d.state_dict() inventory, registration order (diffusion.py:128-172).
+std::vector<Shape> inventory(int dim, int n_spks, int spk_emb_dim, int n_feats) {
+  std::vector<Shape> v;
+  if (n_spks > 1 || n_spks == -1) {
+    v.push_back({"spk_mlp.0.weight", {spk_emb_dim * 4, spk_emb_dim}});
+    v.push_back({"spk_mlp.0.bias", {spk_emb_dim * 4}});
+    v.push_back({"spk_mlp.2.weight", {n_feats, spk_emb_dim * 4}});
+    v.push_back({"spk_mlp.2.bias", {n_feats}});
+  }
+  v.push_back({"mlp.0.weight", {dim * 4, dim}});
+  v.push_back({"mlp.0.bias", {dim * 4}});
+  v.push_back({"mlp.2.weight", {dim, dim * 4}});
+  v.push_back({"mlp.2.bias", {dim}});
+  const int dims[4] = {2 + (n_spks > 1 ? 1 : 0), dim, dim * 2, dim * 4};
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = "downs." + std::to_string(i) + ".";
+    add_resnet(v, p + "0.", dims[i], dims[i + 1], dim);
+    add_resnet(v, p + "1.", dims[i + 1], dims[i + 1], dim);
+    add_attn(v, p + "2.", dims[i + 1]);
+    if (i < 2) {
+      v.push_back({p + "3.conv.weight", {dims[i + 1], dims[i + 1], 3, 3}});
+      v.push_back({p + "3.conv.bias", {dims[i + 1]}});
+    }
+  }
+  for (int i = 0; i < 2; ++i) {   // reversed(in_out[1:]) = (128,256), (64,128)
+    const int din = dims[2 - i], dout = dims[3 - i];
+    const std::string p = "ups." + std::to_string(i) + ".";
+    add_resnet(v, p + "0.", dout * 2, din, dim);
+    add_resnet(v, p + "1.", din, din, dim);
+    add_attn(v, p + "2.", din);
+    v.push_back({p + "3.conv.weight", {din, din, 4, 4}});
+    v.push_back({p + "3.conv.bias", {din}});
+  }
+  add_resnet(v, "mid_block1.", dims[3], dims[3], dim);
+  add_attn(v, "mid_attn.", dims[3]);
+  add_resnet(v, "mid_block2.", dims[3], dims[3], dim);
+  v.push_back({"final_block.block.0.weight", {dim, dim, 3, 3}});
+  v.push_back({"final_block.block.0.bias", {dim}});
+  v.push_back({"final_block.block.1.weight", {dim}});
+  v.push_back({"final_block.block.1.bias", {dim}});
+  v.push_back({"final_conv.weight", {1, dim, 1, 1}});
+  v.push_back({"final_conv.bias", {1}});
+  return v;
+}
+
+// ResnetBlocks in execution order; their time-bias slices are stacked into one [rows][1792] table.
+const char* kResnets[12] = {"downs.0.0.", "downs.0.1.", "downs.1.0.", "downs.1.1.", "downs.2.0.", "downs.2.1.",
+                            "mid_block1.", "mid_block2.", "ups.0.0.", "ups.0.1.", "ups.1.0.", "ups.1.1."};
+
+bool ends_with(const std::string& s, const char* suf) {
+  const size_t n = strlen(suf);
+  return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+}
+bool starts_with(const std::string& s, const char* pre) { return s.compare(0, strlen(pre), pre) == 0; }
+
+uint16_t f2bf(float f) {   // round to nearest even (finite inputs)
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct Blob {   // host staging of one packed device arena
+  std::vector<uint8_t> bytes;
+  std::map<std::string, size_t> off;
+  size_t put(const std::string& key, const void* src, size_t n) {
+    size_t o = (bytes.size() + 255) & ~size_t(255);
+    bytes.resize(o + n);
+    memcpy(bytes.data() + o, src, n);
+    off[key] = o;
+    return o;
+  }
+};
+
+}  // namespace
+
+struct gt_decoder {
+  int n_feats, dim, n_spks, spk_emb_dim;
+  float beta_min, beta_max, pe_scale;
+  std::vector<Shape> inv;
+  std::map<std::string, int> index;
+  std::vector<std::vector<float>> host;
+  std::vector<bool> set;
+  bool dirty[2] = {true, true};
+  void* arena[2] = {nullptr, nullptr};
+  std::map<std::string, void*> dp[2];
+  std::map<std::string, int> cinpad[2];
+  float freqs[32];
+  // profiling (diagnostics / bench roofline): HIP events around every launch
+  bool prof = false;
+  struct Rec { std::string kernel; double flop, bytes; hipEvent_t e0, e1; };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t pool_used = 0;
+  hipEvent_t ev() {
+    if (pool_used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    return pool[pool_used++];
+  }
+};
+
+namespace {
+
+int ck_of(int dt) { return dt ? 32 : 16; }
+size_t esize(int dt) { return dt ? 2 : 4; }
+
+// pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4]) into [..][Cout][NTAP][Cin_pad] act dtype
+void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const std::vector<float>& w,
+               const std::vector<int64_t>& shp, bool convT) {
+  const int ck = ck_of(dt);
+  std::vector<float> packed;
+  int cin, cout, ntap, npar;
+  if (!convT) {
+    cout = (int)shp[0]; cin = (int)shp[1]; ntap = (int)(shp[2] * shp[3]); npar = 1;
+  } else {
+    cin = (int)shp[0]; cout = (int)shp[1]; ntap = 4; npar = 4;
+  }
+  const int cpad = (cin + ck - 1) / ck * ck;
+  packed.assign((size_t)npar * cout * ntap * cpad, 0.f);
+  if (!convT) {
+    for (int co = 0; co < cout; ++co)
+      for (int ci = 0; ci < cin; ++ci)
+        for (int t = 0; t < ntap; ++t)
+          packed[((size_t)co * ntap + t) * cpad + ci] = w[((size_t)co * cin + ci) * ntap + t];
+  } else {
+    // parity p = 2*pf + pt, tap = 2*a + b; kernel index K(parity, a): p=0 -> {1, 3}, p=1 -> {0, 2}
+    const int K[2][2] = {{1, 3}, {0, 2}};
+    for (int par = 0; par < 4; ++par) {
+      const int pf = par >> 1, pt = par & 1;
+      for (int co = 0; co < cout; ++co)
+        for (int tap = 0; tap < 4; ++tap) {
+          const int kh = K[pf][tap >> 1], kw = K[pt][tap & 1];
+          for (int ci = 0; ci < cin; ++ci)
+            packed[(((size_t)par * cout + co) * 4 + tap) * cpad + ci] = w[(((size_t)ci * cout + co) * 4 + kh) * 4 + kw];
+        }
+    }
+  }
+  if (dt) {
+    std::vector<uint16_t> hb(packed.size());
+    for (size_t i = 0; i < packed.size(); ++i) hb[i] = f2bf(packed[i]);
+    blob.put(key, hb.data(), hb.size() * 2);
+  } else {
+    blob.put(key, packed.data(), packed.size() * 4);
+  }
+  d->cinpad[dt][key] = cpad;
+}
+
+int prepare(gt_decoder* d, int dt) {
+  if (!d->dirty[dt]) return GT_OK;
+  for (size_t i = 0; i < d->inv.size(); ++i)
+    if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
+  Blob blob;
+  auto H = [&](const std::string& k) -> const std::vector<float>& { return d->host[d->index.at(k)]; };
+  for (size_t i = 0; i < d->inv.size(); ++i) {
+    const std::string& k = d->inv[i].name;
+    const auto& shp = d->inv[i].dims;
+    const auto& w = d->host[i];
+    if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
+        ends_with(k, "res_conv.weight")) {
+      pack_conv(blob, d, dt, k, w, shp, false);
+    } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
+      pack_conv(blob, d, dt, k, w, shp, true);
+    } else if (ends_with(k, "to_qkv.weight")) {
+      const int C = (int)shp[1];
+      std::vector<float> q(w.begin(), w.begin() + 128 * C);
+      blob.put(k + ".q", q.data(), q.size() * 4);
+      std::vector<float> kv(w.begin() + 128 * C, w.end());   // [256][C], Cpad == C (multiple of 32)
+      if (dt) {
+        std::vector<uint16_t> hb(kv.size());
+        for (size_t j = 0; j < kv.size(); ++j) hb[j] = f2bf(kv[j]);
+        blob.put(k, hb.data(), hb.size() * 2);
+      } else {
+        blob.put(k, kv.data(), kv.size() * 4);
+      }
+    } else {
+      blob.put(k, w.data(), w.size() * 4);
+      if (ends_with(k, "to_out.bias")) {   // Rezero: g * (W_out o + b_out) -> fold g into the bias
+        const std::string gk = k.substr(0, k.size() - strlen("fn.to_out.bias")) + "g";
+        const float g = H(gk)[0];
+        std::vector<float> gb(w.size());
+        for (size_t j = 0; j < w.size(); ++j) gb[j] = g * w[j];
+        blob.put(k + ".g", gb.data(), gb.size() * 4);
+      }
+    }
+  }
+  {   // stacked ResnetBlock time MLPs
+    std::vector<float> wr, br;
+    for (const char* rk : kResnets) {
+      const auto& W = H(std::string(rk) + "mlp.1.weight");
+      const auto& Bv = H(std::string(rk) + "mlp.1.bias");
+      wr.insert(wr.end(), W.begin(), W.end());
+      br.insert(br.end(), Bv.begin(), Bv.end());
+    }
+    blob.put("tb.w", wr.data(), wr.size() * 4);
+    blob.put("tb.b", br.data(), br.size() * 4);
+  }
+  blob.put("freqs", d->freqs, sizeof(d->freqs));
+  if (d->arena[dt]) { (void)hipFree(d->arena[dt]); d->arena[dt] = nullptr; }
+  if (hipMalloc(&d->arena[dt], blob.bytes.size()) != hipSuccess) return fail(GT_ERR_HIP, "hipMalloc(weights) failed");
+  if (hipMemcpy(d->arena[dt], blob.bytes.data(), blob.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipMemcpy(weights) failed");
+  d->dp[dt].clear();
+  for (auto& kv : blob.off) d->dp[dt][kv.first] = (uint8_t*)d->arena[dt] + kv.second;
+  d->dirty[dt] = false;
+  return GT_OK;
+}
+
+// ---------------------------------------------------------------- workspace
+struct Layout {
+  size_t act[3][5];        // per level: 4-5 activation buffers
+  size_t stats, part, G, Mw, tb, spk, total;
+  int tile_pos[3], ntile[3];
+};
+
+void attn_tiles(int64_t B, int64_t n, int& tile_pos, int& ntile) {
+  int64_t tp = (B * n + 1023) / 1024;
+  tp = (tp + 63) / 64 * 64;
+  if (tp < 64) tp = 64;
+  tile_pos = (int)tp;
+  ntile = (int)((n + tp - 1) / tp);
+}
+
+Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
+  Layout L{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) { size_t r = o; o = (o + bytes + 255) & ~size_t(255); return r; };
+  const int C[3] = {64, 128, 256};
+  for (int l = 0; l < 3; ++l) {
+    const size_t n = (size_t)B * (80 >> l) * (T >> l) * C[l] * esize(dt);
+    for (int i = 0; i < 5; ++i) L.act[l][i] = take(n);
+  }
+  L.stats = take((size_t)25 * B * 16 * sizeof(double));
+  int maxtile = 0;
+  for (int l = 0; l < 3; ++l) {
+    attn_tiles(B, (int64_t)(80 >> l) * (T >> l), L.tile_pos[l], L.ntile[l]);
+    maxtile = std::max(maxtile, L.ntile[l]);
+  }
+  L.part = take((size_t)B * maxtile * 4 * 1088 * 4);
+  L.G = take((size_t)B * 128 * 256 * 4);
+  L.Mw = take((size_t)B * 256 * 256 * esize(dt));
+  L.tb = take((size_t)std::max<int64_t>(B, N) * 1792 * 4);
+  L.spk = take((size_t)B * 80 * 4);
+  L.total = o;
+  return L;
+}
+
+// ---------------------------------------------------------------- one U-Net evaluation
+struct Run {
+  gt_decoder* d;
+  int dt;
+  int B, T;
+  hipStream_t s;
+  uint8_t* ws;
+  Layout L;
+  const float* mask; const float* mu; const float* xt; const float* spk_s;
+  const float* tb; long tb_bstride;
+  int stat_slot = 0;
+  hipError_t err = hipSuccess;
+  const char* probe = nullptr;   // diagnostics: copy the activation named `probe` to probe_out (NCHW fp32)
+  float* probe_out = nullptr;
+  bool probed = false;
+
+  template <class Fn>
+  void timed(const std::string& kernel, double flop, double bytes, Fn&& fn) {
+    if (!d->prof) { chk(fn()); return; }
+    hipEvent_t e0 = d->ev(), e1 = d->ev();
+    if (e0) chk(hipEventRecord(e0, s));
+    chk(fn());
+    if (e1) chk(hipEventRecord(e1, s));
+    if (e0 && e1) d->recs.push_back({kernel, flop, bytes, e0, e1});
+  }
+
+  // conv launch with its algorithmic FLOPs (the reference's conv MACs x 2) and compulsory HBM bytes
+  void conv(ConvKind kind, InMode im, OutMode om, const ConvParams& p) {
+    const double es = (double)esize(dt);
+    const double pin = (double)p.B * p.Fin * p.Tin, pout = (double)p.B * p.Fout * p.Tout;
+    const int taps = kind == CONV1 ? 1 : 9;
+    double flop = kind == CONVT4 ? 2.0 * p.Cin * p.Cout * 16 * pin : 2.0 * p.Cin * p.Cout * taps * pout;
+    double bytes = (im == IN_INPUT ? pin * p.Cin * 4.0 : pin * p.Cin * es) + pout * p.Cout * es +
+                   (double)p.Cout * taps * p.Cin_pad * es * (p.w_bstride ? p.B : 1);
+    if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
+    const int rb = kind == CONV3_S2 ? 1 : 2;
+    const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
+                             "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(rb) + ">";
+    timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
+  }
+
+  void tap(const std::string& name, int lvl, const void* buf, int C) {
+    if (probe && !probed && name == probe) {
+      chk(launch_to_nchw(dt, buf, B, Fl(lvl), Tl(lvl), C, probe_out, s));
+      probed = true;
+    }
+  }
+
+  void* W(const std::string& k) { return d->dp[dt].at(k); }
+  const float* Fp(const std::string& k) { return (const float*)d->dp[dt].at(k); }
+  void* act(int l, int i) { return ws + L.act[l][i]; }
+  double* stats() { return (double*)(ws + L.stats) + (size_t)(stat_slot++) * B * 16; }
+  int Fl(int l) const { return 80 >> l; }
+  int Tl(int l) const { return T >> l; }
+  void chk(hipError_t e) { if (err == hipSuccess && e != hipSuccess) err = e; }
+
+  ConvParams base(int lvl_in, int lvl_out) {
+    ConvParams p;
+    memset(&p, 0, sizeof(p));
+    p.B = B; p.T0 = T; p.mask = mask;
+    p.Fin = Fl(lvl_in); p.Tin = Tl(lvl_in); p.Fout = Fl(lvl_out); p.Tout = Tl(lvl_out);
+    p.lvl_in = lvl_in; p.lvl_out = lvl_out;
+    return p;
+  }
+
+  // ResnetBlock (diffusion.py:61-79). `in1` != null: channel concat (up path). in0 == null: U-Net input.
+  void resnet(const std::string& k, int lvl, const void* in0, int C0, const void* in1, int C1, int Cout, void* out,
+              int tb_off) {
+    const bool input = (in0 == nullptr);
+    const int cin = input ? (d->n_spks > 1 ? 3 : 2) : C0 + C1;
+    void* pre1 = act(lvl, 3);
+    void* pre2 = act(lvl, 4);
+    double* st1 = stats();
+    double* st2 = stats();
+    const long count = (long)(Cout / 8) * Fl(lvl) * Tl(lvl);
+    {   // block1 conv on x*mask
+      ConvParams p = base(lvl, lvl);
+      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block1.block.0.weight");
+      p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
+      p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
+      p.w = W(k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
+      p.out = pre1; p.out_stats = st1;
+      conv(CONV3, input ? IN_INPUT : IN_MASK, OUT_STATS, p);
+      tap(k + "pre1", lvl, pre1, Cout);
+    }
+    {   // block2 conv on (Mish(GN(h1))*m + tb)*m
+      ConvParams p = base(lvl, lvl);
+      p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block2.block.0.weight");
+      p.in0 = pre1; p.C0 = Cout;
+      p.gn_stats = st1; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
+      p.gn_count = count; p.tb = tb + tb_off; p.tb_bstride = tb_bstride;
+      p.w = W(k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
+      p.out = pre2; p.out_stats = st2;
+      conv(CONV3, IN_GN, OUT_STATS, p);
+      tap(k + "pre2", lvl, pre2, Cout);
+    }
+    if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
+      ConvParams p = base(lvl, lvl);
+      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "res_conv.weight");
+      p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
+      p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
+      p.w = W(k + "res_conv.weight"); p.bias = Fp(k + "res_conv.bias");
+      p.pre = pre2; p.pre_stats = st2; p.pre_gamma = Fp(k + "block2.block.1.weight");
+      p.pre_beta = Fp(k + "block2.block.1.bias"); p.pre_count = count;
+      p.out = out;
+      conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
+    } else {                                       // Mish(GN(h2))*m + x*m
+      RbOutParams p;
+      p.pre = pre2; p.stats = st2; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
+      p.count = count; p.x = in0; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = Cout;
+      p.T0 = T; p.lvl = lvl;
+      const double by = 3.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt);
+      timed(std::string("rbout_identity_kernel<") + (dt ? "bf16>" : "float>"), 0.0, by,
+            [&] { return launch_rbout_identity(dt, p, s); });
+    }
+    tap(k.substr(0, k.size() - 1), lvl, out, Cout);
+  }
+
+  // Residual(Rezero(LinearAttention)) (diffusion.py:82-110)
+  void attention(const std::string& k, int lvl, const void* in, int C, void* out) {
+    float* part = (float*)(ws + L.part);
+    float* G = (float*)(ws + L.G);
+    void* Mw = ws + L.Mw;
+    AttnKVParams a;
+    a.x = in; a.B = B; a.n = Fl(lvl) * Tl(lvl); a.C = C; a.Cpad = C;
+    a.wkv = W(k + "fn.fn.to_qkv.weight");
+    a.tile_pos = L.tile_pos[lvl]; a.ntile = L.ntile[lvl]; a.part = part;
+    const double npos = (double)B * a.n;
+    // reference FLOPs of the attention block: qkv 1x1 (2*C*384) + two einsums (2 * 2*4*32*32) + to_out (2*128*C)
+    timed(std::string("attn_kv_kernel<") + (dt ? "bf16>" : "float>"), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
+          npos * C * esize(dt), [&] { return launch_attn_kv(dt, a, s); });
+    timed("attn_merge_kernel", 0.0, 0.0,
+          [&] { return launch_attn_merge(part, B, a.ntile, C, Fp(k + "fn.fn.to_qkv.weight.q"), G, s); });
+    timed(std::string("attn_mbuild_kernel<") + (dt ? "bf16>" : "float>"), 0.0, 0.0,
+          [&] { return launch_attn_mbuild(dt, G, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), B, C, Mw, s); });
+    ConvParams p = base(lvl, lvl);
+    p.Cin = C; p.Cout = C; p.Cin_pad = C;
+    p.in0 = in; p.C0 = C;
+    p.w = Mw; p.w_bstride = (long)C * C; p.bias = Fp(k + "fn.fn.to_out.bias.g");
+    p.out = out;
+    conv(CONV1, IN_PLAIN, OUT_RESID, p);
+    tap(k.substr(0, k.size() - 1), lvl, out, C);
+  }
+
+  void downsample(const std::string& k, int lvl, const void* in, int C, void* out) {   // diffusion.py:30-36
+    ConvParams p = base(lvl, lvl + 1);
+    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[dt].at(k + "conv.weight");
+    p.in0 = in; p.C0 = C;
+    p.w = W(k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
+    conv(CONV3_S2, IN_MASK, OUT_PLAIN, p);
+    tap(k.substr(0, k.size() - 1), lvl + 1, out, C);
+  }
+
+  void upsample(const std::string& k, int lvl, const void* in, int C, void* out) {     // diffusion.py:21-27
+    ConvParams p = base(lvl, lvl - 1);
+    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[dt].at(k + "conv.weight");
+    p.in0 = in; p.C0 = C;
+    p.w = W(k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
+    conv(CONVT4, IN_MASK, OUT_PLAIN, p);
+    tap(k.substr(0, k.size() - 1), lvl - 1, out, C);
+  }
+
+  // GradLogPEstimator2d.forward body; final stage either writes the score or does the Euler update.
+  void unet(int euler, float* out, float* xt_inout, float beta_t, float hstep) {
+    stat_slot = 0;
+    chk(hipMemsetAsync(ws + L.stats, 0, (size_t)25 * B * 16 * sizeof(double), s));
+    int tb_off = 0;
+    auto next_tb = [&](int c) { int o = tb_off; tb_off += c; return o; };
+    // down 0 (80 x T, 64 ch)
+    resnet("downs.0.0.", 0, nullptr, 0, nullptr, 0, 64, act(0, 0), next_tb(64));
+    resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64));
+    attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
+    downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
+    // down 1 (40 x T/2, 128 ch); hidden 1 -> act(1,2)
+    resnet("downs.1.0.", 1, act(1, 0), 64, nullptr, 0, 128, act(1, 1), next_tb(128));
+    resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128));
+    attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
+    downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
+    // down 2 (20 x T/4, 256 ch); hidden 2 -> act(2,2); Identity(x*mask) is absorbed by the next block's mask
+    resnet("downs.2.0.", 2, act(2, 0), 128, nullptr, 0, 256, act(2, 1), next_tb(256));
+    resnet("downs.2.1.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
+    attention("downs.2.2.", 2, act(2, 0), 256, act(2, 2));
+    // mid
+    resnet("mid_block1.", 2, act(2, 2), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
+    attention("mid_attn.", 2, act(2, 0), 256, act(2, 1));
+    resnet("mid_block2.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
+    // up 0 at level 2: cat(x, hidden2) -> 128 ch, then ConvTranspose to level 1
+    resnet("ups.0.0.", 2, act(2, 0), 256, act(2, 2), 256, 128, act(2, 1), next_tb(128));
+    resnet("ups.0.1.", 2, act(2, 1), 128, nullptr, 0, 128, act(2, 0), next_tb(128));
+    attention("ups.0.2.", 2, act(2, 0), 128, act(2, 1));
+    upsample("ups.0.3.", 2, act(2, 1), 128, act(1, 0));
+    // up 1 at level 1: cat(x, hidden1) -> 64 ch, then ConvTranspose to level 0
+    resnet("ups.1.0.", 1, act(1, 0), 128, act(1, 2), 128, 64, act(1, 1), next_tb(64));
+    resnet("ups.1.1.", 1, act(1, 1), 64, nullptr, 0, 64, act(1, 0), next_tb(64));
+    attention("ups.1.2.", 1, act(1, 0), 64, act(1, 1));
+    upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
+    // final_block conv (+GN sums), then the fused GN/Mish/final_conv/(Euler) kernel
+    double* st = stats();
+    {
+      ConvParams p = base(0, 0);
+      p.Cin = 64; p.Cout = 64; p.Cin_pad = d->cinpad[dt].at("final_block.block.0.weight");
+      p.in0 = act(0, 0); p.C0 = 64;
+      p.w = W("final_block.block.0.weight"); p.bias = Fp("final_block.block.0.bias");
+      p.out = act(0, 3); p.out_stats = st;
+      conv(CONV3, IN_MASK, OUT_STATS, p);
+      tap("final_block.pre", 0, act(0, 3), 64);
+    }
+    FinalParams f;
+    f.pre = act(0, 3); f.stats = st; f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
+    f.count = (long)8 * 80 * T; f.wf = Fp("final_conv.weight"); f.bf = Fp("final_conv.bias");
+    f.mask = mask; f.B = B; f.T = T; f.euler = euler; f.out = out; f.mu = mu; f.xt = xt_inout;
+    f.beta_t = beta_t; f.hstep = hstep;
+    timed(std::string("final_kernel<") + (dt ? "bf16>" : "float>"), 2.0 * 64 * B * 80 * T,
+          (double)B * 80 * T * (64 * esize(dt) + 16), [&] { return launch_final(dt, f, s); });
+  }
+};
+
+int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_t ws_bytes, int32_t N) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  if (dtype != GT_F32 && dtype != GT_BF16) return fail(GT_ERR_ARG, "dtype must be GT_F32 or GT_BF16");
+  if (B <= 0 || T <= 0) return fail(GT_ERR_ARG, "B and T must be positive");
+  if (T % 4 != 0) return fail(GT_ERR_ARG, "T must be a multiple of 4 (fix_len_compatibility)");
+  if (B > 65535 || T > (1 << 20)) return fail(GT_ERR_UNSUPPORTED, "B or T too large");
+  if (!ws) return fail(GT_ERR_ARG, "null workspace");
+  if (ws_bytes < gt_decoder_workspace_bytes(d, dtype, B, T, N)) return fail(GT_ERR_WORKSPACE, "workspace too small");
+  return GT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gt_version(void) { return "gradtts-mi355x 0.1 (gfx950)"; }
+const char* gt_last_error(void) { return g_err.c_str(); }
+
+int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float beta_min, float beta_max,
+                      float pe_scale, gt_decoder** out) {
+  if (!out) return fail(GT_ERR_ARG, "null out");
+  *out = nullptr;
+  if (n_feats != 80 || dim != 64 || spk_emb_dim != 64)
+    return fail(GT_ERR_UNSUPPORTED, "kernels implement n_feats=80, dim=64, spk_emb_dim=64");
+  if (!(n_spks == 1 || n_spks == -1 || n_spks > 1)) return fail(GT_ERR_ARG, "n_spks must be 1, -1 or > 1");
+  gt_decoder* d = new gt_decoder();
+  d->n_feats = n_feats; d->dim = dim; d->n_spks = n_spks; d->spk_emb_dim = spk_emb_dim;
+  d->beta_min = beta_min; d->beta_max = beta_max; d->pe_scale = pe_scale;
+  d->inv = inventory(dim, n_spks, spk_emb_dim, n_feats);
+  for (size_t i = 0; i < d->inv.size(); ++i) d->index[d->inv[i].name] = (int)i;
+  d->host.resize(d->inv.size());
+  d->set.assign(d->inv.size(), false);
+  // SinusoidalPosEmb frequencies, as torch computes them: exp(float(k) * float(-ln(1e4)/31)) in fp32
+  const float negc = (float)(-std::log(10000.0) / 31.0);
+  for (int k = 0; k < 32; ++k) d->freqs[k] = expf((float)k * negc);
+  *out = d;
+  return GT_OK;
+}
+
+void gt_decoder_destroy(gt_decoder* d) {
+  if (!d) return;
+  for (auto e : d->pool) (void)hipEventDestroy(e);
+  for (int i = 0; i < 2; ++i)
+    if (d->arena[i]) (void)hipFree(d->arena[i]);
+  delete d;
+}
+
+int gt_decoder_profile_enable(gt_decoder* d, int on) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  d->prof = on != 0;
+  return GT_OK;
+}
+
+int gt_decoder_profile_read(gt_decoder* d, char* buf, size_t cap) {
+  if (!d || !buf || cap == 0) return fail(GT_ERR_ARG, "null argument");
+  struct Agg { long n = 0; double ms = 0, flop = 0, bytes = 0; };
+  std::map<std::string, Agg> agg;
+  for (auto& r : d->recs) {
+    if (hipEventSynchronize(r.e1) != hipSuccess) return fail(GT_ERR_HIP, "hipEventSynchronize failed");
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.e0, r.e1) != hipSuccess) return fail(GT_ERR_HIP, "hipEventElapsedTime failed");
+    Agg& a = agg[r.kernel];
+    a.n += 1; a.ms += ms; a.flop += r.flop; a.bytes += r.bytes;
+  }
+  std::string js = "[";
+  for (auto& kv : agg) {
+    char line[512];
+    snprintf(line, sizeof(line), "%s{\"kernel\": \"%s\", \"launches\": %ld, \"ms\": %.6f, \"flop\": %.6e, \"bytes\": %.6e}",
+             js.size() > 1 ? ", " : "", kv.first.c_str(), kv.second.n, kv.second.ms, kv.second.flop, kv.second.bytes);
+    js += line;
+  }
+  js += "]";
+  d->recs.clear();
+  d->pool_used = 0;
+  if (js.size() + 1 > cap) return fail(GT_ERR_ARG, "buffer too small");
+  memcpy(buf, js.c_str(), js.size() + 1);
+  return GT_OK;
+}
+
+int gt_decoder_num_params(const gt_decoder* d) { return d ? (int)d->inv.size() : 0; }
+const char* gt_decoder_param_name(const gt_decoder* d, int i) {
+  return (d && i >= 0 && i < (int)d->inv.size()) ? d->inv[i].name.c_str() : nullptr;
+}
+int64_t gt_decoder_param_numel(const gt_decoder* d, int i) {
+  return (d && i >= 0 && i < (int)d->inv.size()) ? d->inv[i].numel() : -1;
+}
+
+int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int64_t numel) {
+  if (!d || !name || !data) return fail(GT_ERR_ARG, "null argument");
+  auto it = d->index.find(name);
+  if (it == d->index.end()) return fail(GT_ERR_PARAM, std::string("unknown parameter: ") + name);
+  const Shape& sh = d->inv[it->second];
+  if (numel != sh.numel()) return fail(GT_ERR_PARAM, std::string("numel mismatch for ") + name);
+  d->host[it->second].assign(data, data + numel);
+  d->set[it->second] = true;
+  d->dirty[0] = d->dirty[1] = true;
+  return GT_OK;
+}
+
+size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int64_t T, int32_t n_timesteps) {
+  (void)d;
+  if (B <= 0 || T <= 0) return 0;
+  return layout(dtype ? 1 : 0, B, T, n_timesteps).total;
+}
+
+static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
+                          const float* t, const float* spk, int64_t B, int64_t T, float* out, void* workspace,
+                          size_t workspace_bytes, void* stream, const char* probe, float* probe_out) {
+  int rc = check_common(d, dtype, B, T, workspace, workspace_bytes, 0);
+  if (rc) return rc;
+  if (!x || !mask || !mu || !t || !out) return fail(GT_ERR_ARG, "null tensor");
+  if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
+  if ((rc = prepare(d, dtype))) return rc;
+  Run R;
+  R.d = d; R.dt = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream; R.ws = (uint8_t*)workspace;
+  R.L = layout(dtype, B, T, 0);
+  R.mask = mask; R.mu = mu; R.xt = x; R.spk_s = nullptr;
+  R.probe = probe; R.probe_out = probe_out;
+  float* tbuf = (float*)(R.ws + R.L.tb);
+  TembParams tp;
+  tp.rows = (int)B; tp.tvals = t; tp.n_steps = 0; tp.pe_scale = d->pe_scale; tp.freqs = R.Fp("freqs");
+  tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
+  tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = 1792; tp.tb = tbuf;
+  R.chk(launch_temb(tp, R.s));
+  if (d->n_spks > 1) {
+    float* sbuf = (float*)(R.ws + R.L.spk);
+    R.chk(launch_spk_mlp(spk, (int)B, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"), R.Fp("spk_mlp.2.weight"),
+                         R.Fp("spk_mlp.2.bias"), sbuf, R.s));
+    R.spk_s = sbuf;
+  }
+  R.tb = tbuf; R.tb_bstride = 1792;
+  R.unet(0, out, nullptr, 0.f, 0.f);
+  if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
+  if (probe && !R.probed) return fail(GT_ERR_ARG, std::string("unknown probe stage: ") + probe);
+  return GT_OK;
+}
+
+int gt_estimator_forward(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu, const float* t,
+                         const float* spk, int64_t B, int64_t T, float* out, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  return estimator_impl(d, dtype, x, mask, mu, t, spk, B, T, out, workspace, workspace_bytes, stream, nullptr, nullptr);
+}
+
+int gt_estimator_probe(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu, const float* t,
+                       const float* spk, int64_t B, int64_t T, const char* stage, float* probe_out, float* out,
+                       void* workspace, size_t workspace_bytes, void* stream) {
+  if (!stage || !probe_out) return fail(GT_ERR_ARG, "null stage / probe_out");
+  return estimator_impl(d, dtype, x, mask, mu, t, spk, B, T, out, workspace, workspace_bytes, stream, stage, probe_out);
+}
+
+int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* mask, const float* mu, const float* spk,
+                         int64_t B, int64_t T, int32_t n_timesteps, float* out, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  int rc = check_common(d, dtype, B, T, workspace, workspace_bytes, n_timesteps);
+  if (rc) return rc;
+  if (!z || !mask || !mu || !out) return fail(GT_ERR_ARG, "null tensor");
+  if (n_timesteps < 0) return fail(GT_ERR_ARG, "n_timesteps must be >= 0");
+  if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
+  if ((rc = prepare(d, dtype))) return rc;
+  Run R;
+  R.d = d; R.dt = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream; R.ws = (uint8_t*)workspace;
+  R.L = layout(dtype, B, T, n_timesteps);
+  R.mask = mask; R.mu = mu; R.xt = out; R.spk_s = nullptr;
+  R.chk(launch_mask_copy(z, mask, (int)B, 80, (int)T, out, R.s));   // xt = z * mask  (diffusion.py:257)
+  if (n_timesteps > 0) {
+    float* tbuf = (float*)(R.ws + R.L.tb);
+    TembParams tp;
+    tp.rows = n_timesteps; tp.tvals = nullptr; tp.n_steps = n_timesteps; tp.pe_scale = d->pe_scale;
+    tp.freqs = R.Fp("freqs");
+    tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
+    tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = 1792; tp.tb = tbuf;
+    R.chk(launch_temb(tp, R.s));
+    if (d->n_spks > 1) {
+      float* sbuf = (float*)(R.ws + R.L.spk);
+      R.chk(launch_spk_mlp(spk, (int)B, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"), R.Fp("spk_mlp.2.weight"),
+                           R.Fp("spk_mlp.2.bias"), sbuf, R.s));
+      R.spk_s = sbuf;
+    }
+    const double h = 1.0 / (double)n_timesteps;
+    const float hf = (float)h;
+    const float bmin = d->beta_min, bdelta = (float)((double)d->beta_max - (double)d->beta_min);
+    for (int i = 0; i < n_timesteps; ++i) {
+      // t = (1 - (i + 0.5) h) in fp32; noise_t = beta_min + (beta_max - beta_min) * t  (diffusion.py:259-263)
+      const float t = (float)(1.0 - ((double)i + 0.5) * h);
+      volatile float prod = bdelta * t;   // keep the two fp32 roundings of the reference (no fma)
+      const float beta_t = bmin + prod;
+      R.tb = tbuf + (size_t)i * 1792; R.tb_bstride = 0;
+      R.unet(1, nullptr, out, beta_t, hf);
+      if (R.err != hipSuccess) break;
+    }
+  }
+  if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
+  return GT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// Kernel parameter blocks + host launchers for the Grad-TTS decoder (gfx950).
+// Tensor layout in HBM ("frame rows of channel vectors"): an activation at U-Net level l is
+// [B][F_l][T_l][C] (channels contiguous), F_l = 80 >> l, T_l = T >> l. The sampler state
+// (x_t, mu, z, output) keeps the reference layout [B][80][T] in fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gt {
+
+enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3 };
+enum OutMode { OUT_STATS = 0, OUT_PLAIN = 1, OUT_RBOUT = 2, OUT_RESID = 3 };
+enum ConvKind { CONV3 = 0, CONV3_S2 = 1, CONV1 = 2, CONVT4 = 3 };
+
+struct ConvParams {
+  int B, Fin, Tin, Fout, Tout;   // CONVT4: (Fin,Tin) coarse input grid, (Fout,Tout) = 2x fine grid
+  int Cin, Cout, Cin_pad;
+  int T0;                        // level-0 frame count (mask row length)
+  const float* mask;             // [B][T0]
+  int lvl_in, lvl_out;           // mask pyramid level of input / output grid (mask[..., ::2] per level)
+  // ---- input
+  const void* in0; const void* in1; int C0, C1;      // channels-last sources, concatenated on C
+  const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
+  const double* gn_stats; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
+  const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
+  // ---- weights
+  const void* w; long w_bstride;                      // packed [.][Cout][NTAP][Cin_pad]; per-batch stride
+  const float* bias;                                  // [Cout]
+  // ---- output
+  void* out; double* out_stats;                       // OUT_STATS: GroupNorm sums of the output
+  const void* pre; const double* pre_stats; const float* pre_gamma; const float* pre_beta; long pre_count;  // OUT_RBOUT
+};
+
+hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
+
+struct AttnKVParams {
+  const void* x; int B, n, C, Cpad;   // x: [B][n][C] (n = F*T)
+  const void* wkv;                    // [256][Cpad]: rows 0..127 = k (head*32+d), 128..255 = v
+  int tile_pos, ntile;                // positions per workgroup (multiple of 64), tiles per batch item
+  float* part;                        // [B][ntile][4][1088] = {m[32], l[32], ctx[32][32]}
+};
+hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
+hipError_t launch_attn_merge(const float* part, int B, int ntile, int C, const float* wq, float* G, hipStream_t s);
+hipError_t launch_attn_mbuild(int act_bf16, const float* G, const float* wout, const float* g, int B, int C,
+                              void* Mw, hipStream_t s);
+
+struct FinalParams {
+  const void* pre; const double* stats; const float* gamma; const float* beta; long count;
+  const float* wf; const float* bf;   // final_conv [64], [1]
+  const float* mask; int B, T;
+  int euler;                          // 0: out = score s; 1: Euler update of xt in place
+  float* out; const float* mu; float* xt; float beta_t; float hstep;
+};
+hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s);
+
+struct RbOutParams {
+  const void* pre; const double* stats; const float* gamma; const float* beta; long count;
+  const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
+};
+hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s);
+
+struct TembParams {
+  int rows; const float* tvals;   // tvals == nullptr: row i is Euler step i of n_steps (t computed on device)
+  int n_steps; float pe_scale; const float* freqs;   // freqs [32]
+  const float* w0; const float* b0; const float* w2; const float* b2;   // mlp.0 [256][64], mlp.2 [64][256]
+  const float* wr; const float* br; int nr;           // stacked ResnetBlock mlp.1: [nr][64], [nr]
+  float* tb;                                          // [rows][nr]
+};
+hipError_t launch_temb(const TembParams& p, hipStream_t s);
+hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float* b0, const float* w2,
+                          const float* b2, float* s_out, hipStream_t s);
+hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s);
+// debug probe: channels-last activation [B][F][T][C] (act dtype) -> fp32 NCHW [B][C][F][T]
+hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, int C, float* dst, hipStream_t s);
+
+}  // namespace gt

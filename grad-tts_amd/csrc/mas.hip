@@ -1,0 +1,189 @@
+// Monotonic Alignment Search on gfx950 -- bit-exact replacement of model/monotonic_align/core.pyx.
+//
+// Reference (core.pyx:9-35, generated C core.c:2653-2940), per utterance:
+//   forward  for y < t_y, x in [max(0, t_x+y-t_y), min(t_x, y+1)):
+//              v_cur  = (x == y) ? NEG : V[x, y-1];  v_prev = (x == 0) ? (y == 0 ? 0 : NEG) : V[x-1, y-1]
+//              V[x, y] = ((v_prev > v_cur) ? v_prev : v_cur) + V[x, y]          (one fp32 max + one fp32 add)
+//   backtrack idx = t_x-1; for y = t_y-1..0: P[idx, y] = 1;
+//              if idx != 0 && (idx == y || V[idx, y-1] < V[idx-1, y-1]) idx -= 1
+// Column y depends only on column y-1, so the DP runs column-parallel: ONE wave per utterance, lane L
+// owns rows x = L*XPL .. L*XPL+XPL-1 in registers; the only cross-lane traffic per column is the
+// neighbour's last row (one shuffle). The backtrack needs only the comparison V[x,y-1] < V[x-1,y-1] that
+// the forward already evaluates for in-band cells, so the forward stores one "step down" bit per cell
+// (in LDS, XPL bits per lane per column) instead of the fp32 DP table. Both steps use exactly the
+// reference's fp32 operations in the same order -> bit-identical paths.
+// The {0,1} path tensor is then written by a separate full-bandwidth kernel from the per-column row
+// index (t_y ints per utterance).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gradtts.h"
+
+namespace {
+
+template <int XPL, int YCAP>
+__global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ values, const int32_t* t_xs,
+                                                    const int32_t* t_ys, int tx_max, int ty_max, float neg,
+                                                    int32_t* __restrict__ pidx) {
+  constexpr int kYB = XPL >= 16 ? 2 : (XPL >= 8 ? 4 : 8);   // value columns prefetched per block
+  __shared__ uint16_t bits[YCAP][64];
+  const int b = blockIdx.x, L = threadIdx.x;
+  int tx = t_xs[b], ty = t_ys[b];
+  tx = tx > tx_max ? tx_max : tx;
+  ty = ty > ty_max ? ty_max : ty;
+  int32_t* P = pidx + (long)b * ty_max;
+  if (tx <= 0 || ty <= 0) {
+    for (int y = L; y < ty_max; y += 64) P[y] = -1;
+    return;
+  }
+  const float* V0 = values + (long)b * tx_max * ty_max;
+  float V[XPL];
+  float cur[XPL][kYB], nxt[XPL][kYB];
+#pragma unroll
+  for (int i = 0; i < XPL; ++i) V[i] = 0.f;
+
+  auto load_block = [&](float (&dst)[XPL][kYB], int y0) {
+#pragma unroll
+    for (int i = 0; i < XPL; ++i) {
+      const int x = L * XPL + i;
+#pragma unroll
+      for (int k = 0; k < kYB; ++k) {
+        const int y = y0 + k;
+        dst[i][k] = (x < tx_max && y < ty) ? V0[(long)x * ty_max + y] : 0.f;
+      }
+    }
+  };
+  load_block(cur, 0);
+  for (int y0 = 0; y0 < ty; y0 += kYB) {
+    if (y0 + kYB < ty) load_block(nxt, y0 + kYB);
+#pragma unroll
+    for (int k = 0; k < kYB; ++k) {
+      const int y = y0 + k;
+      if (y < ty) {   // wave-uniform
+        const float left = __shfl_up(V[XPL - 1], 1);   // V[L*XPL-1, y-1] from lane L-1
+        const int lo = tx + y - ty;                     // band: lo <= x < min(tx, y+1)
+        const int hi = min(tx, y + 1);
+        uint32_t w = 0;
+#pragma unroll
+        for (int i = XPL - 1; i >= 0; --i) {
+          const int x = L * XPL + i;
+          const float vc_real = V[i];
+          const float vp_real = (i > 0) ? V[i - 1] : left;
+          const float v_cur = (x == y) ? neg : vc_real;
+          const float v_prev = (x == 0) ? (y == 0 ? 0.f : neg) : vp_real;
+          const float mx = (v_prev > v_cur) ? v_prev : v_cur;
+          const bool in_band = (x >= lo) && (x < hi);
+          const float val = cur[i][k];
+          V[i] = in_band ? (mx + val) : val;
+          const bool down = in_band && (x != 0) && ((x == y) || (vc_real < vp_real));
+          w |= (down ? 1u : 0u) << i;
+        }
+        bits[y][L] = (uint16_t)w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XPL; ++i)
+#pragma unroll
+      for (int k = 0; k < kYB; ++k) cur[i][k] = nxt[i][k];
+  }
+  __syncthreads();
+  if (L == 0) {
+    int idx = tx - 1;
+    for (int y = ty - 1; y >= 0; --y) {
+      P[y] = idx;
+      const uint32_t w = bits[y][idx / XPL];
+      if ((w >> (idx % XPL)) & 1u) idx -= 1;
+    }
+  }
+  for (int y = ty + L; y < ty_max; y += 64) P[y] = -1;
+}
+
+// Serial fallback for utterances beyond the register/LDS budget (t_x > 1024 or t_y > 1024): the
+// reference loop verbatim on a scratch copy of `values`, one thread per utterance.
+__global__ void mas_serial_kernel(const float* values, float* scratch, const int32_t* t_xs, const int32_t* t_ys,
+                                  int b_total, int tx_max, int ty_max, float neg, int32_t* pidx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= b_total) return;
+  const long base = (long)b * tx_max * ty_max;
+  float* V = scratch + base;
+  for (long i = 0; i < (long)tx_max * ty_max; ++i) V[i] = values[base + i];
+  int tx = min(t_xs[b], tx_max), ty = min(t_ys[b], ty_max);
+  int32_t* P = pidx + (long)b * ty_max;
+  for (int y = 0; y < ty_max; ++y) P[y] = -1;
+  if (tx <= 0 || ty <= 0) return;
+  for (int y = 0; y < ty; ++y) {
+    const int lo = max(0, tx + y - ty), hi = min(tx, y + 1);
+    for (int x = lo; x < hi; ++x) {
+      const float v_cur = (x == y) ? neg : V[(long)x * ty_max + y - 1];
+      const float v_prev = (x == 0) ? (y == 0 ? 0.f : neg) : V[(long)(x - 1) * ty_max + y - 1];
+      const float mx = (v_prev > v_cur) ? v_prev : v_cur;
+      V[(long)x * ty_max + y] = mx + V[(long)x * ty_max + y];
+    }
+  }
+  int idx = tx - 1;
+  for (int y = ty - 1; y >= 0; --y) {
+    P[y] = idx;
+    if (idx != 0 && (idx == y || (y > 0 && V[(long)idx * ty_max + y - 1] < V[(long)(idx - 1) * ty_max + y - 1]))) idx -= 1;
+  }
+}
+
+// paths[b][x][y] = (pidx[b][y] == x): every element written once, coalesced along y.
+__global__ __launch_bounds__(256) void mas_fill_kernel(const int32_t* __restrict__ pidx, int tx_max, int ty_max,
+                                                       int32_t* __restrict__ paths) {
+  const int b = blockIdx.y;
+  const long row = (long)blockIdx.x;   // x
+  const int x = (int)row;
+  const int32_t* P = pidx + (long)b * ty_max;
+  int32_t* out = paths + ((long)b * tx_max + x) * ty_max;
+  for (int y = threadIdx.x; y < ty_max; y += 256) out[y] = (P[y] == x) ? 1 : 0;
+}
+
+template <int XPL>
+hipError_t launch_dp(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
+                     int ty_max, float neg, int32_t* pidx, hipStream_t s) {
+  if (ycap <= 256) hipLaunchKernelGGL((mas_dp_kernel<XPL, 256>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
+  else hipLaunchKernelGGL((mas_dp_kernel<XPL, 1024>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gt_maximum_path_workspace_bytes(int64_t b, int64_t tx_max, int64_t ty_max) {
+  if (b <= 0 || tx_max <= 0 || ty_max <= 0) return 0;
+  size_t n = ((size_t)b * ty_max * 4 + 255) & ~size_t(255);
+  if (tx_max > 1024 || ty_max > 1024) n += (size_t)b * tx_max * ty_max * 4;
+  return n;
+}
+
+int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, const int32_t* t_ys, int64_t b,
+                    int64_t tx_max, int64_t ty_max, float max_neg_val, void* workspace, size_t workspace_bytes,
+                    void* stream) {
+  if (b == 0) return GT_OK;
+  if (!paths || !values || !t_xs || !t_ys || b < 0 || tx_max <= 0 || ty_max <= 0) return GT_ERR_ARG;
+  if (b > 65535 || tx_max > (1 << 20) || ty_max > (1 << 20)) return GT_ERR_UNSUPPORTED;
+  if (!workspace || workspace_bytes < gt_maximum_path_workspace_bytes(b, tx_max, ty_max)) return GT_ERR_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* pidx = (int32_t*)workspace;
+  const int B = (int)b, TX = (int)tx_max, TY = (int)ty_max;
+  hipError_t e;
+  if (TX > 1024 || TY > 1024) {
+    float* scratch = (float*)((uint8_t*)workspace + (((size_t)b * ty_max * 4 + 255) & ~size_t(255)));
+    hipLaunchKernelGGL(mas_serial_kernel, dim3((B + 63) / 64), dim3(64), 0, s, values, scratch, t_xs, t_ys, B, TX, TY,
+                       max_neg_val, pidx);
+    e = hipGetLastError();
+  } else {
+    const int xpl = (TX + 63) / 64;
+    if (xpl <= 1) e = launch_dp<1>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    else if (xpl <= 2) e = launch_dp<2>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    else if (xpl <= 4) e = launch_dp<4>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    else if (xpl <= 8) e = launch_dp<8>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    else e = launch_dp<16>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+  }
+  if (e != hipSuccess) return GT_ERR_HIP;
+  hipLaunchKernelGGL(mas_fill_kernel, dim3(TX, B), dim3(256), 0, s, pidx, TX, TY, paths);
+  return hipGetLastError() == hipSuccess ? GT_OK : GT_ERR_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+// Small fused kernels of the Grad-TTS decoder step (gfx950).
+//   final_kernel          final_block GN-apply + Mish + mask, final_conv 1x1 (64->1), mask, and either
+//                         the score output (GradLogPEstimator2d.forward, diffusion.py:212-216) or the
+//                         Euler update of Diffusion.reverse_diffusion (diffusion.py:264-267) in place.
+//   rbout_identity_kernel ResnetBlock output with identity residual: Mish(GN(h2))*m + x*m (diffusion.py:77-79)
+//   temb_kernel           SinusoidalPosEmb -> time MLP -> every ResnetBlock's Mish+Linear time bias
+//                         (diffusion.py:113-125, 143-144, 64-65, 76); one row per Euler step.
+//   spk_mlp_kernel        spk_mlp (diffusion.py:139-141, 175-176)
+//   mask_copy_kernel      x_T = z * mask (diffusion.py:257)
+#include "common.h"
+#include "kernels.h"
+
+namespace gt {
+
+template <class A>
+__global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
+  __shared__ float s_sc[64], s_sh[64], s_w[64];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  if (tid < 64) {
+    float sc, sh;
+    gn_scale_shift(p.stats, b, 64, tid, p.count, p.gamma, p.beta, sc, sh);
+    s_sc[tid] = sc; s_sh[tid] = sh; s_w[tid] = p.wf[tid];
+  }
+  __syncthreads();
+  const long idx = (long)blockIdx.x * 256 + tid;   // position within [80][T]
+  if (idx >= 80L * p.T) return;
+  const int t = (int)(idx % p.T);
+  const float m = p.mask[(long)b * p.T + t];
+  const A* pre = reinterpret_cast<const A*>(p.pre) + ((long)b * 80 * p.T + idx) * 64;
+  constexpr int ICH = Act<A>::kItemCh;
+  float acc = 0.f;
+#pragma unroll
+  for (int it = 0; it < 64 / ICH; ++it) {
+    float v[ICH];
+    item_to_f(reinterpret_cast<const uint4*>(pre)[it], v, A());
+#pragma unroll
+    for (int k = 0; k < ICH; ++k) {
+      const int c = it * ICH + k;
+      const float y = mishf(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
+      acc += s_w[c] * (y * m);                               // final_conv(x * mask)
+    }
+  }
+  const float s = (acc + p.bf[0]) * m;                       // (output * mask).squeeze(1)
+  const long o = (long)b * 80 * p.T + idx;
+  if (!p.euler) {
+    p.out[o] = s;
+  } else {
+    const float x = p.xt[o];
+    float dxt = 0.5f * ((p.mu[o] - x) - s);
+    dxt = dxt * p.beta_t;
+    dxt = dxt * p.hstep;
+    p.xt[o] = (x - dxt) * m;
+  }
+}
+
+template <class A>
+__global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
+  __shared__ float s_sc[256], s_sh[256];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  for (int c = tid; c < p.C; c += 256) {
+    float sc, sh;
+    gn_scale_shift(p.stats, b, p.C, c, p.count, p.gamma, p.beta, sc, sh);
+    s_sc[c] = sc; s_sh[c] = sh;
+  }
+  __syncthreads();
+  constexpr int ICH = Act<A>::kItemCh;
+  const long items = (long)p.F * p.T * p.C / ICH;
+  const long it = (long)blockIdx.x * 256 + tid;
+  if (it >= items) return;
+  const long e0 = it * ICH;                 // element offset within batch item
+  const int c0 = (int)(e0 % p.C);
+  const int t = (int)((e0 / p.C) % p.T);
+  const float m = mask_at(p.mask, p.T0, b, t, p.lvl);
+  const long base = (long)b * p.F * p.T * p.C + e0;
+  float v[ICH], x[ICH];
+  item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + base), v, A());
+  item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.x) + base), x, A());
+#pragma unroll
+  for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * s_sc[c0 + k] + s_sh[c0 + k]) * m + x[k] * m;
+  *reinterpret_cast<uint4*>(reinterpret_cast<A*>(p.out) + base) = f_to_item(v, A());
+}
+
+__global__ __launch_bounds__(256) void temb_kernel(TembParams p) {
+  __shared__ float s_emb[64], s_h[256], s_t[64];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  float t;
+  if (p.tvals) t = p.tvals[row];
+  else t = (float)(1.0 - ((double)row + 0.5) * (1.0 / (double)p.n_steps));   // diffusion.py:259-260
+  if (tid < 64) {
+    const int k = tid & 31;
+    const float arg = (p.pe_scale * t) * p.freqs[k];       // scale * x * emb (diffusion.py:122)
+    s_emb[tid] = tid < 32 ? sinf(arg) : cosf(arg);
+  }
+  __syncthreads();
+  {   // mlp.0 (64 -> 256) + Mish
+    float s = p.b0[tid];
+    for (int k = 0; k < 64; ++k) s += p.w0[tid * 64 + k] * s_emb[k];
+    s_h[tid] = mishf(s);
+  }
+  __syncthreads();
+  if (tid < 64) {   // mlp.2 (256 -> 64), then the Mish that opens every ResnetBlock.mlp
+    float s = p.b2[tid];
+    for (int k = 0; k < 256; ++k) s += p.w2[tid * 256 + k] * s_h[k];
+    s_t[tid] = mishf(s);
+  }
+  __syncthreads();
+  for (int j = tid; j < p.nr; j += 256) {
+    float s = p.br[j];
+    for (int k = 0; k < 64; ++k) s += p.wr[(long)j * 64 + k] * s_t[k];
+    p.tb[(long)row * p.nr + j] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void spk_mlp_kernel(const float* spk, const float* w0, const float* b0, const float* w2,
+                                                     const float* b2, float* s_out) {
+  __shared__ float s_x[64], s_h[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid < 64) s_x[tid] = spk[b * 64 + tid];
+  __syncthreads();
+  float s = b0[tid];
+  for (int k = 0; k < 64; ++k) s += w0[tid * 64 + k] * s_x[k];
+  s_h[tid] = mishf(s);
+  __syncthreads();
+  if (tid < 80) {
+    float o = b2[tid];
+    for (int k = 0; k < 256; ++k) o += w2[tid * 256 + k] * s_h[k];
+    s_out[b * 80 + tid] = o;
+  }
+}
+
+__global__ void mask_copy_kernel(const float* z, const float* mask, int F, int T, long n, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long b = i / ((long)F * T);
+  const int t = (int)(i % T);
+  out[i] = z[i] * mask[b * T + t];
+}
+
+template <class A>
+__global__ void to_nchw_kernel(const A* src, int F, int T, int C, long n, float* dst) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // index into dst [B][C][F][T]
+  if (i >= n) return;
+  const int t = (int)(i % T);
+  const int f = (int)((i / T) % F);
+  const int c = (int)((i / ((long)T * F)) % C);
+  const long b = i / ((long)T * F * C);
+  dst[i] = Act<A>::to_f(src[((b * F + f) * T + t) * C + c]);
+}
+
+hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, int C, float* dst, hipStream_t s) {
+  const long n = (long)B * C * F * T;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (act_bf16) hipLaunchKernelGGL(to_nchw_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)src, F, T, C, n, dst);
+  else hipLaunchKernelGGL(to_nchw_kernel<float>, grid, dim3(256), 0, s, (const float*)src, F, T, C, n, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s) {
+  dim3 grid((unsigned)((80L * p.T + 255) / 256), (unsigned)p.B);
+  if (act_bf16) hipLaunchKernelGGL(final_kernel<bf16>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
+  const long items = (long)p.F * p.T * p.C / (act_bf16 ? 8 : 4);
+  dim3 grid((unsigned)((items + 255) / 256), (unsigned)p.B);
+  if (act_bf16) hipLaunchKernelGGL(rbout_identity_kernel<bf16>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(rbout_identity_kernel<float>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_temb(const TembParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(temb_kernel, dim3(p.rows), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float* b0, const float* w2, const float* b2,
+                          float* s_out, hipStream_t s) {
+  hipLaunchKernelGGL(spk_mlp_kernel, dim3(B), dim3(256), 0, s, spk, w0, b0, w2, b2, s_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s) {
+  const long n = (long)B * F * T;
+  hipLaunchKernelGGL(mask_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, mask, F, T, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace gt

@@ -1,0 +1,73 @@
+"""ctypes binding of the C ABI in include/gradtts.h (libgradtts.so, gfx950).
+
+This is the binding a maintainer of the reference would add. There is no CPU
+fallback: if the library is missing the import fails loudly, and every compute entry point needs
+HIP device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GRADTTS_LIB", os.path.join(_HERE, "libgradtts.so"))
+
+GT_OK, GT_ERR_ARG, GT_ERR_HIP, GT_ERR_PARAM, GT_ERR_UNSUPPORTED, GT_ERR_WORKSPACE = range(6)
+GT_F32, GT_BF16 = 0, 1
+
+# (name, restype, argtypes) for every symbol declared in include/gradtts.h
+_c = ctypes
+SIGNATURES = [
+    ("gt_version", _c.c_char_p, []),
+    ("gt_last_error", _c.c_char_p, []),
+    ("gt_decoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float, _c.c_float,
+                                     _c.POINTER(_c.c_void_p)]),
+    ("gt_decoder_destroy", None, [_c.c_void_p]),
+    ("gt_decoder_num_params", _c.c_int, [_c.c_void_p]),
+    ("gt_decoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),
+    ("gt_decoder_param_numel", _c.c_int64, [_c.c_void_p, _c.c_int]),
+    ("gt_decoder_set_param", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_void_p, _c.c_int64]),
+    ("gt_decoder_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64, _c.c_int32]),
+    ("gt_estimator_forward", _c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+                                        _c.c_void_p]),
+    ("gt_reverse_diffusion", _c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_int64, _c.c_int64, _c.c_int32, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+                                        _c.c_void_p]),
+    ("gt_estimator_probe", _c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                      _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_char_p, _c.c_void_p, _c.c_void_p,
+                                      _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_decoder_profile_enable", _c.c_int, [_c.c_void_p, _c.c_int]),
+    ("gt_decoder_profile_read", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_size_t]),
+    ("gt_maximum_path_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
+    ("gt_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64,
+                                   _c.c_int64, _c.c_float, _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libgradtts.so once (raises if it has not been built: `python grad-tts_amd/build.py`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not found: build it with `python grad-tts_amd/build.py` "
+                              "(no CPU fallback exists for the decoder or MAS)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+class GradTTSError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str):
+    if rc != GT_OK:
+        msg = lib().gt_last_error()
+        raise GradTTSError(f"{what} failed (code {rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,316 @@
+"""Drop-in ``Diffusion`` / ``GradLogPEstimator2d`` backed by the gfx950 HIP decoder (libgradtts.so).
+
+Mirrors ``/root/reference/model/diffusion.py``:
+
+* same constructor arguments (``Diffusion`` :228-242, ``GradLogPEstimator2d`` :128-172);
+* same sub-module attribute names, so ``state_dict()`` keys are identical and reference checkpoints
+  (``train.py:174-175`` -> ``inference.py:66``) load with ``load_state_dict`` unchanged;
+* same call signatures and semantics: ``Diffusion.forward/reverse_diffusion(z, mask, mu, n_timesteps,
+  stoc=False, spk=None)`` (:254-272, deterministic Euler, ``stoc`` ignored as in the reference) and
+  ``GradLogPEstimator2d.forward(x, mask, mu, t, spk=None)`` (:174-216).
+
+The sub-modules are parameter containers only: the whole U-Net (and the whole N-step sampler) runs
+inside the HIP library; there is no PyTorch compute path. Compute dtype is an extension:
+``compute_dtype=torch.float32`` (parity path, default) or ``torch.bfloat16`` (throughput path; fp32
+accumulation, fp32 sampler state).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import GT_BF16, GT_F32, check, lib
+
+
+class _ParamOnly(torch.nn.Module):
+    def forward(self, *args, **kwargs):  # pragma: no cover - guard
+        raise RuntimeError(f"{type(self).__name__} is a parameter container; the U-Net runs as one HIP graph "
+                           "(call GradLogPEstimator2d / Diffusion instead)")
+
+
+class Mish(_ParamOnly):
+    pass
+
+
+class SinusoidalPosEmb(_ParamOnly):
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+
+
+class Upsample(_ParamOnly):
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = torch.nn.ConvTranspose2d(dim, dim, 4, 2, 1)
+
+
+class Downsample(_ParamOnly):
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = torch.nn.Conv2d(dim, dim, 3, 2, 1)
+
+
+class Rezero(_ParamOnly):
+    def __init__(self, fn):
+        super().__init__()
+        self.fn = fn
+        self.g = torch.nn.Parameter(torch.zeros(1))
+
+
+class Residual(_ParamOnly):
+    def __init__(self, fn):
+        super().__init__()
+        self.fn = fn
+
+
+class Block(_ParamOnly):
+    def __init__(self, dim, dim_out, groups=8):
+        super().__init__()
+        self.block = torch.nn.Sequential(torch.nn.Conv2d(dim, dim_out, 3, padding=1),
+                                         torch.nn.GroupNorm(groups, dim_out), Mish())
+
+
+class ResnetBlock(_ParamOnly):
+    def __init__(self, dim, dim_out, time_emb_dim, groups=8):
+        super().__init__()
+        self.mlp = torch.nn.Sequential(Mish(), torch.nn.Linear(time_emb_dim, dim_out))
+        self.block1 = Block(dim, dim_out, groups=groups)
+        self.block2 = Block(dim_out, dim_out, groups=groups)
+        self.res_conv = torch.nn.Conv2d(dim, dim_out, 1) if dim != dim_out else torch.nn.Identity()
+
+
+class LinearAttention(_ParamOnly):
+    def __init__(self, dim, heads=4, dim_head=32):
+        super().__init__()
+        self.heads = heads
+        hidden_dim = dim_head * heads
+        self.to_qkv = torch.nn.Conv2d(dim, hidden_dim * 3, 1, bias=False)
+        self.to_out = torch.nn.Conv2d(hidden_dim, dim, 1)
+
+
+def _dtype_code(dt):
+    if dt in (torch.float32, "fp32", "float32", GT_F32):
+        return GT_F32
+    if dt in (torch.bfloat16, "bf16", "bfloat16", GT_BF16):
+        return GT_BF16
+    raise ValueError(f"compute_dtype must be float32 or bfloat16, got {dt}")
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_cuda(*tensors):
+    if not torch.cuda.is_available():
+        raise RuntimeError("gradtts_amd needs a HIP (MI355X) device; there is no CPU path")
+    dev = None
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            dev = t.device
+            break
+    return dev if dev is not None else torch.device("cuda", torch.cuda.current_device())
+
+
+def _f32c(t, device):
+    return None if t is None else t.to(device=device, dtype=torch.float32).contiguous()
+
+
+class GradLogPEstimator2d(torch.nn.Module):
+    """Score network s_theta (model/diffusion.py:128-216) -- parameters here, compute in libgradtts.so."""
+
+    def __init__(self, dim, dim_mults=(1, 2, 4), groups=8, n_spks=None, spk_emb_dim=64, n_feats=80, pe_scale=1000,
+                 compute_dtype=torch.float32):
+        super().__init__()
+        if tuple(dim_mults) != (1, 2, 4) or groups != 8:
+            raise ValueError("the HIP U-Net implements dim_mults=(1,2,4), groups=8 (the reference configuration)")
+        self.dim = dim
+        self.dim_mults = dim_mults
+        self.groups = groups
+        self.n_spks = n_spks if n_spks is not None else 1
+        self.spk_emb_dim = spk_emb_dim
+        self.n_feats = n_feats
+        self.pe_scale = pe_scale
+        self.compute_dtype = compute_dtype
+        n_spks = self.n_spks
+        if n_spks > 1 or n_spks == -1:
+            self.spk_mlp = torch.nn.Sequential(torch.nn.Linear(spk_emb_dim, spk_emb_dim * 4), Mish(),
+                                               torch.nn.Linear(spk_emb_dim * 4, n_feats))
+        self.time_pos_emb = SinusoidalPosEmb(dim)
+        self.mlp = torch.nn.Sequential(torch.nn.Linear(dim, dim * 4), Mish(), torch.nn.Linear(dim * 4, dim))
+        dims = [2 + (1 if n_spks > 1 else 0), *map(lambda m: dim * m, dim_mults)]
+        in_out = list(zip(dims[:-1], dims[1:]))
+        self.downs = torch.nn.ModuleList([])
+        self.ups = torch.nn.ModuleList([])
+        for ind, (dim_in, dim_out) in enumerate(in_out):
+            is_last = ind >= len(in_out) - 1
+            self.downs.append(torch.nn.ModuleList([
+                ResnetBlock(dim_in, dim_out, time_emb_dim=dim), ResnetBlock(dim_out, dim_out, time_emb_dim=dim),
+                Residual(Rezero(LinearAttention(dim_out))),
+                Downsample(dim_out) if not is_last else torch.nn.Identity()]))
+        mid_dim = dims[-1]
+        self.mid_block1 = ResnetBlock(mid_dim, mid_dim, time_emb_dim=dim)
+        self.mid_attn = Residual(Rezero(LinearAttention(mid_dim)))
+        self.mid_block2 = ResnetBlock(mid_dim, mid_dim, time_emb_dim=dim)
+        for dim_in, dim_out in reversed(in_out[1:]):
+            self.ups.append(torch.nn.ModuleList([
+                ResnetBlock(dim_out * 2, dim_in, time_emb_dim=dim), ResnetBlock(dim_in, dim_in, time_emb_dim=dim),
+                Residual(Rezero(LinearAttention(dim_in))), Upsample(dim_in)]))
+        self.final_block = Block(dim, dim)
+        self.final_conv = torch.nn.Conv2d(dim, 1, 1)
+        self._handle = None
+        self._synced = None
+        self._ws = {}
+
+    # ------------------------------------------------------------------ native handle
+    def _native(self, beta_min=0.05, beta_max=20.0):
+        if self._handle is None:
+            h = ctypes.c_void_p()
+            check(lib().gt_decoder_create(self.n_feats, self.dim, self.n_spks, self.spk_emb_dim, float(beta_min),
+                                          float(beta_max), float(self.pe_scale), ctypes.byref(h)), "gt_decoder_create")
+            self._handle = h
+            self._beta = (beta_min, beta_max)
+        elif self._beta != (beta_min, beta_max):
+            self._free_native()
+            return self._native(beta_min, beta_max)
+        sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        if sig != self._synced:
+            L = lib()
+            params = dict(self.named_parameters())
+            for i in range(L.gt_decoder_num_params(self._handle)):
+                name = L.gt_decoder_param_name(self._handle, i).decode()
+                arr = np.ascontiguousarray(params[name].detach().to("cpu", torch.float32).numpy())
+                check(L.gt_decoder_set_param(self._handle, name.encode(), arr.ctypes.data, arr.size),
+                      f"gt_decoder_set_param({name})")
+            self._synced = sig
+        return self._handle
+
+    def _free_native(self):
+        if self._handle is not None and _lib._lib is not None:
+            _lib._lib.gt_decoder_destroy(self._handle)
+        self._handle = None
+        self._synced = None
+
+    def __del__(self):
+        try:
+            self._free_native()
+        except Exception:
+            pass
+
+    def _workspace(self, device, dcode, B, T, N):
+        nbytes = lib().gt_decoder_workspace_bytes(self._handle, dcode, B, T, N)
+        key = (device, dcode)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self._ws[key] = ws
+        return ws
+
+    def _check_shapes(self, x, mask, mu):
+        if x.dim() != 3 or x.shape[1] != self.n_feats or mu.shape != x.shape or mask.shape != (x.shape[0], 1, x.shape[2]):
+            raise ValueError(f"expected x, mu [B,{self.n_feats},T] and mask [B,1,T]; got {tuple(x.shape)}, "
+                             f"{tuple(mu.shape)}, {tuple(mask.shape)}")
+        if x.shape[2] % 4 != 0:
+            raise ValueError("T must be a multiple of 4 (use fix_len_compatibility, model/utils.py:13-17)")
+
+    def _spk(self, spk, B, device):
+        if spk is None:
+            if self.n_spks > 1:
+                raise ValueError("n_spks > 1 needs spk [B, spk_emb_dim]")
+            return None
+        if not (self.n_spks > 1 or self.n_spks == -1):
+            raise AttributeError("'GradLogPEstimator2d' object has no attribute 'spk_mlp' (n_spks == 1 takes no spk)")
+        spk = _f32c(spk, device)
+        if spk.shape != (B, self.spk_emb_dim):
+            raise ValueError(f"spk must be [B,{self.spk_emb_dim}]")
+        return spk
+
+    @torch.no_grad()
+    def forward(self, x, mask, mu, t, spk=None):
+        """s_theta(x_t, t) -> [B, n_feats, T]  (model/diffusion.py:174-216)."""
+        device = _require_cuda(x, mu, mask)
+        self._check_shapes(x, mask, mu)
+        B, _, T = x.shape
+        out_dtype = x.dtype
+        x32, m32, mu32 = _f32c(x, device), _f32c(mask, device), _f32c(mu, device)
+        t32 = _f32c(torch.as_tensor(t).reshape(-1).expand(B) if torch.as_tensor(t).numel() == 1 else t, device)
+        spk32 = self._spk(spk, B, device)
+        dcode = _dtype_code(self.compute_dtype)
+        with torch.cuda.device(device):
+            h = self._native(*getattr(self, "_beta_override", (0.05, 20.0)))
+            out = torch.empty((B, self.n_feats, T), dtype=torch.float32, device=device)
+            ws = self._workspace(device, dcode, B, T, 0)
+            check(lib().gt_estimator_forward(h, dcode, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
+                                             spk32.data_ptr() if spk32 is not None else None, B, T, out.data_ptr(),
+                                             ws.data_ptr(), ws.numel(), _stream_ptr(device)), "gt_estimator_forward")
+        return out.to(out_dtype)
+
+
+def get_noise(t, beta_init, beta_term, cumulative=False):
+    """``get_noise`` (model/diffusion.py:219-224)."""
+    if cumulative:
+        return beta_init * t + 0.5 * (beta_term - beta_init) * (t ** 2)
+    return beta_init + (beta_term - beta_init) * t
+
+
+class Diffusion(torch.nn.Module):
+    """Score-based decoder (model/diffusion.py:227-287); reverse_diffusion runs fully on the HIP path."""
+
+    def __init__(self, n_feats, dim, n_spks=1, spk_emb_dim=64, beta_min=0.05, beta_max=20, pe_scale=1000,
+                 compute_dtype=torch.float32):
+        super().__init__()
+        self.n_feats = n_feats
+        self.dim = dim
+        self.n_spks = n_spks
+        self.spk_emb_dim = spk_emb_dim
+        self.beta_min = beta_min
+        self.beta_max = beta_max
+        self.pe_scale = pe_scale
+        self.estimator = GradLogPEstimator2d(dim, n_spks=n_spks, spk_emb_dim=spk_emb_dim, n_feats=n_feats,
+                                             pe_scale=pe_scale, compute_dtype=compute_dtype)
+        self.estimator._beta_override = (beta_min, beta_max)
+
+    @property
+    def compute_dtype(self):
+        return self.estimator.compute_dtype
+
+    @compute_dtype.setter
+    def compute_dtype(self, dt):
+        self.estimator.compute_dtype = dt
+
+    @torch.no_grad()
+    def reverse_diffusion(self, z, mask, mu, n_timesteps, stoc=False, spk=None):
+        """Deterministic Euler sampler (model/diffusion.py:254-268); ``stoc`` is accepted and ignored there too."""
+        est = self.estimator
+        device = _require_cuda(z, mu, mask)
+        est._check_shapes(z, mask, mu)
+        B, _, T = z.shape
+        out_dtype = z.dtype
+        z32, m32, mu32 = _f32c(z, device), _f32c(mask, device), _f32c(mu, device)
+        spk32 = est._spk(spk, B, device)
+        dcode = _dtype_code(est.compute_dtype)
+        N = int(n_timesteps)
+        with torch.cuda.device(device):
+            h = est._native(self.beta_min, self.beta_max)
+            out = torch.empty((B, self.n_feats, T), dtype=torch.float32, device=device)
+            ws = est._workspace(device, dcode, B, T, N)
+            check(lib().gt_reverse_diffusion(h, dcode, z32.data_ptr(), m32.data_ptr(), mu32.data_ptr(),
+                                             spk32.data_ptr() if spk32 is not None else None, B, T, N, out.data_ptr(),
+                                             ws.data_ptr(), ws.numel(), _stream_ptr(device)), "gt_reverse_diffusion")
+        return out.to(out_dtype)
+
+    @torch.no_grad()
+    def forward(self, z, mask, mu, n_timesteps, stoc=False, spk=None):
+        return self.reverse_diffusion(z, mask, mu, n_timesteps, stoc, spk)
+
+    def forward_diffusion(self, x0, mask, mu, t):
+        raise NotImplementedError("training path (forward_diffusion/loss_t/compute_loss, diffusion.py:244-287) is "
+                                  "outside this round's hot-path scope (SURVEY.md §8f row 1)")
+
+    def loss_t(self, x0, mask, mu, t, spk=None):
+        raise NotImplementedError("training path is outside this round's hot-path scope (SURVEY.md §8f row 1)")
+
+    def compute_loss(self, x0, mask, mu, spk=None, offset=1e-5):
+        raise NotImplementedError("training path is outside this round's hot-path scope (SURVEY.md §8f row 1)")

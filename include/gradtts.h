@@ -1,0 +1,106 @@
+/*
+ * gradtts.h -- C ABI of the MI355X-native Grad-TTS reverse-diffusion decoder and monotonic alignment.
+ *
+ * Library: grad-tts_amd/gradtts_amd/libgradtts.so (hipcc, gfx950). Plain pointers and sizes only.
+ * Device pointers (all tensors passed to compute calls) must be HIP device memory; `stream` is a
+ * hipStream_t (NULL = default stream). Every compute call is stream-ordered and asynchronous.
+ * Return value: GT_OK or an error code; gt_last_error() gives a thread-local message.
+ *
+ * Reference interfaces replaced (Mattias421/Grad-TTS, files under model/):
+ *   gt_decoder_create        <- Diffusion.__init__ / GradLogPEstimator2d.__init__   diffusion.py:228-242, 128-172
+ *   gt_decoder_set_param     <- nn.Module.load_state_dict on the estimator           (keys: diffusion.py:128-172,
+ *                               saved by train.py:174-175, loaded by inference.py:66)
+ *   gt_estimator_forward     <- GradLogPEstimator2d.forward(x, mask, mu, t, spk)     diffusion.py:174-216
+ *   gt_reverse_diffusion     <- Diffusion.forward / reverse_diffusion(z, mask, mu, n_timesteps, stoc, spk)
+ *                                                                                     diffusion.py:254-272
+ *   gt_maximum_path          <- monotonic_align.core.maximum_path_c(paths, values, t_xs, t_ys, max_neg_val)
+ *                                                                                     monotonic_align/core.pyx:38-45
+ */
+#ifndef GRADTTS_H
+#define GRADTTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  GT_OK = 0,
+  GT_ERR_ARG = 1,          /* bad shape / pointer / value */
+  GT_ERR_HIP = 2,          /* a HIP runtime call failed */
+  GT_ERR_PARAM = 3,        /* unknown parameter name, wrong numel, or a parameter was never set */
+  GT_ERR_UNSUPPORTED = 4,  /* configuration outside what the kernels implement */
+  GT_ERR_WORKSPACE = 5     /* workspace smaller than the *_workspace_bytes() query */
+};
+
+/* Compute dtype of the U-Net activations / MFMA operands (accumulation is always fp32;
+ * the sampler state x_t, mu, z and outputs are always fp32). */
+enum { GT_F32 = 0, GT_BF16 = 1 };
+
+typedef struct gt_decoder gt_decoder;
+
+const char* gt_version(void);
+const char* gt_last_error(void);
+
+/* Diffusion(n_feats, dim, n_spks, spk_emb_dim, beta_min, beta_max, pe_scale).
+ * Supported: n_feats == 80, dim == 64, spk_emb_dim == 64 (the reference configurations, params.py). */
+int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float beta_min, float beta_max,
+                      float pe_scale, gt_decoder** out);
+void gt_decoder_destroy(gt_decoder* dec);
+
+/* Parameter inventory = GradLogPEstimator2d.state_dict() keys in registration order (no "estimator." prefix). */
+int gt_decoder_num_params(const gt_decoder* dec);
+const char* gt_decoder_param_name(const gt_decoder* dec, int i);
+int64_t gt_decoder_param_numel(const gt_decoder* dec, int i);
+/* Copy one parameter (host fp32, contiguous, reference shape) into the decoder. Packing to device
+ * layouts happens lazily at the next compute call (synchronously, outside any stream capture). */
+int gt_decoder_set_param(gt_decoder* dec, const char* name, const float* host_data, int64_t numel);
+
+/* Workspace (device bytes) needed by a compute call with this batch B, padded frame count T and
+ * step count (0 for gt_estimator_forward). */
+size_t gt_decoder_workspace_bytes(const gt_decoder* dec, int dtype, int64_t B, int64_t T, int32_t n_timesteps);
+
+/* One score evaluation: out[B,80,T] = s_theta(x, mask, mu, t, spk).
+ * x, mu, out: [B,80,T] fp32; mask: [B,1,T] fp32 (0/1); t: [B] fp32; spk: [B,64] fp32 or NULL.
+ * T must be a multiple of 4 (fix_len_compatibility, model/utils.py:13-17). */
+int gt_estimator_forward(gt_decoder* dec, int dtype, const float* x, const float* mask, const float* mu,
+                         const float* t, const float* spk, int64_t B, int64_t T, float* out, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+/* Full sampler: out[B,80,T] = x_0 after n_timesteps deterministic Euler steps from x_T = z*mask
+ * (reverse_diffusion ignores `stoc` in the reference; so does this). */
+int gt_reverse_diffusion(gt_decoder* dec, int dtype, const float* z, const float* mask, const float* mu,
+                         const float* spk, int64_t B, int64_t T, int32_t n_timesteps, float* out, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+/* Diagnostics: run gt_estimator_forward and additionally copy the activation produced by `stage`
+ * (a module path of the reference, e.g. "downs.0.1", "downs.1.2", "mid_block1", "ups.0.3", with
+ * ".pre1"/".pre2" for a ResnetBlock's pre-GroupNorm conv outputs, or "final_block.pre") to
+ * probe_out as fp32 [B, C, F_l, T_l]. Used by the parity tests to localise a mismatch. */
+int gt_estimator_probe(gt_decoder* dec, int dtype, const float* x, const float* mask, const float* mu,
+                       const float* t, const float* spk, int64_t B, int64_t T, const char* stage, float* probe_out,
+                       float* out, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Profiling: when enabled, every kernel launch of subsequent compute calls is bracketed by HIP events
+ * on the caller's stream. gt_decoder_profile_read synchronises on them and writes a JSON array
+ * aggregated per kernel: [{"kernel": name, "launches": n, "ms": total, "flop": algorithmic FLOPs,
+ * "bytes": compulsory HBM bytes}, ...] (FLOPs as the reference counts them). */
+int gt_decoder_profile_enable(gt_decoder* dec, int on);
+int gt_decoder_profile_read(gt_decoder* dec, char* json_buf, size_t capacity);
+
+/* Monotonic alignment search.  values: [b, tx_max, ty_max] fp32 (already multiplied by the mask,
+ * as maximum_path does before calling the Cython core); t_xs, t_ys: [b] int32 (device);
+ * paths: [b, tx_max, ty_max] int32 output, fully written (0/1). `values` is not modified
+ * (the reference mutates only its private numpy copy). Requires t_x <= t_y per item (t_x > t_y
+ * makes the reference read out of bounds, core.pyx:34). */
+size_t gt_maximum_path_workspace_bytes(int64_t b, int64_t tx_max, int64_t ty_max);
+int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, const int32_t* t_ys, int64_t b,
+                    int64_t tx_max, int64_t ty_max, float max_neg_val, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GRADTTS_H */

@@ -40,27 +40,32 @@ def linear(p, key, x):
     return F.linear(x, p[key + ".weight"], p[key + ".bias"])
 
 
-def block(p, key, x, mask):
+def block(p, key, x, mask, taps=None, tap_name=None):
     """``Block`` diffusion.py:49-58: Mish(GN8(conv3x3(x*mask))) * mask."""
     y = F.conv2d(x * mask, p[key + ".block.0.weight"], p[key + ".block.0.bias"], padding=1)
+    if taps is not None and tap_name:
+        taps[tap_name] = y
     y = F.group_norm(y, GROUPS, p[key + ".block.1.weight"], p[key + ".block.1.bias"], eps=1e-5)
     return mish(y) * mask
 
 
-def resnet_block(p, key, x, mask, t_emb):
+def resnet_block(p, key, x, mask, t_emb, taps=None):
     """``ResnetBlock`` diffusion.py:61-79."""
-    h = block(p, key + ".block1", x, mask)
+    h = block(p, key + ".block1", x, mask, taps, key + ".pre1")
     tb = F.linear(mish(t_emb), p[key + ".mlp.1.weight"], p[key + ".mlp.1.bias"])
     h = h + tb.unsqueeze(-1).unsqueeze(-1)
-    h = block(p, key + ".block2", h, mask)
+    h = block(p, key + ".block2", h, mask, taps, key + ".pre2")
     if (key + ".res_conv.weight") in p:
         res = F.conv2d(x * mask, p[key + ".res_conv.weight"], p[key + ".res_conv.bias"])
     else:
         res = x * mask
-    return h + res
+    out = h + res
+    if taps is not None:
+        taps[key] = out
+    return out
 
 
-def linear_attention(p, key, x):
+def linear_attention(p, key, x, taps=None):
     """``Residual(Rezero(LinearAttention))`` diffusion.py:39-46, 82-110."""
     b, c, hh, ww = x.shape
     qkv = F.conv2d(x, p[key + ".fn.fn.to_qkv.weight"])
@@ -71,11 +76,17 @@ def linear_attention(p, key, x):
     out = torch.einsum("bhde,bhdn->bhen", context, q)
     out = out.reshape(b, HEADS * DIM_HEAD, hh, ww)
     out = F.conv2d(out, p[key + ".fn.fn.to_out.weight"], p[key + ".fn.fn.to_out.bias"])
-    return out * p[key + ".fn.g"] + x
+    y = out * p[key + ".fn.g"] + x
+    if taps is not None:
+        taps[key] = y
+    return y
 
 
-def estimator(p, x, mask, mu, t, spk=None, n_spks=1, pe_scale=1000.0, dim=64):
-    """``GradLogPEstimator2d.forward`` diffusion.py:174-216. x, mu: [B,80,T]; mask [B,1,T]; t [B]."""
+def estimator(p, x, mask, mu, t, spk=None, n_spks=1, pe_scale=1000.0, dim=64, taps=None):
+    """``GradLogPEstimator2d.forward`` diffusion.py:174-216. x, mu: [B,80,T]; mask [B,1,T]; t [B].
+
+    ``taps`` (optional dict) receives intermediate activations under the stage names the HIP library's
+    probe uses (include/gradtts.h gt_estimator_probe)."""
     s = None
     if spk is not None:
         s = F.linear(mish(linear(p, "spk_mlp.0", spk)), p["spk_mlp.2.weight"], p["spk_mlp.2.bias"])
@@ -90,28 +101,32 @@ def estimator(p, x, mask, mu, t, spk=None, n_spks=1, pe_scale=1000.0, dim=64):
     n_levels = 3
     for i in range(n_levels):
         m = masks[-1]
-        h = resnet_block(p, f"downs.{i}.0", h, m, t_emb)
-        h = resnet_block(p, f"downs.{i}.1", h, m, t_emb)
-        h = linear_attention(p, f"downs.{i}.2", h)
+        h = resnet_block(p, f"downs.{i}.0", h, m, t_emb, taps)
+        h = resnet_block(p, f"downs.{i}.1", h, m, t_emb, taps)
+        h = linear_attention(p, f"downs.{i}.2", h, taps)
         hiddens.append(h)
         if i < n_levels - 1:   # Downsample (diffusion.py:30-36) on x*mask
             h = F.conv2d(h * m, p[f"downs.{i}.3.conv.weight"], p[f"downs.{i}.3.conv.bias"], stride=2, padding=1)
+            if taps is not None:
+                taps[f"downs.{i}.3"] = h
         else:                  # Identity(x*mask)
             h = h * m
         masks.append(m[:, :, :, ::2])
     masks = masks[:-1]
     m = masks[-1]
-    h = resnet_block(p, "mid_block1", h, m, t_emb)
-    h = linear_attention(p, "mid_attn", h)
-    h = resnet_block(p, "mid_block2", h, m, t_emb)
+    h = resnet_block(p, "mid_block1", h, m, t_emb, taps)
+    h = linear_attention(p, "mid_attn", h, taps)
+    h = resnet_block(p, "mid_block2", h, m, t_emb, taps)
     for i in range(n_levels - 1):
         m = masks.pop()
         h = torch.cat((h, hiddens.pop()), dim=1)
-        h = resnet_block(p, f"ups.{i}.0", h, m, t_emb)
-        h = resnet_block(p, f"ups.{i}.1", h, m, t_emb)
-        h = linear_attention(p, f"ups.{i}.2", h)
+        h = resnet_block(p, f"ups.{i}.0", h, m, t_emb, taps)
+        h = resnet_block(p, f"ups.{i}.1", h, m, t_emb, taps)
+        h = linear_attention(p, f"ups.{i}.2", h, taps)
         h = F.conv_transpose2d(h * m, p[f"ups.{i}.3.conv.weight"], p[f"ups.{i}.3.conv.bias"], stride=2, padding=1)
-    h = block(p, "final_block", h, mask)
+        if taps is not None:
+            taps[f"ups.{i}.3"] = h
+    h = block(p, "final_block", h, mask, taps, "final_block.pre")
     out = F.conv2d(h * mask, p["final_conv.weight"], p["final_conv.bias"])
     return (out * mask).squeeze(1)
 

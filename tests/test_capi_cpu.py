@@ -1,0 +1,103 @@
+"""CPU-only checks of the C ABI and the host mirror (no GPU compute is issued here).
+
+* libgradtts.so loads and exports every function declared in include/gradtts.h;
+* the library's parameter inventory == params.py inventory == the module's state_dict keys
+  (== the reference registration order, pinned by make_golden.py against the real reference);
+* argument validation happens before any HIP call.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from gradtts_amd import _lib
+from gradtts_amd.diffusion import Diffusion, GradLogPEstimator2d
+from gradtts_amd.params import estimator_param_shapes, synthetic_state_dict
+
+
+def header_functions():
+    txt = open(os.path.join(REPO, "include", "gradtts.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gt_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    names = header_functions()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in gradtts.h but not exported"
+    assert {s[0] for s in _lib.SIGNATURES} == set(names), "ctypes table out of sync with the header"
+    assert b"gfx950" in L.gt_version()
+
+
+@pytest.mark.parametrize("n_spks", [1, 247, -1])
+def test_inventory_matches_params_and_module(n_spks):
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    _lib.check(L.gt_decoder_create(80, 64, n_spks, 64, 0.05, 20.0, 1000.0, ctypes.byref(h)), "create")
+    try:
+        names = [L.gt_decoder_param_name(h, i).decode() for i in range(L.gt_decoder_num_params(h))]
+        numels = [L.gt_decoder_param_numel(h, i) for i in range(L.gt_decoder_num_params(h))]
+        shapes = estimator_param_shapes(64, n_spks)
+        assert names == list(shapes.keys())
+        assert numels == [int(np.prod(s)) for s in shapes.values()]
+        est = GradLogPEstimator2d(64, n_spks=n_spks)
+        sd = est.state_dict()
+        assert list(sd.keys()) == names
+        assert [tuple(v.shape) for v in sd.values()] == [tuple(s) for s in shapes.values()]
+    finally:
+        L.gt_decoder_destroy(h)
+
+
+def test_reference_state_dict_loads_into_module():
+    dec = Diffusion(80, 64, 1, 64, 0.05, 20, 1000)
+    sd = synthetic_state_dict(seed=3)
+    missing, unexpected = dec.load_state_dict({"estimator." + k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    assert not missing and not unexpected
+    assert torch.equal(dec.estimator.downs[1][2].fn.fn.to_qkv.weight, torch.from_numpy(sd["downs.1.2.fn.fn.to_qkv.weight"]))
+
+
+def test_argument_validation_before_any_hip_call():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.gt_decoder_create(80, 32, 1, 64, 0.05, 20.0, 1000.0, ctypes.byref(h)) == _lib.GT_ERR_UNSUPPORTED
+    assert L.gt_decoder_create(80, 64, 1, 64, 0.05, 20.0, 1000.0, ctypes.byref(h)) == _lib.GT_OK
+    try:
+        x = np.zeros(4, np.float32)
+        assert L.gt_decoder_set_param(h, b"nope.weight", x.ctypes.data, 4) == _lib.GT_ERR_PARAM
+        assert L.gt_decoder_set_param(h, b"final_conv.bias", x.ctypes.data, 4) == _lib.GT_ERR_PARAM  # numel 1
+        assert L.gt_decoder_set_param(h, b"final_conv.bias", x.ctypes.data, 1) == _lib.GT_OK
+        ws = L.gt_decoder_workspace_bytes(h, _lib.GT_BF16, 32, 512, 50)
+        assert ws > 0 and L.gt_decoder_workspace_bytes(h, _lib.GT_F32, 32, 512, 50) > ws
+        fake = ctypes.c_void_p(16)
+        # T not a multiple of 4 -> GT_ERR_ARG (fix_len_compatibility contract), no device access
+        rc = L.gt_reverse_diffusion(h, _lib.GT_F32, fake, fake, fake, None, 2, 30, 10, fake, fake, 1 << 40, None)
+        assert rc == _lib.GT_ERR_ARG and b"multiple of 4" in L.gt_last_error()
+        rc = L.gt_reverse_diffusion(h, _lib.GT_F32, fake, fake, fake, None, 2, 32, 10, fake, fake, 16, None)
+        assert rc == _lib.GT_ERR_WORKSPACE
+        rc = L.gt_reverse_diffusion(h, 7, fake, fake, fake, None, 2, 32, 10, fake, fake, 1 << 40, None)
+        assert rc == _lib.GT_ERR_ARG
+        # every parameter must be set before compute -> GT_ERR_PARAM from the lazy packer
+        rc = L.gt_reverse_diffusion(h, _lib.GT_F32, fake, fake, fake, None, 2, 32, 10, fake, fake, 1 << 40, None)
+        assert rc == _lib.GT_ERR_PARAM and b"never set" in L.gt_last_error()
+    finally:
+        L.gt_decoder_destroy(h)
+    assert L.gt_maximum_path(None, None, None, None, 2, 3, 4, -1e9, None, 0, None) == _lib.GT_ERR_ARG
+    assert L.gt_maximum_path_workspace_bytes(2, 30, 100) >= 2 * 100 * 4
+
+
+def test_product_path_fails_loudly_without_gpu():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    dec = Diffusion(80, 64)
+    z = torch.zeros(1, 80, 8)
+    with pytest.raises(RuntimeError, match="HIP"):
+        dec(z, torch.ones(1, 1, 8), z, 2)
+    from gradtts_amd.monotonic_align import maximum_path
+    with pytest.raises(RuntimeError, match="HIP"):
+        maximum_path(torch.zeros(1, 3, 4), torch.ones(1, 3, 4))
