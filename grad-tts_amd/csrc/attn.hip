@@ -17,6 +17,7 @@
 // attn_mbuild: M_b = g * W_out G  written in the activation dtype as the per-batch 1x1 weight.
 #include "common.h"
 #include "kernels.h"
+#include "wimage.h"
 
 namespace gt {
 
@@ -177,21 +178,24 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int 
   }
 }
 
-// grid (B, C/16): M_b[co][ci] = g * sum_r Wout[co][r] G[b][r][ci]   -> activation dtype [B][C][C]
+// grid (B, C/16): M_b[co][ci] = g * sum_r Wout[co][r] G[b][r][ci], written straight into the packed
+// 1x1 weight image (wimage.h) that conv_kernel DMAs into LDS.
 template <class A>
-__global__ __launch_bounds__(256) void attn_mbuild_kernel(const float* G, const float* wout, const float* g, int C, A* Mw) {
+__global__ __launch_bounds__(256) void attn_mbuild_kernel(const float* G, const float* wout, const float* g, int C,
+                                                          char* Mw, WImg W) {
   __shared__ float s_w[16][129];
   const int b = blockIdx.x, co0 = blockIdx.y * 16, tid = threadIdx.x;
   for (int i = tid; i < 16 * 128; i += 256) s_w[i >> 7][i & 127] = wout[(long)(co0 + (i >> 7)) * 128 + (i & 127)];
   __syncthreads();
   const float gg = g[0];
   const float* Gb = G + (long)b * 128 * C;
+  char* img = Mw + (long)b * W.total;
   const int row = tid >> 4;   // 16 rows x 16 column lanes
   for (int ci = tid & 15; ci < C; ci += 16) {
     float s = 0.f;
 #pragma unroll 8
     for (int k = 0; k < 128; ++k) s += s_w[row][k] * Gb[(long)k * C + ci];
-    Mw[((long)b * C + co0 + row) * C + ci] = Act<A>::from_f(gg * s);
+    *reinterpret_cast<A*>(img + conv_wimg_off(W, co0 + row, 0, ci, (int)sizeof(A))) = Act<A>::from_f(gg * s);
   }
 }
 
@@ -214,10 +218,11 @@ hipError_t launch_attn_merge(const float* part, int B, int ntile, int C, const f
 
 hipError_t launch_attn_mbuild(int act_bf16, const float* G, const float* wout, const float* g, int B, int C, void* Mw,
                               hipStream_t s) {
+  const WImg W = conv_wimg(act_bf16, 1, C, C);
   if (act_bf16)
-    hipLaunchKernelGGL(attn_mbuild_kernel<bf16>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (bf16*)Mw);
+    hipLaunchKernelGGL(attn_mbuild_kernel<bf16>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (char*)Mw, W);
   else
-    hipLaunchKernelGGL(attn_mbuild_kernel<float>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (float*)Mw);
+    hipLaunchKernelGGL(attn_mbuild_kernel<float>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (char*)Mw, W);
   return hipGetLastError();
 }
 

@@ -21,10 +21,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // ---------------------------------------------------------------- numerics
 // Mish (model/diffusion.py:16-18) = x * tanh(softplus(x)); torch softplus returns x for x > 20.
 // tanh(log1p(e^x)) = n / (n + 2) with n = e^x (e^x + 2): one exp + one divide.
+// For x > 20 the clamp keeps e finite and n/(n+2) rounds to 1, i.e. Mish(x) = x as torch's threshold gives.
 GT_DEV float mishf(float x) {
-  if (x > 20.f) return x;  // softplus(x) = x and tanh(x) == 1.0f in fp32 for x > 20
-  float e = __expf(x);
-  float n = e * (e + 2.f);
+  const float e = __expf(fminf(x, 20.f));
+  const float n = e * (e + 2.f);
   return x * __fdividef(n, n + 2.f);
 }
 

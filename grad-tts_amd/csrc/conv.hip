@@ -5,57 +5,93 @@
 //   CONV3_S2 3x3 stride 2 pad 1   -- Downsample                (diffusion.py:33)
 //   CONV1    1x1                  -- ResnetBlock.res_conv (:70) and the folded LinearAttention output
 //   CONVT4   ConvTranspose 4x4 s2 -- Upsample (diffusion.py:24) as four 2x2 sub-pixel convolutions
-// GEMM view: M = output frames of a tile (4 mel rows x 32*RB frames), N = 64 output channels,
-// K = taps x input channels. Four waves, wave w owns mel row f0+w; each wave holds RB x 2 32x32 fp32
-// accumulators. Per input-channel chunk (64 B per position = 32 bf16 / 16 fp32 channels) the
-// workgroup stages the input patch (with the producer's GroupNorm-apply + Mish + mask + time-bias
-// fused into the load: "IN_GN") and the weight slab into LDS, then runs the tap x k-step MFMA loop.
-// LDS rows are padded to 80 B per position / NTAP*64+16 B per output channel so the 16-B fragment
-// reads of a 16-lane group hit 16 distinct bank slots.
-// Epilogues: +bias, GroupNorm partial sums (fp64 atomics, all grid positions incl. padded frames),
-// ResnetBlock output (Mish(GN(h2))*mask + res), attention residual.
+//
+// GEMM view: M = output positions of a tile (4 mel rows x TT frames), N = NT output channels (64 or
+// 128), K = taps x input channels, walked in chunks of CKB bytes per position.
+//   waves: NT=64  -> 4 waves along M (1 mel row each);  NT=128 -> 2 x 2 waves (2 mel rows x 64 ch each)
+//   each wave holds RBW x 2 fp32 32x32 accumulators (v_mfma_f32_32x32x16_bf16 / 32x32x2_f32).
+// Per chunk:
+//   * weight slab: one contiguous global_load_lds DMA of the pre-packed image (wimage.h) -- no VGPRs;
+//   * input patch: prefetched into registers while the previous chunk's MFMAs run, then transformed in
+//     registers (IN_GN: the producer's GroupNorm apply + Mish + mask + time bias, diffusion.py:57-58,76)
+//     and written to LDS (position rows padded to an odd number of 16-B slots: conflict-free fragments);
+//   * 9 (or 4, 1) taps x k-steps of MFMA.
+// Epilogue: each 32x32 accumulator block is transposed through LDS so every lane owns 8 consecutive
+// output channels of one position: 16-B vector stores, vector loads of the ResnetBlock pre-activation
+// (OUT_RBOUT) or the attention residual (OUT_RESID), and GroupNorm sums over all grid positions
+// (padded frames included, as torch's group_norm does) reduced in registers + fp64 atomics.
 #include "common.h"
 #include "kernels.h"
+#include "wimage.h"
 
 namespace gt {
 
-template <class A, int KIND, int IN, int OUT, int RB>
-__global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
-  constexpr bool CONVT = KIND == CONVT4;
-  constexpr int KS = (KIND == CONV1) ? 1 : 3;
-  constexpr int S = (KIND == CONV3_S2) ? 2 : 1;
-  constexpr int TF = 4, TT = 32 * RB;
-  constexpr int NTAP = CONVT ? 4 : KS * KS;
-  constexpr int PAD = (KIND == CONV1) ? 0 : 1;
-  constexpr int PR = (TF - 1) * S + KS;
-  constexpr int PC = (TT - 1) * S + KS;
-  constexpr int POSB = 80;
-  constexpr int WROW = NTAP * 64 + 16;
-  constexpr int CK = 64 / (int)sizeof(A);
-  constexpr int ICH = 16 / (int)sizeof(A);
-  constexpr int KSTEP_B = 16 * (int)sizeof(A);
-  constexpr int KSTEPS = 64 / KSTEP_B;
-  typedef typename Mma<A>::frag frag;
+template <class A, int KIND, int IN, int OUT, int NT>
+struct ConvCfg {
+  static constexpr bool CONVT = KIND == CONVT4;
+  static constexpr int KS = (KIND == CONV1) ? 1 : 3;
+  static constexpr int S = (KIND == CONV3_S2) ? 2 : 1;
+  static constexpr int TF = 4;
+  static constexpr int TT = (KIND == CONV3_S2) ? 32 : 64;
+  static constexpr int RBT = TT / 32;
+  static constexpr int WN = NT / 64;
+  static constexpr int WM = 4 / WN;
+  static constexpr int RW = TF / WM;
+  static constexpr int RBW = RW * RBT;
+  static constexpr int NTAP = CONVT ? 4 : KS * KS;
+  static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
+  static constexpr int PR = (TF - 1) * S + KS;
+  static constexpr int PC = (TT - 1) * S + KS;
+  static constexpr int CKB = conv_ckb(NT);
+  static constexpr int SUBS = CKB / 16;
+  static constexpr int POSB = CKB + 16;
+  static constexpr int WROW = conv_wrow(NTAP, CKB);
+  static constexpr int WBYTES = conv_wbytes(NT, NTAP, CKB);
+  static constexpr int CK = CKB / (int)sizeof(A);
+  static constexpr int ICH = 16 / (int)sizeof(A);
+  static constexpr int KSTEP_B = 16 * (int)sizeof(A);
+  static constexpr int KSTEPS = CKB / KSTEP_B;
+  static constexpr int PITEMS = PR * PC * SUBS;
+  static constexpr int PPT = (PITEMS + 255) / 256;
+  static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
+  static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
+  static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
+  static constexpr int SMEM = A_BYTES + WBYTES + 3 * 256 * 4;
+  static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
+  static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
+};
 
-  __shared__ __attribute__((aligned(16))) char smem[PR * PC * POSB + 64 * WROW];
-  __shared__ float s_sc[256], s_sh[256], s_tb[256];   // IN_GN: per input channel; OUT_RBOUT: per tile cout
+template <class A, int KIND, int IN, int OUT, int NT>
+__global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
+  typedef ConvCfg<A, KIND, IN, OUT, NT> C;
+  typedef typename Mma<A>::frag frag;
+  constexpr bool CONVT = C::CONVT;
+
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];   // ONE LDS object (see guide §5 trap a)
   char* sA = smem;
-  char* sW = smem + PR * PC * POSB;
+  char* sW = smem + C::A_BYTES;
+  float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBYTES);
+  float* s_sh = s_sc + 256;
+  float* s_tb = s_sh + 256;
 
   const int Fg = CONVT ? p.Fin : p.Fout;
   const int Tg = CONVT ? p.Tin : p.Tout;
-  const int n_ft = Fg / TF, n_tt = (Tg + TT - 1) / TT;
+  const int n_ft = Fg / C::TF, n_tt = (Tg + C::TT - 1) / C::TT;
   int bid = blockIdx.x;
   const int tt = bid % n_tt; bid /= n_tt;
   const int ft = bid % n_ft;
   const int b = bid / n_ft;
-  const int f0 = ft * TF, t0 = tt * TT;
-  const int cout0 = blockIdx.y * 64;
+  const int f0 = ft * C::TF, t0 = tt * C::TT;
+  const int ntile = blockIdx.y;
+  const int cout0 = ntile * NT;
   const int par = blockIdx.z, pf = par >> 1, pt = par & 1;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int fi0 = f0 * S - PAD, ti0 = t0 * S - PAD;
+  const int wm = wv % C::WM, wn = wv / C::WM;
+  const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
+  const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
 
+  // per-channel GroupNorm scale/shift and time bias of the INPUT (IN_GN) / OUTPUT (OUT_RBOUT) channels
   if (IN == IN_GN) {
     for (int c = tid; c < p.Cin; c += 256) {
       float sc, sh;
@@ -64,83 +100,114 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     }
   }
   if (OUT == OUT_RBOUT) {
-    if (tid < 64) {
+    for (int c = tid; c < NT; c += 256) {
       float sc, sh;
-      gn_scale_shift(p.pre_stats, b, p.Cout, cout0 + tid, p.pre_count, p.pre_gamma, p.pre_beta, sc, sh);
-      s_sc[tid] = sc; s_sh[tid] = sh;
+      gn_scale_shift(p.pre_stats, b, p.Cout, cout0 + c, p.pre_count, p.pre_gamma, p.pre_beta, sc, sh);
+      s_sc[c] = sc; s_sh[c] = sh;
     }
   }
 
-  f32x16 acc[RB][2];
+  // ---- per-thread patch items: input position index (or -1) and mask, computed once
+  int pidx[C::PPT];
+  float pm[C::PPT];
 #pragma unroll
-  for (int i = 0; i < RB; ++i)
+  for (int j = 0; j < C::PPT; ++j) {
+    const int it = tid + 256 * j;
+    const int pos = it / C::SUBS;
+    const int pr = pos / C::PC, pc = pos - pr * C::PC;
+    const int fi = fi0 + pr, ti = ti0 + pc;
+    const bool ok = it < C::PITEMS && fi >= 0 && fi < p.Fin && ti >= 0 && ti < p.Tin;
+    pidx[j] = ok ? ((b * p.Fin + fi) * p.Tin + ti) : -1;
+    pm[j] = ok ? mask_at(p.mask, p.T0, b, ti, p.lvl_in) : 0.f;
+  }
+
+  uint4 preg[C::PPT];
+  auto load_patch = [&](int c0) {
+    if (IN == IN_INPUT) {   // channels {mu, x_t, spk} (diffusion.py:181/184) -- single chunk
+#pragma unroll
+      for (int j = 0; j < C::PPT; ++j) {
+        uint4 u = make_uint4(0, 0, 0, 0);
+        if (pidx[j] >= 0 && sub == 0) {
+          u.x = __float_as_uint(p.mu[pidx[j]]);
+          u.y = __float_as_uint(p.xt[pidx[j]]);
+          if (p.cin_input == 3) u.z = __float_as_uint(p.spk_s[(long)b * p.Fin + (pidx[j] / p.Tin) % p.Fin]);
+        }
+        preg[j] = u;
+      }
+    } else {
+      const A* src;
+      int cs, Cs;
+      if (c0 < p.C0) { src = reinterpret_cast<const A*>(p.in0); cs = c0; Cs = p.C0; }
+      else { src = reinterpret_cast<const A*>(p.in1); cs = c0 - p.C0; Cs = p.C1; }
+      src += cs + sub * C::ICH;
+#pragma unroll
+      for (int j = 0; j < C::PPT; ++j)
+        preg[j] = pidx[j] >= 0 ? *reinterpret_cast<const uint4*>(src + (long)pidx[j] * Cs) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_patch = [&](int c0) {
+    float sc[C::ICH], sh[C::ICH], tb[C::ICH];
+    if (IN == IN_GN) {
+#pragma unroll
+      for (int k = 0; k < C::ICH; ++k) {
+        const int c = c0 + sub * C::ICH + k;
+        sc[k] = s_sc[c]; sh[k] = s_sh[c]; tb[k] = s_tb[c];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < C::PPT; ++j) {
+      const int it = tid + 256 * j;
+      if (it < C::PITEMS) {
+        float v[C::ICH];
+        const float m = pm[j];
+        if (IN == IN_INPUT) {
+          const float f3[3] = {__uint_as_float(preg[j].x), __uint_as_float(preg[j].y), __uint_as_float(preg[j].z)};
+#pragma unroll
+          for (int k = 0; k < C::ICH; ++k) v[k] = (k < 3 ? f3[k < 3 ? k : 0] : 0.f) * m;
+        } else {
+          item_to_f(preg[j], v, A());
+          if (IN == IN_GN) {
+#pragma unroll
+            for (int k = 0; k < C::ICH; ++k)   // (Mish(GN(h)) * m + tb) * m, m in {0,1}
+              v[k] = (mishf(v[k] * sc[k] + sh[k]) + tb[k]) * m;
+          } else if (IN == IN_MASK) {
+#pragma unroll
+            for (int k = 0; k < C::ICH; ++k) v[k] *= m;
+          }
+        }
+        *reinterpret_cast<uint4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = f_to_item(v, A());
+      }
+    }
+  };
+
+  f32x16 acc[C::RBW][2];
+#pragma unroll
+  for (int i = 0; i < C::RBW; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
 
-  const A* wbase = reinterpret_cast<const A*>(p.w) + (long)b * p.w_bstride +
-                   (CONVT ? (long)par * p.Cout * NTAP * p.Cin_pad : 0L);
-  const int nchunk = p.Cin_pad / CK;
+  const char* wimg = reinterpret_cast<const char*>(p.w) + (long)b * p.w_bstride;
+  const int nchunk = p.Cin_pad / C::CK;
+  wimg += ((long)(par * gridDim.y + ntile) * nchunk) * C::WBYTES;
 
+  load_patch(0);
   for (int ch = 0; ch < nchunk; ++ch) {
-    const int c0 = ch * CK;
-    __syncthreads();
-    // ---- stage the input patch (transform fused into the load)
-    for (int it = tid; it < PR * PC * 4; it += 256) {
-      const int sub = it & 3, pos = it >> 2;
-      const int pr = pos / PC, pc = pos - pr * PC;
-      const int fi = fi0 + pr, ti = ti0 + pc;
-      float v[ICH];
+    const int c0 = ch * C::CK;
+    __syncthreads();                                   // previous chunk's fragments are consumed
+    {   // weight slab: contiguous DMA, 1 KiB per wave instruction
+      const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
 #pragma unroll
-      for (int k = 0; k < ICH; ++k) v[k] = 0.f;
-      if (fi >= 0 && fi < p.Fin && ti >= 0 && ti < p.Tin) {
-        const int c = c0 + sub * ICH;
-        const float m = mask_at(p.mask, p.T0, b, ti, p.lvl_in);
-        if (IN == IN_INPUT) {
-          const long o = ((long)b * p.Fin + fi) * p.Tin + ti;
-#pragma unroll
-          for (int k = 0; k < ICH; ++k) {
-            const int cc = c + k;
-            float x = 0.f;
-            if (cc == 0) x = p.mu[o];
-            else if (cc == 1) x = p.xt[o];
-            else if (cc == 2 && p.cin_input == 3) x = p.spk_s[(long)b * p.Fin + fi];
-            v[k] = x * m;
-          }
-        } else {
-          const A* src; int cs, Cs;
-          if (c < p.C0) { src = reinterpret_cast<const A*>(p.in0); cs = c; Cs = p.C0; }
-          else { src = reinterpret_cast<const A*>(p.in1); cs = c - p.C0; Cs = p.C1; }
-          const uint4 u = *reinterpret_cast<const uint4*>(src + (((long)b * p.Fin + fi) * p.Tin + ti) * Cs + cs);
-          item_to_f(u, v, A());
-          if (IN == IN_GN) {
-#pragma unroll
-            for (int k = 0; k < ICH; ++k) {
-              const float y = v[k] * s_sc[c + k] + s_sh[c + k];
-              float z = mishf(y) * m;          // Block: Mish(GN(.)) * mask            (diffusion.py:57-58)
-              z = (z + s_tb[c + k]) * m;       // h += mlp(t) ; block2 conv input h*mask (diffusion.py:76,57)
-              v[k] = z;
-            }
-          } else if (IN == IN_MASK) {
-#pragma unroll
-            for (int k = 0; k < ICH; ++k) v[k] *= m;
-          }
-        }
-      }
-      *reinterpret_cast<uint4*>(sA + pos * POSB + sub * 16) = f_to_item(v, A());
+      for (int i = wv; i < C::WBYTES / 1024; i += 4)
+        __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
+                                         (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
     }
-    // ---- stage the weight slab [64 cout][NTAP][chunk]
-    for (int it = tid; it < 64 * NTAP * 4; it += 256) {
-      const int sub = it & 3, rowi = it >> 2;
-      const int n = rowi / NTAP, tap = rowi - n * NTAP;
-      const uint4 u = *reinterpret_cast<const uint4*>(wbase + ((long)(cout0 + n) * NTAP + tap) * p.Cin_pad + c0 + sub * ICH);
-      *reinterpret_cast<uint4*>(sW + n * WROW + tap * 64 + sub * 16) = u;
-    }
-    __syncthreads();
-    // ---- MFMA main loop
+    store_patch(c0);
+    __syncthreads();                                   // waits for the DMA (vmcnt) and the LDS writes
+    if (ch + 1 < nchunk) load_patch(c0 + C::CK);       // in flight during this chunk's MFMAs
 #pragma unroll
-    for (int tap = 0; tap < NTAP; ++tap) {
+    for (int tap = 0; tap < C::NTAP; ++tap) {
       int dr, dc;
       if (CONVT) {
         // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0,
@@ -149,76 +216,109 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
         dr = 1 + (pf ? (a ? 0 : 1) : (a ? -1 : 0));
         dc = 1 + (pt ? (bb ? 0 : 1) : (bb ? -1 : 0));
       } else {
-        dr = tap / KS;
-        dc = tap - dr * KS;
+        dr = tap / C::KS;
+        dc = tap - dr * C::KS;
       }
 #pragma unroll
-      for (int ks = 0; ks < KSTEPS; ++ks) {
-        frag af[RB], bfr[2];
+      for (int ks = 0; ks < C::KSTEPS; ++ks) {
+        const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
+        frag af[C::RBW], bfr[2];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-          const int prow = wv * S + dr;
-          const int pcol = (rb * 32 + r) * S + dc;
-          af[rb] = Mma<A>::load(sA + (prow * PC + pcol) * POSB + ks * KSTEP_B + h * (KSTEP_B / 2));
+        for (int rb = 0; rb < C::RBW; ++rb) {
+          const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+          const int prow = lrow * C::S + dr;
+          const int pcol = (tblk * 32 + r) * C::S + dc;
+          af[rb] = Mma<A>::load(sA + (prow * C::PC + pcol) * C::POSB + koff);
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          bfr[cb] = Mma<A>::load(sW + (cb * 32 + r) * WROW + tap * 64 + ks * KSTEP_B + h * (KSTEP_B / 2));
+          bfr[cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < C::RBW; ++rb)
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) Mma<A>::mma(af[rb], bfr[cb], acc[rb][cb]);
       }
     }
   }
 
-  // ---- epilogue
-  A* out = reinterpret_cast<A*>(p.out);
-  const int frow = f0 + wv;
+  // ---- epilogue: transpose each 32x32 block through LDS -> lane = (position, 8 channels)
+  __syncthreads();
+  float* scr = reinterpret_cast<float*>(sA) + wv * 32 * C::EPI_ROW;
+  const int g8 = lane & 3;                 // 8-channel group within the 32-channel block
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+  A* out = reinterpret_cast<A*>(p.out);
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int co = cout0 + cb * 32 + r;
-    const float bias = p.bias[co];
+  for (int rb = 0; rb < C::RBW; ++rb) {
+    const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
+    for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int tc = t0 + rb * 32 + acc_row(j, h);
+      for (int j = 0; j < 16; ++j) scr[acc_row(j, h) * C::EPI_ROW + r] = acc[rb][cb][j];
+      __syncthreads();
+      const int cl = wn * 64 + cb * 32 + g8 * 8;       // tile-local first channel of this lane
+      const int co = cout0 + cl;
+      float bias[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) bias[k] = p.bias[co + k];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int pos = (lane >> 2) + 16 * half;
+        const int tc = t0 + tblk * 32 + pos;
+        float v[8];
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8 + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { v[k] = lo[k] + bias[k]; v[4 + k] = hi[k] + bias[4 + k]; }
         if (tc < Tg) {
+          const int frow = f0 + lrow;
           const int fo = CONVT ? 2 * frow + pf : frow;
           const int to = CONVT ? 2 * tc + pt : tc;
           const long o = (((long)b * p.Fout + fo) * p.Tout + to) * p.Cout + co;
-          float v = acc[rb][cb][j] + bias;
           if (OUT == OUT_STATS) {
-            gs[cb] += v;
-            gq[cb] += v * v;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { gs[cb] += v[k]; gq[cb] += v[k] * v[k]; }
           } else if (OUT == OUT_RBOUT) {
-            // ResnetBlock output: Block2 result + res_conv(x*mask)   (diffusion.py:77-78)
+            // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
             const float m = mask_at(p.mask, p.T0, b, to, p.lvl_out);
-            const float pre = Act<A>::to_f(reinterpret_cast<const A*>(p.pre)[o]);
-            v = mishf(pre * s_sc[cb * 32 + r] + s_sh[cb * 32 + r]) * m + v;
-          } else if (OUT == OUT_RESID) {
-            v = v + Act<A>::to_f(reinterpret_cast<const A*>(p.in0)[o]);   // Residual (diffusion.py:108)
+            float pre[8];
+            if (sizeof(A) == 2) {
+              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o), pre, A());
+            } else {
+              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o), pre, A());
+              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o + 4), pre + 4, A());
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = mishf(pre[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
+          } else if (OUT == OUT_RESID) {   // Residual: fn(x) + x   (diffusion.py:108)
+            float res[8];
+            item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.in0) + o), res, A());
+            if (sizeof(A) == 4)
+              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.in0) + o + 4), res + 4, A());
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += res[k];
           }
-          out[o] = Act<A>::from_f(v);
+          if (sizeof(A) == 2) {
+            *reinterpret_cast<uint4*>(out + o) = f_to_item(v, A());
+          } else {
+            *reinterpret_cast<uint4*>(out + o) = f_to_item(v, A());
+            *reinterpret_cast<uint4*>(out + o + 4) = f_to_item(v + 4, A());
+          }
         }
       }
+      __syncthreads();
     }
   }
   if (OUT == OUT_STATS) {
-    const int gsz = p.Cout / 8;   // channels per GroupNorm group: 8, 16 or 32
+    const int gsz = p.Cout / 8;            // channels per GroupNorm group: 8, 16 or 32
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       float s = gs[cb], q = gq[cb];
-      for (int off = 1; off < gsz && off < 32; off <<= 1) {
-        s += __shfl_xor(s, off);
-        q += __shfl_xor(q, off);
-      }
-      s += __shfl_xor(s, 32);
-      q += __shfl_xor(q, 32);
-      const int co = cout0 + cb * 32 + r;
-      if (h == 0 && (r % gsz) == 0) {
+#pragma unroll
+      for (int off = 4; off < 64; off <<= 1) { s += __shfl_xor(s, off); q += __shfl_xor(q, off); }
+      if (gsz >= 16) { s += __shfl_xor(s, 1); q += __shfl_xor(q, 1); }
+      if (gsz >= 32) { s += __shfl_xor(s, 2); q += __shfl_xor(q, 2); }
+      const int co = cout0 + wn * 64 + cb * 32 + g8 * 8;
+      if (lane < 4 && (co % gsz) == 0) {
         const int g = co / gsz;
         atomicAdd(p.out_stats + (b * 8 + g) * 2 + 0, (double)s);
         atomicAdd(p.out_stats + (b * 8 + g) * 2 + 1, (double)q);
@@ -227,34 +327,35 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   }
 }
 
-template <class A, int KIND, int IN, int OUT>
+template <class A, int KIND, int IN, int OUT, int NT>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
-  constexpr int RB = (KIND == CONV3_S2) ? 1 : 2;
-  constexpr int TT = 32 * RB;
+  typedef ConvCfg<A, KIND, IN, OUT, NT> C;
   const int Fg = (KIND == CONVT4) ? p.Fin : p.Fout;
   const int Tg = (KIND == CONVT4) ? p.Tin : p.Tout;
-  if (Fg % 4 != 0 || p.Cout % 64 != 0) return hipErrorInvalidValue;
-  dim3 grid((unsigned)(p.B * (Fg / 4) * ((Tg + TT - 1) / TT)), (unsigned)(p.Cout / 64), KIND == CONVT4 ? 4u : 1u);
-  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, RB>), grid, dim3(256), 0, s, p);
+  if (Fg % C::TF != 0 || p.Cout % NT != 0 || p.Cin_pad % C::CK != 0) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
+            KIND == CONVT4 ? 4u : 1u);
+  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
-template <class A>
+template <class A, int NT>
 static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   // Instantiated combinations (the U-Net uses exactly these):
-  if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_t<A, CONV3, IN_INPUT, OUT_STATS>(p, s);
-  if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_t<A, CONV3, IN_MASK, OUT_STATS>(p, s);
-  if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_t<A, CONV3, IN_GN, OUT_STATS>(p, s);
-  if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_t<A, CONV1, IN_INPUT, OUT_RBOUT>(p, s);
-  if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_t<A, CONV1, IN_MASK, OUT_RBOUT>(p, s);
-  if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_t<A, CONV1, IN_PLAIN, OUT_RESID>(p, s);
-  if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONV3_S2, IN_MASK, OUT_PLAIN>(p, s);
-  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN>(p, s);
+  if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_t<A, CONV3, IN_INPUT, OUT_STATS, NT>(p, s);
+  if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_t<A, CONV3, IN_MASK, OUT_STATS, NT>(p, s);
+  if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_t<A, CONV3, IN_GN, OUT_STATS, NT>(p, s);
+  if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_t<A, CONV1, IN_INPUT, OUT_RBOUT, NT>(p, s);
+  if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_t<A, CONV1, IN_MASK, OUT_RBOUT, NT>(p, s);
+  if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_t<A, CONV1, IN_PLAIN, OUT_RESID, NT>(p, s);
+  if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONV3_S2, IN_MASK, OUT_PLAIN, NT>(p, s);
+  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT>(p, s);
   return hipErrorNotSupported;
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
-  return act_bf16 ? dispatch<bf16>(kind, im, om, p, s) : dispatch<float>(kind, im, om, p, s);
+  if (!act_bf16) return dispatch<float, 64>(kind, im, om, p, s);
+  return conv_nt(1, p.Cout) == 128 ? dispatch<bf16, 128>(kind, im, om, p, s) : dispatch<bf16, 64>(kind, im, om, p, s);
 }
 
 }  // namespace gt

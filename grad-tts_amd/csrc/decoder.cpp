@@ -21,6 +21,7 @@
 
 #include "gradtts.h"
 #include "kernels.h"
+#include "wimage.h"
 
 using namespace gt;
 
@@ -167,24 +168,28 @@ namespace {
 int ck_of(int dt) { return dt ? 32 : 16; }
 size_t esize(int dt) { return dt ? 2 : 4; }
 
-// pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4]) into [..][Cout][NTAP][Cin_pad] act dtype
+// pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4], as 4 parity images) into the
+// conv_kernel weight image (wimage.h) in the compute dtype
 void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const std::vector<float>& w,
                const std::vector<int64_t>& shp, bool convT) {
-  const int ck = ck_of(dt);
-  std::vector<float> packed;
   int cin, cout, ntap, npar;
   if (!convT) {
     cout = (int)shp[0]; cin = (int)shp[1]; ntap = (int)(shp[2] * shp[3]); npar = 1;
   } else {
     cin = (int)shp[0]; cout = (int)shp[1]; ntap = 4; npar = 4;
   }
-  const int cpad = (cin + ck - 1) / ck * ck;
-  packed.assign((size_t)npar * cout * ntap * cpad, 0.f);
+  const WImg W = conv_wimg(dt, ntap, cin, cout);
+  const int es = (int)esize(dt);
+  std::vector<uint8_t> img((size_t)npar * W.total, 0);
+  auto put = [&](int par, int co, int tap, int ci, float v) {
+    uint8_t* q = img.data() + (size_t)par * W.total + conv_wimg_off(W, co, tap, ci, es);
+    if (dt) { const uint16_t hb = f2bf(v); memcpy(q, &hb, 2); }
+    else memcpy(q, &v, 4);
+  };
   if (!convT) {
     for (int co = 0; co < cout; ++co)
       for (int ci = 0; ci < cin; ++ci)
-        for (int t = 0; t < ntap; ++t)
-          packed[((size_t)co * ntap + t) * cpad + ci] = w[((size_t)co * cin + ci) * ntap + t];
+        for (int t = 0; t < ntap; ++t) put(0, co, t, ci, w[((size_t)co * cin + ci) * ntap + t]);
   } else {
     // parity p = 2*pf + pt, tap = 2*a + b; kernel index K(parity, a): p=0 -> {1, 3}, p=1 -> {0, 2}
     const int K[2][2] = {{1, 3}, {0, 2}};
@@ -193,19 +198,12 @@ void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const 
       for (int co = 0; co < cout; ++co)
         for (int tap = 0; tap < 4; ++tap) {
           const int kh = K[pf][tap >> 1], kw = K[pt][tap & 1];
-          for (int ci = 0; ci < cin; ++ci)
-            packed[(((size_t)par * cout + co) * 4 + tap) * cpad + ci] = w[(((size_t)ci * cout + co) * 4 + kh) * 4 + kw];
+          for (int ci = 0; ci < cin; ++ci) put(par, co, tap, ci, w[(((size_t)ci * cout + co) * 4 + kh) * 4 + kw]);
         }
     }
   }
-  if (dt) {
-    std::vector<uint16_t> hb(packed.size());
-    for (size_t i = 0; i < packed.size(); ++i) hb[i] = f2bf(packed[i]);
-    blob.put(key, hb.data(), hb.size() * 2);
-  } else {
-    blob.put(key, packed.data(), packed.size() * 4);
-  }
-  d->cinpad[dt][key] = cpad;
+  blob.put(key, img.data(), img.size());
+  d->cinpad[dt][key] = W.nchunk * W.ck;
 }
 
 int prepare(gt_decoder* d, int dt) {
@@ -275,8 +273,11 @@ struct Layout {
   int tile_pos[3], ntile[3];
 };
 
-void attn_tiles(int64_t B, int64_t n, int& tile_pos, int& ntile) {
-  int64_t tp = (B * n + 1023) / 1024;
+// Attention tile size depends only on the positions per utterance (never on B), so an utterance gets
+// the same online-softmax partition -- hence bit-identical arithmetic -- whatever batch or GPU shard it
+// is decoded in (sharded runs must match the single-GPU run).
+void attn_tiles(int64_t n, int& tile_pos, int& ntile) {
+  int64_t tp = (n + 63) / 64;
   tp = (tp + 63) / 64 * 64;
   if (tp < 64) tp = 64;
   tile_pos = (int)tp;
@@ -295,12 +296,12 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.stats = take((size_t)25 * B * 16 * sizeof(double));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
-    attn_tiles(B, (int64_t)(80 >> l) * (T >> l), L.tile_pos[l], L.ntile[l]);
+    attn_tiles((int64_t)(80 >> l) * (T >> l), L.tile_pos[l], L.ntile[l]);
     maxtile = std::max(maxtile, L.ntile[l]);
   }
   L.part = take((size_t)B * maxtile * 4 * 1088 * 4);
   L.G = take((size_t)B * 128 * 256 * 4);
-  L.Mw = take((size_t)B * 256 * 256 * esize(dt));
+  L.Mw = take((size_t)B * conv_wimg(dt, 1, 256, 256).total);
   L.tb = take((size_t)std::max<int64_t>(B, N) * 1792 * 4);
   L.spk = take((size_t)B * 80 * 4);
   L.total = o;
@@ -340,7 +341,7 @@ struct Run {
     const int taps = kind == CONV1 ? 1 : 9;
     double flop = kind == CONVT4 ? 2.0 * p.Cin * p.Cout * 16 * pin : 2.0 * p.Cin * p.Cout * taps * pout;
     double bytes = (im == IN_INPUT ? pin * p.Cin * 4.0 : pin * p.Cin * es) + pout * p.Cout * es +
-                   (double)p.Cout * taps * p.Cin_pad * es * (p.w_bstride ? p.B : 1);
+                   (double)p.Cout * (kind == CONVT4 ? 16 : taps) * p.Cin_pad * es * (p.w_bstride ? p.B : 1);
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
     const int rb = kind == CONV3_S2 ? 1 : 2;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
@@ -445,7 +446,7 @@ struct Run {
     ConvParams p = base(lvl, lvl);
     p.Cin = C; p.Cout = C; p.Cin_pad = C;
     p.in0 = in; p.C0 = C;
-    p.w = Mw; p.w_bstride = (long)C * C; p.bias = Fp(k + "fn.fn.to_out.bias.g");
+    p.w = Mw; p.w_bstride = conv_wimg(dt, 1, C, C).total; p.bias = Fp(k + "fn.fn.to_out.bias.g");
     p.out = out;
     conv(CONV1, IN_PLAIN, OUT_RESID, p);
     tap(k.substr(0, k.size() - 1), lvl, out, C);

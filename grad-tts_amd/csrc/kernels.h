@@ -24,7 +24,7 @@ struct ConvParams {
   const double* gn_stats; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
   // ---- weights
-  const void* w; long w_bstride;                      // packed [.][Cout][NTAP][Cin_pad]; per-batch stride
+  const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* bias;                                  // [Cout]
   // ---- output
   void* out; double* out_stats;                       // OUT_STATS: GroupNorm sums of the output

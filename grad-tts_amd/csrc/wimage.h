@@ -1,0 +1,50 @@
+// Packed weight image of one convolution, shared by the host packer (decoder.cpp), the attention
+// matrix builder (attn.hip) and conv_kernel (conv.hip).
+//
+// The image is laid out in exactly the order conv_kernel keeps the weight slab in LDS, so staging a
+// K-chunk is a straight, fully coalesced global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction) with no register round trip:
+//   image[n_tile][chunk] = WBYTES bytes = NT rows (output channels) x WROW bytes, zero padded;
+//   row n           = NTAP taps x CKB bytes (CK input channels of this chunk) + 16 B pad
+// The 16-byte row pad makes the row stride an odd number of 16-B LDS slots, so the 16 lanes of a
+// ds_read_b128 group (16 different output channels) hit 16 different slots.
+#pragma once
+
+namespace gt {
+
+// output channels per workgroup: 128 for bf16 layers with >= 128 output channels, else 64
+inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { return (act_bf16 && cout >= 128) ? 128 : 64; }
+// bytes of one position's channel chunk in LDS: 32 B (16 bf16 ch) for the 128-wide tile, else 64 B
+inline __host__ __device__ constexpr int conv_ckb(int nt) { return nt == 128 ? 32 : 64; }
+inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }
+inline __host__ __device__ constexpr int conv_wbytes(int nt, int ntap, int ckb) {
+  return ((nt * conv_wrow(ntap, ckb) + 4095) / 4096) * 4096;
+}
+
+struct WImg {
+  int nt, ckb, ck, ntap, wrow, wbytes, nchunk, nntile;
+  long total;   // bytes of the whole image
+};
+
+inline __host__ __device__ WImg conv_wimg(int act_bf16, int ntap, int cin, int cout) {
+  WImg w;
+  w.nt = conv_nt(act_bf16, cout);
+  w.ckb = conv_ckb(w.nt);
+  w.ck = w.ckb / (act_bf16 ? 2 : 4);
+  w.ntap = ntap;
+  w.wrow = conv_wrow(ntap, w.ckb);
+  w.wbytes = conv_wbytes(w.nt, ntap, w.ckb);
+  w.nchunk = (cin + w.ck - 1) / w.ck;
+  w.nntile = (cout + w.nt - 1) / w.nt;
+  w.total = (long)w.nntile * w.nchunk * w.wbytes;
+  return w;
+}
+
+// byte offset of weight (co, tap, ci) inside the image (element size esz)
+inline __host__ __device__ long conv_wimg_off(const WImg& w, int co, int tap, int ci, int esz) {
+  const int tile = co / w.nt, n = co - tile * w.nt;
+  const int ch = ci / w.ck, k = ci - ch * w.ck;
+  return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + (long)tap * w.ckb + (long)k * esz;
+}
+
+}  // namespace gt

@@ -69,7 +69,7 @@ def test_maximum_path_known_answers():
     g = load_golden("mas_logprior.npz")
     p = _mas(g["value"], g["mask"])
     for b in range(p.shape[0]):
-        tx, ty = int(g["mask"][b].sum(1)[0]), int(g["mask"][b].sum(0).max())
+        tx, ty = int(g["mask"][b].sum(0)[0]), int(g["mask"][b].sum(1)[0])
         rows = p[b, :, :ty].argmax(0)
         assert (p[b, :, :ty].sum(0) == 1).all() and (np.diff(rows) >= 0).all() and (np.diff(rows) <= 1).all()
         assert p[b, 0, 0] == 1 and p[b, tx - 1, ty - 1] == 1 and p[b, :, ty:].sum() == 0
