@@ -109,4 +109,9 @@ GT_DEV void gn_scale_shift(const double* stats, int b, int C, int c, long count,
   shift = beta[c] - (float)mean * scale;
 }
 
+// Exact-summation grid for the GroupNorm partial sums (see conv_kernel epilogue): |sum| < 2^33 and
+// |sum of squares| < 2^41 per (utterance, group) keep every partial and total exactly representable.
+GT_DEV double gn_snap_sum(double v) { return rint(v * 1048576.0) * (1.0 / 1048576.0); }
+GT_DEV double gn_snap_sq(double v) { return rint(v * 4096.0) * (1.0 / 4096.0); }
+
 GT_DEV float mask_at(const float* mask, int T0, int b, int t, int lvl) { return mask[(long)b * T0 + ((long)t << lvl)]; }

@@ -320,8 +320,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       const int co = cout0 + wn * 64 + cb * 32 + g8 * 8;
       if (lane < 4 && (co % gsz) == 0) {
         const int g = co / gsz;
-        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 0, (double)s);
-        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 1, (double)q);
+        // Partials are snapped to a fixed binary grid so that every fp64 addition is exact: the sums
+        // (hence the whole network) are then independent of atomic order, i.e. deterministic run to run
+        // and identical whatever batch/shard an utterance is decoded in.
+        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 0, gn_snap_sum((double)s));
+        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 1, gn_snap_sq((double)q));
       }
     }
   }

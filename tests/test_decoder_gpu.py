@@ -120,19 +120,19 @@ def test_estimator_vs_oracle_other_shapes(B, T, lengths):
     assert rel_err(y16, ref) <= BF16_EST_TOL
 
 
-def test_bench_shape_properties():
-    """BASELINE config 2 shape (B=32, T=512, bf16): finite, deterministic across runs, and each
-    utterance equals the same utterance computed in a smaller batch (batch independence)."""
+@pytest.mark.parametrize("cdt", [torch.bfloat16, torch.float32])
+def test_bench_shape_deterministic_and_batch_invariant(cdt):
+    """BASELINE config 2 shape (B=32, T=512): finite, bit-identical across runs, and each utterance
+    bit-identical to the same utterance decoded in a smaller batch (what an 8-GPU shard computes).
+    GroupNorm sums are exact (grid-snapped fp64 partials) and attention tiles depend only on T, so
+    no result depends on atomic order or batch composition."""
     from gradtts_amd.params import synthetic_inputs
-    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    dec, _ = make_decoder(1, 0, cdt)
     mu, z, mask, _ = synthetic_inputs(1234, 32, 512)
     zc, mc, muc = _cuda(z), _cuda(mask), _cuda(mu)
     y1 = dec(zc, mc, muc, 3)
     y2 = dec(zc, mc, muc, 3)
     assert torch.isfinite(y1).all()
     sub = dec(zc[5:7].contiguous(), mc[5:7].contiguous(), muc[5:7].contiguous(), 3)
-    d_run = (y1 - y2).abs().max().item()
-    d_batch = (y1[5:7] - sub).abs().max().item()
-    scale = y1.abs().max().item()
-    assert d_run <= 1e-3 * scale, d_run     # GN sums use fp64 atomics: order may vary, not the result
-    assert d_batch <= 1e-3 * scale, d_batch
+    assert torch.equal(y1, y2), (y1 - y2).abs().max().item()
+    assert torch.equal(y1[5:7], sub), (y1[5:7] - sub).abs().max().item()
