@@ -204,7 +204,11 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
                                          (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
     }
     store_patch(c0);
-    __syncthreads();                                   // waits for the DMA (vmcnt) and the LDS writes
+    // The weight DMA must have landed before any wave reads sW. hipcc does NOT reliably emit this
+    // vmcnt(0) for global_load_lds before a barrier (it was missing in the 1x1/128-wide instantiation:
+    // an intermittent, load-dependent race), so it is explicit. Nothing else is in flight here.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (ch + 1 < nchunk) load_patch(c0 + C::CK);       // in flight during this chunk's MFMAs
 #pragma unroll
     for (int tap = 0; tap < C::NTAP; ++tap) {

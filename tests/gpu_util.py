@@ -10,7 +10,7 @@ from gradtts_amd.diffusion import Diffusion, _dtype_code, _stream_ptr
 from gradtts_amd.params import synthetic_state_dict
 
 STAGES = (["downs.0.0.pre1", "downs.0.0.pre2", "downs.0.0", "downs.0.1", "downs.0.2", "downs.0.3",
-           "downs.1.0.pre1", "downs.1.0", "downs.1.1", "downs.1.2", "downs.1.3",
+           "downs.1.0.pre1", "downs.1.0.pre2", "downs.1.0", "downs.1.1.pre1", "downs.1.1.pre2", "downs.1.1", "downs.1.2", "downs.1.3",
            "downs.2.0", "downs.2.1", "downs.2.2", "mid_block1", "mid_attn", "mid_block2",
            "ups.0.0.pre1", "ups.0.0", "ups.0.1", "ups.0.2", "ups.0.3",
            "ups.1.0", "ups.1.1", "ups.1.2", "ups.1.3", "final_block.pre"])
