@@ -94,24 +94,42 @@ template <> struct Mma<float> {
 GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
 
 // ---------------------------------------------------------------- GroupNorm statistics
-// stats[(b * 8 + g) * 2 + {0,1}] = {sum, sum of squares} over (C/8) x F x T (all grid positions,
-// padded frames included: model/diffusion.py:52-54 normalises over the whole padded tensor).
-GT_DEV void gn_scale_shift(const double* stats, int b, int C, int c, long count, const float* gamma,
-                           const float* beta, float& scale, float& shift) {
-  const int g = c / (C / 8);
-  const double s = stats[(b * 8 + g) * 2 + 0];
-  const double q = stats[(b * 8 + g) * 2 + 1];
-  const double mean = s / (double)count;
-  double var = q / (double)count - mean * mean;
-  var = var > 0.0 ? var : 0.0;
-  const float rstd = (float)(1.0 / sqrt(var + 1e-5));
-  scale = gamma[c] * rstd;
-  shift = beta[c] - (float)mean * scale;
+// GroupNorm (model/diffusion.py:53, 8 groups, eps 1e-5) normalises over (C/8) x F x T -- every grid
+// position, padded frames included. The producing conv writes, per workgroup, the fp32 sum and sum of
+// squares of each of the 8 groups it touches into its own slot
+//     part[(b * nparts + slot) * 16 + g * 2 + {0,1}]      (plain stores, no atomics, no memset)
+// and every consumer reduces the slots of its utterance in a fixed order in fp64: deterministic,
+// and independent of how many utterances share the launch.
+// gn_reduce: call with all 256 threads; leaves mean/rstd of the 8 groups in s_mean/s_rstd (LDS).
+GT_DEV void gn_reduce(const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd) {
+  const int t = threadIdx.x, g = t >> 5, j = t & 31;
+  const float* pb = part + (long)b * nparts * 16 + g * 2;
+  double s = 0.0, q = 0.0;
+  for (int i = j; i < nparts; i += 32) {
+    s += (double)pb[(long)i * 16];
+    q += (double)pb[(long)i * 16 + 1];
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    q += __shfl_xor(q, off);
+  }
+  if (j == 0) {
+    const double mean = s / (double)count;
+    double var = q / (double)count - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    s_mean[g] = (float)mean;
+    s_rstd[g] = (float)(1.0 / sqrt(var + 1e-5));
+  }
+  __syncthreads();
 }
 
-// Exact-summation grid for the GroupNorm partial sums (see conv_kernel epilogue): |sum| < 2^33 and
-// |sum of squares| < 2^41 per (utterance, group) keep every partial and total exactly representable.
-GT_DEV double gn_snap_sum(double v) { return rint(v * 1048576.0) * (1.0 / 1048576.0); }
-GT_DEV double gn_snap_sq(double v) { return rint(v * 4096.0) * (1.0 / 4096.0); }
+// per-channel affine of the normalisation: y = x * scale + shift
+GT_DEV void gn_affine(const float* s_mean, const float* s_rstd, int C, int c, const float* gamma, const float* beta,
+                      float& scale, float& shift) {
+  const int g = c / (C / 8);
+  scale = gamma[c] * s_rstd[g];
+  shift = beta[c] - s_mean[g] * scale;
+}
 
 GT_DEV float mask_at(const float* mask, int T0, int b, int t, int lvl) { return mask[(long)b * T0 + ((long)t << lvl)]; }

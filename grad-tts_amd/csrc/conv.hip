@@ -56,7 +56,7 @@ struct ConvCfg {
   static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
   static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
   static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
-  static constexpr int SMEM = A_BYTES + WBYTES + 3 * 256 * 4;
+  static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 64 + 16) * 4;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
 };
@@ -73,6 +73,9 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBYTES);
   float* s_sh = s_sc + 256;
   float* s_tb = s_sh + 256;
+  float* s_sub = s_tb + 256;     // [4 waves][2 col blocks][4 x 8-channel groups][2] GroupNorm sub-partials
+  float* s_mean = s_sub + 64;
+  float* s_rstd = s_mean + 8;
 
   const int Fg = CONVT ? p.Fin : p.Fout;
   const int Tg = CONVT ? p.Tin : p.Tout;
@@ -93,16 +96,18 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
 
   // per-channel GroupNorm scale/shift and time bias of the INPUT (IN_GN) / OUTPUT (OUT_RBOUT) channels
   if (IN == IN_GN) {
+    gn_reduce(p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd);
     for (int c = tid; c < p.Cin; c += 256) {
       float sc, sh;
-      gn_scale_shift(p.gn_stats, b, p.Cin, c, p.gn_count, p.gn_gamma, p.gn_beta, sc, sh);
+      gn_affine(s_mean, s_rstd, p.Cin, c, p.gn_gamma, p.gn_beta, sc, sh);
       s_sc[c] = sc; s_sh[c] = sh; s_tb[c] = p.tb[(long)b * p.tb_bstride + c];
     }
   }
   if (OUT == OUT_RBOUT) {
+    gn_reduce(p.pre_part, p.pre_nparts, b, p.pre_count, s_mean, s_rstd);
     for (int c = tid; c < NT; c += 256) {
       float sc, sh;
-      gn_scale_shift(p.pre_stats, b, p.Cout, cout0 + c, p.pre_count, p.pre_gamma, p.pre_beta, sc, sh);
+      gn_affine(s_mean, s_rstd, p.Cout, cout0 + c, p.pre_gamma, p.pre_beta, sc, sh);
       s_sc[c] = sc; s_sh[c] = sh;
     }
   }
@@ -313,23 +318,36 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     }
   }
   if (OUT == OUT_STATS) {
-    const int gsz = p.Cout / 8;            // channels per GroupNorm group: 8, 16 or 32
+    // per 8-channel sub-group: reduce over the wave's positions (lanes with equal lane&3) ...
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       float s = gs[cb], q = gq[cb];
 #pragma unroll
       for (int off = 4; off < 64; off <<= 1) { s += __shfl_xor(s, off); q += __shfl_xor(q, off); }
-      if (gsz >= 16) { s += __shfl_xor(s, 1); q += __shfl_xor(q, 1); }
-      if (gsz >= 32) { s += __shfl_xor(s, 2); q += __shfl_xor(q, 2); }
-      const int co = cout0 + wn * 64 + cb * 32 + g8 * 8;
-      if (lane < 4 && (co % gsz) == 0) {
-        const int g = co / gsz;
-        // Partials are snapped to a fixed binary grid so that every fp64 addition is exact: the sums
-        // (hence the whole network) are then independent of atomic order, i.e. deterministic run to run
-        // and identical whatever batch/shard an utterance is decoded in.
-        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 0, gn_snap_sum((double)s));
-        atomicAdd(p.out_stats + (b * 8 + g) * 2 + 1, gn_snap_sq((double)q));
+      if (lane < 4) {
+        s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 0] = s;
+        s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
       }
+    }
+    __syncthreads();
+    // ... then per GroupNorm group over waves / sub-groups in a fixed order, one slot per workgroup
+    if (tid < 8) {
+      const int gsz = p.Cout / 8;
+      float S = 0.f, Q = 0.f;
+      for (int w = 0; w < 4; ++w)
+        for (int cb = 0; cb < 2; ++cb)
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const int co = cout0 + (w / C::WM) * 64 + cb * 32 + g8 * 8;
+            if (co / gsz == tid) {
+              S += s_sub[((w * 2 + cb) * 4 + g8) * 2 + 0];
+              Q += s_sub[((w * 2 + cb) * 4 + g8) * 2 + 1];
+            }
+          }
+      const int nparts = n_ft * n_tt * gridDim.y;
+      const int slot = (ft * n_tt + tt) * gridDim.y + ntile;
+      float* dst = p.out_part + ((long)b * nparts + slot) * 16 + tid * 2;
+      dst[0] = S;
+      dst[1] = Q;
     }
   }
 }
@@ -358,6 +376,10 @@ static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParam
   if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONV3_S2, IN_MASK, OUT_PLAIN, NT>(p, s);
   if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT>(p, s);
   return hipErrorNotSupported;
+}
+
+int conv_gn_nparts(int act_bf16, int F, int T, int Cout) {   // CONV3 tiles: 4 rows x 64 frames x NT channels
+  return (F / 4) * ((T + 63) / 64) * (Cout / conv_nt(act_bf16, Cout));
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {

@@ -270,6 +270,7 @@ int prepare(gt_decoder* d, int dt) {
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
   size_t stats, part, G, Mw, tb, spk, total;
+  int pmax;
   int tile_pos[3], ntile[3];
 };
 
@@ -293,7 +294,8 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
     const size_t n = (size_t)B * (80 >> l) * (T >> l) * C[l] * esize(dt);
     for (int i = 0; i < 5; ++i) L.act[l][i] = take(n);
   }
-  L.stats = take((size_t)25 * B * 16 * sizeof(double));
+  L.pmax = 20 * (int)((T + 63) / 64);   // GroupNorm partial slots per utterance: largest producer grid (level 0)
+  L.stats = take((size_t)25 * B * L.pmax * 16 * sizeof(float));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
     attn_tiles((int64_t)(80 >> l) * (T >> l), L.tile_pos[l], L.ntile[l]);
@@ -359,7 +361,7 @@ struct Run {
   void* W(const std::string& k) { return d->dp[dt].at(k); }
   const float* Fp(const std::string& k) { return (const float*)d->dp[dt].at(k); }
   void* act(int l, int i) { return ws + L.act[l][i]; }
-  double* stats() { return (double*)(ws + L.stats) + (size_t)(stat_slot++) * B * 16; }
+  float* stats() { return (float*)(ws + L.stats) + (size_t)(stat_slot++) * B * L.pmax * 16; }
   int Fl(int l) const { return 80 >> l; }
   int Tl(int l) const { return T >> l; }
   void chk(hipError_t e) { if (err == hipSuccess && e != hipSuccess) err = e; }
@@ -380,8 +382,9 @@ struct Run {
     const int cin = input ? (d->n_spks > 1 ? 3 : 2) : C0 + C1;
     void* pre1 = act(lvl, 3);
     void* pre2 = act(lvl, 4);
-    double* st1 = stats();
-    double* st2 = stats();
+    float* st1 = stats();
+    float* st2 = stats();
+    const int np = conv_gn_nparts(dt, Fl(lvl), Tl(lvl), Cout);
     const long count = (long)(Cout / 8) * Fl(lvl) * Tl(lvl);
     {   // block1 conv on x*mask
       ConvParams p = base(lvl, lvl);
@@ -389,7 +392,7 @@ struct Run {
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
       p.w = W(k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
-      p.out = pre1; p.out_stats = st1;
+      p.out = pre1; p.out_part = st1;
       conv(CONV3, input ? IN_INPUT : IN_MASK, OUT_STATS, p);
       tap(k + "pre1", lvl, pre1, Cout);
     }
@@ -397,10 +400,10 @@ struct Run {
       ConvParams p = base(lvl, lvl);
       p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block2.block.0.weight");
       p.in0 = pre1; p.C0 = Cout;
-      p.gn_stats = st1; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
+      p.gn_part = st1; p.gn_nparts = np; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
       p.gn_count = count; p.tb = tb + tb_off; p.tb_bstride = tb_bstride;
       p.w = W(k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
-      p.out = pre2; p.out_stats = st2;
+      p.out = pre2; p.out_part = st2;
       conv(CONV3, IN_GN, OUT_STATS, p);
       tap(k + "pre2", lvl, pre2, Cout);
     }
@@ -410,13 +413,13 @@ struct Run {
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
       p.w = W(k + "res_conv.weight"); p.bias = Fp(k + "res_conv.bias");
-      p.pre = pre2; p.pre_stats = st2; p.pre_gamma = Fp(k + "block2.block.1.weight");
+      p.pre = pre2; p.pre_part = st2; p.pre_nparts = np; p.pre_gamma = Fp(k + "block2.block.1.weight");
       p.pre_beta = Fp(k + "block2.block.1.bias"); p.pre_count = count;
       p.out = out;
       conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
     } else {                                       // Mish(GN(h2))*m + x*m
       RbOutParams p;
-      p.pre = pre2; p.stats = st2; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
+      p.pre = pre2; p.part = st2; p.nparts = np; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
       p.count = count; p.x = in0; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = Cout;
       p.T0 = T; p.lvl = lvl;
       const double by = 3.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt);
@@ -473,7 +476,6 @@ struct Run {
   // GradLogPEstimator2d.forward body; final stage either writes the score or does the Euler update.
   void unet(int euler, float* out, float* xt_inout, float beta_t, float hstep) {
     stat_slot = 0;
-    chk(hipMemsetAsync(ws + L.stats, 0, (size_t)25 * B * 16 * sizeof(double), s));
     int tb_off = 0;
     auto next_tb = [&](int c) { int o = tb_off; tb_off += c; return o; };
     // down 0 (80 x T, 64 ch)
@@ -505,18 +507,18 @@ struct Run {
     attention("ups.1.2.", 1, act(1, 0), 64, act(1, 1));
     upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
     // final_block conv (+GN sums), then the fused GN/Mish/final_conv/(Euler) kernel
-    double* st = stats();
+    float* st = stats();
     {
       ConvParams p = base(0, 0);
       p.Cin = 64; p.Cout = 64; p.Cin_pad = d->cinpad[dt].at("final_block.block.0.weight");
       p.in0 = act(0, 0); p.C0 = 64;
       p.w = W("final_block.block.0.weight"); p.bias = Fp("final_block.block.0.bias");
-      p.out = act(0, 3); p.out_stats = st;
+      p.out = act(0, 3); p.out_part = st;
       conv(CONV3, IN_MASK, OUT_STATS, p);
       tap("final_block.pre", 0, act(0, 3), 64);
     }
     FinalParams f;
-    f.pre = act(0, 3); f.stats = st; f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
+    f.pre = act(0, 3); f.part = st; f.nparts = conv_gn_nparts(dt, 80, T, 64); f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
     f.count = (long)8 * 80 * T; f.wf = Fp("final_conv.weight"); f.bf = Fp("final_conv.bias");
     f.mask = mask; f.B = B; f.T = T; f.euler = euler; f.out = out; f.mu = mu; f.xt = xt_inout;
     f.beta_t = beta_t; f.hstep = hstep;

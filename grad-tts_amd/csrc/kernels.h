@@ -21,17 +21,19 @@ struct ConvParams {
   // ---- input
   const void* in0; const void* in1; int C0, C1;      // channels-last sources, concatenated on C
   const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
-  const double* gn_stats; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
+  const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* bias;                                  // [Cout]
   // ---- output
-  void* out; double* out_stats;                       // OUT_STATS: GroupNorm sums of the output
-  const void* pre; const double* pre_stats; const float* pre_gamma; const float* pre_beta; long pre_count;  // OUT_RBOUT
+  void* out; float* out_part;                         // OUT_STATS: GroupNorm partials of the output (common.h)
+  const void* pre; const float* pre_part; int pre_nparts; const float* pre_gamma; const float* pre_beta; long pre_count;  // OUT_RBOUT
 };
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
+// number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid
+int conv_gn_nparts(int act_bf16, int F, int T, int Cout);
 
 struct AttnKVParams {
   const void* x; int B, n, C, Cpad;   // x: [B][n][C] (n = F*T)
@@ -45,7 +47,7 @@ hipError_t launch_attn_mbuild(int act_bf16, const float* G, const float* wout, c
                               void* Mw, hipStream_t s);
 
 struct FinalParams {
-  const void* pre; const double* stats; const float* gamma; const float* beta; long count;
+  const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
   const float* wf; const float* bf;   // final_conv [64], [1]
   const float* mask; int B, T;
   int euler;                          // 0: out = score s; 1: Euler update of xt in place
@@ -54,7 +56,7 @@ struct FinalParams {
 hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s);
 
 struct RbOutParams {
-  const void* pre; const double* stats; const float* gamma; const float* beta; long count;
+  const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
   const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
 };
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s);

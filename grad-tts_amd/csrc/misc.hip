@@ -14,11 +14,12 @@ namespace gt {
 
 template <class A>
 __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
-  __shared__ float s_sc[64], s_sh[64], s_w[64];
+  __shared__ float s_sc[64], s_sh[64], s_w[64], s_mean[8], s_rstd[8];
   const int b = blockIdx.y, tid = threadIdx.x;
+  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd);
   if (tid < 64) {
     float sc, sh;
-    gn_scale_shift(p.stats, b, 64, tid, p.count, p.gamma, p.beta, sc, sh);
+    gn_affine(s_mean, s_rstd, 64, tid, p.gamma, p.beta, sc, sh);
     s_sc[tid] = sc; s_sh[tid] = sh; s_w[tid] = p.wf[tid];
   }
   __syncthreads();
@@ -55,11 +56,12 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 
 template <class A>
 __global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
-  __shared__ float s_sc[256], s_sh[256];
+  __shared__ float s_sc[256], s_sh[256], s_mean[8], s_rstd[8];
   const int b = blockIdx.y, tid = threadIdx.x;
+  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd);
   for (int c = tid; c < p.C; c += 256) {
     float sc, sh;
-    gn_scale_shift(p.stats, b, p.C, c, p.count, p.gamma, p.beta, sc, sh);
+    gn_affine(s_mean, s_rstd, p.C, c, p.gamma, p.beta, sc, sh);
     s_sc[c] = sc; s_sh[c] = sh;
   }
   __syncthreads();
