@@ -22,8 +22,12 @@ OUT = os.path.join(HERE, "gradtts_amd", "libgradtts.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GRADTTS_ARCH", "gfx950")
 SOURCES = ["conv.hip", "attn.hip", "misc.hip", "mas.hip", "decoder.cpp"]
+# -packed-fp32-ops: keep the compiler from emitting v_pk_{fma,add,mul}_f32. With them the GroupNorm
+# sum-of-squares chain in conv_kernel's epilogue produced timing-dependent (run-to-run different)
+# results on MI355X while the plain sums stayed bit-exact (tools/diag_parts.py); without them every
+# stage is bit-reproducible. (The host compile ignores the feature with a one-line note.)
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(REPO, "include"), "-I", CSRC,
-         "-Wno-unused-result"]
+         "-Wno-unused-result", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 
 
 def _deps_mtime():

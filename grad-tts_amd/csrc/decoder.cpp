@@ -351,6 +351,16 @@ struct Run {
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
+  // diagnostics: "gnpart.<k>" copies GroupNorm partial slot k (B x pmax x 16 floats) after the launch that
+  // produced it
+  void tap_part(int k) {
+    if (probe && !probed && std::string(probe) == "gnpart." + std::to_string(k)) {
+      chk(hipMemcpyAsync(probe_out, ws + L.stats + (size_t)k * B * L.pmax * 16 * sizeof(float),
+                         (size_t)B * L.pmax * 16 * sizeof(float), hipMemcpyDeviceToDevice, s));
+      probed = true;
+    }
+  }
+
   void tap(const std::string& name, int lvl, const void* buf, int C) {
     if (probe && !probed && name == probe) {
       chk(launch_to_nchw(dt, buf, B, Fl(lvl), Tl(lvl), C, probe_out, s));
@@ -395,6 +405,7 @@ struct Run {
       p.out = pre1; p.out_part = st1;
       conv(CONV3, input ? IN_INPUT : IN_MASK, OUT_STATS, p);
       tap(k + "pre1", lvl, pre1, Cout);
+      tap_part(stat_slot - 2);
     }
     {   // block2 conv on (Mish(GN(h1))*m + tb)*m
       ConvParams p = base(lvl, lvl);
@@ -406,6 +417,7 @@ struct Run {
       p.out = pre2; p.out_part = st2;
       conv(CONV3, IN_GN, OUT_STATS, p);
       tap(k + "pre2", lvl, pre2, Cout);
+      tap_part(stat_slot - 1);
     }
     if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);

@@ -1,0 +1,31 @@
+"""Compare GroupNorm partial slots between identical runs (GPU diagnostic)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "grad-tts_amd"), os.path.join(REPO, "tests"), REPO]
+from gpu_util import make_decoder, probe  # noqa: E402
+from gradtts_amd.params import synthetic_inputs  # noqa: E402
+
+B, T = int(os.environ.get("B", 32)), int(os.environ.get("T", 512))
+cdt = torch.bfloat16 if (len(sys.argv) < 2 or sys.argv[1] == "bf16") else torch.float32
+dec, _ = make_decoder(1, 0, cdt)
+mu, z, mask, _ = synthetic_inputs(1234, B, T)
+t = np.full(B, 0.5, np.float32)
+args = [torch.from_numpy(a).cuda() for a in (z, mask, mu, t)]
+pmax = 20 * ((T + 63) // 64)
+for k in range(24):
+    outs = []
+    for rep in range(4):
+        _, pr = probe(dec.estimator, cdt, *args, None, f"gnpart.{k}", (B, pmax, 8, 2))
+        outs.append(pr.cpu().numpy())
+    d = [np.argwhere(o != outs[0]) for o in outs[1:]]
+    n = [len(x) for x in d]
+    msg = f"slot {k:2d}: differing per rep {n}"
+    if any(n):
+        x = next(x for x in d if len(x))
+        msg += f"  e.g. (b, part, g, s/q) {x[:4].tolist()}  vals {[(float(outs[0][tuple(i)]), float(o[tuple(i)])) for o in outs[1:] for i in x[:1]]}"
+    print(msg, flush=True)
