@@ -13,37 +13,38 @@
 // online softmax (running max m, running sum l, 32x32 context) where the context update
 // ctx += P^T V uses the two fp32 accumulator tiles directly as MFMA operands (both are indexed by
 // position along their rows, so no LDS transpose is needed). Tiles write {m, l, ctx} partials.
-// attn_merge: rescale+sum the partials -> normalised ctx, then G_h = ctx_h^T W_q,h  (fp32).
-// attn_mbuild: M_b = g * W_out G  written in the activation dtype as the per-batch 1x1 weight.
+// attn_merge: rescale+sum the partials -> normalised ctx (fp32).
+// attn_fold:  M_b = g * W_out blockdiag(ctx^T) W_q, register-blocked, written as the per-batch 1x1 weight image.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
 
 namespace gt {
 
-template <class A, bool RES>
+template <class A, int CPR>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
 __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
+  constexpr bool RES = CPR > 0;
   constexpr int CK = 64 / (int)sizeof(A);
   constexpr int ICH = 16 / (int)sizeof(A);
   constexpr int KSTEP_B = 16 * (int)sizeof(A);
-  constexpr int XROW_MAX = 256 + 16;   // resident layout only used when Cpad*sizeof(A) <= 256 B
-  constexpr int SX_BYTES = RES ? 64 * XROW_MAX : 64 * 80;
-  constexpr int SW_BYTES = RES ? 256 * XROW_MAX : 256 * 80;
+  constexpr int ROWB = RES ? CPR * (int)sizeof(A) + 16 : 80;   // LDS row stride: odd number of 16-B slots
+  constexpr int IPR = RES ? CPR / ICH : 4;                      // 16-B items per staged row
+  constexpr int XIT = 64 * IPR / 256;                           // x items per thread per sub-block
+  static_assert(64 * IPR % 256 == 0, "x staging must split evenly");
   typedef typename Mma<A>::frag frag;
-  __shared__ __attribute__((aligned(16))) char sX[SX_BYTES];
-  __shared__ __attribute__((aligned(16))) char sW[SW_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[(64 + 256) * ROWB];
+  char* sX = smem;
+  char* sW = smem + 64 * ROWB;
 
   const int b = blockIdx.x / p.ntile, tile = blockIdx.x % p.ntile;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int row_b = RES ? p.Cpad * (int)sizeof(A) + 16 : 80;   // LDS row stride (odd # of 16-B slots)
   const A* x = reinterpret_cast<const A*>(p.x) + (long)b * p.n * p.C;
   const A* wkv = reinterpret_cast<const A*>(p.wkv);
-  const int itemsPerRow = RES ? p.Cpad / ICH : 4;
 
-  if (RES) {   // whole [256][Cpad] k/v projection resident in LDS
-    for (int it = tid; it < 256 * itemsPerRow; it += 256) {
-      const int row = it / itemsPerRow, sub = it - row * itemsPerRow;
-      *reinterpret_cast<uint4*>(sW + row * row_b + sub * 16) =
+  if (RES) {   // whole [256][C] k/v projection resident in LDS
+    for (int it = tid; it < 256 * IPR; it += 256) {
+      const int row = it / IPR, sub = it - row * IPR;
+      *reinterpret_cast<uint4*>(sW + row * ROWB + sub * 16) =
           *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + sub * ICH);
     }
   }
@@ -56,6 +57,23 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
 
   const int tbeg = tile * p.tile_pos;
   const int tend = min(p.n, tbeg + p.tile_pos);
+  uint4 xr[XIT];
+  auto load_x = [&](int pos0, int c0) {
+#pragma unroll
+    for (int j = 0; j < XIT; ++j) {
+      const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
+      const int pos = pos0 + row;
+      xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + (long)pos * p.C + c0 + sub * ICH) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int j = 0; j < XIT; ++j) {
+      const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
+      *reinterpret_cast<uint4*>(sX + row * ROWB + sub * 16) = xr[j];
+    }
+  };
+  if (RES) load_x(tbeg, 0);
   for (int pos0 = tbeg; pos0 < tend; pos0 += 64) {
     f32x16 ak[2], av[2];
 #pragma unroll
@@ -66,37 +84,34 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
     const int nch = RES ? 1 : p.Cpad / CK;
     for (int ch = 0; ch < nch; ++ch) {
       __syncthreads();
-      const int c0 = ch * CK;
-      for (int it = tid; it < 64 * itemsPerRow; it += 256) {
-        const int row = it / itemsPerRow, sub = it - row * itemsPerRow;
-        const int pos = pos0 + row;
-        uint4 u = make_uint4(0, 0, 0, 0);
-        if (pos < tend) u = *reinterpret_cast<const uint4*>(x + (long)pos * p.C + c0 + sub * ICH);
-        *reinterpret_cast<uint4*>(sX + row * row_b + sub * 16) = u;
-      }
-      if (!RES) {
+      if (RES) {
+        store_x();
+      } else {
+        load_x(pos0, ch * CK);
+        store_x();
         for (int it = tid; it < 256 * 4; it += 256) {
           const int row = it >> 2, sub = it & 3;
           *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
-              *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + c0 + sub * ICH);
+              *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
         }
       }
       __syncthreads();
-      const int nks = RES ? p.Cpad / 16 : CK / 16;
+      if (RES && pos0 + 64 < tend) load_x(pos0 + 64, 0);   // next sub-block in flight during the MFMAs
+      const int nks = RES ? CPR / 16 : CK / 16;
       for (int ks = 0; ks < nks; ++ks) {
         const int off = ks * KSTEP_B + h * (KSTEP_B / 2);
-        const frag bk = Mma<A>::load(sW + (wv * 32 + r) * row_b + off);
-        const frag bv = Mma<A>::load(sW + (128 + wv * 32 + r) * row_b + off);
+        const frag bk = Mma<A>::load(sW + (wv * 32 + r) * ROWB + off);
+        const frag bv = Mma<A>::load(sW + (128 + wv * 32 + r) * ROWB + off);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
-          const frag a = Mma<A>::load(sX + (rb * 32 + r) * row_b + off);
+          const frag a = Mma<A>::load(sX + (rb * 32 + r) * ROWB + off);
           Mma<A>::mma(a, bk, ak[rb]);
           Mma<A>::mma(a, bv, av[rb]);
         }
       }
     }
 
-    // ---- online softmax over positions (k.softmax(dim=-1), diffusion.py:95) for column d = r
+  // ---- online softmax over positions (k.softmax(dim=-1), diffusion.py:95) for column d = r
     float mloc = NEG_INF;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -147,82 +162,123 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
   for (int j = 0; j < 16; ++j) part[64 + acc_row(j, h) * 32 + r] = ctx[j];
 }
 
-// grid (B, 4 heads): merge tile partials, normalise, G[b][32h+e][ci] = sum_d ctx[d][e] Wq[32h+d][ci]
-__global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, int C, const float* wq, float* G) {
-  __shared__ float s_ctx[32][33];
+// grid (B, 4 heads): merge the tiles' online-softmax partials and normalise:
+//   ctx_h[d][e] = sum_t exp(m_t[d] - M[d]) ctx_t[d][e] / sum_t exp(m_t[d] - M[d]) l_t[d]
+__global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, float* ctxn) {
   const int b = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
   const int d = tid >> 3, e0 = (tid & 7) * 4;
   const float* base = part + ((long)b * ntile * 4 + hd) * 1088;
   const long tstride = 4 * 1088;
   float M = -__builtin_huge_valf();
+#pragma unroll 8
   for (int t = 0; t < ntile; ++t) M = fmaxf(M, base[t * tstride + d]);
   float L = 0.f, c[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
   for (int t = 0; t < ntile; ++t) {
     const float* pt = base + t * tstride;
     const float w = __expf(pt[d] - M);
     L += w * pt[32 + d];
+    const f32x4 v = *reinterpret_cast<const f32x4*>(pt + 64 + d * 32 + e0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) c[k] += w * pt[64 + d * 32 + e0 + k];
+    for (int k = 0; k < 4; ++k) c[k] += w * v[k];
   }
   const float inv = 1.f / L;
+  float* dst = ctxn + ((long)b * 4 + hd) * 1024 + d * 32 + e0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = c[k] * inv;
-  __syncthreads();
-  float* Gb = G + (long)b * 128 * C;
-  for (int idx = tid; idx < 32 * C; idx += 256) {
-    const int e = idx / C, ci = idx - e * C;
-    float s = 0.f;
-#pragma unroll 8
-    for (int dd = 0; dd < 32; ++dd) s += s_ctx[dd][e] * wq[(long)(hd * 32 + dd) * C + ci];
-    Gb[(long)(hd * 32 + e) * C + ci] = s;
-  }
+  for (int k = 0; k < 4; ++k) dst[k] = c[k] * inv;
 }
 
-// grid (B, C/16): M_b[co][ci] = g * sum_r Wout[co][r] G[b][r][ci], written straight into the packed
-// 1x1 weight image (wimage.h) that conv_kernel DMAs into LDS.
+// grid (B, C/64): fold the whole attention output path into one C x C matrix per utterance
+//   A[co][32h+d] = sum_e Wout[co][32h+e] ctx_h[d][e]          (einsum 'bhde,bhdn->bhen' then to_out)
+//   M_b[co][ci]  = g * sum_r A[co][r] Wq[r][ci]               (q = to_qkv rows 0..127)
+// written straight into the packed 1x1 weight image (wimage.h) that conv_kernel DMAs into LDS.
+// Register-blocked fp32: each thread owns 4 output rows x 16 columns.
 template <class A>
-__global__ __launch_bounds__(256) void attn_mbuild_kernel(const float* G, const float* wout, const float* g, int C,
-                                                          char* Mw, WImg W) {
-  __shared__ float s_w[16][129];
-  const int b = blockIdx.x, co0 = blockIdx.y * 16, tid = threadIdx.x;
-  for (int i = tid; i < 16 * 128; i += 256) s_w[i >> 7][i & 127] = wout[(long)(co0 + (i >> 7)) * 128 + (i & 127)];
+__global__ __launch_bounds__(256) void attn_fold_kernel(const float* ctxn, const float* wout, const float* wq,
+                                                        const float* g, int C, char* Mw, WImg W) {
+  __shared__ __attribute__((aligned(16))) float s_ctx[4][32][33];
+  __shared__ __attribute__((aligned(16))) float s_w[64][129];   // W_out rows, then reused for Wq chunks
+  __shared__ __attribute__((aligned(16))) float s_a[128][68];   // A transposed: [r][co]
+  const int b = blockIdx.x, co0 = blockIdx.y * 64, tid = threadIdx.x;
+  for (int i = tid; i < 4096; i += 256) s_ctx[i >> 10][(i >> 5) & 31][i & 31] = ctxn[(long)b * 4096 + i];
+  for (int i = tid; i < 64 * 128; i += 256) s_w[i >> 7][i & 127] = wout[(long)(co0 + (i >> 7)) * 128 + (i & 127)];
   __syncthreads();
-  const float gg = g[0];
-  const float* Gb = G + (long)b * 128 * C;
-  char* img = Mw + (long)b * W.total;
-  const int row = tid >> 4;   // 16 rows x 16 column lanes
-  for (int ci = tid & 15; ci < C; ci += 16) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < 128; ++k) s += s_w[row][k] * Gb[(long)k * C + ci];
-    *reinterpret_cast<A*>(img + conv_wimg_off(W, co0 + row, 0, ci, (int)sizeof(A))) = Act<A>::from_f(gg * s);
+  {   // A: thread -> (co = tid / 4, head h = tid % 4), 32 outputs
+    const int co = tid >> 2, hh = tid & 3;
+    float w[32];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) w[e] = s_w[co][hh * 32 + e];
+    for (int dd = 0; dd < 32; ++dd) {
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) acc += w[e] * s_ctx[hh][dd][e];
+      s_a[hh * 32 + dd][co] = acc;
+    }
+  }
+  __syncthreads();
+  const int ncg = C / 16;                 // 16-column groups
+  const int cog = tid / ncg, cig = tid % ncg;
+  const bool active = tid < 16 * ncg;     // 16 groups of 4 rows
+  float acc[4][16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
+  float* s_q = &s_w[0][0];                // Wq chunk [32][C] (fits: 32 * 256 <= 64 * 129)
+  for (int r0 = 0; r0 < 128; r0 += 32) {
+    __syncthreads();
+    for (int i = tid; i < 32 * C; i += 256) s_q[i] = wq[(long)r0 * C + i];
+    __syncthreads();
+    if (active) {
+      for (int r = 0; r < 32; ++r) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(&s_a[r0 + r][cog * 4]);
+        const f32x4* qv = reinterpret_cast<const f32x4*>(s_q + r * C + cig * 16);
+        f32x4 q4[4] = {qv[0], qv[1], qv[2], qv[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[i][j] += av[i] * q4[j >> 2][j & 3];
+      }
+    }
+  }
+  if (active) {
+    const float gg = g[0];
+    char* img = Mw + (long)b * W.total;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        *reinterpret_cast<A*>(img + conv_wimg_off(W, co0 + cog * 4 + i, 0, cig * 16 + j, (int)sizeof(A))) =
+            Act<A>::from_f(gg * acc[i][j]);
   }
 }
 
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (act_bf16) {
-    if (p.Cpad * 2 <= 256) hipLaunchKernelGGL((attn_kv_kernel<bf16, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_kv_kernel<bf16, false>), grid, dim3(256), 0, s, p);
+    if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<bf16, 64>), grid, dim3(256), 0, s, p);
+    else if (p.Cpad <= 128) hipLaunchKernelGGL((attn_kv_kernel<bf16, 128>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_kv_kernel<bf16, 0>), grid, dim3(256), 0, s, p);
   } else {
-    if (p.Cpad * 4 <= 256) hipLaunchKernelGGL((attn_kv_kernel<float, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_kv_kernel<float, false>), grid, dim3(256), 0, s, p);
+    if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<float, 64>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_kv_kernel<float, 0>), grid, dim3(256), 0, s, p);
   }
   return hipGetLastError();
 }
 
-hipError_t launch_attn_merge(const float* part, int B, int ntile, int C, const float* wq, float* G, hipStream_t s) {
-  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, C, wq, G);
+hipError_t launch_attn_merge(const float* part, int B, int ntile, float* ctxn, hipStream_t s) {
+  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, ctxn);
   return hipGetLastError();
 }
 
-hipError_t launch_attn_mbuild(int act_bf16, const float* G, const float* wout, const float* g, int B, int C, void* Mw,
-                              hipStream_t s) {
+hipError_t launch_attn_fold(int act_bf16, const float* ctxn, const float* wout, const float* wq, const float* g, int B,
+                            int C, void* Mw, hipStream_t s) {
+  if (C % 64 != 0 || C > 256) return hipErrorInvalidValue;
   const WImg W = conv_wimg(act_bf16, 1, C, C);
   if (act_bf16)
-    hipLaunchKernelGGL(attn_mbuild_kernel<bf16>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (char*)Mw, W);
+    hipLaunchKernelGGL(attn_fold_kernel<bf16>, dim3(B, C / 64), dim3(256), 0, s, ctxn, wout, wq, g, C, (char*)Mw, W);
   else
-    hipLaunchKernelGGL(attn_mbuild_kernel<float>, dim3(B, C / 16), dim3(256), 0, s, G, wout, g, C, (char*)Mw, W);
+    hipLaunchKernelGGL(attn_fold_kernel<float>, dim3(B, C / 64), dim3(256), 0, s, ctxn, wout, wq, g, C, (char*)Mw, W);
   return hipGetLastError();
 }
 

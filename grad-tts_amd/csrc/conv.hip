@@ -165,6 +165,12 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
       if (it < C::PITEMS) {
         float v[C::ICH];
         const float m = pm[j];
+        if ((IN == IN_MASK || IN == IN_PLAIN) && (IN == IN_PLAIN || m == 1.f || m == 0.f)) {
+          // x * m for m in {0, 1} (sequence_mask) is a select on the stored bits: no unpack / repack
+          const uint4 u = (IN == IN_PLAIN || m != 0.f) ? preg[j] : make_uint4(0, 0, 0, 0);
+          *reinterpret_cast<uint4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = u;
+          continue;
+        }
         if (IN == IN_INPUT) {
           const float f3[3] = {__uint_as_float(preg[j].x), __uint_as_float(preg[j].y), __uint_as_float(preg[j].z)};
 #pragma unroll
