@@ -175,8 +175,12 @@ def main():
                          "flop_per_launch": dom["flop"] / dom["launches"],
                          "traffic": pmc_traffic(dom["kernel"]),
                          "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"]},
-            "kernel_time_share": {p["kernel"]: round(p["ms"] / total_kernel_ms, 4) for p in
-                                  sorted(prof, key=lambda p: -p["ms"])[:8]},
+            "kernels": {p["kernel"]: {"share": round(p["ms"] / total_kernel_ms, 4),
+                                      "avg_us": round(p["ms"] / p["launches"] * 1e3, 2),
+                                      "per_step": p["launches"] // args.steps,
+                                      "tflops": round(p["flop"] / (p["ms"] * 1e-3) / 1e12, 1) if p["flop"] else None,
+                                      "gbps": round(p["bytes"] / (p["ms"] * 1e-3) / 1e9, 0) if p["bytes"] else None}
+                        for p in sorted(prof, key=lambda p: -p["ms"])[:14]},
             "kernel_busy_frac": total_kernel_ms / args.steps / 1e3 / sec,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -13,8 +13,8 @@
 // online softmax (running max m, running sum l, 32x32 context) where the context update
 // ctx += P^T V uses the two fp32 accumulator tiles directly as MFMA operands (both are indexed by
 // position along their rows, so no LDS transpose is needed). Tiles write {m, l, ctx} partials.
-// attn_merge: rescale+sum the partials -> normalised ctx (fp32).
-// attn_fold:  M_b = g * W_out blockdiag(ctx^T) W_q, register-blocked, written as the per-batch 1x1 weight image.
+// attn_merge: rescale+sum the partials -> normalised ctx -> A_b = g W_out blockdiag(ctx^T)   (fp32, C x 128)
+// attn_fold:  M_b = A_b W_q on fp32 MFMA, written as the per-batch 1x1 weight image.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
@@ -162,9 +162,13 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
   for (int j = 0; j < 16; ++j) part[64 + acc_row(j, h) * 32 + r] = ctx[j];
 }
 
-// grid (B, 4 heads): merge the tiles' online-softmax partials and normalise:
-//   ctx_h[d][e] = sum_t exp(m_t[d] - M[d]) ctx_t[d][e] / sum_t exp(m_t[d] - M[d]) l_t[d]
-__global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, float* ctxn) {
+// grid (B, 4 heads): merge the tiles' online-softmax partials, normalise, and fold the head's part of
+// the output projection:
+//   ctx_h[d][e]  = sum_t exp(m_t[d] - M[d]) ctx_t[d][e] / sum_t exp(m_t[d] - M[d]) l_t[d]
+//   A[co][32h+d] = g * sum_e Wout[co][32h+e] ctx_h[d][e]     (einsum 'bhde,bhdn->bhen' + to_out + Rezero)
+__global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
+                                                         int C, float* Aout) {
+  __shared__ float s_ctx[32][33];
   const int b = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
   const int d = tid >> 3, e0 = (tid & 7) * 4;
   const float* base = part + ((long)b * ntile * 4 + hd) * 1088;
@@ -183,73 +187,49 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int 
     for (int k = 0; k < 4; ++k) c[k] += w * v[k];
   }
   const float inv = 1.f / L;
-  float* dst = ctxn + ((long)b * 4 + hd) * 1024 + d * 32 + e0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) dst[k] = c[k] * inv;
+  for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = c[k] * inv;
+  __syncthreads();
+  const float gg = g[0];
+  for (int idx = tid; idx < C * 32; idx += 256) {      // (co, d), d fastest
+    const int co = idx >> 5, dd = idx & 31;
+    const float* wrow = wout + (long)co * 128 + hd * 32;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int e = 0; e < 32; ++e) acc += wrow[e] * s_ctx[dd][e];
+    Aout[((long)b * C + co) * 128 + hd * 32 + dd] = gg * acc;
+  }
 }
 
-// grid (B, C/64): fold the whole attention output path into one C x C matrix per utterance
-//   A[co][32h+d] = sum_e Wout[co][32h+e] ctx_h[d][e]          (einsum 'bhde,bhdn->bhen' then to_out)
-//   M_b[co][ci]  = g * sum_r A[co][r] Wq[r][ci]               (q = to_qkv rows 0..127)
-// written straight into the packed 1x1 weight image (wimage.h) that conv_kernel DMAs into LDS.
-// Register-blocked fp32: each thread owns 4 output rows x 16 columns.
+// grid (B, C/64, C/64): M_b = A_b Wq  (C x 128 times 128 x C) with exact-fp32 MFMA (v_mfma_f32_32x32x2_f32),
+// 4 waves x one 32x32 block each, written straight into the packed 1x1 weight image (wimage.h).
 template <class A>
-__global__ __launch_bounds__(256) void attn_fold_kernel(const float* ctxn, const float* wout, const float* wq,
-                                                        const float* g, int C, char* Mw, WImg W) {
-  __shared__ __attribute__((aligned(16))) float s_ctx[4][32][33];
-  __shared__ __attribute__((aligned(16))) float s_w[64][129];   // W_out rows, then reused for Wq chunks
-  __shared__ __attribute__((aligned(16))) float s_a[128][68];   // A transposed: [r][co]
-  const int b = blockIdx.x, co0 = blockIdx.y * 64, tid = threadIdx.x;
-  for (int i = tid; i < 4096; i += 256) s_ctx[i >> 10][(i >> 5) & 31][i & 31] = ctxn[(long)b * 4096 + i];
-  for (int i = tid; i < 64 * 128; i += 256) s_w[i >> 7][i & 127] = wout[(long)(co0 + (i >> 7)) * 128 + (i & 127)];
-  __syncthreads();
-  {   // A: thread -> (co = tid / 4, head h = tid % 4), 32 outputs
-    const int co = tid >> 2, hh = tid & 3;
-    float w[32];
-#pragma unroll
-    for (int e = 0; e < 32; ++e) w[e] = s_w[co][hh * 32 + e];
-    for (int dd = 0; dd < 32; ++dd) {
-      float acc = 0.f;
-#pragma unroll
-      for (int e = 0; e < 32; ++e) acc += w[e] * s_ctx[hh][dd][e];
-      s_a[hh * 32 + dd][co] = acc;
-    }
+__global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const float* wq, int C, char* Mw, WImg W) {
+  __shared__ float s_a[64][129];    // A rows co0..co0+63, k = 0..127
+  __shared__ float s_q[64][129];    // Wq^T: [ci - ci0][k]
+  const int b = blockIdx.x, co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64, tid = threadIdx.x;
+  for (int i = tid; i < 64 * 128; i += 256) {
+    const int r = i >> 7, k = i & 127;
+    s_a[r][k] = Ain[((long)b * C + co0 + r) * 128 + k];
+  }
+  for (int i = tid; i < 64 * 128; i += 256) {
+    const int k = i >> 6, cc = i & 63;                 // coalesced along ci
+    s_q[cc][k] = wq[(long)k * C + ci0 + cc];
   }
   __syncthreads();
-  const int ncg = C / 16;                 // 16-column groups
-  const int cog = tid / ncg, cig = tid % ncg;
-  const bool active = tid < 16 * ncg;     // 16 groups of 4 rows
-  float acc[4][16];
+  const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int bm = (wv >> 1) * 32, bn = (wv & 1) * 32;
+  f32x16 acc;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < 128; k += 2)   // A[i = lane&31][k + h], B[k + h][j = lane&31]
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_a[bm + r][k + h], s_q[bn + r][k + h], acc, 0, 0, 0);
+  char* img = Mw + (long)b * W.total;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) acc[i][j] = 0.f;
-  float* s_q = &s_w[0][0];                // Wq chunk [32][C] (fits: 32 * 256 <= 64 * 129)
-  for (int r0 = 0; r0 < 128; r0 += 32) {
-    __syncthreads();
-    for (int i = tid; i < 32 * C; i += 256) s_q[i] = wq[(long)r0 * C + i];
-    __syncthreads();
-    if (active) {
-      for (int r = 0; r < 32; ++r) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(&s_a[r0 + r][cog * 4]);
-        const f32x4* qv = reinterpret_cast<const f32x4*>(s_q + r * C + cig * 16);
-        f32x4 q4[4] = {qv[0], qv[1], qv[2], qv[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) acc[i][j] += av[i] * q4[j >> 2][j & 3];
-      }
-    }
-  }
-  if (active) {
-    const float gg = g[0];
-    char* img = Mw + (long)b * W.total;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        *reinterpret_cast<A*>(img + conv_wimg_off(W, co0 + cog * 4 + i, 0, cig * 16 + j, (int)sizeof(A))) =
-            Act<A>::from_f(gg * acc[i][j]);
+  for (int j = 0; j < 16; ++j) {
+    const int co = co0 + bm + acc_row(j, h), ci = ci0 + bn + r;
+    *reinterpret_cast<A*>(img + conv_wimg_off(W, co, 0, ci, (int)sizeof(A))) = Act<A>::from_f(acc[j]);
   }
 }
 
@@ -266,19 +246,18 @@ hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_attn_merge(const float* part, int B, int ntile, float* ctxn, hipStream_t s) {
-  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, ctxn);
+hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, wout, g, C, Aout);
   return hipGetLastError();
 }
 
-hipError_t launch_attn_fold(int act_bf16, const float* ctxn, const float* wout, const float* wq, const float* g, int B,
-                            int C, void* Mw, hipStream_t s) {
-  if (C % 64 != 0 || C > 256) return hipErrorInvalidValue;
+hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s) {
+  if (C % 64 != 0) return hipErrorInvalidValue;
   const WImg W = conv_wimg(act_bf16, 1, C, C);
-  if (act_bf16)
-    hipLaunchKernelGGL(attn_fold_kernel<bf16>, dim3(B, C / 64), dim3(256), 0, s, ctxn, wout, wq, g, C, (char*)Mw, W);
-  else
-    hipLaunchKernelGGL(attn_fold_kernel<float>, dim3(B, C / 64), dim3(256), 0, s, ctxn, wout, wq, g, C, (char*)Mw, W);
+  const dim3 grid(B, C / 64, C / 64);
+  if (act_bf16) hipLaunchKernelGGL(attn_fold_kernel<bf16>, grid, dim3(256), 0, s, Ain, wq, C, (char*)Mw, W);
+  else hipLaunchKernelGGL(attn_fold_kernel<float>, grid, dim3(256), 0, s, Ain, wq, C, (char*)Mw, W);
   return hipGetLastError();
 }
 

@@ -454,11 +454,11 @@ struct Run {
     // reference FLOPs of the attention block: qkv 1x1 (2*C*384) + two einsums (2 * 2*4*32*32) + to_out (2*128*C)
     timed(std::string("attn_kv_kernel<") + (dt ? "bf16>" : "float>"), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
           npos * C * esize(dt), [&] { return launch_attn_kv(dt, a, s); });
-    timed("attn_merge_kernel", 0.0, 0.0, [&] { return launch_attn_merge(part, B, a.ntile, G, s); });
-    timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>"), 0.0, 0.0, [&] {
-      return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.fn.to_qkv.weight.q"), Fp(k + "fn.g"), B,
-                              C, Mw, s);
+    timed("attn_merge_kernel", 0.0, 0.0, [&] {
+      return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);
     });
+    timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>"), 2.0 * B * C * 128.0 * C, 0.0,
+          [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
     ConvParams p = base(lvl, lvl);
     p.Cin = C; p.Cout = C; p.Cin_pad = C;
     p.in0 = in; p.C0 = C;

@@ -42,9 +42,9 @@ struct AttnKVParams {
   float* part;                        // [B][ntile][4][1088] = {m[32], l[32], ctx[32][32]}
 };
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
-hipError_t launch_attn_merge(const float* part, int B, int ntile, float* ctxn, hipStream_t s);
-hipError_t launch_attn_fold(int act_bf16, const float* ctxn, const float* wout, const float* wq, const float* g, int B,
-                            int C, void* Mw, hipStream_t s);
+hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
+                             hipStream_t s);
+hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s);
 
 struct FinalParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
