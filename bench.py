@@ -138,7 +138,14 @@ def main():
     elapsed = time.perf_counter() - t0
     L.gt_decoder_profile_enable(handle, 0)
     _lib.check(L.gt_decoder_profile_read(handle, buf, len(buf)), "gt_decoder_profile_read")
-    prof = json.loads(buf.value.decode())
+    shapes = json.loads(buf.value.decode())      # per "<kernel>@<shape>" entries
+    prof = {}
+    for e in shapes:
+        k = e["kernel"].split("@")[0]
+        a = prof.setdefault(k, {"kernel": k, "ms": 0.0, "launches": 0, "flop": 0.0, "bytes": 0.0})
+        for f in ("ms", "launches", "flop", "bytes"):
+            a[f] += e[f]
+    prof = list(prof.values())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -181,6 +188,10 @@ def main():
                                       "tflops": round(p["flop"] / (p["ms"] * 1e-3) / 1e12, 1) if p["flop"] else None,
                                       "gbps": round(p["bytes"] / (p["ms"] * 1e-3) / 1e9, 0) if p["bytes"] else None}
                         for p in sorted(prof, key=lambda p: -p["ms"])[:14]},
+            "conv_shapes": {e["kernel"]: {"avg_us": round(e["ms"] / e["launches"] * 1e3, 2),
+                                          "per_step": e["launches"] // args.steps,
+                                          "tflops": round(e["flop"] / (e["ms"] * 1e-3) / 1e12, 1)}
+                            for e in sorted(shapes, key=lambda e: -e["ms"]) if "@" in e["kernel"]},
             "kernel_busy_frac": total_kernel_ms / args.steps / 1e3 / sec,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -169,6 +169,7 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
 __global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
                                                          int C, float* Aout) {
   __shared__ float s_ctx[32][33];
+  __shared__ float s_w[256][33];
   const int b = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
   const int d = tid >> 3, e0 = (tid & 7) * 4;
   const float* base = part + ((long)b * ntile * 4 + hd) * 1088;
@@ -189,14 +190,19 @@ __global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int 
   const float inv = 1.f / L;
 #pragma unroll
   for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = c[k] * inv;
+  for (int i = tid; i < C * 8; i += 256) {             // Wout[:, 32h : 32h+32] -> LDS (float4 loads)
+    const int co = i >> 3, e4 = (i & 7) * 4;
+    const f32x4 w = *reinterpret_cast<const f32x4*>(wout + (long)co * 128 + hd * 32 + e4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_w[co][e4 + k] = w[k];
+  }
   __syncthreads();
   const float gg = g[0];
-  for (int idx = tid; idx < C * 32; idx += 256) {      // (co, d), d fastest
+  for (int idx = tid; idx < C * 32; idx += 256) {      // (co, d), d fastest: s_w broadcast, s_ctx stride 33
     const int co = idx >> 5, dd = idx & 31;
-    const float* wrow = wout + (long)co * 128 + hd * 32;
     float acc = 0.f;
-#pragma unroll 8
-    for (int e = 0; e < 32; ++e) acc += wrow[e] * s_ctx[dd][e];
+#pragma unroll
+    for (int e = 0; e < 32; ++e) acc += s_w[co][e] * s_ctx[dd][e];
     Aout[((long)b * C + co) * 128 + hd * 32 + dd] = gg * acc;
   }
 }
@@ -208,13 +214,19 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
   __shared__ float s_a[64][129];    // A rows co0..co0+63, k = 0..127
   __shared__ float s_q[64][129];    // Wq^T: [ci - ci0][k]
   const int b = blockIdx.x, co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64, tid = threadIdx.x;
-  for (int i = tid; i < 64 * 128; i += 256) {
-    const int r = i >> 7, k = i & 127;
-    s_a[r][k] = Ain[((long)b * C + co0 + r) * 128 + k];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = tid + 256 * j, rr = i >> 5, k4 = (i & 31) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(Ain + ((long)b * C + co0 + rr) * 128 + k4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_a[rr][k4 + k] = v[k];
   }
-  for (int i = tid; i < 64 * 128; i += 256) {
-    const int k = i >> 6, cc = i & 63;                 // coalesced along ci
-    s_q[cc][k] = wq[(long)k * C + ci0 + cc];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = tid + 256 * j, k = i >> 4, c4 = (i & 15) * 4;   // coalesced along ci
+    const f32x4 v = *reinterpret_cast<const f32x4*>(wq + (long)k * C + ci0 + c4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s_q[c4 + c][k] = v[c];
   }
   __syncthreads();
   const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -248,6 +260,7 @@ hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
 
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              hipStream_t s) {
+  if (C > 256 || C % 4 != 0) return hipErrorInvalidValue;    // s_w holds at most 256 output rows
   hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, wout, g, C, Aout);
   return hipGetLastError();
 }

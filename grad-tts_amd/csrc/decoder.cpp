@@ -345,9 +345,11 @@ struct Run {
     double bytes = (im == IN_INPUT ? pin * p.Cin * 4.0 : pin * p.Cin * es) + pout * p.Cout * es +
                    (double)p.Cout * (kind == CONVT4 ? 16 : taps) * p.Cin_pad * es * (p.w_bstride ? p.B : 1);
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
-    const int rb = kind == CONV3_S2 ? 1 : 2;
+    // "<instantiation as rocprof names it>@<shape>": bench.py aggregates per instantiation
+    const int nt = dt ? conv_nt(1, p.Cout) : 64;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
-                             "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(rb) + ">";
+                             "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
+                             ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
