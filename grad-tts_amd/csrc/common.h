@@ -100,9 +100,11 @@ GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
 //     part[(b * nparts + slot) * 16 + g * 2 + {0,1}]      (plain stores, no atomics, no memset)
 // and every consumer reduces the slots of its utterance in a fixed order in fp64: deterministic,
 // and independent of how many utterances share the launch.
-// gn_reduce: call with all 256 threads; leaves mean/rstd of the 8 groups in s_mean/s_rstd (LDS).
+// gn_reduce: call with all threads of the block (>= 256); leaves mean/rstd of the 8 groups in
+// s_mean/s_rstd (LDS). Threads 0..255 reduce, group g = thread/32, in a fixed order.
 GT_DEV void gn_reduce(const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd) {
   const int t = threadIdx.x, g = t >> 5, j = t & 31;
+  if (t >= 256) { __syncthreads(); return; }
   const float* pb = part + (long)b * nparts * 16 + g * 2;
   double s = 0.0, q = 0.0;
   for (int i = j; i < nparts; i += 32) {

@@ -55,28 +55,22 @@ struct ConvCfg {
   static constexpr int PPT = (PITEMS + 255) / 256;
   static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
   static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
-  static constexpr int PATCH_BYTES = PR * PC * POSB;
-  static constexpr int SMALL_BYTES = (3 * 256 + 64 + 16) * 4;
-  // weight slabs are always double-buffered; the patch too when both fit in the 160 KB of LDS
-  static constexpr bool DBA = 2 * PATCH_BYTES + 2 * WBYTES + SMALL_BYTES <= 160 * 1024;
-  static constexpr int A_REGION = (DBA ? 2 : 1) * PATCH_BYTES;
-  static constexpr int A_BYTES = A_REGION > EPI_BYTES ? A_REGION : EPI_BYTES;
-  static constexpr int SMEM = A_BYTES + 2 * WBYTES + SMALL_BYTES;
-  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
+  static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 64 + 16) * 4;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
 };
 
 template <class A, int KIND, int IN, int OUT, int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void conv_kernel(ConvParams p) {
+__global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   typedef ConvCfg<A, KIND, IN, OUT, NT> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
 
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];   // ONE LDS object (see guide §5 trap a)
-  char* const sA0 = smem;                         // patch buffer(s)
-  char* const sW0 = smem + C::A_BYTES;             // two weight slabs
-  float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + 2 * C::WBYTES);
+  char* sA = smem;
+  char* sW = smem + C::A_BYTES;
+  float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBYTES);
   float* s_sh = s_sc + 256;
   float* s_tb = s_sh + 256;
   float* s_sub = s_tb + 256;     // [4 waves][2 col blocks][4 x 8-channel groups][2] GroupNorm sub-partials
@@ -156,7 +150,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         preg[j] = pidx[j] >= 0 ? *reinterpret_cast<const uint4*>(src + (long)pidx[j] * Cs) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_patch = [&](int c0, char* sA) {
+  auto store_patch = [&](int c0) {
     float sc[C::ICH], sh[C::ICH], tb[C::ICH];
     if (IN == IN_GN) {
 #pragma unroll
@@ -209,41 +203,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int nchunk = p.Cin_pad / C::CK;
   wimg += ((long)(par * gridDim.y + ntile) * nchunk) * C::WBYTES;
 
-  auto dma_weights = [&](int ch, char* sW) {   // contiguous slab, 1 KiB per wave instruction, no VGPRs
-    const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
-#pragma unroll
-    for (int i = wv; i < C::WBYTES / 1024; i += 4)
-      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
-                                       (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
-  };
-
-  // Software pipeline, one barrier per chunk: the weight DMA and the patch loads of chunk ch+1 are in
-  // flight during chunk ch's MFMAs; the patch of ch+1 is transformed and stored (into the other buffer)
-  // right after them. Without the second patch buffer (stride-2 tiles) the store waits for a barrier.
-  dma_weights(0, sW0);
   load_patch(0);
-  if (C::DBA) store_patch(0, sA0);
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
-    char* sW = sW0 + (ch & 1) * C::WBYTES;
-    char* sA = sA0 + (C::DBA ? (ch & 1) * C::PATCH_BYTES : 0);
-    if (!C::DBA) {
-      if (ch > 0) __syncthreads();                     // everyone is done reading the single patch buffer
-      store_patch(c0, sA);
+    __syncthreads();                                   // previous chunk's fragments are consumed
+    {   // weight slab: contiguous DMA, 1 KiB per wave instruction
+      const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
+#pragma unroll
+      for (int i = wv; i < C::WBYTES / 1024; i += 4)
+        __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
+                                         (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
     }
+    store_patch(c0);
     // The weight DMA must have landed before any wave reads sW. hipcc does NOT reliably emit this
     // vmcnt(0) for global_load_lds before a barrier (it was missing in the 1x1/128-wide instantiation:
-    // an intermittent, load-dependent race), so it is explicit. Only this chunk's DMA is in flight here.
+    // an intermittent, load-dependent race), so it is explicit. Nothing else is in flight here.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                                   // chunk ch visible; chunk ch-1's buffers are free
-    if (ch + 1 < nchunk) {
-      dma_weights(ch + 1, sW0 + ((ch + 1) & 1) * C::WBYTES);
-      load_patch(c0 + C::CK);
-    }
-    // MFMA sweep over (tap, k-step), fragments software-pipelined one step ahead in registers
-    frag af[2][C::RBW], bfr[2][2];
-    auto load_frags = [&](int st, int buf) {
-      const int tap = st / C::KSTEPS, ks = st - tap * C::KSTEPS;
+    __syncthreads();
+    if (ch + 1 < nchunk) load_patch(c0 + C::CK);       // in flight during this chunk's MFMAs
+#pragma unroll
+    for (int tap = 0; tap < C::NTAP; ++tap) {
       int dr, dc;
       if (CONVT) {
         // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0,
@@ -255,42 +234,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         dr = tap / C::KS;
         dc = tap - dr * C::KS;
       }
-      const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
 #pragma unroll
-      for (int rb = 0; rb < C::RBW; ++rb) {
-        const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
-        const int prow = lrow * C::S + dr;
-        const int pcol = (tblk * 32 + r) * C::S + dc;
-        af[buf][rb] = Mma<A>::load(sA + (prow * C::PC + pcol) * C::POSB + koff);
-      }
+      for (int ks = 0; ks < C::KSTEPS; ++ks) {
+        const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
+        frag af[C::RBW], bfr[2];
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-        bfr[buf][cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
-    };
-    constexpr int NSTEP = C::NTAP * C::KSTEPS;
-    load_frags(0, 0);
-#pragma unroll
-    for (int st = 0; st < NSTEP; ++st) {
-      if (st + 1 < NSTEP) load_frags(st + 1, (st + 1) & 1);
-#pragma unroll
-      for (int rb = 0; rb < C::RBW; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) Mma<A>::mma(af[st & 1][rb], bfr[st & 1][cb], acc[rb][cb]);
-      // pin the interleave: MFMA, next-step ds_read, MFMA, ... (<= 2 ds_read_b128 per MFMA gap are free)
-      if (st + 1 < NSTEP) {
-#pragma unroll
-        for (int q = 0; q < 2 * C::RBW; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                      // MFMA
-          if (q < C::RBW + 2) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        for (int rb = 0; rb < C::RBW; ++rb) {
+          const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+          const int prow = lrow * C::S + dr;
+          const int pcol = (tblk * 32 + r) * C::S + dc;
+          af[rb] = Mma<A>::load(sA + (prow * C::PC + pcol) * C::POSB + koff);
         }
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          bfr[cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
+#pragma unroll
+        for (int rb = 0; rb < C::RBW; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) Mma<A>::mma(af[rb], bfr[cb], acc[rb][cb]);
       }
     }
-    if (C::DBA && ch + 1 < nchunk) store_patch(c0 + C::CK, sA0 + ((ch + 1) & 1) * C::PATCH_BYTES);
   }
 
   // ---- epilogue: transpose each 32x32 block through LDS -> lane = (position, 8 channels)
   __syncthreads();
-  float* scr = reinterpret_cast<float*>(sA0) + wv * 32 * C::EPI_ROW;
+  float* scr = reinterpret_cast<float*>(sA) + wv * 32 * C::EPI_ROW;
   const int g8 = lane & 3;                 // 8-channel group within the 32-channel block
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
   A* out = reinterpret_cast<A*>(p.out);
