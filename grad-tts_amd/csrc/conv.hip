@@ -7,19 +7,22 @@
 //   CONVT4   ConvTranspose 4x4 s2 -- Upsample (diffusion.py:24) as four 2x2 sub-pixel convolutions
 //
 // GEMM view: M = output positions of a tile (4 mel rows x TT frames), N = NT output channels (64 or
-// 128), K = taps x input channels, walked in chunks of CKB bytes per position.
+// 128), K = taps x input channels, walked in chunks of 16 channels (one MFMA k-step) per position.
 //   waves: NT=64  -> 4 waves along M (1 mel row each);  NT=128 -> 2 x 2 waves (2 mel rows x 64 ch each)
 //   each wave holds RBW x 2 fp32 32x32 accumulators (v_mfma_f32_32x32x16_bf16 / 32x32x2_f32).
+//   occupancy: 3 workgroups per CU for NT=64 (42 KB LDS), 2 for NT=128.
 // Per chunk:
 //   * weight slab: one contiguous global_load_lds DMA of the pre-packed image (wimage.h) -- no VGPRs;
-//   * input patch: prefetched into registers while the previous chunk's MFMAs run, then transformed in
-//     registers (IN_GN: the producer's GroupNorm apply + Mish + mask + time bias, diffusion.py:57-58,76)
-//     and written to LDS (position rows padded to an odd number of 16-B slots: conflict-free fragments);
-//   * 9 (or 4, 1) taps x k-steps of MFMA.
-// Epilogue: each 32x32 accumulator block is transposed through LDS so every lane owns 8 consecutive
-// output channels of one position: 16-B vector stores, vector loads of the ResnetBlock pre-activation
-// (OUT_RBOUT) or the attention residual (OUT_RESID), and GroupNorm sums over all grid positions
-// (padded frames included, as torch's group_norm does) reduced in registers + fp64 atomics.
+//   * input patch: raw buffer loads at precomputed 32-bit offsets, prefetched into registers while the
+//     previous chunk's MFMAs run. Padding and masked frames (mask 0) point past the end of the tensor,
+//     so the range check returns zeros: no address arithmetic or selects per chunk. IN_GN transforms
+//     in registers (the producer's GroupNorm apply + Mish + mask + time bias, diffusion.py:57-58,76);
+//     rows are padded to an odd number of 16-B slots in LDS (conflict-free fragments);
+//   * 9 (or 4, 1) taps of MFMA.
+// Epilogue: each 32x32 accumulator block is transposed through the wave's own LDS scratch so every lane
+// owns 8 consecutive output channels of one position: 16-B vector stores, vector loads of the
+// ResnetBlock pre-activation (OUT_RBOUT) or the attention residual (OUT_RESID), and GroupNorm partial
+// sums (padded frames included, as torch's group_norm does) written to this workgroup's slot.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
@@ -42,11 +45,12 @@ struct ConvCfg {
   static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
   static constexpr int PR = (TF - 1) * S + KS;
   static constexpr int PC = (TT - 1) * S + KS;
-  static constexpr int CKB = conv_ckb(NT);
+  static constexpr int CKB = conv_ckb(sizeof(A) == 2);
   static constexpr int SUBS = CKB / 16;
   static constexpr int POSB = CKB + 16;
   static constexpr int WROW = conv_wrow(NTAP, CKB);
   static constexpr int WBYTES = conv_wbytes(NT, NTAP, CKB);
+  static constexpr int WPIECES = WBYTES / 1024 / 4;       // 1 KiB DMA pieces per wave per chunk
   static constexpr int CK = CKB / (int)sizeof(A);
   static constexpr int ICH = 16 / (int)sizeof(A);
   static constexpr int KSTEP_B = 16 * (int)sizeof(A);
@@ -59,10 +63,14 @@ struct ConvCfg {
   static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 64 + 16) * 4;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
+  static_assert(WBYTES % 4096 == 0, "whole DMA rounds");
 };
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 template <class A, int KIND, int IN, int OUT, int NT>
-__global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
+// 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
   typedef ConvCfg<A, KIND, IN, OUT, NT> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
@@ -112,9 +120,12 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     }
   }
 
-  // ---- per-thread patch items: input position index (or -1) and mask, computed once
+  // ---- per-thread patch items, computed once: input position (npos = out of range) and mask
+  constexpr int ES = (int)sizeof(A);
+  const int npos = p.B * p.Fin * p.Tin;
   int pidx[C::PPT];
   float pm[C::PPT];
+  bool frac = false;     // a mask value other than 0/1 among this thread's items (sequence_mask gives 0/1)
 #pragma unroll
   for (int j = 0; j < C::PPT; ++j) {
     const int it = tid + 256 * j;
@@ -122,32 +133,48 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     const int pr = pos / C::PC, pc = pos - pr * C::PC;
     const int fi = fi0 + pr, ti = ti0 + pc;
     const bool ok = it < C::PITEMS && fi >= 0 && fi < p.Fin && ti >= 0 && ti < p.Tin;
-    pidx[j] = ok ? ((b * p.Fin + fi) * p.Tin + ti) : -1;
-    pm[j] = ok ? mask_at(p.mask, p.T0, b, ti, p.lvl_in) : 0.f;
+    const float m = ok ? mask_at(p.mask, p.T0, b, ti, p.lvl_in) : 0.f;
+    int q = ok ? ((b * p.Fin + fi) * p.Tin + ti) : npos;
+    if (IN == IN_MASK) {
+      if (m == 0.f) q = npos;              // x * 0: the range-checked load returns zeros
+      frac |= (m != 0.f && m != 1.f);
+    }
+    pidx[j] = q;
+    pm[j] = m;
   }
 
-  uint4 preg[C::PPT];
+  // raw buffer descriptors over the (one or two) input tensors: an offset past the end reads 0
+  const __amdgpu_buffer_rsrc_t rs0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * p.C0 * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.in1 ? p.in1 : p.in0), (short)0, npos * (p.in1 ? p.C1 : p.C0) * ES, 0x00020000);
+  int voff[C::PPT];
+  auto set_offsets = [&](int Cs) {
+#pragma unroll
+    for (int j = 0; j < C::PPT; ++j) voff[j] = pidx[j] * (Cs * ES) + sub * 16;
+  };
+  if (IN != IN_INPUT) set_offsets(p.C0);
+
+  u32x4 preg[C::PPT];
   auto load_patch = [&](int c0) {
     if (IN == IN_INPUT) {   // channels {mu, x_t, spk} (diffusion.py:181/184) -- single chunk
 #pragma unroll
       for (int j = 0; j < C::PPT; ++j) {
-        uint4 u = make_uint4(0, 0, 0, 0);
-        if (pidx[j] >= 0 && sub == 0) {
-          u.x = __float_as_uint(p.mu[pidx[j]]);
-          u.y = __float_as_uint(p.xt[pidx[j]]);
-          if (p.cin_input == 3) u.z = __float_as_uint(p.spk_s[(long)b * p.Fin + (pidx[j] / p.Tin) % p.Fin]);
+        u32x4 u = {0u, 0u, 0u, 0u};
+        if (pidx[j] < npos && sub == 0) {
+          u[0] = __float_as_uint(p.mu[pidx[j]]);
+          u[1] = __float_as_uint(p.xt[pidx[j]]);
+          if (p.cin_input == 3) u[2] = __float_as_uint(p.spk_s[(long)b * p.Fin + (pidx[j] / p.Tin) % p.Fin]);
         }
         preg[j] = u;
       }
+    } else if (c0 < p.C0) {
+#pragma unroll
+      for (int j = 0; j < C::PPT; ++j) preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs0, voff[j], c0 * ES, 0);
     } else {
-      const A* src;
-      int cs, Cs;
-      if (c0 < p.C0) { src = reinterpret_cast<const A*>(p.in0); cs = c0; Cs = p.C0; }
-      else { src = reinterpret_cast<const A*>(p.in1); cs = c0 - p.C0; Cs = p.C1; }
-      src += cs + sub * C::ICH;
 #pragma unroll
       for (int j = 0; j < C::PPT; ++j)
-        preg[j] = pidx[j] >= 0 ? *reinterpret_cast<const uint4*>(src + (long)pidx[j] * Cs) : make_uint4(0, 0, 0, 0);
+        preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, voff[j], (c0 - p.C0) * ES, 0);
     }
   };
   auto store_patch = [&](int c0) {
@@ -163,30 +190,32 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     for (int j = 0; j < C::PPT; ++j) {
       const int it = tid + 256 * j;
       if (it < C::PITEMS) {
-        float v[C::ICH];
-        const float m = pm[j];
-        if ((IN == IN_MASK || IN == IN_PLAIN) && (IN == IN_PLAIN || m == 1.f || m == 0.f)) {
-          // x * m for m in {0, 1} (sequence_mask) is a select on the stored bits: no unpack / repack
-          const uint4 u = (IN == IN_PLAIN || m != 0.f) ? preg[j] : make_uint4(0, 0, 0, 0);
-          *reinterpret_cast<uint4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = u;
+        char* dst = sA + (it / C::SUBS) * C::POSB + sub * 16;
+        const u32x4 u = preg[j];
+        if (IN == IN_PLAIN || (IN == IN_MASK && !frac)) {   // zeros already came from the range check
+          *reinterpret_cast<u32x4*>(dst) = u;
           continue;
         }
+        const float m = pm[j];
+        float v[C::ICH];
+        const uint4 w = make_uint4(u[0], u[1], u[2], u[3]);
         if (IN == IN_INPUT) {
-          const float f3[3] = {__uint_as_float(preg[j].x), __uint_as_float(preg[j].y), __uint_as_float(preg[j].z)};
+          const float f3[3] = {__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z)};
 #pragma unroll
           for (int k = 0; k < C::ICH; ++k) v[k] = (k < 3 ? f3[k < 3 ? k : 0] : 0.f) * m;
         } else {
-          item_to_f(preg[j], v, A());
+          item_to_f(w, v, A());
           if (IN == IN_GN) {
 #pragma unroll
             for (int k = 0; k < C::ICH; ++k)   // (Mish(GN(h)) * m + tb) * m, m in {0,1}
               v[k] = (mishf(v[k] * sc[k] + sh[k]) + tb[k]) * m;
-          } else if (IN == IN_MASK) {
+          } else {                             // IN_MASK, a fractional mask among this thread's items
 #pragma unroll
             for (int k = 0; k < C::ICH; ++k) v[k] *= m;
           }
         }
-        *reinterpret_cast<uint4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = f_to_item(v, A());
+        const uint4 o = f_to_item(v, A());
+        *reinterpret_cast<u32x4*>(dst) = u32x4{o.x, o.y, o.z, o.w};
       }
     }
   };
@@ -207,12 +236,14 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
     __syncthreads();                                   // previous chunk's fragments are consumed
-    {   // weight slab: contiguous DMA, 1 KiB per wave instruction
+    {   // weight slab: contiguous DMA, 1 KiB per wave instruction, a compile-time count per wave
       const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
 #pragma unroll
-      for (int i = wv; i < C::WBYTES / 1024; i += 4)
+      for (int k = 0; k < C::WPIECES; ++k) {
+        const int i = wv + 4 * k;
         __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
                                          (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
+      }
     }
     store_patch(c0);
     // The weight DMA must have landed before any wave reads sW. hipcc does NOT reliably emit this
@@ -220,7 +251,10 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     // an intermittent, load-dependent race), so it is explicit. Nothing else is in flight here.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (ch + 1 < nchunk) load_patch(c0 + C::CK);       // in flight during this chunk's MFMAs
+    if (ch + 1 < nchunk) {
+      if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && c0 + C::CK == p.C0) set_offsets(p.C1);
+      load_patch(c0 + C::CK);                          // in flight during this chunk's MFMAs
+    }
 #pragma unroll
     for (int tap = 0; tap < C::NTAP; ++tap) {
       int dr, dc;
@@ -256,7 +290,13 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     }
   }
 
-  // ---- epilogue: transpose each 32x32 block through LDS -> lane = (position, 8 channels)
+  // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
+  // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
+  auto wave_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   __syncthreads();
   float* scr = reinterpret_cast<float*>(sA) + wv * 32 * C::EPI_ROW;
   const int g8 = lane & 3;                 // 8-channel group within the 32-channel block
@@ -269,7 +309,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
     for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) scr[acc_row(j, h) * C::EPI_ROW + r] = acc[rb][cb][j];
-      __syncthreads();
+      wave_sync();
       const int cl = wn * 64 + cb * 32 + g8 * 8;       // tile-local first channel of this lane
       const int co = cout0 + cl;
       float bias[8];
@@ -320,7 +360,7 @@ __global__ __launch_bounds__(256) void conv_kernel(ConvParams p) {
           }
         }
       }
-      __syncthreads();
+      wave_sync();
     }
   }
   if (OUT == OUT_STATS) {
@@ -364,6 +404,8 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   const int Fg = (KIND == CONVT4) ? p.Fin : p.Fout;
   const int Tg = (KIND == CONVT4) ? p.Tin : p.Tout;
   if (Fg % C::TF != 0 || p.Cout % NT != 0 || p.Cin_pad % C::CK != 0) return hipErrorInvalidValue;
+  if ((long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * (long)sizeof(A) >= (1L << 31))
+    return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
   dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
             KIND == CONVT4 ? 4u : 1u);
   hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT>), grid, dim3(256), 0, s, p);

@@ -14,8 +14,8 @@ namespace gt {
 
 // output channels per workgroup: 128 for bf16 layers with >= 128 output channels, else 64
 inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { return (act_bf16 && cout >= 128) ? 128 : 64; }
-// bytes of one position's channel chunk in LDS: 32 B (16 bf16 ch) for the 128-wide tile, else 64 B
-inline __host__ __device__ constexpr int conv_ckb(int nt) { return nt == 128 ? 32 : 64; }
+// bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
+inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
 inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }
 inline __host__ __device__ constexpr int conv_wbytes(int nt, int ntap, int ckb) {
   return ((nt * conv_wrow(ntap, ckb) + 4095) / 4096) * 4096;
@@ -29,7 +29,7 @@ struct WImg {
 inline __host__ __device__ WImg conv_wimg(int act_bf16, int ntap, int cin, int cout) {
   WImg w;
   w.nt = conv_nt(act_bf16, cout);
-  w.ckb = conv_ckb(w.nt);
+  w.ckb = conv_ckb(act_bf16);
   w.ck = w.ckb / (act_bf16 ? 2 : 4);
   w.ntap = ntap;
   w.wrow = conv_wrow(ntap, w.ckb);
