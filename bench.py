@@ -34,6 +34,7 @@ sys.path.insert(0, os.path.join(REPO, "grad-tts_amd"))
 from gradtts_amd import _lib  # noqa: E402
 from gradtts_amd.diffusion import Diffusion  # noqa: E402
 from gradtts_amd.params import estimator_flops, synthetic_inputs, synthetic_state_dict  # noqa: E402
+from gradtts_amd.shard import gather_shards  # noqa: E402
 
 PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}   # dense MFMA peaks (MI355X_MICROARCH.md)
 HBM_PEAK = 8.0e12
@@ -110,12 +111,11 @@ def main():
     mu, z, mask, spk = synthetic_inputs(1234 + rank, B, T)
     mu, z, mask = (torch.from_numpy(a).to(dev) for a in (mu, z, mask))
     spk = torch.from_numpy(spk).to(dev) if args.n_spks > 1 else None
-    gathered = torch.empty((world * B, 80, T), dtype=torch.float32, device=dev) if world > 1 else None
 
     def step():
         y = dec(z, mask, mu, N, False, spk)
-        if world > 1:
-            torch.distributed.all_gather_into_tensor(gathered, y)
+        if world > 1:   # every rank decodes its own shard of utterances; mels gathered in utterance order
+            gather_shards(y, world * B, world)
         return y
 
     L = _lib.lib()
