@@ -189,10 +189,10 @@ def main():
                                       "tflops": round(p["flop"] / (p["ms"] * 1e-3) / 1e12, 1) if p["flop"] else None,
                                       "gbps": round(p["bytes"] / (p["ms"] * 1e-3) / 1e9, 0) if p["bytes"] else None}
                         for p in sorted(prof, key=lambda p: -p["ms"])[:14]},
-            "conv_shapes": {e["kernel"]: {"avg_us": round(e["ms"] / e["launches"] * 1e3, 2),
-                                          "per_step": e["launches"] // args.steps,
-                                          "tflops": round(e["flop"] / (e["ms"] * 1e-3) / 1e12, 1)}
-                            for e in sorted(shapes, key=lambda e: -e["ms"]) if "@" in e["kernel"]},
+            "shapes": {e["kernel"]: {"avg_us": round(e["ms"] / e["launches"] * 1e3, 2),
+                                     "per_step": e["launches"] // args.steps,
+                                     "tflops": round(e["flop"] / (e["ms"] * 1e-3) / 1e12, 1)}
+                       for e in sorted(shapes, key=lambda e: -e["ms"]) if "@" in e["kernel"]},
             "kernel_busy_frac": total_kernel_ms / args.steps / 1e3 / sec,
         }
         if world == 1 and not args.no_cpu_baseline:

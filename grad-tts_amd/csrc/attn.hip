@@ -166,39 +166,67 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
 // the output projection:
 //   ctx_h[d][e]  = sum_t exp(m_t[d] - M[d]) ctx_t[d][e] / sum_t exp(m_t[d] - M[d]) l_t[d]
 //   A[co][32h+d] = g * sum_e Wout[co][32h+e] ctx_h[d][e]     (einsum 'bhde,bhdn->bhen' + to_out + Rezero)
-__global__ __launch_bounds__(256) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
-                                                         int C, float* Aout) {
+__global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
+                                                          int C, float* Aout) {
   __shared__ float s_ctx[32][33];
   __shared__ float s_w[256][33];
+  __shared__ float s_gc[4][32][33];   // per tile group: unnormalised context, running max, running sum
+  __shared__ float s_gm[4][32], s_gl[4][32];
   const int b = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
-  const int d = tid >> 3, e0 = (tid & 7) * 4;
+  const int grp = tid >> 8, lt = tid & 255;
+  const int d = lt >> 3, e0 = (lt & 7) * 4;
+  // tile group grp merges tiles [t0, t1) online (running max), in tile order
+  const int per = (ntile + 3) / 4, t0 = grp * per, t1 = min(ntile, t0 + per);
   const float* base = part + ((long)b * ntile * 4 + hd) * 1088;
   const long tstride = 4 * 1088;
-  float M = -__builtin_huge_valf();
-#pragma unroll 8
-  for (int t = 0; t < ntile; ++t) M = fmaxf(M, base[t * tstride + d]);
-  float L = 0.f, c[4] = {0.f, 0.f, 0.f, 0.f};
+  float M = -__builtin_huge_valf(), L = 0.f, c[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 4
-  for (int t = 0; t < ntile; ++t) {
+  for (int t = t0; t < t1; ++t) {
     const float* pt = base + t * tstride;
-    const float w = __expf(pt[d] - M);
-    L += w * pt[32 + d];
+    const float mt = pt[d], lt_ = pt[32 + d];
     const f32x4 v = *reinterpret_cast<const f32x4*>(pt + 64 + d * 32 + e0);
+    if (mt > M) {                                      // rescale what was merged so far
+      const float r = __expf(M - mt);
+      L *= r;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c[k] *= r;
+      M = mt;
+    }
+    const float w = __expf(mt - M);
+    L += w * lt_;
 #pragma unroll
     for (int k = 0; k < 4; ++k) c[k] += w * v[k];
   }
-  const float inv = 1.f / L;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = c[k] * inv;
-  for (int i = tid; i < C * 8; i += 256) {             // Wout[:, 32h : 32h+32] -> LDS (float4 loads)
+  for (int k = 0; k < 4; ++k) s_gc[grp][d][e0 + k] = c[k];
+  if ((lt & 7) == 0) { s_gm[grp][d] = M; s_gl[grp][d] = L; }
+  for (int i = tid; i < C * 8; i += 1024) {            // Wout[:, 32h : 32h+32] -> LDS (float4 loads)
     const int co = i >> 3, e4 = (i & 7) * 4;
     const f32x4 w = *reinterpret_cast<const f32x4*>(wout + (long)co * 128 + hd * 32 + e4);
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_w[co][e4 + k] = w[k];
   }
   __syncthreads();
+  if (grp == 0) {                                      // combine the 4 groups in a fixed order
+    float Mt = -__builtin_huge_valf();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Mt = fmaxf(Mt, s_gm[q][d]);
+    float Lt = 0.f, ct[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (s_gl[q][d] == 0.f) continue;                 // empty group (ntile < 4)
+      const float r = __expf(s_gm[q][d] - Mt);
+      Lt += r * s_gl[q][d];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ct[k] += r * s_gc[q][d][e0 + k];
+    }
+    const float inv = 1.f / Lt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = ct[k] * inv;
+  }
+  __syncthreads();
   const float gg = g[0];
-  for (int idx = tid; idx < C * 32; idx += 256) {      // (co, d), d fastest: s_w broadcast, s_ctx stride 33
+  for (int idx = tid; idx < C * 32; idx += 1024) {     // (co, d), d fastest: s_w broadcast, s_ctx stride 33
     const int co = idx >> 5, dd = idx & 31;
     float acc = 0.f;
 #pragma unroll
@@ -261,7 +289,7 @@ hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              hipStream_t s) {
   if (C > 256 || C % 4 != 0) return hipErrorInvalidValue;    // s_w holds at most 256 output rows
-  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(256), 0, s, part, ntile, wout, g, C, Aout);
+  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(1024), 0, s, part, ntile, wout, g, C, Aout);
   return hipGetLastError();
 }
 

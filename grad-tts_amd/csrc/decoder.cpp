@@ -437,7 +437,8 @@ struct Run {
       p.count = count; p.x = in0; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = Cout;
       p.T0 = T; p.lvl = lvl;
       const double by = 3.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt);
-      timed(std::string("rbout_identity_kernel<") + (dt ? "bf16>" : "float>"), 0.0, by,
+      timed(std::string("rbout_identity_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
+                std::to_string(Fl(lvl)), 0.0, by,
             [&] { return launch_rbout_identity(dt, p, s); });
     }
     tap(k.substr(0, k.size() - 1), lvl, out, Cout);
@@ -454,7 +455,8 @@ struct Run {
     a.tile_pos = L.tile_pos[lvl]; a.ntile = L.ntile[lvl]; a.part = part;
     const double npos = (double)B * a.n;
     // reference FLOPs of the attention block: qkv 1x1 (2*C*384) + two einsums (2 * 2*4*32*32) + to_out (2*128*C)
-    timed(std::string("attn_kv_kernel<") + (dt ? "bf16>" : "float>"), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
+    timed(std::string("attn_kv_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C) + "x" +
+              std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
           npos * C * esize(dt), [&] { return launch_attn_kv(dt, a, s); });
     timed("attn_merge_kernel", 0.0, 0.0, [&] {
       return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);

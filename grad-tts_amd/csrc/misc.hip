@@ -12,6 +12,7 @@
 
 namespace gt {
 
+constexpr int FIN_PPT = 1;   // positions per thread (more per thread exposes the 128-B load latency)
 template <class A>
 __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
   __shared__ float s_sc[64], s_sh[64], s_w[64], s_mean[8], s_rstd[8];
@@ -23,63 +24,86 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
     s_sc[tid] = sc; s_sh[tid] = sh; s_w[tid] = p.wf[tid];
   }
   __syncthreads();
-  const long idx = (long)blockIdx.x * 256 + tid;   // position within [80][T]
-  if (idx >= 80L * p.T) return;
-  const int t = (int)(idx % p.T);
-  const float m = p.mask[(long)b * p.T + t];
-  const A* pre = reinterpret_cast<const A*>(p.pre) + ((long)b * 80 * p.T + idx) * 64;
   constexpr int ICH = Act<A>::kItemCh;
-  float acc = 0.f;
+  const int npos = 80 * p.T;
+#pragma unroll 1
+  for (int j = 0; j < FIN_PPT; ++j) {
+    const int idx = (blockIdx.x * FIN_PPT + j) * 256 + tid;   // position within [80][T]
+    if (idx >= npos) return;
+    const int t = idx % p.T;
+    const float m = p.mask[(long)b * p.T + t];
+    const A* pre = reinterpret_cast<const A*>(p.pre) + ((long)b * npos + idx) * 64;
+    uint4 u[64 / ICH];
 #pragma unroll
-  for (int it = 0; it < 64 / ICH; ++it) {
-    float v[ICH];
-    item_to_f(reinterpret_cast<const uint4*>(pre)[it], v, A());
+    for (int it = 0; it < 64 / ICH; ++it) u[it] = reinterpret_cast<const uint4*>(pre)[it];
+    float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < ICH; ++k) {
-      const int c = it * ICH + k;
-      const float y = mishf(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
-      acc += s_w[c] * (y * m);                               // final_conv(x * mask)
+    for (int it = 0; it < 64 / ICH; ++it) {
+      float v[ICH];
+      item_to_f(u[it], v, A());
+#pragma unroll
+      for (int k = 0; k < ICH; ++k) {
+        const int c = it * ICH + k;
+        const float y = mishf(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
+        acc += s_w[c] * (y * m);                               // final_conv(x * mask)
+      }
     }
-  }
-  const float s = (acc + p.bf[0]) * m;                       // (output * mask).squeeze(1)
-  const long o = (long)b * 80 * p.T + idx;
-  if (!p.euler) {
-    p.out[o] = s;
-  } else {
-    const float x = p.xt[o];
-    float dxt = 0.5f * ((p.mu[o] - x) - s);
-    dxt = dxt * p.beta_t;
-    dxt = dxt * p.hstep;
-    p.xt[o] = (x - dxt) * m;
+    const float s = (acc + p.bf[0]) * m;                       // (output * mask).squeeze(1)
+    const long o = (long)b * npos + idx;
+    if (!p.euler) {
+      p.out[o] = s;
+    } else {
+      const float x = p.xt[o];
+      float dxt = 0.5f * ((p.mu[o] - x) - s);
+      dxt = dxt * p.beta_t;
+      dxt = dxt * p.hstep;
+      p.xt[o] = (x - dxt) * m;
+    }
   }
 }
 
+// 8 x 16-B items per thread; the block stride (256 items) is a multiple of C, so every thread keeps one
+// channel group (and its GroupNorm scale/shift) for all of its items.
+constexpr int RB_IPT = 8;
 template <class A>
 __global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
-  __shared__ float s_sc[256], s_sh[256], s_mean[8], s_rstd[8];
+  __shared__ float s_mean[8], s_rstd[8];
   const int b = blockIdx.y, tid = threadIdx.x;
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd);
-  for (int c = tid; c < p.C; c += 256) {
-    float sc, sh;
-    gn_affine(s_mean, s_rstd, p.C, c, p.gamma, p.beta, sc, sh);
-    s_sc[c] = sc; s_sh[c] = sh;
-  }
-  __syncthreads();
   constexpr int ICH = Act<A>::kItemCh;
-  const long items = (long)p.F * p.T * p.C / ICH;
-  const long it = (long)blockIdx.x * 256 + tid;
-  if (it >= items) return;
-  const long e0 = it * ICH;                 // element offset within batch item
-  const int c0 = (int)(e0 % p.C);
-  const int t = (int)((e0 / p.C) % p.T);
-  const float m = mask_at(p.mask, p.T0, b, t, p.lvl);
-  const long base = (long)b * p.F * p.T * p.C + e0;
-  float v[ICH], x[ICH];
-  item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + base), v, A());
-  item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.x) + base), x, A());
+  const int total = p.F * p.T * p.C;                       // elements of one utterance
+  const int e0 = (blockIdx.x * RB_IPT * 256 + tid) * ICH;
+  const int c0 = e0 % p.C;
+  float sc[ICH], sh[ICH];
 #pragma unroll
-  for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * s_sc[c0 + k] + s_sh[c0 + k]) * m + x[k] * m;
-  *reinterpret_cast<uint4*>(reinterpret_cast<A*>(p.out) + base) = f_to_item(v, A());
+  for (int k = 0; k < ICH; ++k) gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
+  const long ub = (long)b * total;
+  const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
+  const A* xin = reinterpret_cast<const A*>(p.x) + ub;
+  A* out = reinterpret_cast<A*>(p.out) + ub;
+  uint4 vp[RB_IPT], vx[RB_IPT];
+#pragma unroll
+  for (int i = 0; i < RB_IPT; ++i) {                        // all loads in flight first
+    const int e = e0 + i * 256 * ICH;
+    if (e < total) {
+      vp[i] = *reinterpret_cast<const uint4*>(pre + e);
+      vx[i] = *reinterpret_cast<const uint4*>(xin + e);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RB_IPT; ++i) {
+    const int e = e0 + i * 256 * ICH;
+    if (e < total) {
+      const int t = (e / p.C) % p.T;
+      const float m = mask_at(p.mask, p.T0, b, t, p.lvl);
+      float v[ICH], x[ICH];
+      item_to_f(vp[i], v, A());
+      item_to_f(vx[i], x, A());
+#pragma unroll
+      for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * sc[k] + sh[k]) * m + x[k] * m;
+      *reinterpret_cast<uint4*>(out + e) = f_to_item(v, A());
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void temb_kernel(TembParams p) {
@@ -158,15 +182,18 @@ hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, in
 }
 
 hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s) {
-  dim3 grid((unsigned)((80L * p.T + 255) / 256), (unsigned)p.B);
+  dim3 grid((unsigned)((80L * p.T + 256 * FIN_PPT - 1) / (256 * FIN_PPT)), (unsigned)p.B);
   if (act_bf16) hipLaunchKernelGGL(final_kernel<bf16>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
-  const long items = (long)p.F * p.T * p.C / (act_bf16 ? 8 : 4);
-  dim3 grid((unsigned)((items + 255) / 256), (unsigned)p.B);
+  const int ich = act_bf16 ? 8 : 4;
+  const long total = (long)p.F * p.T * p.C;
+  if ((256 * ich) % p.C != 0 || total >= (1L << 31)) return hipErrorInvalidValue;
+  const long items = total / ich;
+  dim3 grid((unsigned)((items + 256 * RB_IPT - 1) / (256 * RB_IPT)), (unsigned)p.B);
   if (act_bf16) hipLaunchKernelGGL(rbout_identity_kernel<bf16>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(rbout_identity_kernel<float>, grid, dim3(256), 0, s, p);
   return hipGetLastError();

@@ -13,7 +13,7 @@ vs = sys.argv[1:]
 d = {v: json.load(open(f"gpurun_out/var/{v}.json")) for v in vs}
 print("variant".ljust(12), " ".join(v[:9].rjust(9) for v in vs))
 print("ms/step".ljust(12), " ".join(f"{d[v]['ms_per_step']:9.2f}" for v in vs))
-keys = list(d[vs[0]]["conv_shapes"].keys())[:14]
+keys = list(d[vs[0]]["shapes"].keys())[:14]
 for k in keys:
-    print(k.replace("conv_kernel<bf16,", "c<")[:34].ljust(34), " ".join(f"{d[v]['conv_shapes'].get(k, {}).get('avg_us', 0):9.1f}" for v in vs))
+    print(k.replace("conv_kernel<bf16,", "c<")[:34].ljust(34), " ".join(f"{d[v]['shapes'].get(k, {}).get('avg_us', 0):9.1f}" for v in vs))
 PY

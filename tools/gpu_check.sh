@@ -12,5 +12,5 @@ import json
 d = json.load(open("gpurun_out/bench.json"))
 print(round(d["value"]), "mel-frames/s", round(d["ms_per_step"], 2), "ms/step", d["roofline"]["kernel"], round(d["roofline"]["frac"], 4))
 for k, v in d["kernels"].items(): print(" ", k, v)
-for k, v in list(d["conv_shapes"].items())[:12]: print("   ", k, v)
+for k, v in list(d["shapes"].items())[:24]: print("   ", k, v)
 PY
