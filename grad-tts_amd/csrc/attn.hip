@@ -22,7 +22,7 @@
 namespace gt {
 
 template <class A, int CPR>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
-__global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_kv_kernel(AttnKVParams p) {
   constexpr bool RES = CPR > 0;
   constexpr int CK = 64 / (int)sizeof(A);
   constexpr int ICH = 16 / (int)sizeof(A);
@@ -112,30 +112,53 @@ __global__ __launch_bounds__(256) void attn_kv_kernel(AttnKVParams p) {
     }
 
   // ---- online softmax over positions (k.softmax(dim=-1), diffusion.py:95) for column d = r
+    const bool full = pos0 + 64 <= tend;             // wave-uniform: no per-element validity test
     float mloc = NEG_INF;
+    if (full) {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (pos0 + rb * 32 + acc_row(j, h) < tend) mloc = fmaxf(mloc, ak[rb][j]);
+        for (int j = 0; j < 16; ++j) mloc = fmaxf(mloc, ak[rb][j]);
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (pos0 + rb * 32 + acc_row(j, h) < tend) mloc = fmaxf(mloc, ak[rb][j]);
+    }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
     const float m_new = fmaxf(m_run, mloc);
-    const float alpha = (m_run == NEG_INF) ? 0.f : __expf(m_run - m_new);
     float lsum = 0.f;
+    if (full) {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const bool valid = pos0 + rb * 32 + acc_row(j, h) < tend;
-        const float e = valid ? __expf(ak[rb][j] - m_new) : 0.f;
-        ak[rb][j] = e;
-        lsum += e;
-      }
+        for (int j = 0; j < 16; ++j) {
+          const float e = __expf(ak[rb][j] - m_new);
+          ak[rb][j] = e;
+          lsum += e;
+        }
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const bool valid = pos0 + rb * 32 + acc_row(j, h) < tend;
+          const float e = valid ? __expf(ak[rb][j] - m_new) : 0.f;
+          ak[rb][j] = e;
+          lsum += e;
+        }
+    }
     lsum += __shfl_xor(lsum, 32);
-    l_run = l_run * alpha + lsum;
-    // ctx rows are d = acc_row(j, h); the factor for row d lives in lane d
+    // rescale the running sum/context only where the running max moved (rare after the first blocks)
+    if (__any(m_new != m_run)) {
+      const float alpha = (m_run == NEG_INF) ? 0.f : __expf(m_run - m_new);
+      l_run *= alpha;
+      // ctx rows are d = acc_row(j, h); the factor for row d lives in lane d
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ctx[j] *= __shfl(alpha, acc_row(j, h));
+      for (int j = 0; j < 16; ++j) ctx[j] *= __shfl(alpha, acc_row(j, h));
+    }
+    l_run += lsum;
     // ---- ctx[d][e] += sum_pos P[pos][d] V[pos][e]   (einsum 'bhdn,bhen->bhde', diffusion.py:96)
     if constexpr (sizeof(A) == 2) {
 #pragma unroll
@@ -276,8 +299,9 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (act_bf16) {
+    // resident k/v weights only for C = 64; wider inputs stream 32-channel chunks (3 workgroups/CU,
+    // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
     if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<bf16, 64>), grid, dim3(256), 0, s, p);
-    else if (p.Cpad <= 128) hipLaunchKernelGGL((attn_kv_kernel<bf16, 128>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((attn_kv_kernel<bf16, 0>), grid, dim3(256), 0, s, p);
   } else {
     if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<float, 64>), grid, dim3(256), 0, s, p);
