@@ -29,6 +29,20 @@
 
 namespace gt {
 
+#ifdef GT_STAMPS
+// Diagnostic timeline (tools/stamps.py): s_memtime at phase boundaries of wave 0 of every workgroup of the
+// last launch that matches the filter (3x3, 64->64 at 80 mel rows, IN = GT_STAMPS).
+constexpr int ST_PER_WG = 48, ST_WGS = 8192;
+__device__ unsigned long long g_stamps[ST_WGS * ST_PER_WG];
+__device__ unsigned int g_stamp_hwid[ST_WGS];
+#define STAMP(k)                                                                          \
+  do {                                                                                    \
+    if (stamp_on && threadIdx.x == 0) g_stamps[blockIdx.x * ST_PER_WG + (k)] = __builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 template <class A, int KIND, int IN, int OUT, int NT>
 struct ConvCfg {
   static constexpr bool CONVT = KIND == CONVT4;
@@ -60,7 +74,7 @@ struct ConvCfg {
   static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
   static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
   static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
-  static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 64 + 16) * 4;
+  static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 128 + 64 + 16) * 4;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
   static_assert(WBYTES % 4096 == 0, "whole DMA rounds");
@@ -77,11 +91,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];   // ONE LDS object (see guide §5 trap a)
   char* sA = smem;
-  char* sW = smem + C::A_BYTES;
+  char* const sW = smem + C::A_BYTES;
   float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBYTES);
   float* s_sh = s_sc + 256;
   float* s_tb = s_sh + 256;
-  float* s_sub = s_tb + 256;     // [4 waves][2 col blocks][4 x 8-channel groups][2] GroupNorm sub-partials
+  float* s_bias = s_tb + 256;    // bias of this tile's NT output channels
+  float* s_sub = s_bias + 128;   // [4 waves][2 col blocks][4 x 8-channel groups][2] GroupNorm sub-partials
   float* s_mean = s_sub + 64;
   float* s_rstd = s_mean + 8;
 
@@ -99,6 +114,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int wm = wv % C::WM, wn = wv / C::WM;
+#ifdef GT_STAMPS
+  const bool stamp_on = KIND == CONV3 && IN == GT_STAMPS && sizeof(A) == 2 && p.Cin == 64 && p.Cout == 64 &&
+                        p.Fout == 80 && blockIdx.y == 0 && blockIdx.x < ST_WGS;
+  if (stamp_on && tid == 0) {
+    unsigned int hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_stamp_hwid[blockIdx.x] = hw;
+  }
+#endif
+  STAMP(0);
   const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
   const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
 
@@ -119,6 +144,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       s_sc[c] = sc; s_sh[c] = sh;
     }
   }
+
+  for (int c = tid; c < NT; c += 256) s_bias[c] = p.bias[cout0 + c];   // visible after the chunk barriers
 
   // ---- per-thread patch items, computed once: input position (npos = out of range) and mask
   constexpr int ES = (int)sizeof(A);
@@ -232,25 +259,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int nchunk = p.Cin_pad / C::CK;
   wimg += ((long)(par * gridDim.y + ntile) * nchunk) * C::WBYTES;
 
+  auto dma_weights = [&](int ch) {   // contiguous slab, 1 KiB per wave instruction, compile-time count
+    const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
+#pragma unroll
+    for (int k = 0; k < C::WPIECES; ++k) {
+      const int i = wv + 4 * k;
+      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
+                                       (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
+    }
+  };
+  // Workgroup barrier for the chunk loop without the memory-model fence of __syncthreads() (which waits
+  // for every LDS-DMA in flight); what must be visible is made explicit: own LDS stores (lgkmcnt) and
+  // this chunk's weight DMA (vmcnt below).
+  auto cta_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  STAMP(1);
   load_patch(0);
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
-    __syncthreads();                                   // previous chunk's fragments are consumed
-    {   // weight slab: contiguous DMA, 1 KiB per wave instruction, a compile-time count per wave
-      const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
-#pragma unroll
-      for (int k = 0; k < C::WPIECES; ++k) {
-        const int i = wv + 4 * k;
-        __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
-                                         (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
-      }
-    }
+    STAMP(2 + 5 * ch);
+    cta_sync();                                        // previous chunk's fragments are consumed
+    STAMP(3 + 5 * ch);
+    dma_weights(ch);                                   // issued first: its latency overlaps the patch store
     store_patch(c0);
-    // The weight DMA must have landed before any wave reads sW. hipcc does NOT reliably emit this
-    // vmcnt(0) for global_load_lds before a barrier (it was missing in the 1x1/128-wide instantiation:
-    // an intermittent, load-dependent race), so it is explicit. Nothing else is in flight here.
+    STAMP(4 + 5 * ch);
+    // The weight DMA must have landed before any wave reads sW; the compiler does not track
+    // global_load_lds reliably (it was missing in the 1x1/128-wide instantiation: an intermittent,
+    // load-dependent race), so the wait is explicit.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    STAMP(5 + 5 * ch);
+    cta_sync();
+    STAMP(6 + 5 * ch);
     if (ch + 1 < nchunk) {
       if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && c0 + C::CK == p.C0) set_offsets(p.C1);
       load_patch(c0 + C::CK);                          // in flight during this chunk's MFMAs
@@ -290,101 +328,147 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     }
   }
 
+  STAMP(40);
   // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
   // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
-  auto wave_sync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
+  // LDS instructions of one wave execute in order, so the transposition only needs its own LDS traffic
+  // drained and the compiler kept from reordering memory operations. (A wavefront-scope release fence
+  // would also emit vmcnt(0) and serialise every block behind the previous block's global stores.)
+  auto wave_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   __syncthreads();
   float* scr = reinterpret_cast<float*>(sA) + wv * 32 * C::EPI_ROW;
   const int g8 = lane & 3;                 // 8-channel group within the 32-channel block
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
   A* out = reinterpret_cast<A*>(p.out);
+  // Per (row block, half): element offset of this lane's output position (channel cout0), -1 past T,
+  // and its mask. Stores never wait, but vmcnt is one in-order counter: a load waited on after a
+  // store waits for that store too. So no load may sit between the stores: bias and GroupNorm
+  // coefficients come from LDS, and the residual / pre-activation inputs are loaded up front.
+  long obase[C::RBW][2];
+  float om[C::RBW][2];
 #pragma unroll
   for (int rb = 0; rb < C::RBW; ++rb) {
     const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int tc = t0 + tblk * 32 + (lane >> 2) + 16 * half;
+      const int frow = f0 + lrow;
+      const int fo = CONVT ? 2 * frow + pf : frow;
+      const int to = CONVT ? 2 * tc + pt : tc;
+      const bool valid = tc < Tg;
+      obase[rb][half] = valid ? (((long)b * p.Fout + fo) * p.Tout + to) * p.Cout + cout0 : -1;
+      om[rb][half] = (OUT == OUT_RBOUT && valid) ? mask_at(p.mask, p.T0, b, to, p.lvl_out) : 0.f;
+    }
+  }
+  constexpr bool EIN = OUT == OUT_RBOUT || OUT == OUT_RESID;
+  constexpr int EIPI = (int)sizeof(A) / 2;                         // 16-B items per 8 channels
+  constexpr bool EALL = EIN && C::RBW * 2 * 2 * EIPI <= 16;        // all up front (<= 64 VGPRs)
+  // otherwise (128-wide tiles) row block rb+1's inputs are loaded before row block rb's stores
+  constexpr int NE = EIN ? (EALL ? C::RBW : 2) * 2 * 2 * EIPI : 1;
+  uint4 ein[NE];
+  const A* esrc = reinterpret_cast<const A*>(OUT == OUT_RBOUT ? p.pre : p.in0);
+  auto load_ein = [&](int rb, int slot) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int q = 0; q < EIPI; ++q) {
+          const long ob = obase[rb][half];
+          const int cl = wn * 64 + cb * 32 + g8 * 8 + 4 * q;
+          ein[((slot * 2 + cb) * 2 + half) * EIPI + q] =
+              ob >= 0 ? *reinterpret_cast<const uint4*>(esrc + ob + cl) : make_uint4(0, 0, 0, 0);
+        }
+  };
+  if (EALL) {
+#pragma unroll
+    for (int rb = 0; rb < C::RBW; ++rb) load_ein(rb, rb);
+  } else if (EIN) {
+    load_ein(0, 0);
+  }
+#pragma unroll
+  for (int rb = 0; rb < C::RBW; ++rb) {
+    if (EIN && !EALL && rb + 1 < C::RBW) load_ein(rb + 1, (rb + 1) & 1);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) scr[acc_row(j, h) * C::EPI_ROW + r] = acc[rb][cb][j];
       wave_sync();
       const int cl = wn * 64 + cb * 32 + g8 * 8;       // tile-local first channel of this lane
-      const int co = cout0 + cl;
-      float bias[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) bias[k] = p.bias[co + k];
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int pos = (lane >> 2) + 16 * half;
-        const int tc = t0 + tblk * 32 + pos;
         float v[8];
         const f32x4 lo = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8 + 4);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { v[k] = lo[k] + bias[k]; v[4 + k] = hi[k] + bias[4 + k]; }
-        if (tc < Tg) {
-          const int frow = f0 + lrow;
-          const int fo = CONVT ? 2 * frow + pf : frow;
-          const int to = CONVT ? 2 * tc + pt : tc;
-          const long o = (((long)b * p.Fout + fo) * p.Tout + to) * p.Cout + co;
+        for (int k = 0; k < 4; ++k) { v[k] = lo[k] + b0[k]; v[4 + k] = hi[k] + b1[k]; }
+        const long ob = obase[rb][half];
+        if (ob >= 0) {
           if (OUT == OUT_STATS) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) { gs[cb] += v[k]; gq[cb] += v[k] * v[k]; }
-          } else if (OUT == OUT_RBOUT) {
-            // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
-            const float m = mask_at(p.mask, p.T0, b, to, p.lvl_out);
-            float pre[8];
-            if (sizeof(A) == 2) {
-              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o), pre, A());
-            } else {
-              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o), pre, A());
-              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.pre) + o + 4), pre + 4, A());
+          } else if (EIN) {
+            const int ei = (((EALL ? rb : (rb & 1)) * 2 + cb) * 2 + half) * EIPI;
+            float e[8];
+            item_to_f(ein[ei], e, A());
+            if (EIPI == 2) item_to_f(ein[ei + (EIPI - 1)], e + 4, A());
+            if (OUT == OUT_RBOUT) {
+              // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
+              const float m = om[rb][half];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] = mishf(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
+            } else {                                   // Residual: fn(x) + x   (diffusion.py:108)
+#pragma unroll
+              for (int k = 0; k < 8; ++k) v[k] += e[k];
             }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = mishf(pre[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
-          } else if (OUT == OUT_RESID) {   // Residual: fn(x) + x   (diffusion.py:108)
-            float res[8];
-            item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.in0) + o), res, A());
-            if (sizeof(A) == 4)
-              item_to_f(*reinterpret_cast<const uint4*>(reinterpret_cast<const A*>(p.in0) + o + 4), res + 4, A());
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += res[k];
           }
           if (sizeof(A) == 2) {
-            *reinterpret_cast<uint4*>(out + o) = f_to_item(v, A());
+            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(v, A());
           } else {
-            *reinterpret_cast<uint4*>(out + o) = f_to_item(v, A());
-            *reinterpret_cast<uint4*>(out + o + 4) = f_to_item(v + 4, A());
+            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(v, A());
+            *reinterpret_cast<uint4*>(out + ob + cl + 4) = f_to_item(v + 4, A());
           }
         }
       }
       wave_sync();
     }
   }
+  STAMP(42);
   if (OUT == OUT_STATS) {
-    // per 8-channel sub-group: reduce over the wave's positions (lanes with equal lane&3) ...
+    // per 8-channel sub-group: reduce over the wave's positions (the 16 lanes with equal lane&3):
+    // rotations by 4 and 8 inside each 16-lane row (DPP), then across the four rows
+    auto ror4 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, false)); };
+    auto ror8 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false)); };
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       float s = gs[cb], q = gq[cb];
-#pragma unroll
-      for (int off = 4; off < 64; off <<= 1) { s += __shfl_xor(s, off); q += __shfl_xor(q, off); }
+      s += ror4(s); q += ror4(q);           // DPP row_ror:4 / row_ror:8
+      s += ror8(s); q += ror8(q);
+      s += __shfl_xor(s, 16); q += __shfl_xor(q, 16);
+      s += __shfl_xor(s, 32); q += __shfl_xor(q, 32);
       if (lane < 4) {
         s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 0] = s;
         s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
       }
     }
+    STAMP(43);
     __syncthreads();
+    STAMP(44);
     // ... then per GroupNorm group over waves / sub-groups in a fixed order, one slot per workgroup
     if (tid < 8) {
-      const int gsz = p.Cout / 8;
+      const int gshift = __builtin_ctz(p.Cout >> 3);   // group size Cout/8 is a power of two (host check)
       float S = 0.f, Q = 0.f;
+#pragma unroll
       for (int w = 0; w < 4; ++w)
+#pragma unroll
         for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
           for (int g8 = 0; g8 < 4; ++g8) {
             const int co = cout0 + (w / C::WM) * 64 + cb * 32 + g8 * 8;
-            if (co / gsz == tid) {
+            if ((co >> gshift) == tid) {
               S += s_sub[((w * 2 + cb) * 4 + g8) * 2 + 0];
               Q += s_sub[((w * 2 + cb) * 4 + g8) * 2 + 1];
             }
@@ -396,6 +480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       dst[1] = Q;
     }
   }
+  STAMP(41);
 }
 
 template <class A, int KIND, int IN, int OUT, int NT>
@@ -404,6 +489,7 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   const int Fg = (KIND == CONVT4) ? p.Fin : p.Fout;
   const int Tg = (KIND == CONVT4) ? p.Tin : p.Tout;
   if (Fg % C::TF != 0 || p.Cout % NT != 0 || p.Cin_pad % C::CK != 0) return hipErrorInvalidValue;
+  if (OUT == OUT_STATS && ((p.Cout >> 3) & ((p.Cout >> 3) - 1)) != 0) return hipErrorInvalidValue;  // group size 2^k
   if ((long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * (long)sizeof(A) >= (1L << 31))
     return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
   dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
@@ -435,4 +521,11 @@ hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const
   return conv_nt(1, p.Cout) == 128 ? dispatch<bf16, 128>(kind, im, om, p, s) : dispatch<bf16, 64>(kind, im, om, p, s);
 }
 
+#ifdef GT_STAMPS
+extern "C" int gt_debug_read_stamps(unsigned long long* out, unsigned int* hwid) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(hwid, HIP_SYMBOL(g_stamp_hwid), sizeof(g_stamp_hwid)) != hipSuccess) return -1;
+  return 0;
+}
+#endif
 }  // namespace gt
