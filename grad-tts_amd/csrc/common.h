@@ -100,30 +100,61 @@ GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
 //     part[(b * nparts + slot) * 16 + g * 2 + {0,1}]      (plain stores, no atomics, no memset)
 // and every consumer reduces the slots of its utterance in a fixed order in fp64: deterministic,
 // and independent of how many utterances share the launch.
-// gn_reduce: call with all threads of the block (>= 256); leaves mean/rstd of the 8 groups in
-// s_mean/s_rstd (LDS). Threads 0..255 reduce, group g = thread/32, in a fixed order.
-GT_DEV void gn_reduce(const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd) {
-  const int t = threadIdx.x, g = t >> 5, j = t & 31;
-  if (t >= 256) { __syncthreads(); return; }
-  const float* pb = part + (long)b * nparts * 16 + g * 2;
-  double s = 0.0, q = 0.0;
-  for (int i = j; i < nparts; i += 32) {
-    s += (double)pb[(long)i * 16];
-    q += (double)pb[(long)i * 16 + 1];
-  }
+// Reduction in two halves so callers can overlap other loads with the slot loads:
+//   GnLoad gl = gn_load(part, nparts, b);     issues this thread's slot loads (threads 0..255)
+//   gn_finish(gl, ...);                        fp64 sums in a fixed order -> s_mean / s_rstd (LDS)
+// Thread t reads value k = t & 15 of slots t>>4, t>>4 + 16, ... (16 at once, coalesced 64-B rows); the
+// 256 fp64 partials are then summed per value by 16 threads in slot-group order. The order depends only
+// on nparts: deterministic and independent of the launch. Call with all threads of the block (>= 256).
+// Workgroup barrier that orders LDS only (no memory-model fence: outstanding global loads, e.g. a
+// prefetch, stay in flight).
+GT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct GnLoad {
+  float v[16];
+};
+GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
+  GnLoad g;
+  const int t = threadIdx.x, k = t & 15, grp = t >> 4;
+  const float* pb = part + (long)b * nparts * 16 + k;
 #pragma unroll
-  for (int off = 16; off > 0; off >>= 1) {
-    s += __shfl_xor(s, off);
-    q += __shfl_xor(q, off);
+  for (int q = 0; q < 16; ++q) {
+    const int i = grp + 16 * q;
+    g.v[q] = (t < 256 && i < nparts) ? pb[(long)i * 16] : 0.f;
   }
-  if (j == 0) {
-    const double mean = s / (double)count;
-    double var = q / (double)count - mean * mean;
+  return g;
+}
+// s_red: LDS scratch of >= 272 doubles
+GT_DEV void gn_finish(const GnLoad& g, const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd,
+                      double* s_red) {
+  const int t = threadIdx.x, k = t & 15, grp = t >> 4;
+  if (t < 256) {
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += (double)g.v[q];
+    for (int i = grp + 256; i < nparts; i += 16) acc += (double)part[((long)b * nparts + i) * 16 + k];
+    s_red[t] = acc;
+  }
+  lds_barrier();
+  if (t < 16) {
+    double a = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a += s_red[q * 16 + t];
+    s_red[256 + t] = a;
+  }
+  lds_barrier();
+  if (t < 8) {
+    const double mean = s_red[256 + 2 * t] / (double)count;
+    double var = s_red[256 + 2 * t + 1] / (double)count - mean * mean;
     var = var > 0.0 ? var : 0.0;
-    s_mean[g] = (float)mean;
-    s_rstd[g] = (float)(1.0 / sqrt(var + 1e-5));
+    s_mean[t] = (float)mean;
+    s_rstd[t] = (float)(1.0 / sqrt(var + 1e-5));
   }
-  __syncthreads();
+  lds_barrier();
+}
+GT_DEV void gn_reduce(const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd, double* s_red) {
+  const GnLoad g = gn_load(part, nparts, b);
+  gn_finish(g, part, nparts, b, count, s_mean, s_rstd, s_red);
 }
 
 // per-channel affine of the normalisation: y = x * scale + shift

@@ -115,8 +115,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int wm = wv % C::WM, wn = wv / C::WM;
 #ifdef GT_STAMPS
-  const bool stamp_on = KIND == CONV3 && IN == GT_STAMPS && sizeof(A) == 2 && p.Cin == 64 && p.Cout == 64 &&
-                        p.Fout == 80 && blockIdx.y == 0 && blockIdx.x < ST_WGS;
+#ifndef GT_STAMPS_C
+#define GT_STAMPS_C 64
+#define GT_STAMPS_F 80
+#endif
+  const bool stamp_on = KIND == CONV3 && IN == GT_STAMPS && sizeof(A) == 2 && p.Cin == GT_STAMPS_C &&
+                        p.Cout == GT_STAMPS_C && p.Fout == GT_STAMPS_F && blockIdx.y == 0 && blockIdx.x < ST_WGS;
   if (stamp_on && tid == 0) {
     unsigned int hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -127,27 +131,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
   const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
 
-  // per-channel GroupNorm scale/shift and time bias of the INPUT (IN_GN) / OUTPUT (OUT_RBOUT) channels
-  if (IN == IN_GN) {
-    gn_reduce(p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd);
-    for (int c = tid; c < p.Cin; c += 256) {
-      float sc, sh;
-      gn_affine(s_mean, s_rstd, p.Cin, c, p.gn_gamma, p.gn_beta, sc, sh);
-      s_sc[c] = sc; s_sh[c] = sh; s_tb[c] = p.tb[(long)b * p.tb_bstride + c];
-    }
+  // ---- prologue, ordered so that its global round trips overlap: GroupNorm slot loads, the per-channel
+  // coefficients and the mask are issued together; the first patch prefetch goes out before the fp64
+  // GroupNorm reduction (which needs barriers) runs.
+  double* s_red = reinterpret_cast<double*>(sA);   // the patch area is free until the first chunk
+  GnLoad gl;
+  if (IN == IN_GN) gl = gn_load(p.gn_part, p.gn_nparts, b);
+  if (OUT == OUT_RBOUT) gl = gn_load(p.pre_part, p.pre_nparts, b);
+  float c_g = 0.f, c_b = 0.f, c_t = 0.f;            // gamma, beta, time bias of channel tid
+  if (IN == IN_GN && tid < p.Cin) {
+    c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; c_t = p.tb[(long)b * p.tb_bstride + tid];
   }
-  if (OUT == OUT_RBOUT) {
-    gn_reduce(p.pre_part, p.pre_nparts, b, p.pre_count, s_mean, s_rstd);
-    for (int c = tid; c < NT; c += 256) {
-      float sc, sh;
-      gn_affine(s_mean, s_rstd, p.Cout, cout0 + c, p.pre_gamma, p.pre_beta, sc, sh);
-      s_sc[c] = sc; s_sh[c] = sh;
-    }
-  }
+  if (OUT == OUT_RBOUT && tid < NT) { c_g = p.pre_gamma[cout0 + tid]; c_b = p.pre_beta[cout0 + tid]; }
+  const float c_bias = tid < NT ? p.bias[cout0 + tid] : 0.f;
 
-  for (int c = tid; c < NT; c += 256) s_bias[c] = p.bias[cout0 + c];   // visible after the chunk barriers
-
-  // ---- per-thread patch items, computed once: input position (npos = out of range) and mask
+  // per-thread patch items, computed once: input position (npos = out of range) and mask
   constexpr int ES = (int)sizeof(A);
   const int npos = p.B * p.Fin * p.Tin;
   int pidx[C::PPT];
@@ -272,8 +270,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   // for every LDS-DMA in flight); what must be visible is made explicit: own LDS stores (lgkmcnt) and
   // this chunk's weight DMA (vmcnt below).
   auto cta_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  load_patch(0);                                      // in flight during the GroupNorm reduction
+  if (IN == IN_GN || OUT == OUT_RBOUT) {
+    if (IN == IN_GN) gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
+    else gn_finish(gl, p.pre_part, p.pre_nparts, b, p.pre_count, s_mean, s_rstd, s_red);
+    // per-channel GroupNorm scale/shift (and time bias) of the INPUT (IN_GN) / OUTPUT (OUT_RBOUT) channels
+    if (IN == IN_GN && tid < p.Cin) {
+      const int g = tid / (p.Cin >> 3);
+      const float sc = c_g * s_rstd[g];
+      s_sc[tid] = sc; s_sh[tid] = c_b - s_mean[g] * sc; s_tb[tid] = c_t;
+    }
+    if (OUT == OUT_RBOUT && tid < NT) {
+      const int g = (cout0 + tid) / (p.Cout >> 3);
+      const float sc = c_g * s_rstd[g];
+      s_sc[tid] = sc; s_sh[tid] = c_b - s_mean[g] * sc;
+    }
+  }
+  if (tid < NT) s_bias[tid] = c_bias;                 // all visible after the first chunk barrier
   STAMP(1);
-  load_patch(0);
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
     STAMP(2 + 5 * ch);
@@ -329,6 +343,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   }
 
   STAMP(40);
+#ifdef GT_EXP_DIRECT_EPI
+  constexpr bool DIRECT = OUT == OUT_STATS && sizeof(A) == 2 && KIND != CONVT4;
+#else
+  constexpr bool DIRECT = false;
+#endif
+  if constexpr (DIRECT) {
+    // ---- epilogue straight from the accumulators (bf16 output, GroupNorm sums): register j of lane
+    // (r, h) is position acc_row(j, h) of the block, channel r -- lanes 0..31 of one register are 32
+    // consecutive channels of one position (64 contiguous bytes): 2-byte buffer stores, no LDS, no
+    // barrier. Positions past T get an out-of-range offset (the store is dropped).
+    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        p.out, (short)0, (int)((long)p.B * p.Fout * p.Tout * p.Cout * 2), 0x00020000);
+    float gsum[2] = {0.f, 0.f}, gsq[2] = {0.f, 0.f};
+    const bool full = t0 + C::TT <= Tg;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int cl = wn * 64 + cb * 32 + r;
+      const float bco = s_bias[cl];
+#pragma unroll
+      for (int rb = 0; rb < C::RBW; ++rb) {
+        const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+        const int tcb = t0 + tblk * 32 + 4 * h;                 // + (j&3) + 8(j>>2)
+        const int vbase = (((b * p.Fout + f0 + lrow) * p.Tout + tcb) * p.Cout + cout0 + cl) * 2;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int dj = (j & 3) + 8 * (j >> 2);
+          const float v = acc[rb][cb][j] + bco;
+          const bool ok = full || tcb + dj < Tg;
+          if (ok) { gsum[cb] += v; gsq[cb] += v * v; }
+          const bf16 hv = (bf16)v;
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), ro, ok ? vbase : 0x7ff00000,
+                                                dj * p.Cout * 2, 0);
+        }
+      }
+    }
+    // per 8-channel group: sum the 8 channel lanes (xor 1, 2, 4) and the two position halves (xor 32)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      float sv = gsum[cb], qv = gsq[cb];
+#pragma unroll
+      for (int off = 1; off < 8; off <<= 1) { sv += __shfl_xor(sv, off); qv += __shfl_xor(qv, off); }
+      sv += __shfl_xor(sv, 32); qv += __shfl_xor(qv, 32);
+      if (lane < 32 && (r & 7) == 0) {
+        s_sub[((wv * 2 + cb) * 4 + (r >> 3)) * 2 + 0] = sv;
+        s_sub[((wv * 2 + cb) * 4 + (r >> 3)) * 2 + 1] = qv;
+      }
+    }
+  } else {
   // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
   // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
   // LDS instructions of one wave execute in order, so the transposition only needs its own LDS traffic
@@ -454,6 +516,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
       }
     }
+  }
+  }   // !DIRECT
+  if (OUT == OUT_STATS) {
     STAMP(43);
     __syncthreads();
     STAMP(44);
@@ -504,6 +569,7 @@ static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParam
   if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_t<A, CONV3, IN_INPUT, OUT_STATS, NT>(p, s);
   if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_t<A, CONV3, IN_MASK, OUT_STATS, NT>(p, s);
   if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_t<A, CONV3, IN_GN, OUT_STATS, NT>(p, s);
+  if (kind == CONV3 && im == IN_PLAIN && om == OUT_STATS) return launch_t<A, CONV3, IN_PLAIN, OUT_STATS, NT>(p, s);
   if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_t<A, CONV1, IN_INPUT, OUT_RBOUT, NT>(p, s);
   if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_t<A, CONV1, IN_MASK, OUT_RBOUT, NT>(p, s);
   if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_t<A, CONV1, IN_PLAIN, OUT_RESID, NT>(p, s);

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -168,6 +169,15 @@ namespace {
 int ck_of(int dt) { return dt ? 32 : 16; }
 size_t esize(int dt) { return dt ? 2 : 4; }
 
+// channel count from which block2's GroupNorm/Mish transform runs as a separate in-place pass
+static int gn_apply_min_c() {
+  static const int v = [] {
+    const char* e = getenv("GT_GN_APPLY_MIN_C");
+    return e ? atoi(e) : 256;
+  }();
+  return v;
+}
+
 // pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4], as 4 parity images) into the
 // conv_kernel weight image (wimage.h) in the compute dtype
 void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const std::vector<float>& w,
@@ -206,6 +216,28 @@ void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const 
   d->cinpad[dt][key] = W.nchunk * W.ck;
 }
 
+// pack a 3x3 [Cout][Cin][3][3] weight into the conv4 image (wimage.h conv4_wimg_off), bf16
+void pack_conv4(Blob& blob, const std::string& key, const std::vector<float>& w, int cout, int cin) {
+  const int nt = conv4_pick(cout).nt;
+  std::vector<uint8_t> img((size_t)cout * 9 * cin * 2, 0);
+  for (int co = 0; co < cout; ++co)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int t = 0; t < 9; ++t) {
+        const uint16_t hb = f2bf(w[((size_t)co * cin + ci) * 9 + t]);
+        memcpy(img.data() + conv4_wimg_off(nt, cin, co, t, ci), &hb, 2);
+      }
+  blob.put(key, img.data(), img.size());
+}
+
+// conv4 (LDS-DMA pipeline) for the bf16 3x3 stride-1 convs: GT_CONV4=1 selects it instead of conv_kernel
+static bool conv4_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("GT_CONV4");
+    return e && atoi(e) != 0;   // experimental LDS-DMA pipeline (conv4.hip), off by default
+  }();
+  return v;
+}
+
 int prepare(gt_decoder* d, int dt) {
   if (!d->dirty[dt]) return GT_OK;
   for (size_t i = 0; i < d->inv.size(); ++i)
@@ -219,6 +251,8 @@ int prepare(gt_decoder* d, int dt) {
     if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, k, w, shp, false);
+      if (dt && conv4_enabled() && ends_with(k, ".block.0.weight") && shp[1] % 16 == 0)
+        pack_conv4(blob, k + ".v4", w, (int)shp[0], (int)shp[1]);
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, k, w, shp, true);
     } else if (ends_with(k, "to_qkv.weight")) {
@@ -269,7 +303,7 @@ int prepare(gt_decoder* d, int dt) {
 // ---------------------------------------------------------------- workspace
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
-  size_t stats, part, G, Mw, tb, spk, total;
+  size_t stats, part, G, Mw, tb, spk, flag, total;
   int pmax;
   int tile_pos[3], ntile[3];
 };
@@ -306,6 +340,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.Mw = take((size_t)B * conv_wimg(dt, 1, 256, 256).total);
   L.tb = take((size_t)std::max<int64_t>(B, N) * 1792 * 4);
   L.spk = take((size_t)B * 80 * 4);
+  L.flag = take(sizeof(int));
   L.total = o;
   return L;
 }
@@ -321,6 +356,7 @@ struct Run {
   const float* mask; const float* mu; const float* xt; const float* spk_s;
   const float* tb; long tb_bstride;
   int stat_slot = 0;
+  bool mask01 = true;            // every mask value is 0 or 1 (checked once per API call)
   hipError_t err = hipSuccess;
   const char* probe = nullptr;   // diagnostics: copy the activation named `probe` to probe_out (NCHW fp32)
   float* probe_out = nullptr;
@@ -351,6 +387,28 @@ struct Run {
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
                              ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
+  }
+
+  // 3x3 stride-1 conv with GroupNorm partial sums of the output; returns the number of partial slots per
+  // utterance it wrote. bf16 inputs without a transform (IN_PLAIN, or IN_MASK with a 0/1 mask) take the
+  // LDS-DMA pipeline (conv4.hip); everything else conv_kernel.
+  int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
+    const bool v4 = dt && conv4_enabled() && (im == IN_PLAIN || (im == IN_MASK && mask01)) && p.Cin % 16 == 0 &&
+                    d->dp[dt].count(wkey + ".v4");
+    if (!v4) {
+      conv(CONV3, im, OUT_STATS, p);
+      return conv_gn_nparts(dt, p.Fout, p.Tout, p.Cout);
+    }
+    const Conv4Cfg c = conv4_pick(p.Cout);
+    p.w = W(wkey + ".v4");
+    p.mask_in = im == IN_MASK;
+    const double pos = (double)p.B * p.Fout * p.Tout;
+    const std::string name = "conv4_kernel<" + std::to_string(c.nt) + "," + std::to_string(c.tt) + "," +
+                             std::to_string(c.nw) + "," + std::to_string(c.ns) + ">@" + std::to_string(p.Cin) + "x" +
+                             std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+    timed(name, 2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + (double)p.Cout * 9 * p.Cin * 2.0,
+          [&] { return launch_conv4(p, c, s); });
+    return conv4_nparts(p.Fout, p.Tout, p.Cout, c);
   }
 
   // diagnostics: "gnpart.<k>" copies GroupNorm partial slot k (B x pmax x 16 floats) after the launch that
@@ -396,7 +454,7 @@ struct Run {
     void* pre2 = act(lvl, 4);
     float* st1 = stats();
     float* st2 = stats();
-    const int np = conv_gn_nparts(dt, Fl(lvl), Tl(lvl), Cout);
+    int np1 = 0, np2 = 0;                         // GroupNorm partial slots written by block1 / block2
     const long count = (long)(Cout / 8) * Fl(lvl) * Tl(lvl);
     {   // block1 conv on x*mask
       ConvParams p = base(lvl, lvl);
@@ -405,19 +463,38 @@ struct Run {
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
       p.w = W(k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
       p.out = pre1; p.out_part = st1;
-      conv(CONV3, input ? IN_INPUT : IN_MASK, OUT_STATS, p);
+      if (input) {
+        conv(CONV3, IN_INPUT, OUT_STATS, p);
+        np1 = conv_gn_nparts(dt, Fl(lvl), Tl(lvl), Cout);
+      } else {
+        np1 = conv3_stats(IN_MASK, p, k + "block1.block.0.weight");
+      }
       tap(k + "pre1", lvl, pre1, Cout);
       tap_part(stat_slot - 2);
     }
     {   // block2 conv on (Mish(GN(h1))*m + tb)*m
+      // The transform runs once per element in place (one extra read+write of h1) when the conv4 path
+      // takes the conv (bf16), and on wide fp32 levels (GT_GN_APPLY_MIN_C, default 256 channels), where
+      // the operand-load transform of conv_kernel is recomputed by every 128-channel tile and halo row.
+      const bool apply = (dt && conv4_enabled()) || Cout >= gn_apply_min_c();
+      if (apply) {
+        RbOutParams a{};
+        a.pre = pre1; a.part = st1; a.nparts = np1; a.gamma = Fp(k + "block1.block.1.weight");
+        a.beta = Fp(k + "block1.block.1.bias"); a.count = count; a.out = pre1; a.mask = mask;
+        a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = Cout; a.T0 = T; a.lvl = lvl;
+        a.tb = tb + tb_off; a.tb_bstride = tb_bstride;
+        timed(std::string("gn_apply_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
+                  std::to_string(Fl(lvl)), 0.0, 2.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt),
+              [&] { return launch_gn_apply(dt, a, s); });
+      }
       ConvParams p = base(lvl, lvl);
       p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block2.block.0.weight");
       p.in0 = pre1; p.C0 = Cout;
-      p.gn_part = st1; p.gn_nparts = np; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
+      p.gn_part = st1; p.gn_nparts = np1; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
       p.gn_count = count; p.tb = tb + tb_off; p.tb_bstride = tb_bstride;
       p.w = W(k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
       p.out = pre2; p.out_part = st2;
-      conv(CONV3, IN_GN, OUT_STATS, p);
+      np2 = conv3_stats(apply ? IN_PLAIN : IN_GN, p, k + "block2.block.0.weight");
       tap(k + "pre2", lvl, pre2, Cout);
       tap_part(stat_slot - 1);
     }
@@ -427,13 +504,13 @@ struct Run {
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
       p.w = W(k + "res_conv.weight"); p.bias = Fp(k + "res_conv.bias");
-      p.pre = pre2; p.pre_part = st2; p.pre_nparts = np; p.pre_gamma = Fp(k + "block2.block.1.weight");
+      p.pre = pre2; p.pre_part = st2; p.pre_nparts = np2; p.pre_gamma = Fp(k + "block2.block.1.weight");
       p.pre_beta = Fp(k + "block2.block.1.bias"); p.pre_count = count;
       p.out = out;
       conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
     } else {                                       // Mish(GN(h2))*m + x*m
       RbOutParams p;
-      p.pre = pre2; p.part = st2; p.nparts = np; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
+      p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
       p.count = count; p.x = in0; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = Cout;
       p.T0 = T; p.lvl = lvl;
       const double by = 3.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt);
@@ -525,17 +602,18 @@ struct Run {
     upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
     // final_block conv (+GN sums), then the fused GN/Mish/final_conv/(Euler) kernel
     float* st = stats();
+    int fnp = 0;
     {
       ConvParams p = base(0, 0);
       p.Cin = 64; p.Cout = 64; p.Cin_pad = d->cinpad[dt].at("final_block.block.0.weight");
       p.in0 = act(0, 0); p.C0 = 64;
       p.w = W("final_block.block.0.weight"); p.bias = Fp("final_block.block.0.bias");
       p.out = act(0, 3); p.out_part = st;
-      conv(CONV3, IN_MASK, OUT_STATS, p);
+      fnp = conv3_stats(IN_MASK, p, "final_block.block.0.weight");
       tap("final_block.pre", 0, act(0, 3), 64);
     }
     FinalParams f;
-    f.pre = act(0, 3); f.part = st; f.nparts = conv_gn_nparts(dt, 80, T, 64); f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
+    f.pre = act(0, 3); f.part = st; f.nparts = fnp; f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
     f.count = (long)8 * 80 * T; f.wf = Fp("final_conv.weight"); f.bf = Fp("final_conv.bias");
     f.mask = mask; f.B = B; f.T = T; f.euler = euler; f.out = out; f.mu = mu; f.xt = xt_inout;
     f.beta_t = beta_t; f.hstep = hstep;
@@ -649,6 +727,19 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int
   return layout(dtype ? 1 : 0, B, T, n_timesteps).total;
 }
 
+// Are all mask values 0 or 1 (sequence_mask)? Decides whether conv4 may take x*mask convs (it realises
+// the product as zero-filled loads). One tiny reduction + a 4-byte read-back per API call (a stream sync).
+static bool mask_is_01(Run& R, const float* mask, int64_t B, int64_t T) {
+  if (!R.dt || !conv4_enabled()) return true;
+  int* flag = (int*)(R.ws + R.L.flag);
+  int host = 1;
+  R.chk(hipMemsetAsync(flag, 0, sizeof(int), R.s));
+  R.chk(launch_mask_check(mask, B * T, flag, R.s));
+  R.chk(hipMemcpyAsync(&host, flag, sizeof(int), hipMemcpyDeviceToHost, R.s));
+  R.chk(hipStreamSynchronize(R.s));
+  return R.err == hipSuccess && host == 0;
+}
+
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
                           const float* t, const float* spk, int64_t B, int64_t T, float* out, void* workspace,
                           size_t workspace_bytes, void* stream, const char* probe, float* probe_out) {
@@ -662,6 +753,7 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
   R.L = layout(dtype, B, T, 0);
   R.mask = mask; R.mu = mu; R.xt = x; R.spk_s = nullptr;
   R.probe = probe; R.probe_out = probe_out;
+  R.mask01 = mask_is_01(R, mask, B, T);
   float* tbuf = (float*)(R.ws + R.L.tb);
   TembParams tp;
   tp.rows = (int)B; tp.tvals = t; tp.n_steps = 0; tp.pe_scale = d->pe_scale; tp.freqs = R.Fp("freqs");
@@ -707,6 +799,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
   R.d = d; R.dt = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream; R.ws = (uint8_t*)workspace;
   R.L = layout(dtype, B, T, n_timesteps);
   R.mask = mask; R.mu = mu; R.xt = out; R.spk_s = nullptr;
+  R.mask01 = mask_is_01(R, mask, B, T);
   R.chk(launch_mask_copy(z, mask, (int)B, 80, (int)T, out, R.s));   // xt = z * mask  (diffusion.py:257)
   if (n_timesteps > 0) {
     float* tbuf = (float*)(R.ws + R.L.tb);

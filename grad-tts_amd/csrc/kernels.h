@@ -23,6 +23,7 @@ struct ConvParams {
   const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
   const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
+  int mask_in;                                        // conv4: input is x * mask (0/1 mask)
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* bias;                                  // [Cout]
@@ -58,8 +59,11 @@ hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s);
 struct RbOutParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
   const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
+  const float* tb; long tb_bstride;   // gn_apply only: time bias rows
 };
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s);
+// in place: pre = (Mish(GN(pre))*m + tb)*m   (out must equal pre)
+hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s);
 
 struct TembParams {
   int rows; const float* tvals;   // tvals == nullptr: row i is Euler step i of n_steps (t computed on device)
@@ -74,5 +78,14 @@ hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float*
 hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s);
 // debug probe: channels-last activation [B][F][T][C] (act dtype) -> fp32 NCHW [B][C][F][T]
 hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, int C, float* dst, hipStream_t s);
+
+// 3x3 stride-1 bf16 convolution with LDS-DMA staging (conv4.hip): plain input or x*mask with a 0/1 mask,
+// weights in the conv4 image (wimage.h), GroupNorm partial sums of the output.
+struct Conv4Cfg { int nt, tt, nw, ns; };
+Conv4Cfg conv4_pick(int Cout);
+int conv4_nparts(int F, int T, int Cout, Conv4Cfg c);
+hipError_t launch_conv4(const ConvParams& p, Conv4Cfg c, hipStream_t s);
+// flag = 1 if any mask value is neither 0 nor 1 (flag must be zeroed first)
+hipError_t launch_mask_check(const float* mask, long n, int* flag, hipStream_t s);
 
 }  // namespace gt

@@ -2,11 +2,14 @@
 //   final_kernel          final_block GN-apply + Mish + mask, final_conv 1x1 (64->1), mask, and either
 //                         the score output (GradLogPEstimator2d.forward, diffusion.py:212-216) or the
 //                         Euler update of Diffusion.reverse_diffusion (diffusion.py:264-267) in place.
-//   rbout_identity_kernel ResnetBlock output with identity residual: Mish(GN(h2))*m + x*m (diffusion.py:77-79)
+//   gn_mish_kernel        ResnetBlock output with identity residual: Mish(GN(h2))*m + x*m (diffusion.py:77-79),
+//                         or block2's input (Mish(GN(h1))*m + t_emb)*m applied once in place (wide levels)
 //   temb_kernel           SinusoidalPosEmb -> time MLP -> every ResnetBlock's Mish+Linear time bias
 //                         (diffusion.py:113-125, 143-144, 64-65, 76); one row per Euler step.
 //   spk_mlp_kernel        spk_mlp (diffusion.py:139-141, 175-176)
 //   mask_copy_kernel      x_T = z * mask (diffusion.py:257)
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -16,8 +19,9 @@ constexpr int FIN_PPT = 1;   // positions per thread (more per thread exposes th
 template <class A>
 __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
   __shared__ float s_sc[64], s_sh[64], s_w[64], s_mean[8], s_rstd[8];
+  __shared__ double s_red[272];
   const int b = blockIdx.y, tid = threadIdx.x;
-  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd);
+  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   if (tid < 64) {
     float sc, sh;
     gn_affine(s_mean, s_rstd, 64, tid, p.gamma, p.beta, sc, sh);
@@ -64,22 +68,28 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 
 // 8 x 16-B items per thread; the block stride (256 items) is a multiple of C, so every thread keeps one
 // channel group (and its GroupNorm scale/shift) for all of its items.
+//   APPLY = false: ResnetBlock output, out = Mish(GN(pre))*m + x*m               (diffusion.py:57-58, 77-79)
+//   APPLY = true : block2's conv input in place, pre = (Mish(GN(pre))*m + tb)*m   (diffusion.py:57-58, 76, 52)
 constexpr int RB_IPT = 8;
-template <class A>
-__global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
+template <class A, bool APPLY>
+__global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   __shared__ float s_mean[8], s_rstd[8];
+  __shared__ double s_red[272];
   const int b = blockIdx.y, tid = threadIdx.x;
-  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd);
+  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   constexpr int ICH = Act<A>::kItemCh;
   const int total = p.F * p.T * p.C;                       // elements of one utterance
   const int e0 = (blockIdx.x * RB_IPT * 256 + tid) * ICH;
   const int c0 = e0 % p.C;
-  float sc[ICH], sh[ICH];
+  float sc[ICH], sh[ICH], tb[ICH];
 #pragma unroll
-  for (int k = 0; k < ICH; ++k) gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
+  for (int k = 0; k < ICH; ++k) {
+    gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
+    tb[k] = APPLY ? p.tb[(long)b * p.tb_bstride + c0 + k] : 0.f;
+  }
   const long ub = (long)b * total;
   const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
-  const A* xin = reinterpret_cast<const A*>(p.x) + ub;
+  const A* xin = reinterpret_cast<const A*>(APPLY ? p.pre : p.x) + ub;
   A* out = reinterpret_cast<A*>(p.out) + ub;
   uint4 vp[RB_IPT], vx[RB_IPT];
 #pragma unroll
@@ -87,7 +97,7 @@ __global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
     const int e = e0 + i * 256 * ICH;
     if (e < total) {
       vp[i] = *reinterpret_cast<const uint4*>(pre + e);
-      vx[i] = *reinterpret_cast<const uint4*>(xin + e);
+      if (!APPLY) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
     }
   }
 #pragma unroll
@@ -96,11 +106,17 @@ __global__ __launch_bounds__(256) void rbout_identity_kernel(RbOutParams p) {
     if (e < total) {
       const int t = (e / p.C) % p.T;
       const float m = mask_at(p.mask, p.T0, b, t, p.lvl);
-      float v[ICH], x[ICH];
+      float v[ICH];
       item_to_f(vp[i], v, A());
-      item_to_f(vx[i], x, A());
+      if (APPLY) {
 #pragma unroll
-      for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * sc[k] + sh[k]) * m + x[k] * m;
+        for (int k = 0; k < ICH; ++k) v[k] = (mishf(v[k] * sc[k] + sh[k]) * m + tb[k]) * m;
+      } else {
+        float x[ICH];
+        item_to_f(vx[i], x, A());
+#pragma unroll
+        for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * sc[k] + sh[k]) * m + x[k] * m;
+      }
       *reinterpret_cast<uint4*>(out + e) = f_to_item(v, A());
     }
   }
@@ -188,14 +204,39 @@ hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
+static hipError_t launch_gn_mish(int act_bf16, bool apply, const RbOutParams& p, hipStream_t s) {
   const int ich = act_bf16 ? 8 : 4;
   const long total = (long)p.F * p.T * p.C;
   if ((256 * ich) % p.C != 0 || total >= (1L << 31)) return hipErrorInvalidValue;
   const long items = total / ich;
   dim3 grid((unsigned)((items + 256 * RB_IPT - 1) / (256 * RB_IPT)), (unsigned)p.B);
-  if (act_bf16) hipLaunchKernelGGL(rbout_identity_kernel<bf16>, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(rbout_identity_kernel<float>, grid, dim3(256), 0, s, p);
+  if (act_bf16) {
+    if (apply) hipLaunchKernelGGL((gn_mish_kernel<bf16, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gn_mish_kernel<bf16, false>), grid, dim3(256), 0, s, p);
+  } else {
+    if (apply) hipLaunchKernelGGL((gn_mish_kernel<float, true>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((gn_mish_kernel<float, false>), grid, dim3(256), 0, s, p);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
+  return launch_gn_mish(act_bf16, false, p, s);
+}
+hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s) {
+  return launch_gn_mish(act_bf16, true, p, s);
+}
+
+__global__ __launch_bounds__(256) void mask_check_kernel(const float* mask, long n, int* flag) {
+  int bad = 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float m = mask[i];
+    bad |= (m != 0.f && m != 1.f);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+hipError_t launch_mask_check(const float* mask, long n, int* flag, hipStream_t s) {
+  const unsigned blocks = (unsigned)std::min<long>(256, (n + 255) / 256);
+  hipLaunchKernelGGL(mask_check_kernel, dim3(blocks), dim3(256), 0, s, mask, n, flag);
   return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ def main():
     used = st[:, 0] > 0
     st, hw = st[used], hw[used]
     nwg = len(st)
-    nch = sum(1 for c in range(8) if (st[:, 2 + 5 * c] > 0).all())
+    nch = sum(1 for c in range(8) if (st[:, 2 + 5 * c] > 0).all())   # stamps cover up to 7 chunks
     t0 = st[:, 0].min()
     span = st[:, 41].max() - t0
     print(f"workgroups {nwg}, chunks {nch}, kernel span {span} cycles")
