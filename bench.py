@@ -2,7 +2,7 @@
 """Benchmark: mel-frames/s of the N-step reverse-diffusion decoder on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--frames 512] [--n-timesteps 50]
-                    [--dtype bf16|fp32] [--n-spks 1] [--no-cpu-baseline]
+                    [--dtype bf16|fp32|bf16_w8] [--n-spks 1] [--no-cpu-baseline]
 
 A "step" is one complete ``Diffusion.reverse_diffusion`` call (n_timesteps Euler steps of the U-Net)
 over one batch of synthetic utterances already resident in HBM, followed by the RCCL all_gather of
@@ -36,7 +36,7 @@ from gradtts_amd.diffusion import Diffusion  # noqa: E402
 from gradtts_amd.params import estimator_flops, synthetic_inputs, synthetic_state_dict  # noqa: E402
 from gradtts_amd.shard import gather_shards  # noqa: E402
 
-PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}   # dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK = {"bf16": 2.5e15, "bf16_w8": 2.5e15, "fp32": 157.3e12}   # dense MFMA peaks (MI355X_MICROARCH.md)
 HBM_PEAK = 8.0e12
 
 
@@ -48,7 +48,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=512)
     ap.add_argument("--n-timesteps", type=int, default=50)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "bf16_w8"],
+                    help="bf16_w8: fp8 e4m3 conv weights, bf16 MFMA operands (BASELINE config 5)")
     ap.add_argument("--n-spks", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-batch", type=int, default=4)
@@ -102,7 +103,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    cdt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    cdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "bf16_w8": "bf16_w8"}[args.dtype]
     B, T, N = args.batch, args.frames, args.n_timesteps
     dec = Diffusion(80, 64, args.n_spks, 64, 0.05, 20, 1000, compute_dtype=cdt)
     sd = synthetic_state_dict(seed=0, n_spks=args.n_spks)
@@ -170,7 +171,8 @@ def main():
             "dtype": args.dtype,
             "data": "synthetic: mu~N(0,1), z=mu+N(0,1), full-length masks; random-init weights (seed 0), no checkpoint",
             "config": {"workload": f"LJSpeech single-speaker batch={B}/GPU, T={T} frames, n_timesteps={N}, "
-                                   f"{args.dtype} (BASELINE config 2; N GPUs = config 4 weak-scaled)",
+                                   f"{args.dtype} " + ("(BASELINE config 5: fp8 U-Net weights)" if args.dtype == "bf16_w8" else
+                                                     "(BASELINE config 2; N GPUs = config 4 weak-scaled)"),
                        "global_batch": world * B, "seq_len": T, "n_timesteps": N, "n_spks": args.n_spks,
                        "parallelism": f"dp{world} utterance shards, RCCL all_gather of mels" if world > 1 else "dp1"},
             "rtf": sec * 22050 / (frames * 256),     # inference.py:91 formula

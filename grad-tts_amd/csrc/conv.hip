@@ -43,7 +43,23 @@ __device__ unsigned int g_stamp_hwid[ST_WGS];
 #define STAMP(k) do {} while (0)
 #endif
 
-template <class A, int KIND, int IN, int OUT, int NT>
+#ifndef GT_CAP_T
+#define GT_CAP_T 3
+#endif
+#ifndef GT_CAP_1
+#define GT_CAP_1 3
+#endif
+#ifndef GT_CAP_S2
+#define GT_CAP_S2 2
+#endif
+#ifndef GT_CAP_3
+#define GT_CAP_3 0
+#endif
+#ifndef GT_CAP_3W8
+#define GT_CAP_3W8 3
+#endif
+
+template <class A, int KIND, int IN, int OUT, int NT, int W8>
 struct ConvCfg {
   static constexpr bool CONVT = KIND == CONVT4;
   static constexpr int KS = (KIND == CONV1) ? 1 : 3;
@@ -62,9 +78,11 @@ struct ConvCfg {
   static constexpr int CKB = conv_ckb(sizeof(A) == 2);
   static constexpr int SUBS = CKB / 16;
   static constexpr int POSB = CKB + 16;
-  static constexpr int WROW = conv_wrow(NTAP, CKB);
-  static constexpr int WBYTES = conv_wbytes(NT, NTAP, CKB);
-  static constexpr int WPIECES = WBYTES / 1024 / 4;       // 1 KiB DMA pieces per wave per chunk
+  // weight slab: bf16/fp32 image (conv_wrow) or the fp8 image (conv8_wrow, W8: e4m3 weights, bf16 operands)
+  static constexpr int WROW = W8 ? conv8_wrow(NTAP) : conv_wrow(NTAP, CKB);
+  static constexpr int WBYTES = W8 ? conv8_wbytes(NT, NTAP) : conv_wbytes(NT, NTAP, CKB);
+  static constexpr int WPIECES_ALL = WBYTES / 1024;        // 1 KiB DMA pieces per chunk
+  static constexpr int WPIECES = (WPIECES_ALL + 3) / 4;    // per wave (the last round may be partial)
   static constexpr int CK = CKB / (int)sizeof(A);
   static constexpr int ICH = 16 / (int)sizeof(A);
   static constexpr int KSTEP_B = 16 * (int)sizeof(A);
@@ -74,18 +92,38 @@ struct ConvCfg {
   static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
   static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
   static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
-  static constexpr int SMEM = A_BYTES + WBYTES + (3 * 256 + 128 + 64 + 16) * 4;
+  static constexpr int SMEM0 = A_BYTES + WBYTES + (3 * 256 + 128 + 64 + 16 + 128) * 4;
+  // Workgroups per CU are capped by LDS where more resident tiles measured slower (cache/write
+  // contention, not latency hiding, bounds them): CAP = 0 leaves occupancy to registers and LDS.
+  // (measured, tools/ab_variants.sh: 64-wide 1x1 and sub-pixel convs 3, stride-2 64-wide 2; the fp8-weight
+  // 3x3 tiles need fewer registers than the bf16 ones and would otherwise run 4 per CU)
+  static constexpr int CAP = NT != 64 ? 0 : KIND == CONVT4 ? GT_CAP_T : KIND == CONV1 ? GT_CAP_1
+                           : KIND == CONV3_S2 ? GT_CAP_S2 : (W8 ? GT_CAP_3W8 : GT_CAP_3);
+  static constexpr int SMEM = (CAP && SMEM0 <= 160 * 1024 / (CAP + 1)) ? 160 * 1024 / (CAP + 1) + 512 : SMEM0;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
-  static_assert(WBYTES % 4096 == 0, "whole DMA rounds");
+  static_assert(WBYTES % 1024 == 0, "whole DMA pieces");
+  static_assert(!W8 || (sizeof(A) == 2 && KIND != CONV1), "fp8 weights: bf16 operands, 3x3 / 2x2 convs");
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <class A, int KIND, int IN, int OUT, int NT>
+// fp8 weight fragment (W8): 8 consecutive e4m3 input-channel weights of one output channel -> bf16x8
+// (exact: every e4m3 value is a bf16 value; the per-channel scale is applied to the accumulator)
+GT_DEV bf16x8 w8_frag(const char* src) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const uint2 q = *reinterpret_cast<const uint2*>(src);
+  const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(q.x, 1.0f, false);
+  const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(q.x, 1.0f, true);
+  const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(q.y, 1.0f, false);
+  const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(q.y, 1.0f, true);
+  return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+template <class A, int KIND, int IN, int OUT, int NT, int W8>
 // 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
-  typedef ConvCfg<A, KIND, IN, OUT, NT> C;
+  typedef ConvCfg<A, KIND, IN, OUT, NT, W8> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
 
@@ -99,6 +137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   float* s_sub = s_bias + 128;   // [4 waves][2 col blocks][4 x 8-channel groups][2] GroupNorm sub-partials
   float* s_mean = s_sub + 64;
   float* s_rstd = s_mean + 8;
+  float* s_wsc = s_rstd + 8;     // W8: per-output-channel weight scale of this tile
 
   const int Fg = CONVT ? p.Fin : p.Fout;
   const int Tg = CONVT ? p.Tin : p.Tout;
@@ -144,6 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   }
   if (OUT == OUT_RBOUT && tid < NT) { c_g = p.pre_gamma[cout0 + tid]; c_b = p.pre_beta[cout0 + tid]; }
   const float c_bias = tid < NT ? p.bias[cout0 + tid] : 0.f;
+  const float c_wsc = (W8 && tid < NT) ? p.wscale[cout0 + tid] : 1.f;
 
   // per-thread patch items, computed once: input position (npos = out of range) and mask
   constexpr int ES = (int)sizeof(A);
@@ -262,6 +302,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 #pragma unroll
     for (int k = 0; k < C::WPIECES; ++k) {
       const int i = wv + 4 * k;
+      if (C::WPIECES_ALL % 4 != 0 && i >= C::WPIECES_ALL) break;   // wave-uniform
       __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
                                        (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
     }
@@ -287,6 +328,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     }
   }
   if (tid < NT) s_bias[tid] = c_bias;                 // all visible after the first chunk barrier
+  if (W8 && tid < NT) s_wsc[tid] = c_wsc;
   STAMP(1);
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
@@ -333,7 +375,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         }
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          bfr[cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
+          if constexpr (W8)   // 8-byte units swizzled per row (wimage.h conv8_swz; row base is a multiple of 32)
+            bfr[cb] = w8_frag(sW + (wn * 64 + cb * 32 + r) * C::WROW + ((2 * tap + h) ^ conv8_swz(C::NTAP, r)) * 8);
+          else
+            bfr[cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
 #pragma unroll
         for (int rb = 0; rb < C::RBW; ++rb)
 #pragma unroll
@@ -343,54 +388,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   }
 
   STAMP(40);
-#ifdef GT_EXP_DIRECT_EPI
-  constexpr bool DIRECT = OUT == OUT_STATS && sizeof(A) == 2 && KIND != CONVT4;
-#else
-  constexpr bool DIRECT = false;
-#endif
-  if constexpr (DIRECT) {
-    // ---- epilogue straight from the accumulators (bf16 output, GroupNorm sums): register j of lane
-    // (r, h) is position acc_row(j, h) of the block, channel r -- lanes 0..31 of one register are 32
-    // consecutive channels of one position (64 contiguous bytes): 2-byte buffer stores, no LDS, no
-    // barrier. Positions past T get an out-of-range offset (the store is dropped).
-    __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
-        p.out, (short)0, (int)((long)p.B * p.Fout * p.Tout * p.Cout * 2), 0x00020000);
-    float gsum[2] = {0.f, 0.f}, gsq[2] = {0.f, 0.f};
-    const bool full = t0 + C::TT <= Tg;
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int cl = wn * 64 + cb * 32 + r;
-      const float bco = s_bias[cl];
-#pragma unroll
-      for (int rb = 0; rb < C::RBW; ++rb) {
-        const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
-        const int tcb = t0 + tblk * 32 + 4 * h;                 // + (j&3) + 8(j>>2)
-        const int vbase = (((b * p.Fout + f0 + lrow) * p.Tout + tcb) * p.Cout + cout0 + cl) * 2;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int dj = (j & 3) + 8 * (j >> 2);
-          const float v = acc[rb][cb][j] + bco;
-          const bool ok = full || tcb + dj < Tg;
-          if (ok) { gsum[cb] += v; gsq[cb] += v * v; }
-          const bf16 hv = (bf16)v;
-          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, hv), ro, ok ? vbase : 0x7ff00000,
-                                                dj * p.Cout * 2, 0);
-        }
-      }
-    }
-    // per 8-channel group: sum the 8 channel lanes (xor 1, 2, 4) and the two position halves (xor 32)
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      float sv = gsum[cb], qv = gsq[cb];
-#pragma unroll
-      for (int off = 1; off < 8; off <<= 1) { sv += __shfl_xor(sv, off); qv += __shfl_xor(qv, off); }
-      sv += __shfl_xor(sv, 32); qv += __shfl_xor(qv, 32);
-      if (lane < 32 && (r & 7) == 0) {
-        s_sub[((wv * 2 + cb) * 4 + (r >> 3)) * 2 + 0] = sv;
-        s_sub[((wv * 2 + cb) * 4 + (r >> 3)) * 2 + 1] = qv;
-      }
-    }
-  } else {
   // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
   // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
   // LDS instructions of one wave execute in order, so the transposition only needs its own LDS traffic
@@ -465,8 +462,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         float v[8];
         const f32x4 lo = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8);
         const f32x4 hi = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8 + 4);
+        if (W8) {
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(s_wsc + cl);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(s_wsc + cl + 4);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { v[k] = lo[k] + b0[k]; v[4 + k] = hi[k] + b1[k]; }
+          for (int k = 0; k < 4; ++k) { v[k] = lo[k] * s0[k] + b0[k]; v[4 + k] = hi[k] * s1[k] + b1[k]; }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { v[k] = lo[k] + b0[k]; v[4 + k] = hi[k] + b1[k]; }
+        }
         const long ob = obase[rb][half];
         if (ob >= 0) {
           if (OUT == OUT_STATS) {
@@ -516,9 +520,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
       }
     }
-  }
-  }   // !DIRECT
-  if (OUT == OUT_STATS) {
     STAMP(43);
     __syncthreads();
     STAMP(44);
@@ -548,9 +549,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   STAMP(41);
 }
 
-template <class A, int KIND, int IN, int OUT, int NT>
+template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
-  typedef ConvCfg<A, KIND, IN, OUT, NT> C;
+  typedef ConvCfg<A, KIND, IN, OUT, NT, W8> C;
   const int Fg = (KIND == CONVT4) ? p.Fin : p.Fout;
   const int Tg = (KIND == CONVT4) ? p.Tin : p.Tout;
   if (Fg % C::TF != 0 || p.Cout % NT != 0 || p.Cin_pad % C::CK != 0) return hipErrorInvalidValue;
@@ -559,7 +560,8 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
     return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
   dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
             KIND == CONVT4 ? 4u : 1u);
-  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT>), grid, dim3(256), 0, s, p);
+  if (W8 && !p.wscale) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -578,11 +580,29 @@ static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParam
   return hipErrorNotSupported;
 }
 
+// fp8-weight instantiations (GT_BF16_W8): the 3x3, stride-2 and transposed convs
+template <int NT>
+static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
+  if (kind == CONV3 && om == OUT_STATS) {
+    if (im == IN_INPUT) return launch_t<bf16, CONV3, IN_INPUT, OUT_STATS, NT, 1>(p, s);
+    if (im == IN_MASK) return launch_t<bf16, CONV3, IN_MASK, OUT_STATS, NT, 1>(p, s);
+    if (im == IN_GN) return launch_t<bf16, CONV3, IN_GN, OUT_STATS, NT, 1>(p, s);
+    if (im == IN_PLAIN) return launch_t<bf16, CONV3, IN_PLAIN, OUT_STATS, NT, 1>(p, s);
+  }
+  if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONV3_S2, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
+  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONVT4, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
+  return hipErrorNotSupported;
+}
+
 int conv_gn_nparts(int act_bf16, int F, int T, int Cout) {   // CONV3 tiles: 4 rows x 64 frames x NT channels
   return (F / 4) * ((T + 63) / 64) * (Cout / conv_nt(act_bf16, Cout));
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
+  if (p.wscale) {   // fp8 weight image
+    if (!act_bf16) return hipErrorNotSupported;
+    return conv_nt(1, p.Cout) == 128 ? dispatch_w8<128>(kind, im, om, p, s) : dispatch_w8<64>(kind, im, om, p, s);
+  }
   if (!act_bf16) return dispatch<float, 64>(kind, im, om, p, s);
   return conv_nt(1, p.Cout) == 128 ? dispatch<bf16, 128>(kind, im, om, p, s) : dispatch<bf16, 64>(kind, im, om, p, s);
 }

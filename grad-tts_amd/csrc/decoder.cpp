@@ -143,10 +143,11 @@ struct gt_decoder {
   std::map<std::string, int> index;
   std::vector<std::vector<float>> host;
   std::vector<bool> set;
-  bool dirty[2] = {true, true};
-  void* arena[2] = {nullptr, nullptr};
-  std::map<std::string, void*> dp[2];
-  std::map<std::string, int> cinpad[2];
+  // one packed device arena per compute dtype code (GT_F32, GT_BF16, GT_BF16_W8)
+  bool dirty[3] = {true, true, true};
+  void* arena[3] = {nullptr, nullptr, nullptr};
+  std::map<std::string, void*> dp[3];
+  std::map<std::string, int> cinpad[3];
   float freqs[32];
   // profiling (diagnostics / bench roofline): HIP events around every launch
   bool prof = false;
@@ -180,7 +181,7 @@ static int gn_apply_min_c() {
 
 // pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4], as 4 parity images) into the
 // conv_kernel weight image (wimage.h) in the compute dtype
-void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const std::vector<float>& w,
+void pack_conv(Blob& blob, gt_decoder* d, int dt, int code, const std::string& key, const std::vector<float>& w,
                const std::vector<int64_t>& shp, bool convT) {
   int cin, cout, ntap, npar;
   if (!convT) {
@@ -213,7 +214,91 @@ void pack_conv(Blob& blob, gt_decoder* d, int dt, const std::string& key, const 
     }
   }
   blob.put(key, img.data(), img.size());
-  d->cinpad[dt][key] = W.nchunk * W.ck;
+  d->cinpad[code][key] = W.nchunk * W.ck;
+}
+
+}  // namespace
+
+// e4m3fn (OCP FP8: bias 7, no infinities, 0x7f = NaN, max 448) of a finite float, round to nearest even,
+// saturating at 448 -- the rounding of torch's float8_e4m3fn conversion for in-range values.
+extern "C" uint8_t gt_f32_to_e4m3(float x) {
+  const uint8_t sgn = std::signbit(x) ? 0x80 : 0;
+  const double a = std::fabs((double)x);
+  if (a != a) return 0x7f;
+  if (a < 0.015625) return sgn | (uint8_t)std::nearbyint(a * 512.0);   // subnormals (2^-9 steps); 8 = 2^-6
+  int e;
+  const double m = std::frexp(a, &e);            // a = m * 2^e, m in [0.5, 1)
+  int E = e - 1;
+  int q = (int)std::nearbyint((2.0 * m - 1.0) * 8.0);
+  if (q == 8) { q = 0; ++E; }
+  if (E > 8 || (E == 8 && q == 7)) return sgn | 0x7e;
+  return sgn | (uint8_t)(((E + 7) << 3) | q);
+}
+
+// Per-output-channel e4m3 quantization (GT_BF16_W8): scale[o] = max|w[o,:]| / 448 (1 if the row is zero),
+// q = e4m3(w / scale[o]) in fp32 arithmetic; row o of `rows` is `cols` values at stride `col_stride`
+// starting at o * row_stride.
+extern "C" int gt_quantize_e4m3(const float* w, int64_t rows, int64_t cols, int64_t row_stride, int64_t col_stride,
+                                uint8_t* q, float* scale) {
+  if (!w || !q || !scale || rows < 0 || cols < 0) return GT_ERR_ARG;
+  for (int64_t o = 0; o < rows; ++o) {
+    float amax = 0.f;
+    for (int64_t i = 0; i < cols; ++i) amax = std::max(amax, std::fabs(w[o * row_stride + i * col_stride]));
+    const float sc = amax > 0.f ? amax / 448.0f : 1.0f;
+    scale[o] = sc;
+    for (int64_t i = 0; i < cols; ++i) q[o * row_stride + i * col_stride] = gt_f32_to_e4m3(w[o * row_stride + i * col_stride] / sc);
+  }
+  return GT_OK;
+}
+
+namespace {
+
+// fp8 image (wimage.h conv_wimg8) of a 3x3 [Cout][Cin][3][3] or ConvTranspose [Cin][Cout][4][4] weight,
+// quantized per output channel; the scales go to key + ".s"
+void pack_conv8(Blob& blob, gt_decoder* d, const std::string& key, const std::vector<float>& w,
+                const std::vector<int64_t>& shp, bool convT) {
+  int cin, cout, ntap, npar;
+  if (!convT) {
+    cout = (int)shp[0]; cin = (int)shp[1]; ntap = (int)(shp[2] * shp[3]); npar = 1;
+  } else {
+    cin = (int)shp[0]; cout = (int)shp[1]; ntap = 4; npar = 4;
+  }
+  const int kk = convT ? 16 : ntap;   // kernel taps per (co, ci)
+  std::vector<uint8_t> q(w.size());
+  std::vector<float> sc(cout);
+  if (!convT) gt_quantize_e4m3(w.data(), cout, (int64_t)cin * kk, (int64_t)cin * kk, 1, q.data(), sc.data());
+  else {   // output channel co: elements ci*cout*16 + co*16 + k
+    for (int co = 0; co < cout; ++co) {
+      std::vector<float> row((size_t)cin * 16);
+      for (int ci = 0; ci < cin; ++ci)
+        for (int k = 0; k < 16; ++k) row[(size_t)ci * 16 + k] = w[((size_t)ci * cout + co) * 16 + k];
+      std::vector<uint8_t> qr(row.size());
+      gt_quantize_e4m3(row.data(), 1, (int64_t)row.size(), 0, 1, qr.data(), &sc[co]);
+      for (int ci = 0; ci < cin; ++ci)
+        for (int k = 0; k < 16; ++k) q[((size_t)ci * cout + co) * 16 + k] = qr[(size_t)ci * 16 + k];
+    }
+  }
+  const WImg W = conv_wimg8(ntap, cin, cout);
+  std::vector<uint8_t> img((size_t)npar * W.total, 0);
+  if (!convT) {
+    for (int co = 0; co < cout; ++co)
+      for (int ci = 0; ci < cin; ++ci)
+        for (int t = 0; t < ntap; ++t) img[conv_wimg8_off(W, co, t, ci)] = q[((size_t)co * cin + ci) * ntap + t];
+  } else {
+    const int K[2][2] = {{1, 3}, {0, 2}};   // as pack_conv
+    for (int par = 0; par < 4; ++par) {
+      const int pf = par >> 1, pt = par & 1;
+      for (int co = 0; co < cout; ++co)
+        for (int tap = 0; tap < 4; ++tap) {
+          const int kh = K[pf][tap >> 1], kw = K[pt][tap & 1];
+          for (int ci = 0; ci < cin; ++ci)
+            img[(size_t)par * W.total + conv_wimg8_off(W, co, tap, ci)] = q[(((size_t)ci * cout + co) * 4 + kh) * 4 + kw];
+        }
+    }
+  }
+  blob.put(key, img.data(), img.size());
+  blob.put(key + ".s", sc.data(), sc.size() * 4);
+  d->cinpad[2][key] = W.nchunk * W.ck;
 }
 
 // pack a 3x3 [Cout][Cin][3][3] weight into the conv4 image (wimage.h conv4_wimg_off), bf16
@@ -238,8 +323,10 @@ static bool conv4_enabled() {
   return v;
 }
 
-int prepare(gt_decoder* d, int dt) {
-  if (!d->dirty[dt]) return GT_OK;
+int prepare(gt_decoder* d, int code) {
+  if (!d->dirty[code]) return GT_OK;
+  const int dt = code ? 1 : 0;          // activation dtype: fp32 / bf16
+  const bool w8 = code == GT_BF16_W8;   // fp8 images for the 3x3 / stride-2 / transposed convs
   for (size_t i = 0; i < d->inv.size(); ++i)
     if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
   Blob blob;
@@ -248,13 +335,17 @@ int prepare(gt_decoder* d, int dt) {
     const std::string& k = d->inv[i].name;
     const auto& shp = d->inv[i].dims;
     const auto& w = d->host[i];
-    if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
+    if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
+      pack_conv8(blob, d, k, w, shp, false);
+    } else if (w8 && starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
+      pack_conv8(blob, d, k, w, shp, true);
+    } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
-      pack_conv(blob, d, dt, k, w, shp, false);
+      pack_conv(blob, d, dt, code, k, w, shp, false);
       if (dt && conv4_enabled() && ends_with(k, ".block.0.weight") && shp[1] % 16 == 0)
         pack_conv4(blob, k + ".v4", w, (int)shp[0], (int)shp[1]);
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
-      pack_conv(blob, d, dt, k, w, shp, true);
+      pack_conv(blob, d, dt, code, k, w, shp, true);
     } else if (ends_with(k, "to_qkv.weight")) {
       const int C = (int)shp[1];
       std::vector<float> q(w.begin(), w.begin() + 128 * C);
@@ -290,13 +381,13 @@ int prepare(gt_decoder* d, int dt) {
     blob.put("tb.b", br.data(), br.size() * 4);
   }
   blob.put("freqs", d->freqs, sizeof(d->freqs));
-  if (d->arena[dt]) { (void)hipFree(d->arena[dt]); d->arena[dt] = nullptr; }
-  if (hipMalloc(&d->arena[dt], blob.bytes.size()) != hipSuccess) return fail(GT_ERR_HIP, "hipMalloc(weights) failed");
-  if (hipMemcpy(d->arena[dt], blob.bytes.data(), blob.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
+  if (d->arena[code]) { (void)hipFree(d->arena[code]); d->arena[code] = nullptr; }
+  if (hipMalloc(&d->arena[code], blob.bytes.size()) != hipSuccess) return fail(GT_ERR_HIP, "hipMalloc(weights) failed");
+  if (hipMemcpy(d->arena[code], blob.bytes.data(), blob.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
     return fail(GT_ERR_HIP, "hipMemcpy(weights) failed");
-  d->dp[dt].clear();
-  for (auto& kv : blob.off) d->dp[dt][kv.first] = (uint8_t*)d->arena[dt] + kv.second;
-  d->dirty[dt] = false;
+  d->dp[code].clear();
+  for (auto& kv : blob.off) d->dp[code][kv.first] = (uint8_t*)d->arena[code] + kv.second;
+  d->dirty[code] = false;
   return GT_OK;
 }
 
@@ -348,7 +439,8 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
 // ---------------------------------------------------------------- one U-Net evaluation
 struct Run {
   gt_decoder* d;
-  int dt;
+  int dt;       // activation dtype: 0 fp32, 1 bf16
+  int wi;       // compute dtype code (GT_F32 / GT_BF16 / GT_BF16_W8) = packed arena index
   int B, T;
   hipStream_t s;
   uint8_t* ws;
@@ -379,13 +471,13 @@ struct Run {
     const int taps = kind == CONV1 ? 1 : 9;
     double flop = kind == CONVT4 ? 2.0 * p.Cin * p.Cout * 16 * pin : 2.0 * p.Cin * p.Cout * taps * pout;
     double bytes = (im == IN_INPUT ? pin * p.Cin * 4.0 : pin * p.Cin * es) + pout * p.Cout * es +
-                   (double)p.Cout * (kind == CONVT4 ? 16 : taps) * p.Cin_pad * es * (p.w_bstride ? p.B : 1);
+                   (double)p.Cout * (kind == CONVT4 ? 16 : taps) * p.Cin_pad * (p.wscale ? 1.0 : es) * (p.w_bstride ? p.B : 1);
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
     // "<instantiation as rocprof names it>@<shape>": bench.py aggregates per instantiation
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
-                             ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+                             (p.wscale ? ",w8" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
@@ -394,7 +486,7 @@ struct Run {
   // LDS-DMA pipeline (conv4.hip); everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
     const bool v4 = dt && conv4_enabled() && (im == IN_PLAIN || (im == IN_MASK && mask01)) && p.Cin % 16 == 0 &&
-                    d->dp[dt].count(wkey + ".v4");
+                    d->dp[wi].count(wkey + ".v4");
     if (!v4) {
       conv(CONV3, im, OUT_STATS, p);
       return conv_gn_nparts(dt, p.Fout, p.Tout, p.Cout);
@@ -428,8 +520,14 @@ struct Run {
     }
   }
 
-  void* W(const std::string& k) { return d->dp[dt].at(k); }
-  const float* Fp(const std::string& k) { return (const float*)d->dp[dt].at(k); }
+  void* W(const std::string& k) { return d->dp[wi].at(k); }
+  const float* Fp(const std::string& k) { return (const float*)d->dp[wi].at(k); }
+  // weight image of a conv: its fp8 scales too when the image is fp8 (GT_BF16_W8)
+  void setw(ConvParams& p, const std::string& k) {
+    p.w = W(k);
+    const auto it = d->dp[wi].find(k + ".s");
+    p.wscale = it != d->dp[wi].end() ? (const float*)it->second : nullptr;
+  }
   void* act(int l, int i) { return ws + L.act[l][i]; }
   float* stats() { return (float*)(ws + L.stats) + (size_t)(stat_slot++) * B * L.pmax * 16; }
   int Fl(int l) const { return 80 >> l; }
@@ -458,10 +556,10 @@ struct Run {
     const long count = (long)(Cout / 8) * Fl(lvl) * Tl(lvl);
     {   // block1 conv on x*mask
       ConvParams p = base(lvl, lvl);
-      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block1.block.0.weight");
+      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "block1.block.0.weight");
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
-      p.w = W(k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
+      setw(p, k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
       p.out = pre1; p.out_part = st1;
       if (input) {
         conv(CONV3, IN_INPUT, OUT_STATS, p);
@@ -488,11 +586,11 @@ struct Run {
               [&] { return launch_gn_apply(dt, a, s); });
       }
       ConvParams p = base(lvl, lvl);
-      p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "block2.block.0.weight");
+      p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "block2.block.0.weight");
       p.in0 = pre1; p.C0 = Cout;
       p.gn_part = st1; p.gn_nparts = np1; p.gn_gamma = Fp(k + "block1.block.1.weight"); p.gn_beta = Fp(k + "block1.block.1.bias");
       p.gn_count = count; p.tb = tb + tb_off; p.tb_bstride = tb_bstride;
-      p.w = W(k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
+      setw(p, k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
       p.out = pre2; p.out_part = st2;
       np2 = conv3_stats(apply ? IN_PLAIN : IN_GN, p, k + "block2.block.0.weight");
       tap(k + "pre2", lvl, pre2, Cout);
@@ -500,7 +598,7 @@ struct Run {
     }
     if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);
-      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[dt].at(k + "res_conv.weight");
+      p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "res_conv.weight");
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;
       p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin_input = cin;
       p.w = W(k + "res_conv.weight"); p.bias = Fp(k + "res_conv.bias");
@@ -551,18 +649,18 @@ struct Run {
 
   void downsample(const std::string& k, int lvl, const void* in, int C, void* out) {   // diffusion.py:30-36
     ConvParams p = base(lvl, lvl + 1);
-    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[dt].at(k + "conv.weight");
+    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[wi].at(k + "conv.weight");
     p.in0 = in; p.C0 = C;
-    p.w = W(k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
+    setw(p, k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
     conv(CONV3_S2, IN_MASK, OUT_PLAIN, p);
     tap(k.substr(0, k.size() - 1), lvl + 1, out, C);
   }
 
   void upsample(const std::string& k, int lvl, const void* in, int C, void* out) {     // diffusion.py:21-27
     ConvParams p = base(lvl, lvl - 1);
-    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[dt].at(k + "conv.weight");
+    p.Cin = C; p.Cout = C; p.Cin_pad = d->cinpad[wi].at(k + "conv.weight");
     p.in0 = in; p.C0 = C;
-    p.w = W(k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
+    setw(p, k + "conv.weight"); p.bias = Fp(k + "conv.bias"); p.out = out;
     conv(CONVT4, IN_MASK, OUT_PLAIN, p);
     tap(k.substr(0, k.size() - 1), lvl - 1, out, C);
   }
@@ -605,9 +703,9 @@ struct Run {
     int fnp = 0;
     {
       ConvParams p = base(0, 0);
-      p.Cin = 64; p.Cout = 64; p.Cin_pad = d->cinpad[dt].at("final_block.block.0.weight");
+      p.Cin = 64; p.Cout = 64; p.Cin_pad = d->cinpad[wi].at("final_block.block.0.weight");
       p.in0 = act(0, 0); p.C0 = 64;
-      p.w = W("final_block.block.0.weight"); p.bias = Fp("final_block.block.0.bias");
+      setw(p, "final_block.block.0.weight"); p.bias = Fp("final_block.block.0.bias");
       p.out = act(0, 3); p.out_part = st;
       fnp = conv3_stats(IN_MASK, p, "final_block.block.0.weight");
       tap("final_block.pre", 0, act(0, 3), 64);
@@ -624,7 +722,8 @@ struct Run {
 
 int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_t ws_bytes, int32_t N) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
-  if (dtype != GT_F32 && dtype != GT_BF16) return fail(GT_ERR_ARG, "dtype must be GT_F32 or GT_BF16");
+  if (dtype != GT_F32 && dtype != GT_BF16 && dtype != GT_BF16_W8)
+    return fail(GT_ERR_ARG, "dtype must be GT_F32, GT_BF16 or GT_BF16_W8");
   if (B <= 0 || T <= 0) return fail(GT_ERR_ARG, "B and T must be positive");
   if (T % 4 != 0) return fail(GT_ERR_ARG, "T must be a multiple of 4 (fix_len_compatibility)");
   if (B > 65535 || T > (1 << 20)) return fail(GT_ERR_UNSUPPORTED, "B or T too large");
@@ -664,7 +763,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
 void gt_decoder_destroy(gt_decoder* d) {
   if (!d) return;
   for (auto e : d->pool) (void)hipEventDestroy(e);
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 3; ++i)
     if (d->arena[i]) (void)hipFree(d->arena[i]);
   delete d;
 }
@@ -717,7 +816,7 @@ int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int
   if (numel != sh.numel()) return fail(GT_ERR_PARAM, std::string("numel mismatch for ") + name);
   d->host[it->second].assign(data, data + numel);
   d->set[it->second] = true;
-  d->dirty[0] = d->dirty[1] = true;
+  d->dirty[0] = d->dirty[1] = d->dirty[2] = true;
   return GT_OK;
 }
 
@@ -749,8 +848,9 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
   if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
   if ((rc = prepare(d, dtype))) return rc;
   Run R;
-  R.d = d; R.dt = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream; R.ws = (uint8_t*)workspace;
-  R.L = layout(dtype, B, T, 0);
+  R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
+  R.ws = (uint8_t*)workspace;
+  R.L = layout(R.dt, B, T, 0);
   R.mask = mask; R.mu = mu; R.xt = x; R.spk_s = nullptr;
   R.probe = probe; R.probe_out = probe_out;
   R.mask01 = mask_is_01(R, mask, B, T);
@@ -796,8 +896,9 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
   if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
   if ((rc = prepare(d, dtype))) return rc;
   Run R;
-  R.d = d; R.dt = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream; R.ws = (uint8_t*)workspace;
-  R.L = layout(dtype, B, T, n_timesteps);
+  R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
+  R.ws = (uint8_t*)workspace;
+  R.L = layout(R.dt, B, T, n_timesteps);
   R.mask = mask; R.mu = mu; R.xt = out; R.spk_s = nullptr;
   R.mask01 = mask_is_01(R, mask, B, T);
   R.chk(launch_mask_copy(z, mask, (int)B, 80, (int)T, out, R.s));   // xt = z * mask  (diffusion.py:257)

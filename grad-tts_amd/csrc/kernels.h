@@ -26,6 +26,7 @@ struct ConvParams {
   int mask_in;                                        // conv4: input is x * mask (0/1 mask)
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
+  const float* wscale;                                // non-null: fp8 e4m3 image (conv_wimg8), per-Cout scale
   const float* bias;                                  // [Cout]
   // ---- output
   void* out; float* out_part;                         // OUT_STATS: GroupNorm partials of the output (common.h)

@@ -47,6 +47,39 @@ inline __host__ __device__ long conv_wimg_off(const WImg& w, int co, int tap, in
   return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + (long)tap * w.ckb + (long)k * esz;
 }
 
+// ---- fp8 weight image (GT_BF16_W8: e4m3 weights, bf16 activations) for the 3x3 / strided / transposed
+// convs. Same tiling as above with 1-byte weights and no row pad: row n = NTAP taps x 16 B (16 input
+// channels) = 2*NTAP 8-byte units u = (tap, channels 8h..8h+7), stored at u ^ conv8_swz(NTAP, n).
+// The B fragment is a ds_read_b64: 32 lanes (32 rows, one unit each) per bank group, which must fall on
+// 32 different 8-byte bank units of the 256-B bank row. 3x3 (144-B rows): rows r and r+16 coincide, so
+// rows with bit 4 set swap the two halves of a tap (u ^ 1); 2x2 (64-B rows): rows r, r+4, ..., r+28
+// coincide, so u ^ ((r >> 2) & 7). The slab is a whole number of 1 KiB DMA pieces (9 / 18 for 3x3,
+// 4 / 8 for the 2x2 sub-pixel convs).
+inline __host__ __device__ constexpr int conv8_swz(int ntap, int n) { return ntap == 4 ? (n >> 2) & 7 : (n >> 4) & 1; }
+inline __host__ __device__ constexpr int conv8_wrow(int ntap) { return ntap * 16; }
+inline __host__ __device__ constexpr int conv8_wbytes(int nt, int ntap) { return ((nt * conv8_wrow(ntap) + 1023) / 1024) * 1024; }
+
+inline __host__ __device__ WImg conv_wimg8(int ntap, int cin, int cout) {
+  WImg w;
+  w.nt = conv_nt(1, cout);
+  w.ckb = 16;
+  w.ck = 16;
+  w.ntap = ntap;
+  w.wrow = conv8_wrow(ntap);
+  w.wbytes = conv8_wbytes(w.nt, ntap);
+  w.nchunk = (cin + w.ck - 1) / w.ck;
+  w.nntile = (cout + w.nt - 1) / w.nt;
+  w.total = (long)w.nntile * w.nchunk * w.wbytes;
+  return w;
+}
+
+inline __host__ __device__ long conv_wimg8_off(const WImg& w, int co, int tap, int ci) {
+  const int tile = co / w.nt, n = co - tile * w.nt;
+  const int ch = ci / 16, k = ci & 15;
+  const int unit = (2 * tap + (k >> 3)) ^ conv8_swz(w.ntap, n);
+  return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + unit * 8 + (k & 7);
+}
+
 // ---- conv4 (csrc/conv4.hip) image: per (output-channel tile of NT, 16-channel stage) a slab of
 // [half h (channels 8h..8h+7)][tap][NT output channels] x 16 B, so the LDS-DMA is a straight copy and the
 // MFMA B fragment of lane r (output channel r, half h) is unit (h, tap, r) -- consecutive lanes,

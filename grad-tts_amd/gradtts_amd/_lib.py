@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GRADTTS_LIB", os.path.join(_HERE, "libgradtts.so"))
 
 GT_OK, GT_ERR_ARG, GT_ERR_HIP, GT_ERR_PARAM, GT_ERR_UNSUPPORTED, GT_ERR_WORKSPACE = range(6)
-GT_F32, GT_BF16 = 0, 1
+GT_F32, GT_BF16, GT_BF16_W8 = 0, 1, 2
 
 # (name, restype, argtypes) for every symbol declared in include/gradtts.h
 _c = ctypes
@@ -39,6 +39,9 @@ SIGNATURES = [
                                       _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_decoder_profile_enable", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_profile_read", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_size_t]),
+    ("gt_f32_to_e4m3", _c.c_uint8, [_c.c_float]),
+    ("gt_quantize_e4m3", _c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p,
+                                    _c.c_void_p]),
     ("gt_maximum_path_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64,
                                    _c.c_int64, _c.c_float, _c.c_void_p, _c.c_size_t, _c.c_void_p]),

@@ -11,8 +11,9 @@ Mirrors ``/root/reference/model/diffusion.py``:
 
 The sub-modules are parameter containers only: the whole U-Net (and the whole N-step sampler) runs
 inside the HIP library; there is no PyTorch compute path. Compute dtype is an extension:
-``compute_dtype=torch.float32`` (parity path, default) or ``torch.bfloat16`` (throughput path; fp32
-accumulation, fp32 sampler state).
+``compute_dtype=torch.float32`` (parity path, default), ``torch.bfloat16`` (throughput path; fp32
+accumulation, fp32 sampler state) or ``"bf16_w8"`` (bf16 activations, fp8 e4m3 weights for the 3x3 /
+Downsample / Upsample convs with per-output-channel scales: BASELINE.json config 5).
 """
 from __future__ import annotations
 
@@ -22,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import GT_BF16, GT_F32, check, lib
+from ._lib import GT_BF16, GT_BF16_W8, GT_F32, check, lib
 
 
 class _ParamOnly(torch.nn.Module):
@@ -96,7 +97,9 @@ def _dtype_code(dt):
         return GT_F32
     if dt in (torch.bfloat16, "bf16", "bfloat16", GT_BF16):
         return GT_BF16
-    raise ValueError(f"compute_dtype must be float32 or bfloat16, got {dt}")
+    if dt in ("bf16_w8", "fp8", GT_BF16_W8):
+        return GT_BF16_W8
+    raise ValueError(f"compute_dtype must be float32, bfloat16 or 'bf16_w8', got {dt}")
 
 
 def _stream_ptr(device):

@@ -36,8 +36,12 @@ enum {
 };
 
 /* Compute dtype of the U-Net activations / MFMA operands (accumulation is always fp32;
- * the sampler state x_t, mu, z and outputs are always fp32). */
-enum { GT_F32 = 0, GT_BF16 = 1 };
+ * the sampler state x_t, mu, z and outputs are always fp32).
+ * GT_BF16_W8: bf16 activations with fp8 (OCP e4m3) weights for every 3x3 conv, Downsample and
+ * Upsample (ConvTranspose) -- 90 % of the U-Net's parameters -- quantized per output channel by
+ * gt_quantize_e4m3 when the weights are packed; 1x1, attention and linear weights stay bf16 / fp32
+ * (BASELINE.json config 5). */
+enum { GT_F32 = 0, GT_BF16 = 1, GT_BF16_W8 = 2 };
 
 typedef struct gt_decoder gt_decoder;
 
@@ -89,6 +93,14 @@ int gt_estimator_probe(gt_decoder* dec, int dtype, const float* x, const float* 
  * "bytes": compulsory HBM bytes}, ...] (FLOPs as the reference counts them). */
 int gt_decoder_profile_enable(gt_decoder* dec, int on);
 int gt_decoder_profile_read(gt_decoder* dec, char* json_buf, size_t capacity);
+
+/* fp8 weight quantization used by GT_BF16_W8 (host, no GPU): for each of `rows` output channels o,
+ * scale[o] = max_i |w[o*row_stride + i*col_stride]| / 448 (1 for an all-zero row) and
+ * q[same index] = e4m3(w / scale[o]) (fp32 division, round to nearest even, saturating at 448; the
+ * rounding of torch.Tensor.to(torch.float8_e4m3fn)). gt_f32_to_e4m3 converts one value. */
+uint8_t gt_f32_to_e4m3(float x);
+int gt_quantize_e4m3(const float* w, int64_t rows, int64_t cols, int64_t row_stride, int64_t col_stride, uint8_t* q,
+                     float* scale);
 
 /* Monotonic alignment search.  values: [b, tx_max, ty_max] fp32 (already multiplied by the mask,
  * as maximum_path does before calling the Cython core); t_xs, t_ys: [b] int32 (device);

@@ -155,3 +155,53 @@ def reverse_diffusion(p, z, mask, mu, n_timesteps, spk=None, n_spks=1, beta_min=
 
 def to_torch_params(sd, dtype=torch.float32):
     return {k: torch.as_tensor(v).to(dtype) for k, v in sd.items()}
+
+
+# ---- fp8 weights (BASELINE.json config 5) ----------------------------------------
+# Not in the reference (which is fp32 throughout): the W8 build quantizes the 3x3 convs
+# (``Block.block[0]``, diffusion.py:52), ``Downsample.conv`` (:33) and ``Upsample.conv`` (:24) to OCP
+# e4m3 per output channel. Parity for that mode is "the reference run with the dequantized weights":
+# fp8_params() returns the state dict with those weights replaced by q * scale.
+E4M3_MAX = 448.0
+
+
+def is_fp8_key(key):
+    """The weights the W8 build stores as fp8 (include/gradtts.h GT_BF16_W8)."""
+    return key.endswith(".block.0.weight") or (key.startswith(("downs.", "ups.")) and key.endswith(".3.conv.weight"))
+
+
+def fp8_axis(key):
+    """Output-channel axis: Conv2d [Cout, Cin, kh, kw] -> 0; ConvTranspose2d [Cin, Cout, kh, kw] -> 1."""
+    return 1 if key.startswith("ups.") and key.endswith(".3.conv.weight") else 0
+
+
+def quantize_e4m3(w, axis):
+    """Per-output-channel e4m3: scale = amax / 448 in fp32 (1 for an all-zero channel),
+    q = (w / scale).to(float8_e4m3fn) (round to nearest even). Returns (q as uint8 codes, scale [C])."""
+    w = torch.as_tensor(w, dtype=torch.float32)
+    red = tuple(d for d in range(w.dim()) if d != axis)
+    amax = w.abs().amax(dim=red)
+    scale = torch.where(amax > 0, amax / torch.tensor(E4M3_MAX, dtype=torch.float32), torch.ones_like(amax))
+    shape = [1] * w.dim()
+    shape[axis] = -1
+    q = (w / scale.reshape(shape)).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), scale
+
+
+def dequantize_e4m3(q, scale, axis):
+    shape = [1] * q.dim()
+    shape[axis] = -1
+    return q.view(torch.float8_e4m3fn).to(torch.float32) * scale.reshape(shape)
+
+
+def fp8_params(sd):
+    """State dict as the W8 build sees it: fp8 weights dequantized to fp32, everything else unchanged."""
+    out = {}
+    for k, v in sd.items():
+        v = torch.as_tensor(v, dtype=torch.float32)
+        if is_fp8_key(k):
+            ax = fp8_axis(k)
+            q, s = quantize_e4m3(v, ax)
+            v = dequantize_e4m3(q, s, ax)
+        out[k] = v
+    return out

@@ -136,3 +136,75 @@ def test_bench_shape_deterministic_and_batch_invariant(cdt):
     sub = dec(zc[5:7].contiguous(), mc[5:7].contiguous(), muc[5:7].contiguous(), 3)
     assert torch.equal(y1, y2), (y1 - y2).abs().max().item()
     assert torch.equal(y1[5:7], sub), (y1[5:7] - sub).abs().max().item()
+
+
+# ---- GT_BF16_W8: fp8 e4m3 weights for the 3x3 / Downsample / Upsample convs, bf16 activations
+# (BASELINE.json config 5). Oracle = the reference algorithm run with the dequantized weights
+# (oracle.decoder.fp8_params, whose quantizer is bit-identical to the library's: test_fp8_cpu.py);
+# tolerances are the bf16 ones. The quantization itself moves one estimator call by ~8e-2 and an
+# N = 100 sampler output by ~3e-2 relative to the fp32 weights (synthetic weights).
+W8 = "bf16_w8"
+
+
+@pytest.mark.parametrize("name", EST)
+def test_w8_estimator_matches_oracle_dequantized(name):
+    from oracle import decoder as odec
+    g = load_golden(name)
+    n_spks = int(g["n_spks"])
+    dec, sd = make_decoder(n_spks, int(g["seed_w"]), W8)
+    spk = g["spk"] if n_spks != 1 else None
+    with torch.no_grad():
+        ref = odec.estimator(odec.fp8_params(sd), *(torch.from_numpy(g[k]) for k in ("x", "mask", "mu", "t")),
+                             torch.from_numpy(spk) if spk is not None else None, n_spks).numpy()
+    y = dec.estimator(_cuda(g["x"]), _cuda(g["mask"]), _cuda(g["mu"]), _cuda(g["t"]),
+                      _cuda(spk) if spk is not None else None).cpu().numpy()
+    err = rel_err(y, ref)
+    assert err <= BF16_EST_TOL, f"{name}: rel err {err:.3e}"
+
+
+def test_w8_every_stage_matches_oracle_dequantized():
+    from oracle import decoder as odec
+    g = load_golden("estimator_s1_T132.npz")
+    dec, sd = make_decoder(1, 0, W8)
+    taps = {}
+    with torch.no_grad():
+        odec.estimator(odec.fp8_params(sd), torch.from_numpy(g["x"]), torch.from_numpy(g["mask"]),
+                       torch.from_numpy(g["mu"]), torch.from_numpy(g["t"]), None, taps=taps)
+    args = [_cuda(g[k]) for k in ("x", "mask", "mu", "t")]
+    bad = []
+    for st in STAGES:
+        ref = taps[st].numpy()
+        _, pr = probe(dec.estimator, W8, *args, None, st, ref.shape)
+        e = rel_err(pr.cpu().numpy(), ref)
+        if not e <= BF16_EST_TOL:
+            bad.append(f"{st}: {e:.3e}")
+    assert not bad, "stage mismatches: " + ", ".join(bad)
+
+
+def test_w8_sampler_N1000_matches_oracle_dequantized():
+    """Config 5's step count (n_timesteps = 1000) on a small ragged batch the CPU oracle finishes in ~1 min."""
+    from oracle import decoder as odec
+    from gradtts_amd.params import synthetic_inputs
+    dec, sd = make_decoder(1, 0, W8)
+    mu, z, mask, _ = synthetic_inputs(11, 2, 16, lengths=[16, 12])
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref = odec.reverse_diffusion(odec.fp8_params(sd), torch.from_numpy(z), torch.from_numpy(mask),
+                                 torch.from_numpy(mu), 1000).numpy()
+    y = dec(_cuda(z), _cuda(mask), _cuda(mu), 1000).cpu().numpy()
+    err = rel_err(y, ref)
+    assert err <= BF16_REV_TOL, f"rel err {err:.3e}"
+
+
+def test_w8_bench_shape_deterministic_and_batch_invariant():
+    from gradtts_amd.params import synthetic_inputs
+    dec, _ = make_decoder(1, 0, W8)
+    mu, z, mask, _ = synthetic_inputs(1234, 32, 512)
+    zc, mc, muc = _cuda(z), _cuda(mask), _cuda(mu)
+    y1 = dec(zc, mc, muc, 3)
+    y2 = dec(zc, mc, muc, 3)
+    assert torch.isfinite(y1).all()
+    sub = dec(zc[5:7].contiguous(), mc[5:7].contiguous(), muc[5:7].contiguous(), 3)
+    assert torch.equal(y1, y2) and torch.equal(y1[5:7], sub)
+    dec.compute_dtype = torch.bfloat16
+    y16 = dec(zc, mc, muc, 3)
+    assert rel_err(y1.cpu().numpy(), y16.cpu().numpy()) <= 0.1   # quantization moves it, but not far
