@@ -11,8 +11,10 @@ per GPU, T = 512 frames, N = 50, bf16 compute. With N GPUs every rank decodes it
 (weak scaling: the 8-GPU run is config 4, 256 utterances), ``value`` = all frames / max-rank time.
 
 Printed (rank 0, one JSON line): the driver contract fields plus
-  roofline      the dominant kernel's achieved algorithmic TFLOP/s vs the bf16 dense MFMA peak,
-                measured live with HIP events around every launch during the timed steps;
+  roofline      the dominant kernel's achieved algorithmic TFLOP/s vs the bf16 dense MFMA peak, measured
+                live with a HIP event pair around each of its launches during the timed steps (the other
+                launches run without events: an event pair on every launch costs ~11 % of the step);
+  kernels/shapes per-kernel tables from the warm-up steps, which have events on every launch;
   cpu_baseline  the oracle CPU restatement (oracle/decoder.py, "port") timed on this host for a bounded
                 sample (one Euler step of a smaller batch at the same T), projected to mel-frames/s.
 """
@@ -122,11 +124,31 @@ def main():
     L = _lib.lib()
     handle = dec.estimator._native(dec.beta_min, dec.beta_max)
     buf = ctypes.create_string_buffer(1 << 20)
-    L.gt_decoder_profile_enable(handle, 1)    # warm-up runs profiled too, so the event pool is allocated
+
+    def aggregate(entries):   # "<kernel>@<shape>" entries -> per kernel instantiation
+        agg = {}
+        for e in entries:
+            k = e["kernel"].split("@")[0]
+            a = agg.setdefault(k, {"kernel": k, "ms": 0.0, "launches": 0, "flop": 0.0, "bytes": 0.0})
+            for f in ("ms", "launches", "flop", "bytes"):
+                a[f] += e[f]
+        return list(agg.values())
+
+    # Warm-up steps run with a HIP event pair around every launch: the per-kernel tables and the choice of
+    # the dominant kernel come from them. The timed steps keep events on the dominant kernel's launches
+    # only (each event pair costs stream time: events on every launch slow the whole decode by ~11 %).
+    L.gt_decoder_profile_enable(handle, 1)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     _lib.check(L.gt_decoder_profile_read(handle, buf, len(buf)), "gt_decoder_profile_read")
+    shapes = json.loads(buf.value.decode())
+    table_steps = args.warmup
+    prof = aggregate(shapes)
+    conv = [p for p in prof if p["kernel"].startswith("conv_kernel")]
+    dom_name = max(conv, key=lambda p: p["ms"])["kernel"] if conv else None
+    if dom_name:
+        L.gt_decoder_profile_filter(handle, (dom_name + "@").encode())
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -138,15 +160,12 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     L.gt_decoder_profile_enable(handle, 0)
+    L.gt_decoder_profile_filter(handle, None)
     _lib.check(L.gt_decoder_profile_read(handle, buf, len(buf)), "gt_decoder_profile_read")
-    shapes = json.loads(buf.value.decode())      # per "<kernel>@<shape>" entries
-    prof = {}
-    for e in shapes:
-        k = e["kernel"].split("@")[0]
-        a = prof.setdefault(k, {"kernel": k, "ms": 0.0, "launches": 0, "flop": 0.0, "bytes": 0.0})
-        for f in ("ms", "launches", "flop", "bytes"):
-            a[f] += e[f]
-    prof = list(prof.values())
+    timed = aggregate(json.loads(buf.value.decode()))
+    if not dom_name:   # no warm-up: every launch of the timed steps was profiled
+        shapes, prof, table_steps = json.loads(buf.value.decode()), timed, args.steps
+        dom_name = max([p for p in timed if p["kernel"].startswith("conv_kernel")], key=lambda p: p["ms"])["kernel"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -159,8 +178,7 @@ def main():
         frames = world * B * T
         value = frames / sec
         flop_step = N * estimator_flops(B, T, args.n_spks)
-        conv = [p for p in prof if p["kernel"].startswith("conv_kernel")]
-        dom = max(conv, key=lambda p: p["ms"])
+        dom = next(p for p in timed if p["kernel"] == dom_name)   # events inside the timed region
         avg_s = dom["ms"] / dom["launches"] / 1e3
         achieved = dom["flop"] / dom["launches"] / avg_s
         total_kernel_ms = sum(p["ms"] for p in prof)
@@ -184,18 +202,21 @@ def main():
                          "frac": achieved / PEAK[args.dtype], "avg_launch_us": avg_s * 1e6,
                          "flop_per_launch": dom["flop"] / dom["launches"],
                          "traffic": pmc_traffic(dom["kernel"]),
-                         "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"]},
+                         "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
+                         "timing": "HIP event pair around each launch of this kernel during the timed steps"},
+            "tables_from": (f"{table_steps} warm-up step(s)" if table_steps == args.warmup else "the timed steps")
+                           + " with events on every launch",
             "kernels": {p["kernel"]: {"share": round(p["ms"] / total_kernel_ms, 4),
                                       "avg_us": round(p["ms"] / p["launches"] * 1e3, 2),
-                                      "per_step": p["launches"] // args.steps,
+                                      "per_step": p["launches"] // table_steps,
                                       "tflops": round(p["flop"] / (p["ms"] * 1e-3) / 1e12, 1) if p["flop"] else None,
                                       "gbps": round(p["bytes"] / (p["ms"] * 1e-3) / 1e9, 0) if p["bytes"] else None}
                         for p in sorted(prof, key=lambda p: -p["ms"])[:14]},
             "shapes": {e["kernel"]: {"avg_us": round(e["ms"] / e["launches"] * 1e3, 2),
-                                     "per_step": e["launches"] // args.steps,
+                                     "per_step": e["launches"] // table_steps,
                                      "tflops": round(e["flop"] / (e["ms"] * 1e-3) / 1e12, 1)}
                        for e in sorted(shapes, key=lambda e: -e["ms"]) if "@" in e["kernel"]},
-            "kernel_busy_frac": total_kernel_ms / args.steps / 1e3 / sec,
+            "kernel_busy_frac": total_kernel_ms / table_steps / 1e3 / sec,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, sd)

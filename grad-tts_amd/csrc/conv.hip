@@ -242,7 +242,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, voff[j], (c0 - p.C0) * ES, 0);
     }
   };
+#ifdef GT_EXP_EARLY_GN
+  constexpr bool EARLY = IN == IN_GN;   // transform in registers during the previous chunk's MFMAs
+#else
+  constexpr bool EARLY = false;
+#endif
+  auto transform_patch = [&](int c0) {
+    float sc[C::ICH], sh[C::ICH], tb[C::ICH];
+#pragma unroll
+    for (int k = 0; k < C::ICH; ++k) {
+      const int c = c0 + sub * C::ICH + k;
+      sc[k] = s_sc[c]; sh[k] = s_sh[c]; tb[k] = s_tb[c];
+    }
+#pragma unroll
+    for (int j = 0; j < C::PPT; ++j) {
+      if (tid + 256 * j < C::PITEMS) {
+        const float m = pm[j];
+        float v[C::ICH];
+        const u32x4 u = preg[j];
+        item_to_f(make_uint4(u[0], u[1], u[2], u[3]), v, A());
+#pragma unroll
+        for (int k = 0; k < C::ICH; ++k) v[k] = (mishf(v[k] * sc[k] + sh[k]) + tb[k]) * m;
+        const uint4 o = f_to_item(v, A());
+        preg[j] = u32x4{o.x, o.y, o.z, o.w};
+      }
+    }
+  };
   auto store_patch = [&](int c0) {
+    if (EARLY) {
+      if (c0 == 0) transform_patch(0);
+#pragma unroll
+      for (int j = 0; j < C::PPT; ++j) {
+        const int it = tid + 256 * j;
+        if (it < C::PITEMS) *reinterpret_cast<u32x4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = preg[j];
+      }
+      return;
+    }
     float sc[C::ICH], sh[C::ICH], tb[C::ICH];
     if (IN == IN_GN) {
 #pragma unroll
@@ -351,6 +386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     }
 #pragma unroll
     for (int tap = 0; tap < C::NTAP; ++tap) {
+      if (EARLY && tap == C::NTAP / 2 && ch + 1 < nchunk) transform_patch(c0 + C::CK);
       int dr, dc;
       if (CONVT) {
         // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0,

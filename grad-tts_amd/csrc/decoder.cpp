@@ -151,6 +151,7 @@ struct gt_decoder {
   float freqs[32];
   // profiling (diagnostics / bench roofline): HIP events around every launch
   bool prof = false;
+  std::string prof_prefix;   // non-empty: only launches whose "<kernel>@<shape>" name starts with it
   struct Rec { std::string kernel; double flop, bytes; hipEvent_t e0, e1; };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
@@ -456,7 +457,10 @@ struct Run {
 
   template <class Fn>
   void timed(const std::string& kernel, double flop, double bytes, Fn&& fn) {
-    if (!d->prof) { chk(fn()); return; }
+    if (!d->prof || (!d->prof_prefix.empty() && kernel.compare(0, d->prof_prefix.size(), d->prof_prefix) != 0)) {
+      chk(fn());
+      return;
+    }
     hipEvent_t e0 = d->ev(), e1 = d->ev();
     if (e0) chk(hipEventRecord(e0, s));
     chk(fn());
@@ -771,6 +775,12 @@ void gt_decoder_destroy(gt_decoder* d) {
 int gt_decoder_profile_enable(gt_decoder* d, int on) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
   d->prof = on != 0;
+  return GT_OK;
+}
+
+int gt_decoder_profile_filter(gt_decoder* d, const char* prefix) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  d->prof_prefix = prefix ? prefix : "";
   return GT_OK;
 }
 

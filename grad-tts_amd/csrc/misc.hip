@@ -15,12 +15,26 @@
 
 namespace gt {
 
-constexpr int FIN_PPT = 1;   // positions per thread (more per thread exposes the 128-B load latency)
 template <class A>
 __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
   __shared__ float s_sc[64], s_sh[64], s_w[64], s_mean[8], s_rstd[8];
   __shared__ double s_red[272];
   const int b = blockIdx.y, tid = threadIdx.x;
+  constexpr int ICH = Act<A>::kItemCh;
+  const int npos = 80 * p.T;
+  // this thread's position: pre-activation, mask, x_t and mu loads go out before the GroupNorm reduction
+  const int idx = blockIdx.x * 256 + tid;                    // position within [80][T]
+  const bool live = idx < npos;
+  const long o = (long)b * npos + idx;
+  uint4 u[64 / ICH];
+  float m = 0.f, x = 0.f, mu = 0.f;
+  if (live) {
+    const A* pre = reinterpret_cast<const A*>(p.pre) + o * 64;
+#pragma unroll
+    for (int it = 0; it < 64 / ICH; ++it) u[it] = reinterpret_cast<const uint4*>(pre)[it];
+    m = p.mask[(long)b * p.T + idx % p.T];
+    if (p.euler) { x = p.xt[o]; mu = p.mu[o]; }
+  }
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   if (tid < 64) {
     float sc, sh;
@@ -28,18 +42,8 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
     s_sc[tid] = sc; s_sh[tid] = sh; s_w[tid] = p.wf[tid];
   }
   __syncthreads();
-  constexpr int ICH = Act<A>::kItemCh;
-  const int npos = 80 * p.T;
-#pragma unroll 1
-  for (int j = 0; j < FIN_PPT; ++j) {
-    const int idx = (blockIdx.x * FIN_PPT + j) * 256 + tid;   // position within [80][T]
-    if (idx >= npos) return;
-    const int t = idx % p.T;
-    const float m = p.mask[(long)b * p.T + t];
-    const A* pre = reinterpret_cast<const A*>(p.pre) + ((long)b * npos + idx) * 64;
-    uint4 u[64 / ICH];
-#pragma unroll
-    for (int it = 0; it < 64 / ICH; ++it) u[it] = reinterpret_cast<const uint4*>(pre)[it];
+  {
+    if (!live) return;
     float acc = 0.f;
 #pragma unroll
     for (int it = 0; it < 64 / ICH; ++it) {
@@ -53,12 +57,10 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
       }
     }
     const float s = (acc + p.bf[0]) * m;                       // (output * mask).squeeze(1)
-    const long o = (long)b * npos + idx;
     if (!p.euler) {
       p.out[o] = s;
     } else {
-      const float x = p.xt[o];
-      float dxt = 0.5f * ((p.mu[o] - x) - s);
+      float dxt = 0.5f * ((mu - x) - s);
       dxt = dxt * p.beta_t;
       dxt = dxt * p.hstep;
       p.xt[o] = (x - dxt) * m;
@@ -76,36 +78,43 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   __shared__ float s_mean[8], s_rstd[8];
   __shared__ double s_red[272];
   const int b = blockIdx.y, tid = threadIdx.x;
-  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   constexpr int ICH = Act<A>::kItemCh;
   const int total = p.F * p.T * p.C;                       // elements of one utterance
   const int e0 = (blockIdx.x * RB_IPT * 256 + tid) * ICH;
   const int c0 = e0 % p.C;
+  const long ub = (long)b * total;
+  const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
+  const A* xin = reinterpret_cast<const A*>(APPLY ? p.pre : p.x) + ub;
+  A* out = reinterpret_cast<A*>(p.out) + ub;
+  // Data and mask loads go out first; the GroupNorm reduction (its own loads + LDS barriers) overlaps them.
+  // Item i is position pos0 + i * pstep (C divides the 256-item block stride): frame index by increments.
+  const int pstep = 256 * ICH / p.C;
+  int t = (e0 / p.C) % p.T;
+  uint4 vp[RB_IPT], vx[RB_IPT];
+  float mk[RB_IPT];
+#pragma unroll
+  for (int i = 0; i < RB_IPT; ++i) {
+    const int e = e0 + i * 256 * ICH;
+    if (e < total) {
+      vp[i] = *reinterpret_cast<const uint4*>(pre + e);
+      if (!APPLY) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
+      mk[i] = mask_at(p.mask, p.T0, b, t, p.lvl);
+    }
+    t += pstep;
+    while (t >= p.T) t -= p.T;
+  }
+  gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   float sc[ICH], sh[ICH], tb[ICH];
 #pragma unroll
   for (int k = 0; k < ICH; ++k) {
     gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
     tb[k] = APPLY ? p.tb[(long)b * p.tb_bstride + c0 + k] : 0.f;
   }
-  const long ub = (long)b * total;
-  const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
-  const A* xin = reinterpret_cast<const A*>(APPLY ? p.pre : p.x) + ub;
-  A* out = reinterpret_cast<A*>(p.out) + ub;
-  uint4 vp[RB_IPT], vx[RB_IPT];
-#pragma unroll
-  for (int i = 0; i < RB_IPT; ++i) {                        // all loads in flight first
-    const int e = e0 + i * 256 * ICH;
-    if (e < total) {
-      vp[i] = *reinterpret_cast<const uint4*>(pre + e);
-      if (!APPLY) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
-    }
-  }
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
     const int e = e0 + i * 256 * ICH;
     if (e < total) {
-      const int t = (e / p.C) % p.T;
-      const float m = mask_at(p.mask, p.T0, b, t, p.lvl);
+      const float m = mk[i];
       float v[ICH];
       item_to_f(vp[i], v, A());
       if (APPLY) {
@@ -198,7 +207,7 @@ hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, in
 }
 
 hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s) {
-  dim3 grid((unsigned)((80L * p.T + 256 * FIN_PPT - 1) / (256 * FIN_PPT)), (unsigned)p.B);
+  dim3 grid((unsigned)((80L * p.T + 255) / 256), (unsigned)p.B);
   if (act_bf16) hipLaunchKernelGGL(final_kernel<bf16>, grid, dim3(256), 0, s, p);
   else hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), 0, s, p);
   return hipGetLastError();

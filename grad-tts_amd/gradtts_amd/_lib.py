@@ -39,6 +39,7 @@ SIGNATURES = [
                                       _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_decoder_profile_enable", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_profile_read", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_size_t]),
+    ("gt_decoder_profile_filter", _c.c_int, [_c.c_void_p, _c.c_char_p]),
     ("gt_f32_to_e4m3", _c.c_uint8, [_c.c_float]),
     ("gt_quantize_e4m3", _c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p,
                                     _c.c_void_p]),

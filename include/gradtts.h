@@ -93,6 +93,10 @@ int gt_estimator_probe(gt_decoder* dec, int dtype, const float* x, const float* 
  * "bytes": compulsory HBM bytes}, ...] (FLOPs as the reference counts them). */
 int gt_decoder_profile_enable(gt_decoder* dec, int on);
 int gt_decoder_profile_read(gt_decoder* dec, char* json_buf, size_t capacity);
+/* Restrict profiling to launches whose "<kernel>@<shape>" name starts with `prefix` (NULL or "" = all).
+ * Each event pair costs a few microseconds of stream time, so bench.py times its steps with events on
+ * one kernel instantiation only. */
+int gt_decoder_profile_filter(gt_decoder* dec, const char* prefix);
 
 /* fp8 weight quantization used by GT_BF16_W8 (host, no GPU): for each of `rows` output channels o,
  * scale[o] = max_i |w[o*row_stride + i*col_stride]| / 448 (1 for an all-zero row) and
