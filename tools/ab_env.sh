@@ -5,7 +5,7 @@ mkdir -p gpurun_out/var
 for spec in "$@"; do
   label=${spec%%:*}; rest=${spec#*:}
   if [[ $label == lib ]]; then label=$rest; envs="GRADTTS_LIB=$PWD/ab/$rest/libgradtts.so"; else envs=$rest; fi
-  env $envs GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --n-timesteps 10 > gpurun_out/var/$label.json 2> gpurun_out/var/$label.err
+  env $envs GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 2 --n-timesteps 10 > gpurun_out/var/$label.json 2> gpurun_out/var/$label.err
   rc=$?; echo "$label rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/var/$label.err; exit $rc; }
 done
 python3 - "$@" <<'PY'

@@ -3,7 +3,7 @@
 mkdir -p gpurun_out/var
 for v in "$@"; do
   if [ "$v" = "tree" ]; then unset GRADTTS_LIB; else export GRADTTS_LIB=$PWD/ab/$v/libgradtts.so; fi
-  GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 --n-timesteps 10 $BENCH_ARGS > gpurun_out/var/$v.json 2> gpurun_out/var/$v.err
+  GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 2 --n-timesteps 10 $BENCH_ARGS > gpurun_out/var/$v.json 2> gpurun_out/var/$v.err
   rc=$?; echo "$v rc=$rc"
   case $rc in 0) ;; *) tail -3 gpurun_out/var/$v.err; exit $rc;; esac
 done
