@@ -59,18 +59,17 @@ __device__ unsigned int g_stamp_hwid[ST_WGS];
 #define GT_CAP_3W8 3
 #endif
 
-template <class A, int KIND, int IN, int OUT, int NT, int W8>
+template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 struct ConvCfg {
   static constexpr bool CONVT = KIND == CONVT4;
   static constexpr int KS = (KIND == CONV1) ? 1 : 3;
   static constexpr int S = (KIND == CONV3_S2) ? 2 : 1;
-  static constexpr int TF = 4;
+  static constexpr int TF = TF_;
   static constexpr int TT = (KIND == CONV3_S2) ? 32 : 64;
   static constexpr int RBT = TT / 32;
   static constexpr int WN = NT / 64;
   static constexpr int WM = 4 / WN;
-  static constexpr int RW = TF / WM;
-  static constexpr int RBW = RW * RBT;
+  static constexpr int RBW = TF * RBT / WM;   // 32-position row blocks per wave: wave wm owns blocks wm*RBW ..
   static constexpr int NTAP = CONVT ? 4 : KS * KS;
   static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
   static constexpr int PR = (TF - 1) * S + KS;
@@ -101,6 +100,7 @@ struct ConvCfg {
                            : KIND == CONV3_S2 ? GT_CAP_S2 : (W8 ? GT_CAP_3W8 : GT_CAP_3);
   static constexpr int SMEM = (CAP && SMEM0 <= 160 * 1024 / (CAP + 1)) ? 160 * 1024 / (CAP + 1) + 512 : SMEM0;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
+  static_assert(TF * RBT % WM == 0, "row blocks split evenly over the waves");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
   static_assert(WBYTES % 1024 == 0, "whole DMA pieces");
   static_assert(!W8 || (sizeof(A) == 2 && KIND != CONV1), "fp8 weights: bf16 operands, 3x3 / 2x2 convs");
@@ -120,10 +120,10 @@ GT_DEV bf16x8 w8_frag(const char* src) {
   return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
-template <class A, int KIND, int IN, int OUT, int NT, int W8>
+template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 // 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
-  typedef ConvCfg<A, KIND, IN, OUT, NT, W8> C;
+  typedef ConvCfg<A, KIND, IN, OUT, NT, W8, TF_> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
 
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         frag af[C::RBW], bfr[2];
 #pragma unroll
         for (int rb = 0; rb < C::RBW; ++rb) {
-          const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+          const int blk = wm * C::RBW + rb, lrow = blk / C::RBT, tblk = blk % C::RBT;
           const int prow = lrow * C::S + dr;
           const int pcol = (tblk * 32 + r) * C::S + dc;
           af[rb] = Mma<A>::load(sA + (prow * C::PC + pcol) * C::POSB + koff);
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   float om[C::RBW][2];
 #pragma unroll
   for (int rb = 0; rb < C::RBW; ++rb) {
-    const int lrow = wm * C::RW + rb / C::RBT, tblk = rb % C::RBT;
+    const int blk = wm * C::RBW + rb, lrow = blk / C::RBT, tblk = blk % C::RBT;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int tc = t0 + tblk * 32 + (lane >> 2) + 16 * half;
@@ -585,9 +585,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   STAMP(41);
 }
 
-template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0>
+template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0, int TF_ = 4>
+static hipError_t launch_t(const ConvParams& p, hipStream_t s);
+
+// 3x3 launch with the tile height conv_tf picks (5 rows only exists for 128-wide tiles)
+template <class A, int IN, int NT, int W8>
+static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
+  if constexpr (NT == 128 && IN != IN_GN && IN != IN_INPUT)
+    if (conv_tf(CONV3, IN, NT, p.Cout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
+  return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
+}
+
+template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
-  typedef ConvCfg<A, KIND, IN, OUT, NT, W8> C;
+  typedef ConvCfg<A, KIND, IN, OUT, NT, W8, TF_> C;
   const int Fg = (KIND == CONVT4) ? p.Fin : p.Fout;
   const int Tg = (KIND == CONVT4) ? p.Tin : p.Tout;
   if (Fg % C::TF != 0 || p.Cout % NT != 0 || p.Cin_pad % C::CK != 0) return hipErrorInvalidValue;
@@ -597,7 +608,7 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
             KIND == CONVT4 ? 4u : 1u);
   if (W8 && !p.wscale) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8, TF_>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -605,9 +616,9 @@ template <class A, int NT>
 static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   // Instantiated combinations (the U-Net uses exactly these):
   if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_t<A, CONV3, IN_INPUT, OUT_STATS, NT>(p, s);
-  if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_t<A, CONV3, IN_MASK, OUT_STATS, NT>(p, s);
-  if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_t<A, CONV3, IN_GN, OUT_STATS, NT>(p, s);
-  if (kind == CONV3 && im == IN_PLAIN && om == OUT_STATS) return launch_t<A, CONV3, IN_PLAIN, OUT_STATS, NT>(p, s);
+  if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_c3<A, IN_MASK, NT, 0>(p, s);
+  if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_c3<A, IN_GN, NT, 0>(p, s);
+  if (kind == CONV3 && im == IN_PLAIN && om == OUT_STATS) return launch_c3<A, IN_PLAIN, NT, 0>(p, s);
   if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_t<A, CONV1, IN_INPUT, OUT_RBOUT, NT>(p, s);
   if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_t<A, CONV1, IN_MASK, OUT_RBOUT, NT>(p, s);
   if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_t<A, CONV1, IN_PLAIN, OUT_RESID, NT>(p, s);
@@ -621,17 +632,18 @@ template <int NT>
 static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   if (kind == CONV3 && om == OUT_STATS) {
     if (im == IN_INPUT) return launch_t<bf16, CONV3, IN_INPUT, OUT_STATS, NT, 1>(p, s);
-    if (im == IN_MASK) return launch_t<bf16, CONV3, IN_MASK, OUT_STATS, NT, 1>(p, s);
-    if (im == IN_GN) return launch_t<bf16, CONV3, IN_GN, OUT_STATS, NT, 1>(p, s);
-    if (im == IN_PLAIN) return launch_t<bf16, CONV3, IN_PLAIN, OUT_STATS, NT, 1>(p, s);
+    if (im == IN_MASK) return launch_c3<bf16, IN_MASK, NT, 1>(p, s);
+    if (im == IN_GN) return launch_c3<bf16, IN_GN, NT, 1>(p, s);
+    if (im == IN_PLAIN) return launch_c3<bf16, IN_PLAIN, NT, 1>(p, s);
   }
   if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONV3_S2, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
   if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONVT4, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
   return hipErrorNotSupported;
 }
 
-int conv_gn_nparts(int act_bf16, int F, int T, int Cout) {   // CONV3 tiles: 4 rows x 64 frames x NT channels
-  return (F / 4) * ((T + 63) / 64) * (Cout / conv_nt(act_bf16, Cout));
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout) {   // CONV3 tiles: TF rows x 64 frames x NT
+  const int nt = conv_nt(act_bf16, Cout);
+  return (F / conv_tf(CONV3, im, nt, Cout)) * ((T + 63) / 64) * (Cout / nt);
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {

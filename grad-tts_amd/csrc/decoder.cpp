@@ -481,7 +481,7 @@ struct Run {
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
-                             (p.wscale ? ",w8" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+                             (p.wscale ? ",w8" : "") + (dt && conv_tf(kind, im, nt, p.Cout) == 5 ? ",tf5" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
@@ -493,7 +493,7 @@ struct Run {
                     d->dp[wi].count(wkey + ".v4");
     if (!v4) {
       conv(CONV3, im, OUT_STATS, p);
-      return conv_gn_nparts(dt, p.Fout, p.Tout, p.Cout);
+      return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
     }
     const Conv4Cfg c = conv4_pick(p.Cout);
     p.w = W(wkey + ".v4");
@@ -567,7 +567,7 @@ struct Run {
       p.out = pre1; p.out_part = st1;
       if (input) {
         conv(CONV3, IN_INPUT, OUT_STATS, p);
-        np1 = conv_gn_nparts(dt, Fl(lvl), Tl(lvl), Cout);
+        np1 = conv_gn_nparts(dt, IN_INPUT, Fl(lvl), Tl(lvl), Cout);
       } else {
         np1 = conv3_stats(IN_MASK, p, k + "block1.block.0.weight");
       }

@@ -35,7 +35,7 @@ struct ConvParams {
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid
-int conv_gn_nparts(int act_bf16, int F, int T, int Cout);
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout);
 
 struct AttnKVParams {
   const void* x; int B, n, C, Cpad;   // x: [B][n][C] (n = F*T)

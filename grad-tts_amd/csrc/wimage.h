@@ -14,6 +14,17 @@ namespace gt {
 
 // output channels per workgroup: 128 for bf16 layers with >= 128 output channels, else 64
 inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { return (act_bf16 && cout >= 128) ? 128 : 64; }
+// 3x3 tiles with 256+ output channels (two 128-wide channel tiles) and no operand transform cover 5 mel rows
+// (320 positions): every level's row count (80 >> l) divides by 5, and at B = 32 the level-2 grid becomes one
+// whole round of 2 workgroups per CU (512 tiles instead of 640). The GroupNorm-input variant keeps 4 rows (the
+// extra accumulators spill there), as do 128-output convs (256 tiles would leave half the slots empty).
+#ifndef GT_TF5
+#define GT_TF5 1
+#endif
+// mel rows per 3x3 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels)
+inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout) {
+  return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 && cout >= 256 && im != 2 /*IN_GN*/) ? 5 : 4;
+}
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
 inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }

@@ -28,8 +28,8 @@ def norm(name: str) -> str:
         base = m.group(2)[: int(m.group(1))]
         ty = "bf16" if m.group(3) == "DF16b" else "float"
         ints = re.findall(r"Li(-?\d+)E", m.group(4))
-        if base == "conv_kernel" and len(ints) == 5:   # trailing W8 flag: bench names "...,w8>" / nothing
-            ints = ints[:4] + (["w8"] if ints[4] == "1" else [])
+        if base == "conv_kernel" and len(ints) == 6:   # trailing W8 flag and tile rows: "...,w8,tf5>" / nothing
+            ints = ints[:4] + (["w8"] if ints[4] == "1" else []) + (["tf5"] if ints[5] == "5" else [])
         return f"{base}<{','.join([ty] + ints)}>"
     m = re.match(r"(?:void )?gt::(\w+)(<[^(]*>)?\(", name)
     if m:
