@@ -315,11 +315,36 @@ void pack_conv4(Blob& blob, const std::string& key, const std::vector<float>& w,
   blob.put(key, img.data(), img.size());
 }
 
+// pack a 64->64 3x3 [Cout][Cin][3][3] weight in conv64's register-fragment order (conv64.hip), bf16:
+// [cb 2][chunk 4][tap 9][lane 64][8 ci]: lane (r, h) = output channel cb*32 + r, input channels 16 chunk + 8h .. +7
+void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w) {
+  std::vector<uint16_t> img((size_t)2 * 4 * 9 * 64 * 8);
+  size_t i = 0;
+  for (int cb = 0; cb < 2; ++cb)
+    for (int ch = 0; ch < 4; ++ch)
+      for (int tap = 0; tap < 9; ++tap)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int k = 0; k < 8; ++k) {
+            const int co = cb * 32 + (lane & 31), ci = ch * 16 + (lane >> 5) * 8 + k;
+            img[i++] = f2bf(w[((size_t)co * 64 + ci) * 9 + tap]);
+          }
+  blob.put(key, img.data(), img.size() * 2);
+}
+
 // conv4 (LDS-DMA pipeline) for the bf16 3x3 stride-1 convs: GT_CONV4=1 selects it instead of conv_kernel
 static bool conv4_enabled() {
   static const bool v = [] {
     const char* e = getenv("GT_CONV4");
     return e && atoi(e) != 0;   // experimental LDS-DMA pipeline (conv4.hip), off by default
+  }();
+  return v;
+}
+
+// conv64 (persistent weight-resident 64-channel 3x3 conv, conv64.hip) for bf16; GT_CONV64=0 disables it (A/B)
+static bool conv64_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("GT_CONV64");
+    return !e || atoi(e) != 0;
   }();
   return v;
 }
@@ -343,6 +368,8 @@ int prepare(gt_decoder* d, int code) {
     } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
+      if (dt && ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 64 && shp[2] == 3 && shp[3] == 3)
+        pack_conv64(blob, k + ".w64", w);
       if (dt && conv4_enabled() && ends_with(k, ".block.0.weight") && shp[1] % 16 == 0)
         pack_conv4(blob, k + ".v4", w, (int)shp[0], (int)shp[1]);
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
@@ -489,6 +516,14 @@ struct Run {
   // utterance it wrote. bf16 inputs without a transform (IN_PLAIN, or IN_MASK with a 0/1 mask) take the
   // LDS-DMA pipeline (conv4.hip); everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
+    if (dt && conv64_enabled() && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
+        d->dp[wi].count(wkey + ".w64")) {
+      p.w = W(wkey + ".w64");
+      const double pos = (double)p.B * p.Fout * p.Tout;
+      timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
+            2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, mask01, p, s); });
+      return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
+    }
     const bool v4 = dt && conv4_enabled() && (im == IN_PLAIN || (im == IN_MASK && mask01)) && p.Cin % 16 == 0 &&
                     d->dp[wi].count(wkey + ".v4");
     if (!v4) {
