@@ -31,28 +31,30 @@ namespace gt {
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
 namespace c64 {
-constexpr int TF = 4, TS = 32, PR = TF + 2, PC = TS + 2, NPOS = PR * PC;   // 6 x 34 patch positions
-constexpr int POSB = 144;                                                   // 128 B of channels + 16 B pad
-constexpr int NTHR = 512, NW = 8;
-constexpr int PITEMS = NPOS * 8;                                            // 16-B items: 1632
-constexpr int PPT = (PITEMS + NTHR - 1) / NTHR;                             // 4 per thread
-constexpr int NCH = 4;                                                      // 16-channel chunks
-constexpr int PATCH_B = NPOS * POSB;                                        // 29376
-constexpr int SMEM = 2 * PATCH_B + (2 * 4 * 64 + 64 + 2 * NW * 8 + 16) * 4 + 272 * 8;
-constexpr int SPH = 4;   // stamps per sub-tile (diagnostics)
-static_assert(PATCH_B % 16 == 0, "aligned buffers");
-static_assert(SMEM <= 64 * 1024, "LDS budget");
+constexpr int TF = 4, TT = 32, PC = TT + 2;               // tile: 4 mel rows x 32 frames; patch rows of 34 positions
+constexpr int POSB = 144;                                 // 128 B of channels + 16 B pad (conflict-free fragments)
+constexpr int ROWB = PC * POSB;                           // 4896 B per patch row
+constexpr int RING = 10;                                  // patch rows resident: 6 of the current tile + 4 of the next
+constexpr int NTHR = 256, NW = 4;
+constexpr int NEW_ITEMS = 4 * PC * 8;                     // 16-B items of the 4 new rows per tile: 1088
+constexpr int PPT = (NEW_ITEMS + NTHR - 1) / NTHR;        // 5 (the 5th only for threads < 64)
+constexpr int COLD_ITEMS = 6 * PC * 8;                    // first tile of a segment: all 6 rows
+constexpr int CPT = (COLD_ITEMS + NTHR - 1) / NTHR;       // 7
+constexpr int NCH = 4;                                    // 16-channel chunks
+constexpr int SMEM = RING * ROWB + (2 * 4 * 64 + 64 + 2 * NW * 8 + 16) * 4 + 272 * 8;
+constexpr int SPH = 4;                                    // stamps per tile (diagnostics)
+static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
 
 #ifdef GT_C64_STAMPS
-// Diagnostic timeline (tools/stamps64.py): s_memtime at phase boundaries of waves 0 and 7 of every workgroup,
+// Diagnostic timeline (tools/stamps64.py): s_memtime at phase boundaries of the first and last wave of every workgroup,
 // last launch of conv64_kernel<GT_C64_STAMPS> on an 80-row grid.
-constexpr int S64_WG = 256, S64_TILES = 48, S64_PH = c64::SPH;
+constexpr int S64_WG = 256, S64_TILES = 24, S64_PH = c64::SPH;
 __device__ unsigned long long g_s64[S64_WG * 2 * (2 + S64_TILES * S64_PH)];
 #define ST64(k)                                                                                           \
   do {                                                                                                    \
-    if (st_on && (lane == 0) && (wv == 0 || wv == 7))                                                    \
-      g_s64[(blockIdx.x * 2 + (wv == 7)) * (2 + S64_TILES * S64_PH) + (k)] = __builtin_readcyclecounter(); \
+    if (st_on && (lane == 0) && (wv == 0 || wv == c64::NW - 1))                                          \
+      g_s64[(blockIdx.x * 2 + (wv != 0)) * (2 + S64_TILES * S64_PH) + (k)] = __builtin_readcyclecounter(); \
   } while (0)
 #else
 #define ST64(k) do {} while (0)
@@ -85,29 +87,32 @@ GT_DEV float mish_tb(float y, float tb) {
   return __builtin_fmaf(y, __builtin_fmaf(-2.f, r, 1.f), tb);
 }
 
-// IN: IN_MASK / IN_GN / IN_PLAIN; FRAC (IN_MASK only): the mask may hold values other than 0 and 1
+// IN: IN_MASK / IN_GN / IN_PLAIN; FRAC (IN_MASK only): the mask may hold values other than 0 and 1.
+// One workgroup = one segment: L consecutive 4 x 32 tiles down the mel axis of one utterance's 32-frame column.
+// Two workgroups share a CU (one wave of each per SIMD) and drift out of phase, so one's staging/epilogue VALU
+// work overlaps the other's MFMAs.
 template <int IN, bool FRAC>
-__global__ __launch_bounds__(512) void conv64_kernel(ConvParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
-  char* const sP = smem;                                     // 2 patch buffers
-  float* const s_coef = reinterpret_cast<float*>(smem + 2 * PATCH_B);   // [b & 1][scale, shift, tb, unused][64]
+  char* const sR = smem;                                     // ring of RING patch rows
+  float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB);   // [scale, shift, tb, unused][64]
   float* const s_bias = s_coef + 2 * 4 * 64;
-  float* const s_sub = s_bias + 64;                          // [slot & 1][wave][(pr, h) group][sum, sq]
+  float* const s_sub = s_bias + 64;                          // [tile & 1][wave][(pr, h) group][sum, sq]
   float* const s_mean = s_sub + 2 * NW * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int cb = wv & 1, lrow = wv >> 1;
+  const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
   const int F = p.Fout, T = p.Tout;
-  const int n_ft = F / TF, n_tt = (T + 63) / 64, per_b = n_ft * n_tt;
-  const long nslots = (long)p.B * per_b;
-  const int s_beg = (int)(nslots * blockIdx.x / gridDim.x), s_end = (int)(nslots * (blockIdx.x + 1) / gridDim.x);
-  if (s_beg >= s_end) return;   // whole workgroup (uniform)
-  const int u0 = 2 * s_beg, u_end = 2 * s_end;   // sub-tile u = 2 * slot + half
+  const int n_ft = F / TF, n_tt = (T + TT - 1) / TT;
+  const int kseg = n_ft / L;                                 // segments per column
+  const int col = blockIdx.x / kseg, part = blockIdx.x - col * kseg;
+  const int b = col / n_tt, tt = col - b * n_tt;
+  const int ft0 = part * L;
 #ifdef GT_C64_STAMPS
-  const bool st_on = IN == GT_C64_STAMPS && F == 80 && blockIdx.x < S64_WG && u_end - u0 <= S64_TILES;
+  const bool st_on = IN == GT_C64_STAMPS && F == 80 && blockIdx.x < S64_WG && L <= S64_TILES;
 #endif
   ST64(0);
 
@@ -122,56 +127,32 @@ __global__ __launch_bounds__(512) void conv64_kernel(ConvParams p) {
       for (int tap = 0; tap < 9; ++tap) wf[ch][tap] = src[(ch * 9 + tap) * 64];
   }
   if (tid < 64) s_bias[tid] = p.bias[tid];
-  float c_g = 0.f, c_b = 0.f;
-  if (IN == IN_GN && tid < 64) { c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; }
 
-  // ---- patch items: thread tid owns items tid + 512 j (position it/8, 8-channel group it%8 = tid%8)
+  // ---- staging. Item (row i, column c, 8-channel group sub) of patch row i: input frame t0 - 1 + c, mel row
+  // given by the caller; out-of-range positions read past the end of the tensor (zeros).
   const int sub = tid & 7;
   const int npos = p.B * F * T;
+  const int t0 = tt * TT;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * 128, 0x00020000);
-  u32x4_t preg[PPT];
-  float pm[PPT];
-  auto coords = [&](int u, int& b, int& ft, int& tt, int& t0) {
-    const int slot = u >> 1;
-    b = slot / per_b;
-    const int rem = slot - b * per_b;
-    ft = rem / n_tt;
-    tt = rem - ft * n_tt;
-    t0 = tt * 64 + (u & 1) * TS;
-  };
-  // Item j of a sub-tile: issue its load (u past the range: clamped to the last sub-tile, a harmless reload)
-  // and store it (transformed per IN) into a patch buffer. One item per K-chunk of the MFMA loop keeps the
-  // live transform temporaries to one item.
-  struct Sub { int b, fi0, ti0; };
-  auto sub_of = [&](int u) {
-    u = u < u_end ? u : u_end - 1;
-    int b, ft, tt, t0;
-    coords(u, b, ft, tt, t0);
-    return Sub{b, ft * TF - 1, t0 - 1};
-  };
-  auto issue_item = [&](int j, const Sub& sb) {
-    const int it = tid + NTHR * j;
-    const int pos = it >> 3, pr = pos / PC, pc = pos - pr * PC;
-    const int fi = sb.fi0 + pr, ti = sb.ti0 + pc;
-    const bool ok = it < PITEMS && fi >= 0 && fi < F && ti >= 0 && ti < T;
-    const int q = ok ? (sb.b * F + fi) * T + ti : npos;
-    preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 128 + sub * 16, 0, 0);
+  auto load_item = [&](int it, int frow, u32x4_t& v, float& m) {
+    const int c = (it >> 3) % PC;
+    const int ti = t0 - 1 + c;
+    const bool ok = frow >= 0 && frow < F && ti >= 0 && ti < T;
+    const int q = ok ? (b * F + frow) * T + ti : npos;
+    v = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 128 + sub * 16, 0, 0);
     if (IN != IN_PLAIN) {   // unconditional load at a clamped frame, then select (no branch around the load)
-      const float mv = mask_at(p.mask, p.T0, sb.b, ti < 0 ? 0 : (ti < T ? ti : T - 1), p.lvl_in);
-      pm[j] = ok ? mv : 0.f;
+      const float mv = mask_at(p.mask, p.T0, b, ti < 0 ? 0 : (ti < T ? ti : T - 1), p.lvl_in);
+      m = ok ? mv : 0.f;
     }
   };
-  auto store_item = [&](int j, const Sub& sb, int buf) {
-    const int it = tid + NTHR * j;
-    u32x4_t v4 = preg[j];
+  auto put_item = [&](int it, int slot, u32x4_t v4, float m) {
     if (IN == IN_MASK && !FRAC) {
-      v4 = pm[j] == 0.f ? u32x4_t{0u, 0u, 0u, 0u} : v4;
+      v4 = m == 0.f ? u32x4_t{0u, 0u, 0u, 0u} : v4;
     } else if (IN != IN_PLAIN) {
-      const float m = pm[j];
       float v[8];
       item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
       if (IN == IN_GN) {   // (Mish(GN(h)) * m + tb) * m, m in {0,1}  (diffusion.py:57-58, 76)
-        const float* cf = s_coef + (sb.b & 1) * 256 + sub * 8;
+        const float* cf = s_coef + sub * 8;
         const f32x4 sc0 = *reinterpret_cast<const f32x4*>(cf), sc1 = *reinterpret_cast<const f32x4*>(cf + 4);
         const f32x4 sh0 = *reinterpret_cast<const f32x4*>(cf + 64), sh1 = *reinterpret_cast<const f32x4*>(cf + 68);
         const f32x4 tb0 = *reinterpret_cast<const f32x4*>(cf + 128), tb1 = *reinterpret_cast<const f32x4*>(cf + 132);
@@ -189,131 +170,152 @@ __global__ __launch_bounds__(512) void conv64_kernel(ConvParams p) {
         v4 = u32x4_t{o.x, o.y, o.z, o.w};
       }
     }
-    if (PITEMS % NTHR == 0 || it < PITEMS) *reinterpret_cast<u32x4_t*>(sP + buf * PATCH_B + (it >> 3) * POSB + sub * 16) = v4;
+    *reinterpret_cast<u32x4_t*>(sR + slot * ROWB + ((it >> 3) % PC) * POSB + sub * 16) = v4;
   };
-  // GroupNorm scale/shift (and time bias) of the input channels for utterance b into set b & 1 (IN_GN)
-  auto gn_coefs = [&](int b) {
+
+  // GroupNorm scale/shift (and time bias) of the input channels of utterance b (IN_GN): once per segment
+  if (IN == IN_GN) {
+    const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
+    static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
     const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b);
     const float tbv = tid < 64 ? p.tb[(long)b * p.tb_bstride + tid] : 0.f;
     gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
     if (tid < 64) {
-      float* cf = s_coef + (b & 1) * 256;
       const float sc = c_g * s_rstd[tid >> 3];
-      cf[tid] = sc; cf[64 + tid] = c_b - s_mean[tid >> 3] * sc; cf[128 + tid] = tbv;
+      s_coef[tid] = sc; s_coef[64 + tid] = c_b - s_mean[tid >> 3] * sc; s_coef[128 + tid] = tbv;
     }
     lds_barrier();
-  };
-
-  // ---- prologue: sub-tile u0 into buffer 0, loads of u0 + 1 in flight
-  {
-    const Sub s0 = sub_of(u0), s1 = sub_of(u0 + 1);
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) issue_item(j, s0);
-    if (IN == IN_GN) gn_coefs(s_beg / per_b);
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) store_item(j, s0, 0);
-#pragma unroll
-    for (int j = 0; j < PPT; ++j) issue_item(j, s1);
   }
+
+  // ---- prologue: tile 0's 6 patch rows (mel rows 4 ft0 - 1 .. 4 ft0 + 4) into ring slots 0..5
+  {
+    u32x4_t cv[CPT];
+    float cm[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int it = tid + NTHR * j;
+      load_item(it < COLD_ITEMS ? it : 0, ft0 * TF - 1 + (it < COLD_ITEMS ? it / (PC * 8) : 0), cv[j], cm[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int it = tid + NTHR * j;
+      if (CPT * NTHR == COLD_ITEMS || it < COLD_ITEMS) put_item(it, it / (PC * 8), cv[j], cm[j]);
+    }
+  }
+  // the next tile's 4 new rows (mel rows 4 (ft0+1) + 1 .. + 4) in flight
+  u32x4_t preg[PPT];
+  float pm[PPT];
+  auto issue_new = [&](int j, int k) {   // item j of tile k's new rows (k past the segment: harmless reload)
+    const int it = tid + NTHR * j;
+    const int itc = it < NEW_ITEMS ? it : 0;
+    load_item(itc, (ft0 + k) * TF + 1 + itc / (PC * 8), preg[j], pm[j]);
+  };
+  auto put_new = [&](int j, int k) {     // store item j of tile k's new rows into ring slots 4k + 2 + i
+    const int it = tid + NTHR * j;
+    if (PPT * NTHR == NEW_ITEMS || it < NEW_ITEMS) put_item(it, (4 * k + 2 + it / (PC * 8)) % RING, preg[j], pm[j]);
+  };
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) issue_new(j, 1);
   lds_barrier();
   ST64(1);
 
-  float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};   // per-lane GroupNorm partials of the current slot
-  for (int u = u0; u < u_end; ++u) {
-    const int buf = (u - u0) & 1;
-    int b, ft, tt, t0;
-    coords(u, b, ft, tt, t0);
-    ST64(2 + (u - u0) * SPH + 0);
-
-    f32x16 acc;
+  const int n_t32 = (T + TT - 1) / TT, nparts = n_ft * n_t32;   // GroupNorm partial slots: one per 4 x 32 tile
+  float gs[2], gq[2];
+  for (int k = 0; k < L; ++k) {
+    ST64(2 + k * SPH + 0);
+    const int ft = ft0 + k;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-    const char* pa = sP + buf * PATCH_B + (lrow * PC + r) * POSB + h * 16;
-    const Sub s1 = sub_of(u + 1), s2 = sub_of(u + 2);
+    for (int ps = 0; ps < 2; ++ps) {
+      const int lrow = 2 * rp + ps;
+      // this pass's three patch rows (tap rows dr = 0, 1, 2) in the ring
+      const int sbase = 4 * k + lrow;
+      const char* rowp0 = sR + ((sbase + 0) % RING) * ROWB + r * POSB + h * 16;
+      const char* rowp1 = sR + ((sbase + 1) % RING) * ROWB + r * POSB + h * 16;
+      const char* rowp2 = sR + ((sbase + 2) % RING) * ROWB + r * POSB + h * 16;
+      f32x16 acc;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
+      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int dr = tap / 3, dc = tap - 3 * dr;
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(pa + (dr * PC + dc) * POSB + ch * 32);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ch][tap], x, acc, 0, 0, 0);
-      }
-      // behind this chunk's MFMAs: stage item ch of sub-tile u+1 into the other buffer, then load it for u+2
-      static_assert(PPT == NCH, "one patch item per K-chunk");
-      store_item(ch, s1, buf ^ 1);
-      issue_item(ch, s2);
-    }
-    ST64(2 + (u - u0) * SPH + 1);
-
-    // ---- epilogue. Lane (j = r, h) holds channels cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position j
-    // (registers 0-3, 4-7, 8-11, 12-15); swapping registers 4-7 <-> 0-3 and 12-15 <-> 8-11 across the
-    // half-waves leaves lane h with channels cb*32 + 8h + 0..7 (regs 0-7) and cb*32 + 16 + 8h + 0..7 (8-15).
-    float v[16];
+      for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = acc[k];
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + k]), __float_as_uint(v[8 * pr + 4 + k]),
-                                                         false, false);
-        v[8 * pr + k] = __uint_as_float(sw[0]);
-        v[8 * pr + 4 + k] = __uint_as_float(sw[1]);
-      }
-    const int t = t0 + r;
-    const bool valid = t < T;
-    bf16* const outp = reinterpret_cast<bf16*>(p.out) + (((long)b * F + ft * TF + lrow) * T + t) * 64;
-    const int slot = u >> 1, half = u & 1;
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + c0);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + c0 + 4);
-      float o[8];
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        o[k] = v[8 * pr + k] + (k < 4 ? b0[k] : b1[k - 4]);
-        s += o[k];
-        q += o[k] * o[k];
-      }
-      if (valid) *reinterpret_cast<uint4*>(outp + c0) = f_to_item(o, bf16());
-      // per-lane GroupNorm partials of the slot: half 0, then half 0 + half 1 (fixed order)
-      gs[pr] = (half ? gs[pr] : 0.f) + (valid ? s : 0.f);
-      gq[pr] = (half ? gq[pr] : 0.f) + (valid ? q : 0.f);
-    }
-    if (half) {   // slot complete in this wave: group cb*4 + pr*2 + h, summed over its 64 positions
-      float* const sub_w = s_sub + (slot & 1) * NW * 8 + wv * 8;
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const float s = half_sum32(gs[pr]), q = half_sum32(gq[pr]);
-        if (r == 0) {
-          sub_w[(pr * 2 + h) * 2 + 0] = s;
-          sub_w[(pr * 2 + h) * 2 + 1] = q;
+        for (int tap = 0; tap < 9; ++tap) {
+          const int dr = tap / 3, dc = tap - 3 * dr;
+          const char* rp_ = dr == 0 ? rowp0 : (dr == 1 ? rowp1 : rowp2);
+          const bf16x8 x = *reinterpret_cast<const bf16x8*>(rp_ + dc * POSB + ch * 32);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ch][tap], x, acc, 0, 0, 0);
+        }
+        // behind this chunk's MFMAs: stage one item of tile k+1's new rows, then load it for tile k+2
+        // (items spread over the 8 chunk slots of the two passes)
+        const int j = ps * NCH + ch;
+        if (j < PPT) {
+          put_new(j, k + 1);
+          issue_new(j, k + 2);
         }
       }
+      ST64(2 + k * SPH + 1 + ps);
+
+      // ---- epilogue of this pass. Lane (j = r, h) holds channels cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of
+      // position j (registers 0-3, 4-7, 8-11, 12-15); swapping registers 4-7 <-> 0-3 and 12-15 <-> 8-11 across
+      // the half-waves leaves lane h with channels cb*32 + 8h + 0..7 (regs 0-7) and cb*32 + 16 + 8h + 0..7.
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]), __float_as_uint(v[8 * pr + 4 + q]),
+                                                           false, false);
+          v[8 * pr + q] = __uint_as_float(sw[0]);
+          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        }
+      const int t = t0 + r;
+      const bool valid = t < T;
+      bf16* const outp = reinterpret_cast<bf16*>(p.out) + (((long)b * F + ft * TF + lrow) * T + t) * 64;
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + c0);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + c0 + 4);
+        float o[8];
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = v[8 * pr + e] + (e < 4 ? b0[e] : b1[e - 4]);
+          s += o[e];
+          q += o[e] * o[e];
+        }
+        if (valid) *reinterpret_cast<uint4*>(outp + c0) = f_to_item(o, bf16());
+        // per-lane GroupNorm partials of the tile: pass 0, then pass 0 + pass 1 (fixed order)
+        gs[pr] = (ps ? gs[pr] : 0.f) + (valid ? s : 0.f);
+        gq[pr] = (ps ? gq[pr] : 0.f) + (valid ? q : 0.f);
+      }
     }
-    ST64(2 + (u - u0) * SPH + 2);
-    // coefficients for sub-tile u+2 (staged during the next iteration) when it starts a new utterance
-    if (IN == IN_GN && u + 2 < u_end) {
-      const int b2 = ((u + 2) >> 1) / per_b;
-      if (b2 != ((u + 1) >> 1) / per_b) gn_coefs(b2);   // workgroup-uniform
+    // tile done in this wave: group cb*4 + pr*2 + h over its 64 positions
+    float* const sub_w = s_sub + (k & 1) * NW * 8 + wv * 8;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const float s = half_sum32(gs[pr]), q = half_sum32(gq[pr]);
+      if (r == 0) {
+        sub_w[(pr * 2 + h) * 2 + 0] = s;
+        sub_w[(pr * 2 + h) * 2 + 1] = q;
+      }
     }
-    lds_barrier();   // buffer u+1 complete, buffer u free, sub-partials visible
-    if (half == 1 && tid < 8) {   // slot complete: fixed-order sum over the 4 waves of the group's cb
+    lds_barrier();   // tile k+1's rows complete, sub-partials visible
+    if (tid < 8) {   // fixed-order sum over the 2 waves of the group's cb -> this tile's slot
       const int g = tid, gcb = g >> 2, e = (g & 3) * 2;
       float S = 0.f, Q = 0.f;
 #pragma unroll
-      for (int lr = 0; lr < 4; ++lr) {
-        const float* q = s_sub + (slot & 1) * NW * 8 + (lr * 2 + gcb) * 8 + e;
+      for (int w2 = 0; w2 < 2; ++w2) {
+        const float* q = s_sub + (k & 1) * NW * 8 + (w2 * 2 + gcb) * 8 + e;
         S += q[0];
         Q += q[1];
       }
-      float* dst = p.out_part + ((long)b * per_b + ft * n_tt + tt) * 16 + g * 2;
+      float* dst = p.out_part + ((long)b * nparts + ft * n_t32 + tt) * 16 + g * 2;
       dst[0] = S;
       dst[1] = Q;
     }
-    ST64(2 + (u - u0) * SPH + 3);
+    ST64(2 + k * SPH + 3);
   }
 }
 
@@ -339,14 +341,30 @@ bool conv64_eligible(const ConvParams& p) {
          (long)p.B * p.Fout * p.Tout * 128 < (1L << 31);
 }
 
+// segment length: the longest run of tiles down a column (a divisor of the column's tile count) that still gives
+// every CU two workgroups; the ring then re-reads only the 2 halo columns (and 2 halo rows per segment)
+static int conv64_seg(const ConvParams& p) {
+  const int n_ft = p.Fout / 4;
+  const long ncol = (long)p.B * ((p.Tout + 31) / 32);
+  int L = n_ft;
+  for (int k = 1; k <= n_ft; ++k)
+    if (n_ft % k == 0) {
+      L = n_ft / k;
+      if (ncol * k >= 2L * cu_count()) break;
+    }
+  return L;
+}
+
+int conv64_nparts(int F, int T) { return (F / 4) * ((T + 31) / 32); }
+
 hipError_t launch_conv64(InMode im, bool mask01, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
-  const long nslots = (long)p.B * (p.Fout / 4) * ((p.Tout + 63) / 64);
-  const unsigned grid = (unsigned)(nslots < cu_count() ? nslots : cu_count());
-  if (im == IN_MASK && mask01) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(512), 0, s, p);
-  else if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(512), 0, s, p);
-  else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), dim3(512), 0, s, p);
-  else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), dim3(512), 0, s, p);
+  const int L = conv64_seg(p);
+  const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
+  if (im == IN_MASK && mask01) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(256), 0, s, p, L);
+  else if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(256), 0, s, p, L);
+  else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), dim3(256), 0, s, p, L);
+  else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), dim3(256), 0, s, p, L);
   else return hipErrorNotSupported;
   return hipGetLastError();
 }

@@ -447,7 +447,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
     const size_t n = (size_t)B * (80 >> l) * (T >> l) * C[l] * esize(dt);
     for (int i = 0; i < 5; ++i) L.act[l][i] = take(n);
   }
-  L.pmax = 20 * (int)((T + 63) / 64);   // GroupNorm partial slots per utterance: largest producer grid (level 0)
+  L.pmax = 20 * (int)((T + 31) / 32);   // GroupNorm partial slots per utterance: largest producer grid (level-0 conv64)
   L.stats = take((size_t)25 * B * L.pmax * 16 * sizeof(float));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
@@ -522,7 +522,7 @@ struct Run {
       const double pos = (double)p.B * p.Fout * p.Tout;
       timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, mask01, p, s); });
-      return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
+      return conv64_nparts(p.Fout, p.Tout);
     }
     const bool v4 = dt && conv4_enabled() && (im == IN_PLAIN || (im == IN_MASK && mask01)) && p.Cin % 16 == 0 &&
                     d->dp[wi].count(wkey + ".v4");

@@ -86,8 +86,9 @@ struct Conv4Cfg { int nt, tt, nw, ns; };
 Conv4Cfg conv4_pick(int Cout);
 int conv4_nparts(int F, int T, int Cout, Conv4Cfg c);
 hipError_t launch_conv4(const ConvParams& p, Conv4Cfg c, hipStream_t s);
-// persistent weight-resident 3x3 conv for Cin = Cout = 64, bf16 (conv64.hip); same GroupNorm partial slots as
-// conv_kernel (conv_gn_nparts). conv64_eligible: shape/layout preconditions (no concat, no fp8 image).
+// weight-resident 3x3 conv for Cin = Cout = 64, bf16 (conv64.hip); GroupNorm partial slots: one per 4 x 32 tile
+// (conv64_nparts). conv64_eligible: shape/layout preconditions (no concat, no fp8 image).
+int conv64_nparts(int F, int T);
 bool conv64_eligible(const ConvParams& p);
 hipError_t launch_conv64(InMode im, bool mask01, const ConvParams& p, hipStream_t s);
 // flag = 1 if any mask value is neither 0 nor 1 (flag must be zeroed first)
