@@ -103,26 +103,27 @@ GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
 // Reduction in two halves so callers can overlap other loads with the slot loads:
 //   GnLoad gl = gn_load(part, nparts, b);     issues this thread's slot loads (threads 0..255)
 //   gn_finish(gl, ...);                        fp64 sums in a fixed order -> s_mean / s_rstd (LDS)
-// Thread t reads value k = t & 15 of slots t>>4, t>>4 + 16, ... (16 at once, coalesced 64-B rows); the
+// Thread t reads value k = t & 15 of slots t>>4, t>>4 + 16, ... (GN_Q at once, coalesced 64-B rows); the
 // 256 fp64 partials are then summed per value by 16 threads in slot-group order. The order depends only
 // on nparts: deterministic and independent of the launch. Call with all threads of the block (>= 256).
 // Workgroup barrier that orders LDS only (no memory-model fence: outstanding global loads, e.g. a
 // prefetch, stay in flight).
 GT_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+constexpr int GN_Q = 24;   // slot loads per thread issued up front: 16 thread groups x 24 = 384 slots per utterance
 struct GnLoad {
-  float v[16];
+  float v[GN_Q];
 };
 GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
   GnLoad g;
 #ifdef GT_EXP_NO_GN_REDUCE
-  for (int q = 0; q < 16; ++q) g.v[q] = 0.f;
+  for (int q = 0; q < GN_Q; ++q) g.v[q] = 0.f;
   return g;
 #endif
   const int t = threadIdx.x, k = t & 15, grp = t >> 4;
   const float* pb = part + (long)b * nparts * 16 + k;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < GN_Q; ++q) {
     const int i = grp + 16 * q;
     g.v[q] = (t < 256 && i < nparts) ? pb[(long)i * 16] : 0.f;
   }
@@ -140,8 +141,18 @@ GT_DEV void gn_finish(const GnLoad& g, const float* part, int nparts, int b, lon
   if (t < 256) {
     double acc = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc += (double)g.v[q];
-    for (int i = grp + 256; i < nparts; i += 16) acc += (double)part[((long)b * nparts + i) * 16 + k];
+    for (int q = 0; q < GN_Q; ++q) acc += (double)g.v[q];
+    // slots past the first 16 * GN_Q (long utterances): 8 loads in flight per round, same ascending order
+    for (int i0 = grp + 16 * GN_Q; i0 < nparts; i0 += 16 * 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 16 * u;
+        w[u] = i < nparts ? part[((long)b * nparts + i) * 16 + k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += (double)w[u];
+    }
     s_red[t] = acc;
   }
   lds_barrier();

@@ -6,22 +6,27 @@
 // 5120 short-lived tiles restages the 78 KB weight image from L2 (≈400 MB of L2->LDS traffic per launch) and
 // pays its prologue/epilogue for only 4 K-chunks.
 //
-// Structure (one workgroup of 8 waves per CU, grid = CU count, each workgroup a contiguous run of tiles):
-//   * weights live in REGISTERS for the whole launch: wave w owns output channels 32*(w&1) .. +31 and holds
-//     their 4 chunks x 9 taps of A fragments (144 VGPRs), loaded once from a fragment-ordered image;
-//   * wave w computes mel row (w>>1) of a 4-row x 32-frame sub-tile: one 32x32 accumulator, 36 MFMAs
-//     (v_mfma_f32_32x32x16_bf16, weights as A, patch positions as B -> C = channel x position);
-//   * the 6 x 34-position input patch (64 channels, 144-B rows: conflict-free fragment reads) is
-//     DOUBLE-BUFFERED in LDS: while the MFMAs read sub-tile u from one buffer, the same waves store sub-tile
-//     u+1 into the other (from registers, with the producer's GroupNorm apply + Mish + time bias + mask
-//     for IN_GN, or x * mask) and issue the raw buffer loads of sub-tile u+2 (padding and past-the-end
-//     reads return zeros). One LDS barrier per sub-tile, no weight traffic after the prologue;
+// Structure (4-wave workgroups, two per CU; one workgroup = one SEGMENT: L consecutive 4-row x 32-frame tiles
+// walking down the mel axis of one utterance's 32-frame column):
+//   * weights stay RESIDENT for the whole launch: wave w owns output channels 32*(w&1) .. +31 and holds their
+//     4 chunks x 8 (IN_GN: 7) taps of A fragments in VGPRs, the other taps in LDS, loaded once from a
+//     fragment-ordered image (decoder.cpp pack_conv64) -- no weight traffic after the prologue;
+//   * wave w computes mel rows 2(w>>1) and 2(w>>1)+1 of each tile, one row per pass: one 32x32 accumulator,
+//     36 MFMAs (v_mfma_f32_32x32x16_bf16, weights as A, patch positions as B -> C = channel x position);
+//   * the input lives in a RING of 10 patch rows (34 positions x 64 channels, 144-B rows: conflict-free
+//     fragment reads): tile k reads rows 4k .. 4k+5; while its MFMAs run, the same waves store the 4 new rows of
+//     tile k+1 (from registers, one 16-B item per K-chunk, with the producer's GroupNorm apply + Mish + time
+//     bias + mask for IN_GN, or x * mask) and issue the raw buffer loads of tile k+2's rows (padding reads
+//     past the end of the tensor and returns zeros). Every input row is staged once per segment: 1.06x the
+//     compulsory reads (2 halo columns) instead of the 1.59x of independent 4 x 32 tiles. One LDS barrier per
+//     tile; the two workgroups of a CU drift out of phase, so one's staging VALU overlaps the other's MFMAs;
 //   * epilogue from the accumulators: one v_permlane32_swap per register pair leaves each lane with 8
 //     consecutive output channels (= one GroupNorm group) of one position -> bias, 16-B stores and the
 //     GroupNorm partial sums (DPP row sums + one v_permlane16_swap), no LDS transposition.
-// Tiles of conv_kernel (4 rows x 64 frames) are processed as two 32-frame sub-tiles, so the GroupNorm partial
-// slots are exactly conv_kernel's (conv_gn_nparts): producers and consumers are unchanged, and every slot is
-// summed in a fixed order (deterministic, batch-invariant).
+// GroupNorm partial slots: ONE per segment (conv64_nparts: 16 per utterance at level 0, T = 512, instead of
+// 160 for conv_kernel's tiles), accumulated per lane tile by tile in a fixed order and reduced once at the end --
+// the consumers' per-workgroup slot reduction shrinks accordingly. The segment length depends only on the grid
+// height, so results are deterministic and batch-invariant.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
@@ -41,7 +46,11 @@ constexpr int PPT = (NEW_ITEMS + NTHR - 1) / NTHR;        // 5 (the 5th only for
 constexpr int COLD_ITEMS = 6 * PC * 8;                    // first tile of a segment: all 6 rows
 constexpr int CPT = (COLD_ITEMS + NTHR - 1) / NTHR;       // 7
 constexpr int NCH = 4;                                    // 16-channel chunks
-constexpr int SMEM = RING * ROWB + (2 * 4 * 64 + 64 + 2 * NW * 8 + 16) * 4 + 272 * 8;
+constexpr int WLDS_MAX = 2;                               // taps whose weights live in LDS (the rest in registers)
+constexpr int WTAP_B = 2 * NCH * 64 * 16;                 // one tap's fragments of both channel halves: 8 KB
+constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + NW * 8 + 16) * 4 + 272 * 8;
+// taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room
+constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
 constexpr int SPH = 4;                                    // stamps per tile (diagnostics)
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
@@ -96,10 +105,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   using namespace c64;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
   char* const sR = smem;                                     // ring of RING patch rows
-  float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB);   // [scale, shift, tb, unused][64]
+  constexpr int WREG = wreg_of(IN);
+  char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
+  float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB + WLDS_MAX * WTAP_B);   // [scale, shift, tb, unused][64]
   float* const s_bias = s_coef + 2 * 4 * 64;
-  float* const s_sub = s_bias + 64;                          // [tile & 1][wave][(pr, h) group][sum, sq]
-  float* const s_mean = s_sub + 2 * NW * 8;
+  float* const s_sub = s_bias + 64;                          // [wave][(pr, h) group][sum, sq]
+  float* const s_mean = s_sub + NW * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
 
@@ -118,14 +129,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 
   // ---- weights -> registers: A fragment (ch, tap) = output channel cb*32 + r, input channels 16 ch + 8h .. +7,
   // from the fragment-ordered image (decoder.cpp pack_conv64): one contiguous 1 KiB per wave instruction
-  bf16x8 wf[NCH][9];
+  // (taps 0..WREG-1 in VGPRs; the others from LDS, 4 extra ds_read_b128 per tap and pass, leaving registers for the
+  // staging)
+  bf16x8 wf[NCH][WREG];
   {
     const bf16x8* src = reinterpret_cast<const bf16x8*>(p.w) + cb * NCH * 9 * 64 + lane;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch)
+    for (int ch = 0; ch < NCH; ++ch) {
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) wf[ch][tap] = src[(ch * 9 + tap) * 64];
+      for (int tap = 0; tap < WREG; ++tap) wf[ch][tap] = src[(ch * 9 + tap) * 64];
+      if (wv < 2)
+#pragma unroll
+        for (int tap = WREG; tap < 9; ++tap)
+          reinterpret_cast<bf16x8*>(sWL + (tap - WREG) * WTAP_B)[(cb * NCH + ch) * 64 + lane] = src[(ch * 9 + tap) * 64];
+    }
   }
+  const char* const wlp = sWL + (cb * NCH * 64 + lane) * 16;
   if (tid < 64) s_bias[tid] = p.bias[tid];
 
   // ---- staging. Item (row i, column c, 8-channel group sub) of patch row i: input frame t0 - 1 + c, mel row
@@ -152,14 +171,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       float v[8];
       item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
       if (IN == IN_GN) {   // (Mish(GN(h)) * m + tb) * m, m in {0,1}  (diffusion.py:57-58, 76)
-        const float* cf = s_coef + sub * 8;
-        const f32x4 sc0 = *reinterpret_cast<const f32x4*>(cf), sc1 = *reinterpret_cast<const f32x4*>(cf + 4);
-        const f32x4 sh0 = *reinterpret_cast<const f32x4*>(cf + 64), sh1 = *reinterpret_cast<const f32x4*>(cf + 68);
-        const f32x4 tb0 = *reinterpret_cast<const f32x4*>(cf + 128), tb1 = *reinterpret_cast<const f32x4*>(cf + 132);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[k] = mish_tb(v[k] * sc0[k] + sh0[k], tb0[k]);
-          v[4 + k] = mish_tb(v[4 + k] * sc1[k] + sh1[k], tb1[k]);
+        for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
+          const float* cf = s_coef + sub * 8 + hq * 4;
+          const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
+          const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
+          const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_tb(v[4 * hq + k] * sc[k] + sh[k], tb[k]);
         }
         const uint4 o = f_to_item(v, bf16());
         v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
@@ -219,8 +238,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   lds_barrier();
   ST64(1);
 
-  const int n_t32 = (T + TT - 1) / TT, nparts = n_ft * n_t32;   // GroupNorm partial slots: one per 4 x 32 tile
-  float gs[2], gq[2];
+  // per-lane GroupNorm partials of the whole segment (group cb*4 + pr*2 + h), accumulated tile by tile, pass by
+  // pass in a fixed order; reduced across lanes and waves once, at the end
+  float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
   for (int k = 0; k < L; ++k) {
     ST64(2 + k * SPH + 0);
     const int ft = ft0 + k;
@@ -242,7 +262,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           const int dr = tap / 3, dc = tap - 3 * dr;
           const char* rp_ = dr == 0 ? rowp0 : (dr == 1 ? rowp1 : rowp2);
           const bf16x8 x = *reinterpret_cast<const bf16x8*>(rp_ + dc * POSB + ch * 32);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ch][tap], x, acc, 0, 0, 0);
+          const bf16x8 a = tap < WREG ? wf[ch][tap < WREG ? tap : 0]
+                                      : *reinterpret_cast<const bf16x8*>(wlp + (tap - WREG) * WTAP_B + ch * 1024);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x, acc, 0, 0, 0);
         }
         // behind this chunk's MFMAs: stage one item of tile k+1's new rows, then load it for tile k+2
         // (items spread over the 8 chunk slots of the two passes)
@@ -286,36 +308,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           q += o[e] * o[e];
         }
         if (valid) *reinterpret_cast<uint4*>(outp + c0) = f_to_item(o, bf16());
-        // per-lane GroupNorm partials of the tile: pass 0, then pass 0 + pass 1 (fixed order)
-        gs[pr] = (ps ? gs[pr] : 0.f) + (valid ? s : 0.f);
-        gq[pr] = (ps ? gq[pr] : 0.f) + (valid ? q : 0.f);
+        gs[pr] += valid ? s : 0.f;
+        gq[pr] += valid ? q : 0.f;
       }
     }
-    // tile done in this wave: group cb*4 + pr*2 + h over its 64 positions
-    float* const sub_w = s_sub + (k & 1) * NW * 8 + wv * 8;
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const float s = half_sum32(gs[pr]), q = half_sum32(gq[pr]);
-      if (r == 0) {
-        sub_w[(pr * 2 + h) * 2 + 0] = s;
-        sub_w[(pr * 2 + h) * 2 + 1] = q;
-      }
-    }
-    lds_barrier();   // tile k+1's rows complete, sub-partials visible
-    if (tid < 8) {   // fixed-order sum over the 2 waves of the group's cb -> this tile's slot
-      const int g = tid, gcb = g >> 2, e = (g & 3) * 2;
-      float S = 0.f, Q = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < 2; ++w2) {
-        const float* q = s_sub + (k & 1) * NW * 8 + (w2 * 2 + gcb) * 8 + e;
-        S += q[0];
-        Q += q[1];
-      }
-      float* dst = p.out_part + ((long)b * nparts + ft * n_t32 + tt) * 16 + g * 2;
-      dst[0] = S;
-      dst[1] = Q;
-    }
+    lds_barrier();   // tile k+1's rows complete
     ST64(2 + k * SPH + 3);
+  }
+  // segment done: this wave's groups over its positions, then the 2 waves of each channel half -> one slot
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const float s = half_sum32(gs[pr]), q = half_sum32(gq[pr]);
+    if (r == 0) {
+      s_sub[wv * 8 + (pr * 2 + h) * 2 + 0] = s;
+      s_sub[wv * 8 + (pr * 2 + h) * 2 + 1] = q;
+    }
+  }
+  lds_barrier();
+  if (tid < 8) {   // fixed-order sum over the 2 waves of the group's channel half
+    const int g = tid, gcb = g >> 2, e = (g & 3) * 2;
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2) {
+      const float* q = s_sub + (w2 * 2 + gcb) * 8 + e;
+      S += q[0];
+      Q += q[1];
+    }
+    float* dst = p.out_part + ((long)b * (n_tt * kseg) + tt * kseg + part) * 16 + g * 2;
+    dst[0] = S;
+    dst[1] = Q;
   }
 }
 
@@ -341,25 +362,20 @@ bool conv64_eligible(const ConvParams& p) {
          (long)p.B * p.Fout * p.Tout * 128 < (1L << 31);
 }
 
-// segment length: the longest run of tiles down a column (a divisor of the column's tile count) that still gives
-// every CU two workgroups; the ring then re-reads only the 2 halo columns (and 2 halo rows per segment)
-static int conv64_seg(const ConvParams& p) {
-  const int n_ft = p.Fout / 4;
-  const long ncol = (long)p.B * ((p.Tout + 31) / 32);
-  int L = n_ft;
-  for (int k = 1; k <= n_ft; ++k)
-    if (n_ft % k == 0) {
-      L = n_ft / k;
-      if (ncol * k >= 2L * cu_count()) break;
-    }
-  return L;
+// Segment length: a function of the grid height only (never of B), so the GroupNorm partial slots -- one per
+// segment -- and with them every rounding are the same in any batch or GPU shard. 80 rows: the whole column (20
+// tiles; 512 workgroups at B = 32, T = 512); 40 rows: half a column (5 tiles), which keeps two workgroups per CU
+// at level 1.
+static int conv64_seg(int F) {
+  const int n_ft = F / 4;
+  return (n_ft >= 20 || n_ft % 2) ? n_ft : n_ft / 2;
 }
 
-int conv64_nparts(int F, int T) { return (F / 4) * ((T + 31) / 32); }
+int conv64_nparts(int F, int T) { return ((T + 31) / 32) * ((F / 4) / conv64_seg(F)); }
 
 hipError_t launch_conv64(InMode im, bool mask01, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
-  const int L = conv64_seg(p);
+  const int L = conv64_seg(p.Fout);
   const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
   if (im == IN_MASK && mask01) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(256), 0, s, p, L);
   else if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(256), 0, s, p, L);

@@ -871,10 +871,10 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int
   return layout(dtype ? 1 : 0, B, T, n_timesteps).total;
 }
 
-// Are all mask values 0 or 1 (sequence_mask)? Decides whether conv4 may take x*mask convs (it realises
-// the product as zero-filled loads). One tiny reduction + a 4-byte read-back per API call (a stream sync).
+// Are all mask values 0 or 1 (sequence_mask)? Decides whether conv4 / conv64 may realise x*mask as a
+// select (zero-filled loads) instead of a multiply. One tiny reduction + a 4-byte read-back per API call (a stream sync).
 static bool mask_is_01(Run& R, const float* mask, int64_t B, int64_t T) {
-  if (!R.dt || !conv4_enabled()) return true;
+  if (!R.dt || !(conv4_enabled() || conv64_enabled())) return true;
   int* flag = (int*)(R.ws + R.L.flag);
   int host = 1;
   R.chk(hipMemsetAsync(flag, 0, sizeof(int), R.s));
