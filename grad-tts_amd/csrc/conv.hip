@@ -592,7 +592,7 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
   if constexpr (NT == 128 && IN != IN_GN && IN != IN_INPUT)
-    if (conv_tf(CONV3, IN, NT, p.Cout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
+    if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
 
@@ -643,7 +643,7 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
 
 int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout) {   // CONV3 tiles: TF rows x 64 frames x NT
   const int nt = conv_nt(act_bf16, Cout);
-  return (F / conv_tf(CONV3, im, nt, Cout)) * ((T + 63) / 64) * (Cout / nt);
+  return (F / conv_tf(CONV3, im, nt, Cout, F)) * ((T + 63) / 64) * (Cout / nt);
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {

@@ -508,7 +508,7 @@ struct Run {
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
-                             (p.wscale ? ",w8" : "") + (dt && conv_tf(kind, im, nt, p.Cout) == 5 ? ",tf5" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+                             (p.wscale ? ",w8" : "") + (dt && conv_tf(kind, im, nt, p.Cout, p.Fout) == 5 ? ",tf5" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
@@ -613,7 +613,8 @@ struct Run {
       // The transform runs once per element in place (one extra read+write of h1) when the conv4 path
       // takes the conv (bf16), and on wide fp32 levels (GT_GN_APPLY_MIN_C, default 256 channels), where
       // the operand-load transform of conv_kernel is recomputed by every 128-channel tile and halo row.
-      const bool apply = (dt && conv4_enabled()) || Cout >= gn_apply_min_c();
+      const bool apply = (dt && conv4_enabled()) || Cout >= gn_apply_min_c() ||
+                         (dt && GT_L1_TF5 && Cout == 128 && Fl(lvl) == 40);   // level 1: plain 5-row tiles
       if (apply) {
         RbOutParams a{};
         a.pre = pre1; a.part = st1; a.nparts = np1; a.gamma = Fp(k + "block1.block.1.weight");

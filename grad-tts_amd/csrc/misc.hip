@@ -72,7 +72,10 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 // channel group (and its GroupNorm scale/shift) for all of its items.
 //   APPLY = false: ResnetBlock output, out = Mish(GN(pre))*m + x*m               (diffusion.py:57-58, 77-79)
 //   APPLY = true : block2's conv input in place, pre = (Mish(GN(pre))*m + tb)*m   (diffusion.py:57-58, 76, 52)
-constexpr int RB_IPT = 8;
+#ifndef GT_RB_IPT
+#define GT_RB_IPT 8
+#endif
+constexpr int RB_IPT = GT_RB_IPT;
 template <class A, bool APPLY>
 __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   __shared__ float s_mean[8], s_rstd[8];

@@ -21,9 +21,16 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_TF5
 #define GT_TF5 1
 #endif
-// mel rows per 3x3 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels)
-inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout) {
-  return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 && cout >= 256 && im != 2 /*IN_GN*/) ? 5 : 4;
+// Option (off: measured slower, the level-1 gn_apply pass costs more than the 5-row tiles save): 128-output convs
+// on the 40-row level-1 grid too (1024 tiles at B = 32 instead of 1280); their GroupNorm-input
+// variant then takes the in-place gn_apply pass + plain input (decoder.cpp)
+#ifndef GT_L1_TF5
+#define GT_L1_TF5 0
+#endif
+// mel rows per 3x3 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid rows)
+inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f) {
+  return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 && im != 2 /*IN_GN*/ &&
+          (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ? 5 : 4;
 }
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
