@@ -16,16 +16,25 @@
 // index (t_y ints per utterance).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "gradtts.h"
 
 namespace {
 
-template <int XPL, int YCAP>
+// MODE bits (A/B via GT_MAS_MODE; default 53 = 1|4|16|32, measured 1.9x (b=32, 200x800) and 2.2x (ragged
+// training batch) faster than MODE 0, the first version, on the same box; bench_mas.py):
+//   1  the neighbour row arrives by DPP wave_shr:1 (a VALU op) instead of ds_bpermute
+//   2  deeper register prefetch of the value columns (measured slower; kept for A/B only)
+//   4  windowed backtrack: 64 columns per LDS round trip instead of one dependent LDS read per column
+//  16  lean row update: every row updated unconditionally, one compare serves the max and the step bit
+//  32  16-byte value loads (4 columns of a row per load instruction)
+template <int XPL, int YCAP, int MODE>
 __global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ values, const int32_t* t_xs,
                                                     const int32_t* t_ys, int tx_max, int ty_max, float neg,
                                                     int32_t* __restrict__ pidx) {
-  constexpr int kYB = XPL >= 16 ? 2 : (XPL >= 8 ? 4 : 8);   // value columns prefetched per block
+  constexpr int kYB = (MODE & 32) ? (XPL >= 8 ? 4 : 8) : (MODE & 2) ? (XPL >= 16 ? 4 : (XPL >= 8 ? 8 : 16))
+                           : (XPL >= 16 ? 2 : (XPL >= 8 ? 4 : 8));   // value columns prefetched per block
   __shared__ uint16_t bits[YCAP][64];
   const int b = blockIdx.x, L = threadIdx.x;
   int tx = t_xs[b], ty = t_ys[b];
@@ -42,15 +51,38 @@ __global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ va
 #pragma unroll
   for (int i = 0; i < XPL; ++i) V[i] = 0.f;
 
+  // Unconditional loads at clamped indices (rows >= tx_max read the last row, columns >= ty the last
+  // column): those values never enter the band, so no per-load branch is needed; 32-bit offsets from the
+  // utterance's (uniform) grid base.
+  uint32_t roff[XPL];
+#pragma unroll
+  for (int i = 0; i < XPL; ++i) {
+    const int x = L * XPL + i;
+    roff[i] = (uint32_t)((x < tx_max ? x : tx_max - 1) * ty_max) * 4u;   // bytes
+  }
   auto load_block = [&](float (&dst)[XPL][kYB], int y0) {
+    if constexpr ((MODE & 32) != 0) {
+      // 16-byte loads of 4 consecutive columns per row (rows are only 4-byte aligned: global loads need dword
+      // alignment only). The last block of a grid falls back to clamped dword loads (uniform branch), so no
+      // load reaches past the row end.
+      if (y0 + kYB <= ty_max) {
+        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
 #pragma unroll
-    for (int i = 0; i < XPL; ++i) {
-      const int x = L * XPL + i;
+        for (int q = 0; q < kYB / 4; ++q)
 #pragma unroll
-      for (int k = 0; k < kYB; ++k) {
-        const int y = y0 + k;
-        dst[i][k] = (x < tx_max && y < ty) ? V0[(long)x * ty_max + y] : 0.f;
+          for (int i = 0; i < XPL; ++i) {
+            const f4u v = __builtin_nontemporal_load((const f4u*)((const char*)V0 + (roff[i] + (uint32_t)(y0 + 4 * q) * 4u)));
+            dst[i][4 * q] = v.x; dst[i][4 * q + 1] = v.y; dst[i][4 * q + 2] = v.z; dst[i][4 * q + 3] = v.w;
+          }
+        return;
       }
+    }
+#pragma unroll
+    for (int k = 0; k < kYB; ++k) {
+      const uint32_t y4 = (uint32_t)(y0 + k < ty ? y0 + k : ty - 1) * 4u;
+#pragma unroll
+      for (int i = 0; i < XPL; ++i)
+        dst[i][k] = __builtin_nontemporal_load((const float*)((const char*)V0 + (roff[i] + y4)));
     }
   };
   load_block(cur, 0);
@@ -60,10 +92,34 @@ __global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ va
     for (int k = 0; k < kYB; ++k) {
       const int y = y0 + k;
       if (y < ty) {   // wave-uniform
-        const float left = __shfl_up(V[XPL - 1], 1);   // V[L*XPL-1, y-1] from lane L-1
+        // V[L*XPL-1, y-1] from lane L-1 (lane 0's value is never used: its x = 0 row takes the constant)
+        const float left = (MODE & 1) ? __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(V[XPL - 1]), 0x138,
+                                                                             0xf, 0xf, false))
+                                : __shfl_up(V[XPL - 1], 1);
+        uint32_t w = 0;
+        if constexpr ((MODE & 16) != 0) {
+          // Lean update. Cells in the band (lo <= x < min(tx, y+1), lo = tx + y - ty) read only in-band cells
+          // of column y-1 (or the NEG / 0 constants), and the backtrack visits only in-band cells, so every
+          // row is updated unconditionally: out-of-band rows hold values nothing reads. For x != y, x != 0
+          // the backtrack's compare V[x,y-1] < V[x-1,y-1] is the max's own v_prev > v_cur, so one compare
+          // serves both; x == y forces the step (and takes NEG as v_cur), x == 0 never steps.
+          const int dy = y - L * XPL;   // x == y  <=>  i == dy
+#pragma unroll
+          for (int i = XPL - 1; i >= 0; --i) {
+            const bool diag = dy == i;
+            const float v_cur = diag ? neg : V[i];
+            float v_prev = (i > 0) ? V[i - 1] : left;
+            if (i == 0) v_prev = (L == 0) ? (y == 0 ? 0.f : neg) : v_prev;
+            const bool gt = v_prev > v_cur;
+            V[i] = (gt ? v_prev : v_cur) + cur[i][k];
+            const bool down = (i > 0 || L != 0) && (diag || gt);
+            w |= (down ? 1u : 0u) << i;
+          }
+          bits[y][L] = (uint16_t)w;
+          continue;
+        }
         const int lo = tx + y - ty;                     // band: lo <= x < min(tx, y+1)
         const int hi = min(tx, y + 1);
-        uint32_t w = 0;
 #pragma unroll
         for (int i = XPL - 1; i >= 0; --i) {
           const int x = L * XPL + i;
@@ -87,7 +143,43 @@ __global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ va
       for (int k = 0; k < kYB; ++k) cur[i][k] = nxt[i][k];
   }
   __syncthreads();
-  if (L == 0) {
+  if constexpr ((MODE & 4) != 0) {
+    // Windowed backtrack. Within 64 steps idx falls by at most 63, so for the chunk of columns yc, yc-1, ...,
+    // yc-63 every row visited lies in [idx0-63, idx0]. Lane l gathers the "step down" bits of column yc-l for
+    // exactly those rows into a 64-bit window (parallel LDS reads); the serial walk then reads lane l's
+    // window with v_readlane (scalar registers, no memory latency) and records the falls as a 64-bit mask, from
+    // which every lane recovers its own idx (mbcnt), so the chunk's 64 path entries are one coalesced store.
+    int idx = tx - 1;
+    for (int yc = ty - 1; yc >= 0; yc -= 64) {
+      const int rb = idx - 63;   // window row 0
+      const int y = yc - L;
+      uint64_t win = 0;
+      if (y >= 0) {
+        const int w1 = idx / XPL;
+        for (int lw = (rb > 0 ? rb : 0) / XPL; lw <= w1; ++lw) {
+          const uint64_t w = bits[y][lw];
+          const int rel = lw * XPL - rb;
+          win |= rel >= 0 ? (w << rel) : (w >> (-rel));
+        }
+      }
+      const uint32_t lo = (uint32_t)win, hi = (uint32_t)(win >> 32);
+      const int n = yc + 1 < 64 ? yc + 1 : 64;
+      const int idx0 = idx;
+      uint64_t D = 0;   // bit l: idx fell at step l
+#pragma unroll
+      for (int l = 0; l < 64; ++l) {
+        if (l < n) {
+          const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane(lo, l);   // (readlane returns int)
+          const uint64_t d = (sw >> (idx - rb)) & 1u;
+          D |= d << l;
+          idx -= (int)d;
+        }
+      }
+      // lane L's entry = idx0 - (falls before step L) = idx0 - popcount(D below lane L)
+      if (y >= 0) P[y] = idx0 - (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(D >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)D, 0u));
+    }
+  } else if (L == 0) {
     int idx = tx - 1;
     for (int y = ty - 1; y >= 0; --y) {
       P[y] = idx;
@@ -138,11 +230,29 @@ __global__ __launch_bounds__(256) void mas_fill_kernel(const int32_t* __restrict
   for (int y = threadIdx.x; y < ty_max; y += 256) out[y] = (P[y] == x) ? 1 : 0;
 }
 
+int mas_mode() {
+  static const int v = [] {
+    const char* e = getenv("GT_MAS_MODE");
+    return e ? atoi(e) : 53;
+  }();
+  return v;
+}
+
+template <int XPL, int MODE>
+void launch_dp_v(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
+                 int ty_max, float neg, int32_t* pidx, hipStream_t s) {
+  if (ycap <= 256) hipLaunchKernelGGL((mas_dp_kernel<XPL, 256, MODE>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
+  else hipLaunchKernelGGL((mas_dp_kernel<XPL, 1024, MODE>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
+}
+
 template <int XPL>
 hipError_t launch_dp(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
                      int ty_max, float neg, int32_t* pidx, hipStream_t s) {
-  if (ycap <= 256) hipLaunchKernelGGL((mas_dp_kernel<XPL, 256>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
-  else hipLaunchKernelGGL((mas_dp_kernel<XPL, 1024>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
+  switch (mas_mode()) {
+    case 0: launch_dp_v<XPL, 0>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
+    case 21: launch_dp_v<XPL, 21>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
+    default: launch_dp_v<XPL, 53>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
+  }
   return hipGetLastError();
 }
 
