@@ -25,7 +25,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 GT_DEV float mishf(float x) {
   const float e = __expf(fminf(x, 20.f));
   const float n = e * (e + 2.f);
-  return x * __fdividef(n, n + 2.f);
+  return x * (n * __builtin_amdgcn_rcpf(n + 2.f));   // v_rcp_f32 (1 ulp): __fdividef lowered to the IEEE divide
 }
 
 // ---------------------------------------------------------------- storage
