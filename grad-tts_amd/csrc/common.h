@@ -27,6 +27,15 @@ GT_DEV float mishf(float x) {
   const float n = e * (e + 2.f);
   return x * (n * __builtin_amdgcn_rcpf(n + 2.f));   // v_rcp_f32 (1 ulp): __fdividef lowered to the IEEE divide
 }
+// Mish for a bf16 activation path: tanh(softplus(x)) = 1 - 2 / ((e^x + 1)^2 + 1) -> one exp2, one rcp, four
+// FMA-class ops (conv64.hip's mish_tb form). e^x = inf gives x (torch's threshold); absolute error <= |x| 2^-23
+// (cancellation for x << 0), far below the bf16 rounding of the result. fp32 paths keep mishf.
+template <class A> GT_DEV float mish_act(float x) { return mishf(x); }
+template <> GT_DEV float mish_act<bf16>(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+  const float t = e + 1.f;
+  return x * __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_fmaf(t, t, 1.f)), 1.f);
+}
 
 // ---------------------------------------------------------------- storage
 template <class A> struct Act;

@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         const u32x4 u = preg[j];
         item_to_f(make_uint4(u[0], u[1], u[2], u[3]), v, A());
 #pragma unroll
-        for (int k = 0; k < C::ICH; ++k) v[k] = (mishf(v[k] * sc[k] + sh[k]) + tb[k]) * m;
+        for (int k = 0; k < C::ICH; ++k) v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) + tb[k]) * m;
         const uint4 o = f_to_item(v, A());
         preg[j] = u32x4{o.x, o.y, o.z, o.w};
       }
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
           if (IN == IN_GN) {
 #pragma unroll
             for (int k = 0; k < C::ICH; ++k)   // (Mish(GN(h)) * m + tb) * m, m in {0,1}
-              v[k] = (mishf(v[k] * sc[k] + sh[k]) + tb[k]) * m;
+              v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) + tb[k]) * m;
           } else {                             // IN_MASK, a fractional mask among this thread's items
 #pragma unroll
             for (int k = 0; k < C::ICH; ++k) v[k] *= m;
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
               // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
               const float m = om[rb][half];
 #pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] = mishf(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
+              for (int k = 0; k < 8; ++k) v[k] = mish_act<A>(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
             } else {                                   // Residual: fn(x) + x   (diffusion.py:108)
 #pragma unroll
               for (int k = 0; k < 8; ++k) v[k] += e[k];

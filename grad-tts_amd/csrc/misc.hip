@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 #pragma unroll
       for (int k = 0; k < ICH; ++k) {
         const int c = it * ICH + k;
-        const float y = mishf(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
+        const float y = mish_act<A>(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
         acc += s_w[c] * (y * m);                               // final_conv(x * mask)
       }
     }
@@ -122,12 +122,12 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
       item_to_f(vp[i], v, A());
       if (APPLY) {
 #pragma unroll
-        for (int k = 0; k < ICH; ++k) v[k] = (mishf(v[k] * sc[k] + sh[k]) * m + tb[k]) * m;
+        for (int k = 0; k < ICH; ++k) v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) * m + tb[k]) * m;
       } else {
         float x[ICH];
         item_to_f(vx[i], x, A());
 #pragma unroll
-        for (int k = 0; k < ICH; ++k) v[k] = mishf(v[k] * sc[k] + sh[k]) * m + x[k] * m;
+        for (int k = 0; k < ICH; ++k) v[k] = mish_act<A>(v[k] * sc[k] + sh[k]) * m + x[k] * m;
       }
       *reinterpret_cast<uint4*>(out + e) = f_to_item(v, A());
     }
