@@ -591,7 +591,7 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 // 3x3 launch with the tile height conv_tf picks (5 rows only exists for 128-wide tiles)
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
-  if constexpr (NT == 128 && IN != IN_GN && IN != IN_INPUT)
+  if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }

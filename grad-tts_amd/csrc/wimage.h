@@ -27,10 +27,17 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_L1_TF5
 #define GT_L1_TF5 0
 #endif
+// Option (off: the 5-row GroupNorm-input variant spills 51 VGPRs to scratch at 2 workgroups/CU and measured
+// 196 us vs 139 us per launch, same-box A/B tools/ab_variant.sh): the level-1 GroupNorm-input conv (128 -> 128,
+// 40 rows) on 5-row tiles with the in-register GroupNorm transform, 1024 tiles at B = 32 instead of 1280.
+#ifndef GT_L1_TF5_GN
+#define GT_L1_TF5_GN 0
+#endif
 // mel rows per 3x3 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid rows)
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f) {
-  return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 && im != 2 /*IN_GN*/ &&
-          (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ? 5 : 4;
+  return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
+          ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
+           (GT_L1_TF5_GN && im == 2 && cout == 128 && f == 40))) ? 5 : 4;
 }
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
