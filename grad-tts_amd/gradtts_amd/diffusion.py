@@ -203,8 +203,11 @@ class GradLogPEstimator2d(torch.nn.Module):
             pass
 
     def _workspace(self, device, dcode, B, T, N):
+        # One cached workspace per (device, dtype, STREAM): calls are stream-ordered, so reuse on one stream is
+        # safe, but concurrent calls on two streams must not share scratch (they raced before this was keyed
+        # by stream; tests/test_decoder_gpu.py::test_concurrent_streams_match_one_stream).
         nbytes = lib().gt_decoder_workspace_bytes(self._handle, dcode, B, T, N)
-        key = (device, dcode)
+        key = (device, dcode, torch.cuda.current_stream(device).cuda_stream)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < nbytes:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=device)

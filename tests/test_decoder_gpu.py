@@ -138,6 +138,27 @@ def test_bench_shape_deterministic_and_batch_invariant(cdt):
     assert torch.equal(y1[5:7], sub), (y1[5:7] - sub).abs().max().item()
 
 
+def test_concurrent_streams_match_one_stream():
+    """Two decodes in flight on two HIP streams (each half of a batch) give the same mels as one call on one
+    stream: the module's cached scratch is per stream, and the arithmetic is batch-invariant."""
+    from gradtts_amd.params import synthetic_inputs
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    mu, z, mask, _ = synthetic_inputs(77, 8, 256)
+    zc, mc, muc = _cuda(z), _cuda(mask), _cuda(mu)
+    full = dec(zc, mc, muc, 4)
+    cur = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for i, st in enumerate(streams):
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            s = slice(4 * i, 4 * i + 4)
+            outs.append(dec(zc[s], mc[s], muc[s], 4))
+    for st in streams:
+        cur.wait_stream(st)
+    assert torch.equal(torch.cat(outs), full)
+
+
 # ---- GT_BF16_W8: fp8 e4m3 weights for the 3x3 / Downsample / Upsample convs, bf16 activations
 # (BASELINE.json config 5). Oracle = the reference algorithm run with the dequantized weights
 # (oracle.decoder.fp8_params, whose quantizer is bit-identical to the library's: test_fp8_cpu.py);
