@@ -129,12 +129,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
     const float m_new = fmaxf(m_run, mloc);
     float lsum = 0.f;
+    // exp(a - m) as exp2(fma(a, log2 e, -m log2 e)): one FMA + v_exp_f32 per element instead of sub, mul, exp
+    constexpr float L2E = 1.44269504088896341f;
+    const float mL = m_new * L2E;
     if (full) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          const float e = __expf(ak[rb][j] - m_new);
+          const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(ak[rb][j], L2E, -mL));
           ak[rb][j] = e;
           lsum += e;
         }
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const bool valid = pos0 + rb * 32 + acc_row(j, h) < tend;
-          const float e = valid ? __expf(ak[rb][j] - m_new) : 0.f;
+          const float e = valid ? __builtin_amdgcn_exp2f(__builtin_fmaf(ak[rb][j], L2E, -mL)) : 0.f;
           ak[rb][j] = e;
           lsum += e;
         }
