@@ -238,6 +238,18 @@ int mas_mode() {
   return v;
 }
 
+// ty_max % 4 == 0: 16-byte stores, 4 columns per thread (rows are then 16-byte aligned)
+__global__ __launch_bounds__(256) void mas_fill4_kernel(const int32_t* __restrict__ pidx, int tx_max, int ty_max,
+                                                        int32_t* __restrict__ paths) {
+  const int b = blockIdx.y, x = blockIdx.x;
+  const int4* P = reinterpret_cast<const int4*>(pidx + (long)b * ty_max);
+  int4* out = reinterpret_cast<int4*>(paths + ((long)b * tx_max + x) * ty_max);
+  for (int q = threadIdx.x; q < ty_max / 4; q += 256) {
+    const int4 p = P[q];
+    out[q] = make_int4(p.x == x, p.y == x, p.z == x, p.w == x);
+  }
+}
+
 template <int XPL, int MODE>
 void launch_dp_v(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
                  int ty_max, float neg, int32_t* pidx, hipStream_t s) {
@@ -292,7 +304,8 @@ int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, co
     else e = launch_dp<16>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
   }
   if (e != hipSuccess) return GT_ERR_HIP;
-  hipLaunchKernelGGL(mas_fill_kernel, dim3(TX, B), dim3(256), 0, s, pidx, TX, TY, paths);
+  if (TY % 4 == 0 && ((uintptr_t)paths & 15) == 0) hipLaunchKernelGGL(mas_fill4_kernel, dim3(TX, B), dim3(256), 0, s, pidx, TX, TY, paths);
+  else hipLaunchKernelGGL(mas_fill_kernel, dim3(TX, B), dim3(256), 0, s, pidx, TX, TY, paths);
   return hipGetLastError() == hipSuccess ? GT_OK : GT_ERR_HIP;
 }
 
