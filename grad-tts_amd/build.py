@@ -21,7 +21,7 @@ OBJ = os.path.join(CSRC, "_obj")
 OUT = os.path.join(HERE, "gradtts_amd", "libgradtts.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GRADTTS_ARCH", "gfx950")
-SOURCES = ["conv.hip", "conv4.hip", "conv64.hip", "attn.hip", "misc.hip", "mas.hip", "decoder.cpp"]
+SOURCES = ["conv.hip", "conv64.hip", "attn.hip", "misc.hip", "mas.hip", "decoder.cpp"]
 # -packed-fp32-ops: keep the compiler from emitting v_pk_{fma,add,mul}_f32. With them the GroupNorm
 # sum-of-squares chain in conv_kernel's epilogue produced timing-dependent (run-to-run different)
 # results on MI355X while the plain sums stayed bit-exact (tools/diag_parts.py); without them every

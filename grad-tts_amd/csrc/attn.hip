@@ -127,11 +127,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           if (pos0 + rb * 32 + acc_row(j, h) < tend) mloc = fmaxf(mloc, ak[rb][j]);
     }
     mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
-    const float m_new = fmaxf(m_run, mloc);
-    float lsum = 0.f;
-    // exp(a - m) as exp2(fma(a, log2 e, -m log2 e)): one FMA + v_exp_f32 per element instead of sub, mul, exp
+    // exp(a - m) as exp2(fma(a, log2 e, -mL)) with mL = fl(m log2 e): one FMA + v_exp_f32 per element. The running
+    // statistic is mL itself (rounding is monotonic, so max and argmax are unchanged), and every rescale below and
+    // in attn_merge is exp2 of a difference of these rounded values: the factors cancel exactly across blocks.
     constexpr float L2E = 1.44269504088896341f;
-    const float mL = m_new * L2E;
+    const float mL = fmaxf(m_run, mloc * L2E);
+    const float m_new = mL;
+    float lsum = 0.f;
     if (full) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     lsum += __shfl_xor(lsum, 32);
     // rescale the running sum/context only where the running max moved (rare after the first blocks)
     if (__any(m_new != m_run)) {
-      const float alpha = (m_run == NEG_INF) ? 0.f : __expf(m_run - m_new);
+      const float alpha = (m_run == NEG_INF) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
       l_run *= alpha;
       // ctx rows are d = acc_row(j, h); the factor for row d lives in lane d
 #pragma unroll
@@ -183,14 +185,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   }
 
   float* part = p.part + (((long)b * p.ntile + tile) * 4 + wv) * 1088;
-  if (h == 0) { part[r] = m_run; part[32 + r] = l_run; }
+  if (h == 0) { part[r] = m_run; part[32 + r] = l_run; }   // m_run = fl(max k * log2 e)
 #pragma unroll
   for (int j = 0; j < 16; ++j) part[64 + acc_row(j, h) * 32 + r] = ctx[j];
 }
 
 // grid (B, 4 heads): merge the tiles' online-softmax partials, normalise, and fold the head's part of
-// the output projection:
-//   ctx_h[d][e]  = sum_t exp(m_t[d] - M[d]) ctx_t[d][e] / sum_t exp(m_t[d] - M[d]) l_t[d]
+// the output projection (m_t, M: running maxima in log2 units, as attn_kv keeps them):
+//   ctx_h[d][e]  = sum_t 2^(m_t[d] - M[d]) ctx_t[d][e] / sum_t 2^(m_t[d] - M[d]) l_t[d]
 //   A[co][32h+d] = g * sum_e Wout[co][32h+e] ctx_h[d][e]     (einsum 'bhde,bhdn->bhen' + to_out + Rezero)
 __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
                                                           int C, float* Aout) {
@@ -211,14 +213,14 @@ __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int
     const float* pt = base + t * tstride;
     const float mt = pt[d], lt_ = pt[32 + d];
     const f32x4 v = *reinterpret_cast<const f32x4*>(pt + 64 + d * 32 + e0);
-    if (mt > M) {                                      // rescale what was merged so far
-      const float r = __expf(M - mt);
+    if (mt > M) {                                      // rescale what was merged so far (m in log2 units)
+      const float r = __builtin_amdgcn_exp2f(M - mt);
       L *= r;
 #pragma unroll
       for (int k = 0; k < 4; ++k) c[k] *= r;
       M = mt;
     }
-    const float w = __expf(mt - M);
+    const float w = __builtin_amdgcn_exp2f(mt - M);
     L += w * lt_;
 #pragma unroll
     for (int k = 0; k < 4; ++k) c[k] += w * v[k];
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (s_gl[q][d] == 0.f) continue;                 // empty group (ntile < 4)
-      const float r = __expf(s_gm[q][d] - Mt);
+      const float r = __builtin_amdgcn_exp2f(s_gm[q][d] - Mt);
       Lt += r * s_gl[q][d];
 #pragma unroll
       for (int k = 0; k < 4; ++k) ct[k] += r * s_gc[q][d][e0 + k];

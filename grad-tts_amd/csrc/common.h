@@ -125,10 +125,6 @@ struct GnLoad {
 };
 GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
   GnLoad g;
-#ifdef GT_EXP_NO_GN_REDUCE
-  for (int q = 0; q < GN_Q; ++q) g.v[q] = 0.f;
-  return g;
-#endif
   const int t = threadIdx.x, k = t & 15, grp = t >> 4;
   const float* pb = part + (long)b * nparts * 16 + k;
 #pragma unroll
@@ -142,11 +138,6 @@ GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
 GT_DEV void gn_finish(const GnLoad& g, const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd,
                       double* s_red) {
   const int t = threadIdx.x, k = t & 15, grp = t >> 4;
-#ifdef GT_EXP_NO_GN_REDUCE   // timing-only: what the per-consumer reduction costs
-  if (t < 8) { s_mean[t] = 0.f; s_rstd[t] = 1.f; }
-  lds_barrier();
-  return;
-#endif
   if (t < 256) {
     double acc = 0.0;
 #pragma unroll

@@ -29,20 +29,6 @@
 
 namespace gt {
 
-#ifdef GT_STAMPS
-// Diagnostic timeline (tools/stamps.py): s_memtime at phase boundaries of wave 0 of every workgroup of the
-// last launch that matches the filter (3x3, 64->64 at 80 mel rows, IN = GT_STAMPS).
-constexpr int ST_PER_WG = 48, ST_WGS = 8192;
-__device__ unsigned long long g_stamps[ST_WGS * ST_PER_WG];
-__device__ unsigned int g_stamp_hwid[ST_WGS];
-#define STAMP(k)                                                                          \
-  do {                                                                                    \
-    if (stamp_on && threadIdx.x == 0) g_stamps[blockIdx.x * ST_PER_WG + (k)] = __builtin_readcyclecounter(); \
-  } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
-
 #ifndef GT_CAP_T
 #define GT_CAP_T 3
 #endif
@@ -153,20 +139,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int wm = wv % C::WM, wn = wv / C::WM;
-#ifdef GT_STAMPS
-#ifndef GT_STAMPS_C
-#define GT_STAMPS_C 64
-#define GT_STAMPS_F 80
-#endif
-  const bool stamp_on = KIND == CONV3 && IN == GT_STAMPS && sizeof(A) == 2 && p.Cin == GT_STAMPS_C &&
-                        p.Cout == GT_STAMPS_C && p.Fout == GT_STAMPS_F && blockIdx.y == 0 && blockIdx.x < ST_WGS;
-  if (stamp_on && tid == 0) {
-    unsigned int hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    g_stamp_hwid[blockIdx.x] = hw;
-  }
-#endif
-  STAMP(0);
   const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
   const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
 
@@ -242,42 +214,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, voff[j], (c0 - p.C0) * ES, 0);
     }
   };
-#ifdef GT_EXP_EARLY_GN
-  constexpr bool EARLY = IN == IN_GN;   // transform in registers during the previous chunk's MFMAs
-#else
-  constexpr bool EARLY = false;
-#endif
-  auto transform_patch = [&](int c0) {
-    float sc[C::ICH], sh[C::ICH], tb[C::ICH];
-#pragma unroll
-    for (int k = 0; k < C::ICH; ++k) {
-      const int c = c0 + sub * C::ICH + k;
-      sc[k] = s_sc[c]; sh[k] = s_sh[c]; tb[k] = s_tb[c];
-    }
-#pragma unroll
-    for (int j = 0; j < C::PPT; ++j) {
-      if (tid + 256 * j < C::PITEMS) {
-        const float m = pm[j];
-        float v[C::ICH];
-        const u32x4 u = preg[j];
-        item_to_f(make_uint4(u[0], u[1], u[2], u[3]), v, A());
-#pragma unroll
-        for (int k = 0; k < C::ICH; ++k) v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) + tb[k]) * m;
-        const uint4 o = f_to_item(v, A());
-        preg[j] = u32x4{o.x, o.y, o.z, o.w};
-      }
-    }
-  };
   auto store_patch = [&](int c0) {
-    if (EARLY) {
-      if (c0 == 0) transform_patch(0);
-#pragma unroll
-      for (int j = 0; j < C::PPT; ++j) {
-        const int it = tid + 256 * j;
-        if (it < C::PITEMS) *reinterpret_cast<u32x4*>(sA + (it / C::SUBS) * C::POSB + sub * 16) = preg[j];
-      }
-      return;
-    }
     float sc[C::ICH], sh[C::ICH], tb[C::ICH];
     if (IN == IN_GN) {
 #pragma unroll
@@ -364,29 +301,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   }
   if (tid < NT) s_bias[tid] = c_bias;                 // all visible after the first chunk barrier
   if (W8 && tid < NT) s_wsc[tid] = c_wsc;
-  STAMP(1);
   for (int ch = 0; ch < nchunk; ++ch) {
     const int c0 = ch * C::CK;
-    STAMP(2 + 5 * ch);
     cta_sync();                                        // previous chunk's fragments are consumed
-    STAMP(3 + 5 * ch);
     dma_weights(ch);                                   // issued first: its latency overlaps the patch store
     store_patch(c0);
-    STAMP(4 + 5 * ch);
     // The weight DMA must have landed before any wave reads sW; the compiler does not track
     // global_load_lds reliably (it was missing in the 1x1/128-wide instantiation: an intermittent,
     // load-dependent race), so the wait is explicit.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    STAMP(5 + 5 * ch);
     cta_sync();
-    STAMP(6 + 5 * ch);
     if (ch + 1 < nchunk) {
       if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && c0 + C::CK == p.C0) set_offsets(p.C1);
       load_patch(c0 + C::CK);                          // in flight during this chunk's MFMAs
     }
 #pragma unroll
     for (int tap = 0; tap < C::NTAP; ++tap) {
-      if (EARLY && tap == C::NTAP / 2 && ch + 1 < nchunk) transform_patch(c0 + C::CK);
       int dr, dc;
       if (CONVT) {
         // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0,
@@ -423,7 +353,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     }
   }
 
-  STAMP(40);
   // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
   // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
   // LDS instructions of one wave execute in order, so the transposition only needs its own LDS traffic
@@ -538,7 +467,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       wave_sync();
     }
   }
-  STAMP(42);
   if (OUT == OUT_STATS) {
     // per 8-channel sub-group: reduce over the wave's positions (the 16 lanes with equal lane&3):
     // rotations by 4 and 8 inside each 16-lane row (DPP), then across the four rows
@@ -556,9 +484,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
       }
     }
-    STAMP(43);
     __syncthreads();
-    STAMP(44);
     // ... then per GroupNorm group over waves / sub-groups in a fixed order, one slot per workgroup
     if (tid < 8) {
       const int gshift = __builtin_ctz(p.Cout >> 3);   // group size Cout/8 is a power of two (host check)
@@ -582,7 +508,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       dst[1] = Q;
     }
   }
-  STAMP(41);
 }
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0, int TF_ = 4>
@@ -655,11 +580,4 @@ hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const
   return conv_nt(1, p.Cout) == 128 ? dispatch<bf16, 128>(kind, im, om, p, s) : dispatch<bf16, 64>(kind, im, om, p, s);
 }
 
-#ifdef GT_STAMPS
-extern "C" int gt_debug_read_stamps(unsigned long long* out, unsigned int* hwid) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(hwid, HIP_SYMBOL(g_stamp_hwid), sizeof(g_stamp_hwid)) != hipSuccess) return -1;
-  return 0;
-}
-#endif
 }  // namespace gt

@@ -51,23 +51,8 @@ constexpr int WTAP_B = 2 * NCH * 64 * 16;                 // one tap's fragments
 constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + NW * 8 + 16) * 4 + 272 * 8;
 // taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room
 constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
-constexpr int SPH = 4;                                    // stamps per tile (diagnostics)
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
-
-#ifdef GT_C64_STAMPS
-// Diagnostic timeline (tools/stamps64.py): s_memtime at phase boundaries of the first and last wave of every workgroup,
-// last launch of conv64_kernel<GT_C64_STAMPS> on an 80-row grid.
-constexpr int S64_WG = 256, S64_TILES = 24, S64_PH = c64::SPH;
-__device__ unsigned long long g_s64[S64_WG * 2 * (2 + S64_TILES * S64_PH)];
-#define ST64(k)                                                                                           \
-  do {                                                                                                    \
-    if (st_on && (lane == 0) && (wv == 0 || wv == c64::NW - 1))                                          \
-      g_s64[(blockIdx.x * 2 + (wv != 0)) * (2 + S64_TILES * S64_PH) + (k)] = __builtin_readcyclecounter(); \
-  } while (0)
-#else
-#define ST64(k) do {} while (0)
-#endif
 
 // Sum of x over the 16-lane row (every lane, fixed order): DPP row rotations by 1, 2, 4, 8
 GT_DEV float row_sum16(float x) {
@@ -96,11 +81,12 @@ GT_DEV float mish_tb(float y, float tb) {
   return __builtin_fmaf(y, __builtin_fmaf(-2.f, r, 1.f), tb);
 }
 
-// IN: IN_MASK / IN_GN / IN_PLAIN; FRAC (IN_MASK only): the mask may hold values other than 0 and 1.
+// IN: IN_MASK / IN_GN / IN_PLAIN. Masks from sequence_mask are 0/1: x * m is then a select, decided per item on
+// the device (a fractional mask value takes a multiply in a branch that 0/1 masks never enter).
 // One workgroup = one segment: L consecutive 4 x 32 tiles down the mel axis of one utterance's 32-frame column.
 // Two workgroups share a CU (one wave of each per SIMD) and drift out of phase, so one's staging/epilogue VALU
 // work overlaps the other's MFMAs.
-template <int IN, bool FRAC>
+template <int IN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
@@ -122,10 +108,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int col = blockIdx.x / kseg, part = blockIdx.x - col * kseg;
   const int b = col / n_tt, tt = col - b * n_tt;
   const int ft0 = part * L;
-#ifdef GT_C64_STAMPS
-  const bool st_on = IN == GT_C64_STAMPS && F == 80 && blockIdx.x < S64_WG && L <= S64_TILES;
-#endif
-  ST64(0);
 
   // ---- weights -> registers: A fragment (ch, tap) = output channel cb*32 + r, input channels 16 ch + 8h .. +7,
   // from the fragment-ordered image (decoder.cpp pack_conv64): one contiguous 1 KiB per wave instruction
@@ -165,29 +147,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   };
   auto put_item = [&](int it, int slot, u32x4_t v4, float m) {
-    if (IN == IN_MASK && !FRAC) {
-      v4 = m == 0.f ? u32x4_t{0u, 0u, 0u, 0u} : v4;
-    } else if (IN != IN_PLAIN) {
-      float v[8];
-      item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
-      if (IN == IN_GN) {   // (Mish(GN(h)) * m + tb) * m, m in {0,1}  (diffusion.py:57-58, 76)
-#pragma unroll
-        for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
-          const float* cf = s_coef + sub * 8 + hq * 4;
-          const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
-          const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
-          const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_tb(v[4 * hq + k] * sc[k] + sh[k], tb[k]);
-        }
-        const uint4 o = f_to_item(v, bf16());
-        v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
-      } else {             // x * m, fractional mask
+    if (IN == IN_MASK) {
+      if (__builtin_expect(m != 0.f && m != 1.f, 0)) {   // x * m, fractional mask value
+        float v[8];
+        item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] *= m;
         const uint4 o = f_to_item(v, bf16());
         v4 = u32x4_t{o.x, o.y, o.z, o.w};
+      } else {
+        v4 = m == 0.f ? u32x4_t{0u, 0u, 0u, 0u} : v4;
       }
+    } else if (IN == IN_GN) {   // (Mish(GN(h)) * m + tb) * m, m in {0,1}  (diffusion.py:57-58, 76)
+      float v[8];
+      item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
+        const float* cf = s_coef + sub * 8 + hq * 4;
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
+        const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_tb(v[4 * hq + k] * sc[k] + sh[k], tb[k]);
+      }
+      const uint4 o = f_to_item(v, bf16());
+      v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
     }
     *reinterpret_cast<u32x4_t*>(sR + slot * ROWB + ((it >> 3) % PC) * POSB + sub * 16) = v4;
   };
@@ -236,13 +220,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
   for (int j = 0; j < PPT; ++j) issue_new(j, 1);
   lds_barrier();
-  ST64(1);
 
   // per-lane GroupNorm partials of the whole segment (group cb*4 + pr*2 + h), accumulated tile by tile, pass by
   // pass in a fixed order; reduced across lanes and waves once, at the end
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
   for (int k = 0; k < L; ++k) {
-    ST64(2 + k * SPH + 0);
     const int ft = ft0 + k;
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
@@ -274,7 +256,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           issue_new(j, k + 2);
         }
       }
-      ST64(2 + k * SPH + 1 + ps);
 
       // ---- epilogue of this pass. Lane (j = r, h) holds channels cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of
       // position j (registers 0-3, 4-7, 8-11, 12-15); swapping registers 4-7 <-> 0-3 and 12-15 <-> 8-11 across
@@ -313,7 +294,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       }
     }
     lds_barrier();   // tile k+1's rows complete
-    ST64(2 + k * SPH + 3);
   }
   // segment done: this wave's groups over its positions, then the 2 waves of each channel half -> one slot
 #pragma unroll
@@ -339,12 +319,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[1] = Q;
   }
 }
-
-#ifdef GT_C64_STAMPS
-extern "C" int gt_debug_read_c64_stamps(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_s64), sizeof(g_s64)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 static int cu_count() {
   static int n = [] {
@@ -373,14 +347,13 @@ static int conv64_seg(int F) {
 
 int conv64_nparts(int F, int T) { return ((T + 31) / 32) * ((F / 4) / conv64_seg(F)); }
 
-hipError_t launch_conv64(InMode im, bool mask01, const ConvParams& p, hipStream_t s) {
+hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
   const int L = conv64_seg(p.Fout);
   const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
-  if (im == IN_MASK && mask01) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(256), 0, s, p, L);
-  else if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(256), 0, s, p, L);
-  else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), dim3(256), 0, s, p, L);
-  else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), dim3(256), 0, s, p, L);
+  if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK>), dim3(grid), dim3(256), 0, s, p, L);
+  else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN>), dim3(grid), dim3(256), 0, s, p, L);
+  else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN>), dim3(grid), dim3(256), 0, s, p, L);
   else return hipErrorNotSupported;
   return hipGetLastError();
 }

@@ -149,6 +149,7 @@ struct gt_decoder {
   std::map<std::string, void*> dp[3];
   std::map<std::string, int> cinpad[3];
   float freqs[32];
+  int64_t packs = 0;          // weight packings performed (checkpoint tests: exactly one per parameter change)
   // profiling (diagnostics / bench roofline): HIP events around every launch
   bool prof = false;
   std::string prof_prefix;   // non-empty: only launches whose "<kernel>@<shape>" name starts with it
@@ -302,19 +303,6 @@ void pack_conv8(Blob& blob, gt_decoder* d, const std::string& key, const std::ve
   d->cinpad[2][key] = W.nchunk * W.ck;
 }
 
-// pack a 3x3 [Cout][Cin][3][3] weight into the conv4 image (wimage.h conv4_wimg_off), bf16
-void pack_conv4(Blob& blob, const std::string& key, const std::vector<float>& w, int cout, int cin) {
-  const int nt = conv4_pick(cout).nt;
-  std::vector<uint8_t> img((size_t)cout * 9 * cin * 2, 0);
-  for (int co = 0; co < cout; ++co)
-    for (int ci = 0; ci < cin; ++ci)
-      for (int t = 0; t < 9; ++t) {
-        const uint16_t hb = f2bf(w[((size_t)co * cin + ci) * 9 + t]);
-        memcpy(img.data() + conv4_wimg_off(nt, cin, co, t, ci), &hb, 2);
-      }
-  blob.put(key, img.data(), img.size());
-}
-
 // pack a 64->64 3x3 [Cout][Cin][3][3] weight in conv64's register-fragment order (conv64.hip), bf16:
 // [cb 2][chunk 4][tap 9][lane 64][8 ci]: lane (r, h) = output channel cb*32 + r, input channels 16 chunk + 8h .. +7
 void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w) {
@@ -329,15 +317,6 @@ void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w
             img[i++] = f2bf(w[((size_t)co * 64 + ci) * 9 + tap]);
           }
   blob.put(key, img.data(), img.size() * 2);
-}
-
-// conv4 (LDS-DMA pipeline) for the bf16 3x3 stride-1 convs: GT_CONV4=1 selects it instead of conv_kernel
-static bool conv4_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("GT_CONV4");
-    return e && atoi(e) != 0;   // experimental LDS-DMA pipeline (conv4.hip), off by default
-  }();
-  return v;
 }
 
 // conv64 (persistent weight-resident 64-channel 3x3 conv, conv64.hip) for bf16; GT_CONV64=0 disables it (A/B)
@@ -370,8 +349,6 @@ int prepare(gt_decoder* d, int code) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
       if (dt && ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 64 && shp[2] == 3 && shp[3] == 3)
         pack_conv64(blob, k + ".w64", w);
-      if (dt && conv4_enabled() && ends_with(k, ".block.0.weight") && shp[1] % 16 == 0)
-        pack_conv4(blob, k + ".v4", w, (int)shp[0], (int)shp[1]);
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
     } else if (ends_with(k, "to_qkv.weight")) {
@@ -416,13 +393,14 @@ int prepare(gt_decoder* d, int code) {
   d->dp[code].clear();
   for (auto& kv : blob.off) d->dp[code][kv.first] = (uint8_t*)d->arena[code] + kv.second;
   d->dirty[code] = false;
+  d->packs += 1;
   return GT_OK;
 }
 
 // ---------------------------------------------------------------- workspace
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
-  size_t stats, part, G, Mw, tb, spk, flag, total;
+  size_t stats, part, G, Mw, tb, spk, total;
   int pmax;
   int tile_pos[3], ntile[3];
 };
@@ -459,7 +437,6 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.Mw = take((size_t)B * conv_wimg(dt, 1, 256, 256).total);
   L.tb = take((size_t)std::max<int64_t>(B, N) * 1792 * 4);
   L.spk = take((size_t)B * 80 * 4);
-  L.flag = take(sizeof(int));
   L.total = o;
   return L;
 }
@@ -476,7 +453,6 @@ struct Run {
   const float* mask; const float* mu; const float* xt; const float* spk_s;
   const float* tb; long tb_bstride;
   int stat_slot = 0;
-  bool mask01 = true;            // every mask value is 0 or 1 (checked once per API call)
   hipError_t err = hipSuccess;
   const char* probe = nullptr;   // diagnostics: copy the activation named `probe` to probe_out (NCHW fp32)
   float* probe_out = nullptr;
@@ -513,33 +489,18 @@ struct Run {
   }
 
   // 3x3 stride-1 conv with GroupNorm partial sums of the output; returns the number of partial slots per
-  // utterance it wrote. bf16 inputs without a transform (IN_PLAIN, or IN_MASK with a 0/1 mask) take the
-  // LDS-DMA pipeline (conv4.hip); everything else conv_kernel.
+  // utterance it wrote. bf16 64 -> 64 convs take conv64 (weight-resident), everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
     if (dt && conv64_enabled() && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
         d->dp[wi].count(wkey + ".w64")) {
       p.w = W(wkey + ".w64");
       const double pos = (double)p.B * p.Fout * p.Tout;
       timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
-            2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, mask01, p, s); });
+            2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
       return conv64_nparts(p.Fout, p.Tout);
     }
-    const bool v4 = dt && conv4_enabled() && (im == IN_PLAIN || (im == IN_MASK && mask01)) && p.Cin % 16 == 0 &&
-                    d->dp[wi].count(wkey + ".v4");
-    if (!v4) {
-      conv(CONV3, im, OUT_STATS, p);
-      return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
-    }
-    const Conv4Cfg c = conv4_pick(p.Cout);
-    p.w = W(wkey + ".v4");
-    p.mask_in = im == IN_MASK;
-    const double pos = (double)p.B * p.Fout * p.Tout;
-    const std::string name = "conv4_kernel<" + std::to_string(c.nt) + "," + std::to_string(c.tt) + "," +
-                             std::to_string(c.nw) + "," + std::to_string(c.ns) + ">@" + std::to_string(p.Cin) + "x" +
-                             std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
-    timed(name, 2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + (double)p.Cout * 9 * p.Cin * 2.0,
-          [&] { return launch_conv4(p, c, s); });
-    return conv4_nparts(p.Fout, p.Tout, p.Cout, c);
+    conv(CONV3, im, OUT_STATS, p);
+    return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
   }
 
   // diagnostics: "gnpart.<k>" copies GroupNorm partial slot k (B x pmax x 16 floats) after the launch that
@@ -610,10 +571,10 @@ struct Run {
       tap_part(stat_slot - 2);
     }
     {   // block2 conv on (Mish(GN(h1))*m + tb)*m
-      // The transform runs once per element in place (one extra read+write of h1) when the conv4 path
-      // takes the conv (bf16), and on wide fp32 levels (GT_GN_APPLY_MIN_C, default 256 channels), where
-      // the operand-load transform of conv_kernel is recomputed by every 128-channel tile and halo row.
-      const bool apply = (dt && conv4_enabled()) || Cout >= gn_apply_min_c() ||
+      // The transform runs once per element in place (one extra read+write of h1) on wide levels
+      // (GT_GN_APPLY_MIN_C, default 256 channels), where the operand-load transform of conv_kernel would be
+      // recomputed by every 128-channel tile and halo row.
+      const bool apply = Cout >= gn_apply_min_c() ||
                          (dt && GT_L1_TF5 && Cout == 128 && Fl(lvl) == 40);   // level 1: plain 5-row tiles
       if (apply) {
         RbOutParams a{};
@@ -760,6 +721,8 @@ struct Run {
   }
 };
 
+uint8_t* align_ws(void* ws) { return (uint8_t*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
+
 int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_t ws_bytes, int32_t N) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
   if (dtype != GT_F32 && dtype != GT_BF16 && dtype != GT_BF16_W8)
@@ -846,6 +809,8 @@ int gt_decoder_profile_read(gt_decoder* d, char* buf, size_t cap) {
   return GT_OK;
 }
 
+int64_t gt_decoder_pack_count(const gt_decoder* d) { return d ? d->packs : -1; }
+
 int gt_decoder_num_params(const gt_decoder* d) { return d ? (int)d->inv.size() : 0; }
 const char* gt_decoder_param_name(const gt_decoder* d, int i) {
   return (d && i >= 0 && i < (int)d->inv.size()) ? d->inv[i].name.c_str() : nullptr;
@@ -866,23 +831,11 @@ int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int
   return GT_OK;
 }
 
+// The workspace may have any alignment: compute calls align its base up to 256 bytes (the slack is in the size).
 size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int64_t T, int32_t n_timesteps) {
   (void)d;
   if (B <= 0 || T <= 0) return 0;
-  return layout(dtype ? 1 : 0, B, T, n_timesteps).total;
-}
-
-// Are all mask values 0 or 1 (sequence_mask)? Decides whether conv4 / conv64 may realise x*mask as a
-// select (zero-filled loads) instead of a multiply. One tiny reduction + a 4-byte read-back per API call (a stream sync).
-static bool mask_is_01(Run& R, const float* mask, int64_t B, int64_t T) {
-  if (!R.dt || !(conv4_enabled() || conv64_enabled())) return true;
-  int* flag = (int*)(R.ws + R.L.flag);
-  int host = 1;
-  R.chk(hipMemsetAsync(flag, 0, sizeof(int), R.s));
-  R.chk(launch_mask_check(mask, B * T, flag, R.s));
-  R.chk(hipMemcpyAsync(&host, flag, sizeof(int), hipMemcpyDeviceToHost, R.s));
-  R.chk(hipStreamSynchronize(R.s));
-  return R.err == hipSuccess && host == 0;
+  return layout(dtype ? 1 : 0, B, T, n_timesteps).total + 256;
 }
 
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
@@ -895,11 +848,10 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
   if ((rc = prepare(d, dtype))) return rc;
   Run R;
   R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
-  R.ws = (uint8_t*)workspace;
+  R.ws = align_ws(workspace);
   R.L = layout(R.dt, B, T, 0);
   R.mask = mask; R.mu = mu; R.xt = x; R.spk_s = nullptr;
   R.probe = probe; R.probe_out = probe_out;
-  R.mask01 = mask_is_01(R, mask, B, T);
   float* tbuf = (float*)(R.ws + R.L.tb);
   TembParams tp;
   tp.rows = (int)B; tp.tvals = t; tp.n_steps = 0; tp.pe_scale = d->pe_scale; tp.freqs = R.Fp("freqs");
@@ -943,10 +895,9 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
   if ((rc = prepare(d, dtype))) return rc;
   Run R;
   R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
-  R.ws = (uint8_t*)workspace;
+  R.ws = align_ws(workspace);
   R.L = layout(R.dt, B, T, n_timesteps);
   R.mask = mask; R.mu = mu; R.xt = out; R.spk_s = nullptr;
-  R.mask01 = mask_is_01(R, mask, B, T);
   R.chk(launch_mask_copy(z, mask, (int)B, 80, (int)T, out, R.s));   // xt = z * mask  (diffusion.py:257)
   if (n_timesteps > 0) {
     float* tbuf = (float*)(R.ws + R.L.tb);

@@ -23,7 +23,6 @@ struct ConvParams {
   const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
   const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
-  int mask_in;                                        // conv4: input is x * mask (0/1 mask)
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* wscale;                                // non-null: fp8 e4m3 image (conv_wimg8), per-Cout scale
@@ -80,18 +79,10 @@ hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int
 // debug probe: channels-last activation [B][F][T][C] (act dtype) -> fp32 NCHW [B][C][F][T]
 hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, int C, float* dst, hipStream_t s);
 
-// 3x3 stride-1 bf16 convolution with LDS-DMA staging (conv4.hip): plain input or x*mask with a 0/1 mask,
-// weights in the conv4 image (wimage.h), GroupNorm partial sums of the output.
-struct Conv4Cfg { int nt, tt, nw, ns; };
-Conv4Cfg conv4_pick(int Cout);
-int conv4_nparts(int F, int T, int Cout, Conv4Cfg c);
-hipError_t launch_conv4(const ConvParams& p, Conv4Cfg c, hipStream_t s);
 // weight-resident 3x3 conv for Cin = Cout = 64, bf16 (conv64.hip); GroupNorm partial slots: one per 4 x 32 tile
 // (conv64_nparts). conv64_eligible: shape/layout preconditions (no concat, no fp8 image).
 int conv64_nparts(int F, int T);
 bool conv64_eligible(const ConvParams& p);
-hipError_t launch_conv64(InMode im, bool mask01, const ConvParams& p, hipStream_t s);
-// flag = 1 if any mask value is neither 0 nor 1 (flag must be zeroed first)
-hipError_t launch_mask_check(const float* mask, long n, int* flag, hipStream_t s);
+hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s);
 
 }  // namespace gt

@@ -272,9 +272,11 @@ hipError_t launch_dp(int ycap, const float* values, const int32_t* t_xs, const i
 
 extern "C" {
 
+// Workspace = [<=15 B alignment slack][pidx: b x ty_max int32, 16-B aligned (the 16-byte fill reads it as int4)]
+// [fp32 scratch for the serial path]; any caller alignment works.
 size_t gt_maximum_path_workspace_bytes(int64_t b, int64_t tx_max, int64_t ty_max) {
   if (b <= 0 || tx_max <= 0 || ty_max <= 0) return 0;
-  size_t n = ((size_t)b * ty_max * 4 + 255) & ~size_t(255);
+  size_t n = 16 + (((size_t)b * ty_max * 4 + 255) & ~size_t(255));
   if (tx_max > 1024 || ty_max > 1024) n += (size_t)b * tx_max * ty_max * 4;
   return n;
 }
@@ -287,11 +289,11 @@ int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, co
   if (b > 65535 || tx_max > (1 << 20) || ty_max > (1 << 20)) return GT_ERR_UNSUPPORTED;
   if (!workspace || workspace_bytes < gt_maximum_path_workspace_bytes(b, tx_max, ty_max)) return GT_ERR_WORKSPACE;
   hipStream_t s = (hipStream_t)stream;
-  int32_t* pidx = (int32_t*)workspace;
+  int32_t* pidx = (int32_t*)(((uintptr_t)workspace + 15) & ~(uintptr_t)15);
   const int B = (int)b, TX = (int)tx_max, TY = (int)ty_max;
   hipError_t e;
   if (TX > 1024 || TY > 1024) {
-    float* scratch = (float*)((uint8_t*)workspace + (((size_t)b * ty_max * 4 + 255) & ~size_t(255)));
+    float* scratch = (float*)((uint8_t*)pidx + (((size_t)b * ty_max * 4 + 255) & ~size_t(255)));
     hipLaunchKernelGGL(mas_serial_kernel, dim3((B + 63) / 64), dim3(64), 0, s, values, scratch, t_xs, t_ys, B, TX, TY,
                        max_neg_val, pidx);
     e = hipGetLastError();

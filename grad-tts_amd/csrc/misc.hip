@@ -238,20 +238,6 @@ hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s) {
   return launch_gn_mish(act_bf16, true, p, s);
 }
 
-__global__ __launch_bounds__(256) void mask_check_kernel(const float* mask, long n, int* flag) {
-  int bad = 0;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const float m = mask[i];
-    bad |= (m != 0.f && m != 1.f);
-  }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
-}
-hipError_t launch_mask_check(const float* mask, long n, int* flag, hipStream_t s) {
-  const unsigned blocks = (unsigned)std::min<long>(256, (n + 255) / 256);
-  hipLaunchKernelGGL(mask_check_kernel, dim3(blocks), dim3(256), 0, s, mask, n, flag);
-  return hipGetLastError();
-}
-
 hipError_t launch_temb(const TembParams& p, hipStream_t s) {
   hipLaunchKernelGGL(temb_kernel, dim3(p.rows), dim3(256), 0, s, p);
   return hipGetLastError();

@@ -105,15 +105,4 @@ inline __host__ __device__ long conv_wimg8_off(const WImg& w, int co, int tap, i
   return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + unit * 8 + (k & 7);
 }
 
-// ---- conv4 (csrc/conv4.hip) image: per (output-channel tile of NT, 16-channel stage) a slab of
-// [half h (channels 8h..8h+7)][tap][NT output channels] x 16 B, so the LDS-DMA is a straight copy and the
-// MFMA B fragment of lane r (output channel r, half h) is unit (h, tap, r) -- consecutive lanes,
-// consecutive 16-B units: conflict-free ds_read_b128 with no padding.
-inline __host__ __device__ constexpr int conv4_wplane_bytes(int nt) { return 9 * nt * 16; }
-inline __host__ __device__ long conv4_wimg_off(int nt, int cin, int co, int tap, int ci) {
-  const int tile = co / nt, col = co - tile * nt, ch = ci / 16, hf = (ci & 15) >> 3, k = ci & 7;
-  return ((long)tile * (cin / 16) + ch) * 2 * conv4_wplane_bytes(nt) + (long)hf * conv4_wplane_bytes(nt) +
-         ((long)tap * nt + col) * 16 + k * 2;
-}
-
 }  // namespace gt

@@ -165,7 +165,6 @@ class GradLogPEstimator2d(torch.nn.Module):
         self.final_conv = torch.nn.Conv2d(dim, 1, 1)
         self._handle = None
         self._synced = None
-        self._ws = {}
 
     # ------------------------------------------------------------------ native handle
     def _native(self, beta_min=0.05, beta_max=20.0):
@@ -203,16 +202,12 @@ class GradLogPEstimator2d(torch.nn.Module):
             pass
 
     def _workspace(self, device, dcode, B, T, N):
-        # One cached workspace per (device, dtype, STREAM): calls are stream-ordered, so reuse on one stream is
-        # safe, but concurrent calls on two streams must not share scratch (they raced before this was keyed
-        # by stream; tests/test_decoder_gpu.py::test_concurrent_streams_match_one_stream).
+        # Scratch comes from PyTorch's caching allocator on the CURRENT stream for every call: the allocator is
+        # stream-ordered, so concurrent calls on different streams get disjoint scratch
+        # (tests/test_decoder_gpu.py::test_concurrent_streams_match_one_stream) and nothing is kept alive between
+        # calls; after the first call of a shape this is a free-list lookup.
         nbytes = lib().gt_decoder_workspace_bytes(self._handle, dcode, B, T, N)
-        key = (device, dcode, torch.cuda.current_stream(device).cuda_stream)
-        ws = self._ws.get(key)
-        if ws is None or ws.numel() < nbytes:
-            ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
-            self._ws[key] = ws
-        return ws
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
 
     def _check_shapes(self, x, mask, mu):
         if x.dim() != 3 or x.shape[1] != self.n_feats or mu.shape != x.shape or mask.shape != (x.shape[0], 1, x.shape[2]):

@@ -62,8 +62,12 @@ int64_t gt_decoder_param_numel(const gt_decoder* dec, int i);
  * layouts happens lazily at the next compute call (synchronously, outside any stream capture). */
 int gt_decoder_set_param(gt_decoder* dec, const char* name, const float* host_data, int64_t numel);
 
+/* Number of times the weights were packed into device layouts so far (one per compute dtype in use after
+ * each parameter change; the reference re-reads weights on every call, this library packs them once). */
+int64_t gt_decoder_pack_count(const gt_decoder* dec);
+
 /* Workspace (device bytes) needed by a compute call with this batch B, padded frame count T and
- * step count (0 for gt_estimator_forward). */
+ * step count (0 for gt_estimator_forward). Any alignment: the call aligns the base itself. */
 size_t gt_decoder_workspace_bytes(const gt_decoder* dec, int dtype, int64_t B, int64_t T, int32_t n_timesteps);
 
 /* One score evaluation: out[B,80,T] = s_theta(x, mask, mu, t, spk).
@@ -110,7 +114,8 @@ int gt_quantize_e4m3(const float* w, int64_t rows, int64_t cols, int64_t row_str
  * as maximum_path does before calling the Cython core); t_xs, t_ys: [b] int32 (device);
  * paths: [b, tx_max, ty_max] int32 output, fully written (0/1). `values` is not modified
  * (the reference mutates only its private numpy copy). Requires t_x <= t_y per item (t_x > t_y
- * makes the reference read out of bounds, core.pyx:34). */
+ * makes the reference read out of bounds, core.pyx:34). workspace: device memory of
+ * gt_maximum_path_workspace_bytes() bytes, any alignment. */
 size_t gt_maximum_path_workspace_bytes(int64_t b, int64_t tx_max, int64_t ty_max);
 int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, const int32_t* t_ys, int64_t b,
                     int64_t tx_max, int64_t ty_max, float max_neg_val, void* workspace, size_t workspace_bytes,

@@ -11,7 +11,7 @@
  * Bit-exactness details copied from the generated C (core.c:2848-2859):
  *   max(v_cur, v_prev) lowers to  (v_prev > v_cur) ? v_prev : v_cur
  *   the backtrack compare is a strict  value[i, y-1] < value[i-1, y-1]   (core.c:2907)
- * Pinned against the reference itself: tests/test_mas_oracle.py compares this against the
+ * Pinned against the reference itself: tests/test_oracle_golden.py compares this against the
  * Cython module built from the reference sources (oracle/_ref) and the committed golden paths.
  */
 #include <stdint.h>

@@ -1,6 +1,8 @@
 """Helpers shared by the GPU parity tests and tools: build the HIP-backed modules from the synthetic
 weights a fixture names, and read intermediate stages through gt_estimator_probe."""
 import ctypes
+import json
+import os
 
 import numpy as np
 import torch
@@ -27,6 +29,20 @@ def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def report(name, err, tol, gate=True, **extra):
+    """Print the achieved parity error of one check (visible in the pytest log) and, when GRADTTS_PARITY_LOG
+    names a file, append it there as one JSON line; then gate it."""
+    rec = {"check": name, "err": float(err), "tol": float(tol), **extra}
+    print(f"PARITY {name}: rel err {err:.3e} (gate {tol:.0e})")
+    path = os.environ.get("GRADTTS_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    if gate:
+        assert err <= tol, f"{name}: rel err {err:.3e} > {tol:.0e}"
+    return err <= tol
 
 
 def probe(est, compute_dtype, x, mask, mu, t, spk, stage, shape):

@@ -1,0 +1,126 @@
+"""Every BASELINE.json configuration at its full workload, through the C ABI.
+
+The CPU oracle cannot run B = 32-256 x T = 512 x N = 50-1000 in test time, so full-size runs are checked by
+properties that do not depend on size, and by the GPU fp32 path, which is itself pinned to the reference
+(golden fixtures) and to the oracle at 1e-4 (test_decoder_gpu.py):
+  * finite output, bit-identical reruns;
+  * batch / shard invariance: an utterance decodes to the same bits alone, in its 8-GPU shard, or in the full
+    batch (what config 4's data-parallel split relies on);
+  * bf16 vs fp32 of the same full workload <= 1e-2 of max|y| (the reference's own bf16 autocast is
+    3-4e-3 from fp64 on its sampler fixtures, tests/golden/ref_bf16_envelope.json);
+and small ragged cases at the config's n_spks / N are compared with the oracle directly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+from gpu_util import make_decoder, rel_err, report
+
+pytestmark = pytest.mark.gpu
+
+SAMPLER_BF16_TOL = 1e-2
+FP32_TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _inputs(seed, B, T, ragged=True, n_spks=1):
+    from gradtts_amd.params import synthetic_inputs
+    lengths = None
+    if ragged:   # utterance lengths in [T/2, T] with the longest at T_pad = T (fix_len_compatibility)
+        rng = np.random.default_rng(seed + 1)
+        lengths = [T] + list(rng.integers(T // 2, T + 1, B - 1))
+    mu, z, mask, spk = synthetic_inputs(seed, B, T, lengths=lengths)
+    dev = torch.device("cuda")
+    spk_t = torch.from_numpy(spk).to(dev) if n_spks != 1 else None
+    return (torch.from_numpy(z).to(dev), torch.from_numpy(mask).to(dev), torch.from_numpy(mu).to(dev), spk_t,
+            (mu, z, mask, spk))
+
+
+def _sub(spk, s):
+    return None if spk is None else spk[s].contiguous()
+
+
+def test_c2_full_workload_bf16_vs_fp32():
+    """C2: LJSpeech single speaker, B = 32, T = 512, N = 50, bf16 (the bench workload, ragged masks)."""
+    z, m, mu, _, _ = _inputs(1234, 32, 512)
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    y16 = dec(z, m, mu, 50)
+    assert torch.isfinite(y16).all()
+    assert torch.equal(y16, dec(z, m, mu, 50))
+    dec.compute_dtype = torch.float32
+    y32 = dec(z, m, mu, 50)
+    report("C2 B=32 T=512 N=50 bf16 vs fp32 (GPU)", rel_err(y16.cpu().numpy(), y32.cpu().numpy()), SAMPLER_BF16_TOL)
+
+
+def test_c3_full_workload_multispeaker():
+    """C3: Libri-TTS n_spks = 247, B = 64, T = 512, N = 100: finite, rerun bit-identical, utterances 5..6 decoded
+    alone give the same bits, and bf16 within 1e-2 of the fp32 path on the same full batch."""
+    z, m, mu, spk, _ = _inputs(4321, 64, 512, n_spks=247)
+    dec, _ = make_decoder(247, 3, torch.bfloat16)
+    y = dec(z, m, mu, 100, False, spk)
+    assert torch.isfinite(y).all()
+    assert torch.equal(y, dec(z, m, mu, 100, False, spk))
+    s = slice(5, 7)
+    alone = dec(z[s].contiguous(), m[s].contiguous(), mu[s].contiguous(), 100, False, _sub(spk, s))
+    assert torch.equal(y[s], alone), (y[s] - alone).abs().max().item()
+    dec.compute_dtype = torch.float32
+    y32 = dec(z, m, mu, 100, False, spk)
+    report("C3 B=64 T=512 N=100 n_spks=247 bf16 vs fp32 (GPU)", rel_err(y.cpu().numpy(), y32.cpu().numpy()),
+           SAMPLER_BF16_TOL)
+
+
+def test_c3_small_ragged_vs_oracle():
+    """C3's speaker conditioning and step count (n_spks = 247, N = 100) against the oracle on a ragged batch."""
+    from oracle import decoder as odec
+    z, m, mu, spk, host = _inputs(99, 2, 64, n_spks=247)
+    dec, sd = make_decoder(247, 3, torch.float32)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    with torch.no_grad():
+        ref = odec.reverse_diffusion(odec.to_torch_params(sd), torch.from_numpy(host[1]), torch.from_numpy(host[2]),
+                                     torch.from_numpy(host[0]), 100, torch.from_numpy(host[3]), n_spks=247).numpy()
+    report("C3 small B=2 T=64 N=100 n_spks=247 fp32 vs oracle", rel_err(dec(z, m, mu, 100, False, spk).cpu().numpy(), ref),
+           FP32_TOL)
+    dec.compute_dtype = torch.bfloat16
+    report("C3 small B=2 T=64 N=100 n_spks=247 bf16 vs oracle", rel_err(dec(z, m, mu, 100, False, spk).cpu().numpy(), ref),
+           SAMPLER_BF16_TOL)
+
+
+def test_c4_shard_emulation_matches_full_batch():
+    """C4: 256 utterances (T_pad = 512, N = 50) split over 8 ranks as gradtts_amd.shard does; each rank's decode
+    must equal the same utterances of the one-GPU full-batch decode bit for bit, and the gathered result (rank
+    order) must equal the full batch."""
+    from gradtts_amd.shard import shard, shard_bounds
+    world, n = 8, 256
+    z, m, mu, _, _ = _inputs(2024, n, 512)
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    full = dec(z, m, mu, 50)
+    assert torch.isfinite(full).all()
+    parts = []
+    for r in range(world):
+        lo, hi = shard_bounds(n, r, world)
+        y = dec(shard(z, r, world), shard(m, r, world), shard(mu, r, world), 50)
+        assert torch.equal(y, full[lo:hi]), f"rank {r}: {(y - full[lo:hi]).abs().max().item()}"
+        parts.append(y)
+    assert torch.equal(torch.cat(parts), full)
+
+
+def test_c5_full_workload_fp8_weights():
+    """C5: N = 1000 with fp8 (e4m3) conv weights, B = 32, T = 512: finite, rerun bit-identical, batch-invariant,
+    and close to the bf16-weight decode (the quantization moves the output; the drift is reported, gated loosely;
+    parity of the fp8 path itself is against the dequantized-weight oracle in test_decoder_gpu.py)."""
+    z, m, mu, _, _ = _inputs(555, 32, 512)
+    dec, _ = make_decoder(1, 0, "bf16_w8")
+    y = dec(z, m, mu, 1000)
+    assert torch.isfinite(y).all()
+    assert torch.equal(y, dec(z, m, mu, 1000))
+    s = slice(30, 32)
+    assert torch.equal(y[s], dec(z[s].contiguous(), m[s].contiguous(), mu[s].contiguous(), 1000))
+    dec.compute_dtype = torch.bfloat16
+    y16 = dec(z, m, mu, 1000)
+    report("C5 B=32 T=512 N=1000 fp8-weight vs bf16-weight drift", rel_err(y.cpu().numpy(), y16.cpu().numpy()), 0.1)

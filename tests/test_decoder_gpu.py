@@ -2,23 +2,36 @@
 (a) golden vectors produced by the real reference (tests/golden, make_golden.py) and
 (b) the oracle (oracle/decoder.py, itself pinned to those vectors) on larger / other shapes.
 
-Tolerances (written here): fp32 compute max|d| <= 1e-4 * max|ref| (N <= 50; the
-reference's own fp32-vs-fp64 spread reaches 3.4e-5 at N=50); bf16 compute max|d| <= 2e-2 * max|ref|
-for one estimator call and <= 3e-2 for the sampler (bf16 autocast of the reference itself is 4e-3 off
-fp64 at N=10).
+Tolerances (written here; rel = max|d| / max|ref|):
+  * fp32 compute: 1e-4 (SURVEY.md H7; the reference's own fp32-vs-fp64 spread reaches 3.4e-5 at N = 50);
+  * bf16 sampler: 1e-2; the reference's own bf16 autocast is 2.2-3.9e-3 from its fp32 output on
+    these fixtures (tests/golden/ref_bf16_envelope.json, made by make_bf16_envelope.py from the reference);
+  * bf16, one estimator call: 1.25 x the reference's own bf16-autocast error on the same fixture (1.07-1.92e-2:
+    a single call is dominated by the bf16 rounding of its inputs and activations, which the reference's bf16
+    path has too); 1.5e-2 on oracle-only shapes, the bottom of that envelope.
+Every check prints its achieved error (PARITY lines in the log).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import gpu_available, load_golden
-from gpu_util import STAGES, make_decoder, probe, rel_err
+from conftest import GOLDEN, gpu_available, load_golden
+from gpu_util import STAGES, make_decoder, probe, rel_err, report
 
 pytestmark = pytest.mark.gpu
 
 FP32_TOL = 1e-4
-BF16_EST_TOL = 2e-2
-BF16_REV_TOL = 3e-2
+BF16_EST_TOL = 1.5e-2        # oracle-only shapes (no reference bf16 envelope)
+BF16_REV_TOL = 1e-2
+with open(os.path.join(GOLDEN, "ref_bf16_envelope.json")) as _f:
+    REF_BF16 = json.load(_f)
+
+
+def bf16_est_gate(name):
+    return 1.25 * REF_BF16[name]["ref_bf16_vs_f32"]
 
 EST = ["estimator_s1.npz", "estimator_s247.npz", "estimator_sm1.npz", "estimator_s1_T132.npz", "estimator_s1_T20.npz"]
 REV = ["reverse_s1_N1.npz", "reverse_s1_N2.npz", "reverse_s1_N10.npz", "reverse_s1_N50.npz", "reverse_s247_N10.npz",
@@ -36,16 +49,16 @@ def _cuda(a):
 
 
 @pytest.mark.parametrize("name", EST)
-@pytest.mark.parametrize("cdt,tol", [(torch.float32, FP32_TOL), (torch.bfloat16, BF16_EST_TOL)])
-def test_estimator_matches_reference(name, cdt, tol):
+@pytest.mark.parametrize("cdt", [torch.float32, torch.bfloat16])
+def test_estimator_matches_reference(name, cdt):
+    tol = FP32_TOL if cdt == torch.float32 else bf16_est_gate(name)
     g = load_golden(name)
     n_spks = int(g["n_spks"])
     dec, _ = make_decoder(n_spks, int(g["seed_w"]), cdt)
     spk = _cuda(g["spk"]) if n_spks != 1 else None
     y = dec.estimator(_cuda(g["x"]), _cuda(g["mask"]), _cuda(g["mu"]), _cuda(g["t"]), spk).cpu().numpy()
     assert np.isfinite(y).all()
-    err = rel_err(y, g["out"])
-    assert err <= tol, f"{name} {cdt}: rel err {err:.3e} > {tol}"
+    report(f"estimator {name} {cdt}", rel_err(y, g["out"]), tol)
 
 
 @pytest.mark.parametrize("name", REV)
@@ -55,8 +68,7 @@ def test_reverse_diffusion_fp32_matches_reference(name):
     dec, _ = make_decoder(n_spks, int(g["seed_w"]), torch.float32)
     spk = _cuda(g["spk"]) if n_spks != 1 else None
     y = dec(_cuda(g["z"]), _cuda(g["mask"]), _cuda(g["mu"]), int(g["n_timesteps"]), False, spk).cpu().numpy()
-    err = rel_err(y, g["out"])
-    assert err <= FP32_TOL, f"{name}: rel err {err:.3e}"
+    report(f"reverse fp32 {name}", rel_err(y, g["out"]), FP32_TOL)
 
 
 @pytest.mark.parametrize("name", ["reverse_s1_N10.npz", "reverse_s247_N10.npz", "reverse_s1_N50.npz"])
@@ -66,8 +78,7 @@ def test_reverse_diffusion_bf16_matches_reference(name):
     dec, _ = make_decoder(n_spks, int(g["seed_w"]), torch.bfloat16)
     spk = _cuda(g["spk"]) if n_spks != 1 else None
     y = dec(_cuda(g["z"]), _cuda(g["mask"]), _cuda(g["mu"]), int(g["n_timesteps"]), False, spk).cpu().numpy()
-    err = rel_err(y, g["out"])
-    assert err <= BF16_REV_TOL, f"{name}: rel err {err:.3e}"
+    report(f"reverse bf16 {name}", rel_err(y, g["out"]), BF16_REV_TOL)
 
 
 def test_padding_dependence_reproduced():
@@ -99,7 +110,7 @@ def test_every_stage_matches_oracle(cdt, tol):
         ref = taps[st].numpy()
         _, pr = probe(dec.estimator, cdt, *args, None, st, ref.shape)
         e = rel_err(pr.cpu().numpy(), ref)
-        if not e <= tol:
+        if not report(f"stage {st} {cdt}", e, tol, gate=False):
             bad.append(f"{st}: {e:.3e}")
     assert not bad, "stage mismatches: " + ", ".join(bad)
 
@@ -114,10 +125,46 @@ def test_estimator_vs_oracle_other_shapes(B, T, lengths):
     ref = odec.estimator(odec.to_torch_params(sd), torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu),
                          torch.from_numpy(t)).numpy()
     y32 = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
-    assert rel_err(y32, ref) <= FP32_TOL
+    report(f"estimator fp32 B={B} T={T}", rel_err(y32, ref), FP32_TOL)
     dec.compute_dtype = torch.bfloat16
     y16 = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
-    assert rel_err(y16, ref) <= BF16_EST_TOL
+    report(f"estimator bf16 B={B} T={T}", rel_err(y16, ref), BF16_EST_TOL)
+
+
+@pytest.mark.parametrize("B,T,lengths,scale", [(2, 256, [256, 190], 10.0), (2, 256, [256, 190], 30.0),
+                                              (1, 1024, [1000], 30.0)])
+def test_attention_large_logits_fp32(B, T, lengths, scale):
+    """LinearAttention's softmax over n = F*T positions (diffusion.py:95) with large logits: k rows of every
+    to_qkv scaled by `scale` (|k| reaches the hundreds), Rezero g = 0.5 so the attention term is large. The online
+    softmax runs per position tile in log2 units (attn.hip) and its per-tile rescale factors must cancel exactly
+    when tiles with different running maxima merge. A peaked softmax is ill-conditioned (at scale 300 the
+    reference's own fp32 result is 4.5e-2 from fp64), so the check is against the fp64 oracle, gated at
+    max(1e-4, 4 x the oracle's own fp32-vs-fp64 error on the same inputs)."""
+    from oracle import decoder as odec
+    from gradtts_amd.diffusion import Diffusion
+    from gradtts_amd.params import synthetic_inputs, synthetic_state_dict
+    sd = synthetic_state_dict(seed=2)
+    for k in list(sd):
+        if k.endswith("to_qkv.weight"):
+            w = sd[k].copy()
+            w[128:256] *= scale
+            sd[k] = w
+        elif k.endswith("fn.g"):
+            sd[k] = np.full_like(sd[k], 0.5)
+    dec = Diffusion(80, 64, 1, 64, 0.05, 20, 1000, compute_dtype=torch.float32)
+    dec.estimator.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    dec = dec.cuda()
+    mu, z, mask, _ = synthetic_inputs(17, B, T, lengths=lengths)
+    t = np.linspace(0.8, 0.3, B).astype(np.float32)
+    ins = [torch.from_numpy(a) for a in (z, mask, mu, t)]
+    with torch.no_grad():
+        r32 = odec.estimator(odec.to_torch_params(sd), *ins).numpy()
+        r64 = odec.estimator({k: v.double() for k, v in odec.to_torch_params(sd).items()},
+                             *(a.double() for a in ins)).numpy()
+    cond = rel_err(r32, r64)
+    y = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
+    report(f"attention k x{scale:g} fp32 B={B} T={T} vs fp64 oracle (oracle fp32: {cond:.1e})", rel_err(y, r64),
+           max(FP32_TOL, 4 * cond))
 
 
 @pytest.mark.parametrize("cdt", [torch.bfloat16, torch.float32])
@@ -165,6 +212,7 @@ def test_concurrent_streams_match_one_stream():
 # tolerances are the bf16 ones. The quantization itself moves one estimator call by ~8e-2 and an
 # N = 100 sampler output by ~3e-2 relative to the fp32 weights (synthetic weights).
 W8 = "bf16_w8"
+W8_STAGE_TOL = 2e-2
 
 
 @pytest.mark.parametrize("name", EST)
@@ -179,8 +227,7 @@ def test_w8_estimator_matches_oracle_dequantized(name):
                              torch.from_numpy(spk) if spk is not None else None, n_spks).numpy()
     y = dec.estimator(_cuda(g["x"]), _cuda(g["mask"]), _cuda(g["mu"]), _cuda(g["t"]),
                       _cuda(spk) if spk is not None else None).cpu().numpy()
-    err = rel_err(y, ref)
-    assert err <= BF16_EST_TOL, f"{name}: rel err {err:.3e}"
+    report(f"w8 estimator {name} vs dequantized oracle", rel_err(y, ref), bf16_est_gate(name))
 
 
 def test_w8_every_stage_matches_oracle_dequantized():
@@ -197,7 +244,7 @@ def test_w8_every_stage_matches_oracle_dequantized():
         ref = taps[st].numpy()
         _, pr = probe(dec.estimator, W8, *args, None, st, ref.shape)
         e = rel_err(pr.cpu().numpy(), ref)
-        if not e <= BF16_EST_TOL:
+        if not report(f"w8 stage {st}", e, W8_STAGE_TOL, gate=False):
             bad.append(f"{st}: {e:.3e}")
     assert not bad, "stage mismatches: " + ", ".join(bad)
 
@@ -212,8 +259,7 @@ def test_w8_sampler_N1000_matches_oracle_dequantized():
     ref = odec.reverse_diffusion(odec.fp8_params(sd), torch.from_numpy(z), torch.from_numpy(mask),
                                  torch.from_numpy(mu), 1000).numpy()
     y = dec(_cuda(z), _cuda(mask), _cuda(mu), 1000).cpu().numpy()
-    err = rel_err(y, ref)
-    assert err <= BF16_REV_TOL, f"rel err {err:.3e}"
+    report("w8 reverse N=1000 vs dequantized oracle", rel_err(y, ref), BF16_REV_TOL)
 
 
 def test_w8_bench_shape_deterministic_and_batch_invariant():
