@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   if (OUT == OUT_RBOUT) gl = gn_load(p.pre_part, p.pre_nparts, b);
   float c_g = 0.f, c_b = 0.f, c_t = 0.f;            // gamma, beta, time bias of channel tid
   if (IN == IN_GN && tid < p.Cin) {
-    c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; c_t = p.tb[(long)b * p.tb_bstride + tid];
+    c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; c_t = tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid];
   }
   if (OUT == OUT_RBOUT && tid < NT) { c_g = p.pre_gamma[cout0 + tid]; c_b = p.pre_beta[cout0 + tid]; }
   const float c_bias = tid < NT ? p.bias[cout0 + tid] : 0.f;

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
     static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
     const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b);
-    const float tbv = tid < 64 ? p.tb[(long)b * p.tb_bstride + tid] : 0.f;
+    const float tbv = tid < 64 ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid] : 0.f;
     gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
     if (tid < 64) {
       const float sc = c_g * s_rstd[tid >> 3];

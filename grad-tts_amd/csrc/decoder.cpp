@@ -157,6 +157,18 @@ struct gt_decoder {
   std::vector<Rec> recs;
   std::vector<hipEvent_t> pool;
   size_t pool_used = 0;
+  // captured sampler segments (gt_reverse_diffusion): HIP graphs of S Euler steps, keyed by everything the
+  // captured kernels bake in (shapes, dtype, tensor / workspace / weight-arena addresses)
+  bool graphs = true;
+  hipStream_t cap_stream = nullptr;
+  struct Graph { std::vector<uintptr_t> key; hipGraphExec_t exec; };
+  std::vector<Graph> gcache;   // most recently used last
+  int64_t captures = 0;
+  int64_t max_chunk = 0;       // > 0: cap on utterances per internal batch chunk (GT_MAX_CHUNK, tests)
+  void drop_graphs() {
+    for (auto& g : gcache) (void)hipGraphExecDestroy(g.exec);
+    gcache.clear();
+  }
   hipEvent_t ev() {
     if (pool_used == pool.size()) {
       hipEvent_t e;
@@ -394,13 +406,14 @@ int prepare(gt_decoder* d, int code) {
   for (auto& kv : blob.off) d->dp[code][kv.first] = (uint8_t*)d->arena[code] + kv.second;
   d->dirty[code] = false;
   d->packs += 1;
+  d->drop_graphs();   // captured graphs point into the old arena
   return GT_OK;
 }
 
 // ---------------------------------------------------------------- workspace
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
-  size_t stats, part, G, Mw, tb, spk, total;
+  size_t stats, part, G, Mw, tb, spk, betas, step, total;
   int pmax;
   int tile_pos[3], ntile[3];
 };
@@ -437,6 +450,8 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.Mw = take((size_t)B * conv_wimg(dt, 1, 256, 256).total);
   L.tb = take((size_t)std::max<int64_t>(B, N) * 1792 * 4);
   L.spk = take((size_t)B * 80 * 4);
+  L.betas = take((size_t)std::max<int32_t>(N, 1) * 4);
+  L.step = take(4);
   L.total = o;
   return L;
 }
@@ -452,6 +467,8 @@ struct Run {
   Layout L;
   const float* mask; const float* mu; const float* xt; const float* spk_s;
   const float* tb; long tb_bstride;
+  const int* stepp = nullptr;     // device step index of graph segments (kernels.h tb_at); null = 0
+  const float* betas = nullptr;   // per-step beta(t) table (sampler), indexed by *stepp
   int stat_slot = 0;
   hipError_t err = hipSuccess;
   const char* probe = nullptr;   // diagnostics: copy the activation named `probe` to probe_out (NCHW fp32)
@@ -537,7 +554,7 @@ struct Run {
   ConvParams base(int lvl_in, int lvl_out) {
     ConvParams p;
     memset(&p, 0, sizeof(p));
-    p.B = B; p.T0 = T; p.mask = mask;
+    p.B = B; p.T0 = T; p.mask = mask; p.stepp = stepp;
     p.Fin = Fl(lvl_in); p.Tin = Tl(lvl_in); p.Fout = Fl(lvl_out); p.Tout = Tl(lvl_out);
     p.lvl_in = lvl_in; p.lvl_out = lvl_out;
     return p;
@@ -581,7 +598,7 @@ struct Run {
         a.pre = pre1; a.part = st1; a.nparts = np1; a.gamma = Fp(k + "block1.block.1.weight");
         a.beta = Fp(k + "block1.block.1.bias"); a.count = count; a.out = pre1; a.mask = mask;
         a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = Cout; a.T0 = T; a.lvl = lvl;
-        a.tb = tb + tb_off; a.tb_bstride = tb_bstride;
+        a.tb = tb + tb_off; a.tb_bstride = tb_bstride; a.stepp = stepp;
         timed(std::string("gn_apply_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
                   std::to_string(Fl(lvl)), 0.0, 2.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt),
               [&] { return launch_gn_apply(dt, a, s); });
@@ -608,7 +625,7 @@ struct Run {
       p.out = out;
       conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
     } else {                                       // Mish(GN(h2))*m + x*m
-      RbOutParams p;
+      RbOutParams p{};
       p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
       p.count = count; p.x = in0; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = Cout;
       p.T0 = T; p.lvl = lvl;
@@ -715,13 +732,25 @@ struct Run {
     f.pre = act(0, 3); f.part = st; f.nparts = fnp; f.gamma = Fp("final_block.block.1.weight"); f.beta = Fp("final_block.block.1.bias");
     f.count = (long)8 * 80 * T; f.wf = Fp("final_conv.weight"); f.bf = Fp("final_conv.bias");
     f.mask = mask; f.B = B; f.T = T; f.euler = euler; f.out = out; f.mu = mu; f.xt = xt_inout;
-    f.beta_t = beta_t; f.hstep = hstep;
+    f.beta_t = beta_t; f.hstep = hstep; f.betas = betas; f.stepp = stepp;
     timed(std::string("final_kernel<") + (dt ? "bf16>" : "float>"), 2.0 * 64 * B * 80 * T,
           (double)B * 80 * T * (64 * esize(dt) + 16), [&] { return launch_final(dt, f, s); });
   }
 };
 
 uint8_t* align_ws(void* ws) { return (uint8_t*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
+
+// Utterances per internal batch chunk. The conv kernels address an activation tensor through a raw buffer
+// descriptor with a 32-bit byte range, so one launch covers at most 2^31 bytes of its largest input (the
+// level-0 64-channel activation, B x 80 x T x 64 elements). Larger batches run as consecutive chunks; the
+// arithmetic is batch-invariant (GroupNorm slots and attention tiles are per utterance), so chunked results
+// are bit-identical to one launch over the whole batch.
+int64_t chunk_b(const gt_decoder* d, int dt, int64_t B, int64_t T) {
+  const int64_t per_utt = 80 * T * 64 * (int64_t)esize(dt);
+  int64_t cap = std::max<int64_t>(1, ((int64_t(1) << 31) - 1) / per_utt);
+  if (d && d->max_chunk > 0) cap = std::min(cap, d->max_chunk);   // GT_MAX_CHUNK at creation (tests)
+  return std::min(B, cap);
+}
 
 int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_t ws_bytes, int32_t N) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
@@ -731,6 +760,8 @@ int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_
   if (T % 4 != 0) return fail(GT_ERR_ARG, "T must be a multiple of 4 (fix_len_compatibility)");
   if (B > 65535 || T > (1 << 20)) return fail(GT_ERR_UNSUPPORTED, "B or T too large");
   if (!ws) return fail(GT_ERR_ARG, "null workspace");
+  if (80 * T * 64 * (int64_t)esize(dtype ? 1 : 0) >= (int64_t(1) << 31))
+    return fail(GT_ERR_UNSUPPORTED, "T too large for one utterance per launch");
   if (ws_bytes < gt_decoder_workspace_bytes(d, dtype, B, T, N)) return fail(GT_ERR_WORKSPACE, "workspace too small");
   return GT_OK;
 }
@@ -759,12 +790,16 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   // SinusoidalPosEmb frequencies, as torch computes them: exp(float(k) * float(-ln(1e4)/31)) in fp32
   const float negc = (float)(-std::log(10000.0) / 31.0);
   for (int k = 0; k < 32; ++k) d->freqs[k] = expf((float)k * negc);
+  if (const char* e = getenv("GT_GRAPHS")) d->graphs = atoi(e) != 0;
+  if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
   *out = d;
   return GT_OK;
 }
 
 void gt_decoder_destroy(gt_decoder* d) {
   if (!d) return;
+  d->drop_graphs();
+  if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
   for (auto e : d->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 3; ++i)
     if (d->arena[i]) (void)hipFree(d->arena[i]);
@@ -832,10 +867,12 @@ int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int
 }
 
 // The workspace may have any alignment: compute calls align its base up to 256 bytes (the slack is in the size).
+// Sized for one batch chunk (chunk_b): batches past the 32-bit buffer range run chunk by chunk in it.
 size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int64_t T, int32_t n_timesteps) {
   (void)d;
   if (B <= 0 || T <= 0) return 0;
-  return layout(dtype ? 1 : 0, B, T, n_timesteps).total + 256;
+  const int dt = dtype ? 1 : 0;
+  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps).total + 256;
 }
 
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
@@ -846,28 +883,37 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
   if (!x || !mask || !mu || !t || !out) return fail(GT_ERR_ARG, "null tensor");
   if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
   if ((rc = prepare(d, dtype))) return rc;
-  Run R;
-  R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
-  R.ws = align_ws(workspace);
-  R.L = layout(R.dt, B, T, 0);
-  R.mask = mask; R.mu = mu; R.xt = x; R.spk_s = nullptr;
-  R.probe = probe; R.probe_out = probe_out;
-  float* tbuf = (float*)(R.ws + R.L.tb);
-  TembParams tp;
-  tp.rows = (int)B; tp.tvals = t; tp.n_steps = 0; tp.pe_scale = d->pe_scale; tp.freqs = R.Fp("freqs");
-  tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
-  tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = 1792; tp.tb = tbuf;
-  R.chk(launch_temb(tp, R.s));
-  if (d->n_spks > 1) {
-    float* sbuf = (float*)(R.ws + R.L.spk);
-    R.chk(launch_spk_mlp(spk, (int)B, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"), R.Fp("spk_mlp.2.weight"),
-                         R.Fp("spk_mlp.2.bias"), sbuf, R.s));
-    R.spk_s = sbuf;
+  const int64_t Bc = chunk_b(d, dtype ? 1 : 0, B, T);
+  if (probe && Bc < B) return fail(GT_ERR_UNSUPPORTED, "probes need the batch in one chunk");
+  bool probed = false;
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {   // batch chunks (chunk_b), each a complete evaluation
+    const int64_t nb = std::min(Bc, B - b0);
+    const size_t fo = (size_t)b0 * 80 * T;
+    Run R;
+    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.s = (hipStream_t)stream;
+    R.ws = align_ws(workspace);
+    R.L = layout(R.dt, nb, T, 0);
+    R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = x + fo; R.spk_s = nullptr;
+    R.probe = probe; R.probe_out = probe_out;
+    float* tbuf = (float*)(R.ws + R.L.tb);
+    TembParams tp;
+    tp.rows = (int)nb; tp.tvals = t + b0; tp.n_steps = 0; tp.pe_scale = d->pe_scale; tp.freqs = R.Fp("freqs");
+    tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
+    tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = 1792; tp.tb = tbuf;
+    tp.betas = nullptr; tp.beta_min = 0.f; tp.beta_delta = 0.f;
+    R.chk(launch_temb(tp, R.s));
+    if (d->n_spks > 1) {
+      float* sbuf = (float*)(R.ws + R.L.spk);
+      R.chk(launch_spk_mlp(spk + (size_t)b0 * 64, (int)nb, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"),
+                           R.Fp("spk_mlp.2.weight"), R.Fp("spk_mlp.2.bias"), sbuf, R.s));
+      R.spk_s = sbuf;
+    }
+    R.tb = tbuf; R.tb_bstride = 1792;
+    R.unet(0, out + fo, nullptr, 0.f, 0.f);
+    if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
+    probed = probed || R.probed;
   }
-  R.tb = tbuf; R.tb_bstride = 1792;
-  R.unet(0, out, nullptr, 0.f, 0.f);
-  if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
-  if (probe && !R.probed) return fail(GT_ERR_ARG, std::string("unknown probe stage: ") + probe);
+  if (probe && !probed) return fail(GT_ERR_ARG, std::string("unknown probe stage: ") + probe);
   return GT_OK;
 }
 
@@ -884,6 +930,50 @@ int gt_estimator_probe(gt_decoder* d, int dtype, const float* x, const float* ma
   return estimator_impl(d, dtype, x, mask, mu, t, spk, B, T, out, workspace, workspace_bytes, stream, stage, probe_out);
 }
 
+// Replay (capturing first if needed) the HIP graph of S Euler steps for this key on `stream`.
+static int run_segment_graph(gt_decoder* d, Run& R, const std::vector<uintptr_t>& key, int S, float* xt, float hf,
+                             hipStream_t stream, hipGraphExec_t* out_exec) {
+  for (size_t i = 0; i < d->gcache.size(); ++i)
+    if (d->gcache[i].key == key) {
+      gt_decoder::Graph g = d->gcache[i];
+      d->gcache.erase(d->gcache.begin() + i);
+      d->gcache.push_back(g);
+      *out_exec = g.exec;
+      return GT_OK;
+    }
+  if (!d->cap_stream && hipStreamCreateWithFlags(&d->cap_stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipStreamCreate(capture) failed");
+  if (hipStreamBeginCapture(d->cap_stream, hipStreamCaptureModeRelaxed) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipStreamBeginCapture failed");
+  R.s = d->cap_stream;
+  const float* tb0 = R.tb;
+  const float* be0 = R.betas;
+  for (int j = 0; j < S && R.err == hipSuccess; ++j) {   // step j of the segment reads row (*stepp + j)
+    R.tb = tb0 + (size_t)j * kTbRow;
+    R.betas = be0 + j;
+    R.unet(1, nullptr, xt, 0.f, hf);
+  }
+  R.tb = tb0; R.betas = be0; R.s = stream;
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(d->cap_stream, &g);
+  if (R.err != hipSuccess || ec != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    return fail(GT_ERR_HIP, std::string("graph capture failed: ") + hipGetErrorString(R.err != hipSuccess ? R.err : ec));
+  }
+  hipGraphExec_t ex = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ei != hipSuccess) return fail(GT_ERR_HIP, std::string("hipGraphInstantiate failed: ") + hipGetErrorString(ei));
+  if (d->gcache.size() >= 8) {
+    (void)hipGraphExecDestroy(d->gcache.front().exec);
+    d->gcache.erase(d->gcache.begin());
+  }
+  d->gcache.push_back({key, ex});
+  d->captures += 1;
+  *out_exec = ex;
+  return GT_OK;
+}
+
 int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* mask, const float* mu, const float* spk,
                          int64_t B, int64_t T, int32_t n_timesteps, float* out, void* workspace, size_t workspace_bytes,
                          void* stream) {
@@ -893,41 +983,83 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
   if (n_timesteps < 0) return fail(GT_ERR_ARG, "n_timesteps must be >= 0");
   if (d->n_spks > 1 && !spk) return fail(GT_ERR_ARG, "n_spks > 1 needs spk [B,64]");
   if ((rc = prepare(d, dtype))) return rc;
-  Run R;
-  R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)B; R.T = (int)T; R.s = (hipStream_t)stream;
-  R.ws = align_ws(workspace);
-  R.L = layout(R.dt, B, T, n_timesteps);
-  R.mask = mask; R.mu = mu; R.xt = out; R.spk_s = nullptr;
-  R.chk(launch_mask_copy(z, mask, (int)B, 80, (int)T, out, R.s));   // xt = z * mask  (diffusion.py:257)
-  if (n_timesteps > 0) {
-    float* tbuf = (float*)(R.ws + R.L.tb);
-    TembParams tp;
-    tp.rows = n_timesteps; tp.tvals = nullptr; tp.n_steps = n_timesteps; tp.pe_scale = d->pe_scale;
-    tp.freqs = R.Fp("freqs");
-    tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
-    tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = 1792; tp.tb = tbuf;
-    R.chk(launch_temb(tp, R.s));
-    if (d->n_spks > 1) {
-      float* sbuf = (float*)(R.ws + R.L.spk);
-      R.chk(launch_spk_mlp(spk, (int)B, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"), R.Fp("spk_mlp.2.weight"),
-                           R.Fp("spk_mlp.2.bias"), sbuf, R.s));
-      R.spk_s = sbuf;
+  const hipStream_t st = (hipStream_t)stream;
+  // Graph segments unless profiling (events per launch) or the caller's stream is itself being captured
+  // (then the launches below simply become part of the caller's graph).
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return fail(GT_ERR_HIP, "hipStreamIsCapturing failed");
+  const bool use_graph = d->graphs && !d->prof && cs == hipStreamCaptureStatusNone;
+  const int64_t Bc = chunk_b(d, dtype ? 1 : 0, B, T);
+  for (int64_t b0 = 0; b0 < B; b0 += Bc) {   // batch chunks (chunk_b): independent utterances
+    const int64_t nb = std::min(Bc, B - b0);
+    const size_t fo = (size_t)b0 * 80 * T;
+    Run R;
+    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.s = st;
+    R.ws = align_ws(workspace);
+    R.L = layout(R.dt, nb, T, n_timesteps);
+    R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = out + fo; R.spk_s = nullptr;
+    float* xt = out + fo;
+    R.chk(launch_mask_copy(z + fo, R.mask, (int)nb, 80, (int)T, xt, R.s));   // xt = z * mask  (diffusion.py:257)
+    if (n_timesteps > 0) {
+      float* tbuf = (float*)(R.ws + R.L.tb);
+      float* betas = (float*)(R.ws + R.L.betas);
+      int* stepp = (int*)(R.ws + R.L.step);
+      // time biases and beta(t) of every step (t_i = 1 - (i + 0.5)/N, diffusion.py:259-263), on device
+      TembParams tp;
+      tp.rows = n_timesteps; tp.tvals = nullptr; tp.n_steps = n_timesteps; tp.pe_scale = d->pe_scale;
+      tp.freqs = R.Fp("freqs");
+      tp.w0 = R.Fp("mlp.0.weight"); tp.b0 = R.Fp("mlp.0.bias"); tp.w2 = R.Fp("mlp.2.weight"); tp.b2 = R.Fp("mlp.2.bias");
+      tp.wr = R.Fp("tb.w"); tp.br = R.Fp("tb.b"); tp.nr = kTbRow; tp.tb = tbuf;
+      tp.betas = betas; tp.beta_min = d->beta_min;
+      tp.beta_delta = (float)((double)d->beta_max - (double)d->beta_min);
+      R.chk(launch_temb(tp, R.s));
+      if (d->n_spks > 1) {
+        float* sbuf = (float*)(R.ws + R.L.spk);
+        R.chk(launch_spk_mlp(spk + (size_t)b0 * 64, (int)nb, R.Fp("spk_mlp.0.weight"), R.Fp("spk_mlp.0.bias"),
+                             R.Fp("spk_mlp.2.weight"), R.Fp("spk_mlp.2.bias"), sbuf, R.s));
+        R.spk_s = sbuf;
+      }
+      const float hf = (float)(1.0 / (double)n_timesteps);
+      R.tb_bstride = 0; R.stepp = stepp;
+      R.tb = tbuf; R.betas = betas;
+      if (!use_graph) {
+        R.chk(hipMemsetD32Async((hipDeviceptr_t)stepp, 0, 1, R.s));
+        for (int i = 0; i < n_timesteps && R.err == hipSuccess; ++i) {
+          R.tb = tbuf + (size_t)i * kTbRow;
+          R.betas = betas + i;
+          R.unet(1, nullptr, xt, 0.f, hf);
+        }
+      } else if (R.err == hipSuccess) {
+        // segments of S steps (the whole loop up to 100 steps); a graph's kernels read rows *stepp + j
+        const int S = n_timesteps <= 100 ? n_timesteps : 50;
+        const int q = n_timesteps / S, rem = n_timesteps % S;
+        auto key = [&](int steps) {
+          return std::vector<uintptr_t>{(uintptr_t)dtype, (uintptr_t)nb, (uintptr_t)T, (uintptr_t)steps,
+                                        (uintptr_t)n_timesteps, (uintptr_t)R.ws, (uintptr_t)xt, (uintptr_t)R.mask,
+                                        (uintptr_t)R.mu, (uintptr_t)d->arena[dtype]};
+        };
+        hipGraphExec_t seg = nullptr, tail = nullptr;
+        if ((rc = run_segment_graph(d, R, key(S), S, xt, hf, st, &seg))) return rc;
+        if (rem && (rc = run_segment_graph(d, R, key(rem), rem, xt, hf, st, &tail))) return rc;
+        for (int k = 0; k <= q && R.err == hipSuccess; ++k) {
+          if (k == q && !rem) break;
+          R.chk(hipMemsetD32Async((hipDeviceptr_t)stepp, k * S, 1, st));
+          R.chk(hipGraphLaunch(k < q ? seg : tail, st));
+        }
+      }
     }
-    const double h = 1.0 / (double)n_timesteps;
-    const float hf = (float)h;
-    const float bmin = d->beta_min, bdelta = (float)((double)d->beta_max - (double)d->beta_min);
-    for (int i = 0; i < n_timesteps; ++i) {
-      // t = (1 - (i + 0.5) h) in fp32; noise_t = beta_min + (beta_max - beta_min) * t  (diffusion.py:259-263)
-      const float t = (float)(1.0 - ((double)i + 0.5) * h);
-      volatile float prod = bdelta * t;   // keep the two fp32 roundings of the reference (no fma)
-      const float beta_t = bmin + prod;
-      R.tb = tbuf + (size_t)i * 1792; R.tb_bstride = 0;
-      R.unet(1, nullptr, out, beta_t, hf);
-      if (R.err != hipSuccess) break;
-    }
+    if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
   }
-  if (R.err != hipSuccess) return fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(R.err));
   return GT_OK;
 }
+
+int gt_decoder_set_graphs(gt_decoder* d, int on) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  d->graphs = on != 0;
+  if (!d->graphs) d->drop_graphs();
+  return GT_OK;
+}
+
+int64_t gt_decoder_graph_captures(const gt_decoder* d) { return d ? d->captures : -1; }
 
 }  // extern "C"

@@ -12,6 +12,15 @@ enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3 };
 enum OutMode { OUT_STATS = 0, OUT_PLAIN = 1, OUT_RBOUT = 2, OUT_RESID = 3 };
 enum ConvKind { CONV3 = 0, CONV3_S2 = 1, CONV1 = 2, CONVT4 = 3 };
 
+// Time-bias table: one row of kTbRow floats (the 12 ResnetBlocks' mlp(t_emb) slices) per Euler step.
+// Step-dependent values are addressed through a device step index (`stepp`, may be null = 0): a captured
+// HIP graph of S sampler steps bakes row offsets 0..S-1 into its kernels and is replayed with the index
+// advanced between replays (decoder.cpp, graph segments).
+constexpr int kTbRow = 1792;
+__device__ __forceinline__ const float* tb_at(const float* tb, const int* stepp) {
+  return stepp ? tb + (long)(*stepp) * kTbRow : tb;
+}
+
 struct ConvParams {
   int B, Fin, Tin, Fout, Tout;   // CONVT4: (Fin,Tin) coarse input grid, (Fout,Tout) = 2x fine grid
   int Cin, Cout, Cin_pad;
@@ -23,6 +32,7 @@ struct ConvParams {
   const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
   const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
+  const int* stepp;                                   // IN_GN: device step index (tb_at), or null
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* wscale;                                // non-null: fp8 e4m3 image (conv_wimg8), per-Cout scale
@@ -53,6 +63,7 @@ struct FinalParams {
   const float* mask; int B, T;
   int euler;                          // 0: out = score s; 1: Euler update of xt in place
   float* out; const float* mu; float* xt; float beta_t; float hstep;
+  const float* betas; const int* stepp;   // non-null: beta_t = betas[*stepp] (graph segments)
 };
 hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s);
 
@@ -60,6 +71,7 @@ struct RbOutParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
   const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
   const float* tb; long tb_bstride;   // gn_apply only: time bias rows
+  const int* stepp;                   // gn_apply only: device step index (tb_at), or null
 };
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s);
 // in place: pre = (Mish(GN(pre))*m + tb)*m   (out must equal pre)
@@ -71,6 +83,7 @@ struct TembParams {
   const float* w0; const float* b0; const float* w2; const float* b2;   // mlp.0 [256][64], mlp.2 [64][256]
   const float* wr; const float* br; int nr;           // stacked ResnetBlock mlp.1: [nr][64], [nr]
   float* tb;                                          // [rows][nr]
+  float* betas; float beta_min, beta_delta;           // non-null: betas[row] = beta(t_row) (diffusion.py:262-263)
 };
 hipError_t launch_temb(const TembParams& p, hipStream_t s);
 hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float* b0, const float* w2,

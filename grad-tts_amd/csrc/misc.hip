@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
       p.out[o] = s;
     } else {
       float dxt = 0.5f * ((mu - x) - s);
-      dxt = dxt * p.beta_t;
+      dxt = dxt * (p.betas ? p.betas[*p.stepp] : p.beta_t);
       dxt = dxt * p.hstep;
       p.xt[o] = (x - dxt) * m;
     }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
 #pragma unroll
   for (int k = 0; k < ICH; ++k) {
     gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
-    tb[k] = APPLY ? p.tb[(long)b * p.tb_bstride + c0 + k] : 0.f;
+    tb[k] = APPLY ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + c0 + k] : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
@@ -138,8 +138,13 @@ __global__ __launch_bounds__(256) void temb_kernel(TembParams p) {
   __shared__ float s_emb[64], s_h[256], s_t[64];
   const int row = blockIdx.x, tid = threadIdx.x;
   float t;
-  if (p.tvals) t = p.tvals[row];
-  else t = (float)(1.0 - ((double)row + 0.5) * (1.0 / (double)p.n_steps));   // diffusion.py:259-260
+  if (p.tvals) {
+    t = p.tvals[row];
+  } else {   // t = 1 - (i + 0.5) h in double, rounded once to fp32 (diffusion.py:259-260); no contraction
+    t = (float)__dsub_rn(1.0, __dmul_rn((double)row + 0.5, 1.0 / (double)p.n_steps));
+    // noise_t = beta_min + (beta_max - beta_min) * t with the two fp32 roundings of the reference (:262-263)
+    if (p.betas && tid == 0) p.betas[row] = __fadd_rn(p.beta_min, __fmul_rn(p.beta_delta, t));
+  }
   if (tid < 64) {
     const int k = tid & 31;
     const float arg = (p.pe_scale * t) * p.freqs[k];       // scale * x * emb (diffusion.py:122)

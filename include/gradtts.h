@@ -83,6 +83,20 @@ int gt_reverse_diffusion(gt_decoder* dec, int dtype, const float* z, const float
                          const float* spk, int64_t B, int64_t T, int32_t n_timesteps, float* out, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* HIP-graph replay of the sampler (default on; environment GT_GRAPHS=0 turns it off at creation).
+ * gt_reverse_diffusion captures its Euler steps once per (shape, dtype, tensor and workspace addresses) into
+ * graphs of up to 100 steps (50-step segments plus a remainder beyond that; a device-side step index selects
+ * each step's time-bias row and beta(t)) and replays them on the caller's stream. Captures are skipped while
+ * profiling is on or when the caller's stream is itself being captured (the launches then join the caller's
+ * graph). Results are bit-identical with and without graphs. gt_decoder_graph_captures counts captures. */
+int gt_decoder_set_graphs(gt_decoder* dec, int on);
+int64_t gt_decoder_graph_captures(const gt_decoder* dec);
+
+/* Batches of any size: a compute call runs the batch in chunks of at most
+ * floor((2^31 - 1) / (80 * T * 64 * element_size)) utterances (the kernels' 32-bit buffer ranges), each a
+ * complete evaluation in the same workspace, which gt_decoder_workspace_bytes sizes for one chunk. Results do
+ * not depend on the chunking (per-utterance GroupNorm / attention statistics). */
+
 /* Diagnostics: run gt_estimator_forward and additionally copy the activation produced by `stage`
  * (a module path of the reference, e.g. "downs.0.1", "downs.1.2", "mid_block1", "ups.0.3", with
  * ".pre1"/".pre2" for a ResnetBlock's pre-GroupNorm conv outputs, or "final_block.pre") to
