@@ -102,6 +102,23 @@ template <> struct Mma<float> {
 // col = lane & 31, row = (j & 3) + 8 * (j >> 2) + 4 * h).
 GT_DEV int acc_row(int j, int h) { return (j & 3) + 8 * (j >> 2) + 4 * h; }
 
+// ---------------------------------------------------------------- cross-lane sums
+// Sum of x over the 16-lane row (every lane, fixed order): DPP row rotations by 1, 2, 4, 8
+GT_DEV float row_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, false));
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false));
+  return x;
+}
+// Sum over the 32 lanes of this half-wave, valid in lanes 0 and 32: row sums, then rows 1/3 brought down to
+// rows 0/2 by v_permlane16_swap
+GT_DEV float half_sum32(float x) {
+  const float s = row_sum16(x);
+  const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return s + __uint_as_float(sw[1]);
+}
+
 // ---------------------------------------------------------------- GroupNorm statistics
 // GroupNorm (model/diffusion.py:53, 8 groups, eps 1e-5) normalises over (C/8) x F x T -- every grid
 // position, padded frames included. The producing conv writes, per workgroup, the fp32 sum and sum of

@@ -63,20 +63,28 @@ struct ConvCfg {
   static constexpr int CKB = conv_ckb(sizeof(A) == 2);
   static constexpr int SUBS = CKB / 16;
   static constexpr int POSB = CKB + 16;
-  // weight slab: bf16/fp32 image (conv_wrow) or the fp8 image (conv8_wrow, W8: e4m3 weights, bf16 operands)
-  static constexpr int WROW = W8 ? conv8_wrow(NTAP) : conv_wrow(NTAP, CKB);
-  static constexpr int WBYTES = W8 ? conv8_wbytes(NT, NTAP) : conv_wbytes(NT, NTAP, CKB);
+  // weight slab: bf16/fp32 image (wimage.h: half A = taps [0, NA), half B = the rest) or the fp8 image
+  // (conv8_wrow, W8: e4m3 weights, bf16 operands)
+  static constexpr int ABF = sizeof(A) == 2 ? 1 : 0;
+  static constexpr int NA = W8 ? NTAP : conv_na(ABF, NTAP);
+  static constexpr int WROW = W8 ? conv8_wrow(NTAP) : conv_wrow(NA, CKB);   // half A rows (all taps if unsplit)
+  static constexpr int WROWB = conv_wrow(NTAP - NA, CKB);
+  static constexpr int HA = W8 ? conv8_wbytes(NT, NTAP) : conv_habytes(ABF, NT, NTAP, CKB);
+  static constexpr int WBYTES = W8 ? HA : HA + conv_hbbytes(ABF, NT, NTAP, CKB);
   static constexpr int WPIECES_ALL = WBYTES / 1024;        // 1 KiB DMA pieces per chunk
   static constexpr int WPIECES = (WPIECES_ALL + 3) / 4;    // per wave (the last round may be partial)
+  // Split pipeline (bf16, multi-tap, operand from an activation): the two halves of chunk c+1 are staged while
+  // the other half of chunk c is in the MFMAs. Every wave issues exactly PA / PB DMA pieces per half and PPT
+  // patch loads per chunk, so counted vmcnt waits retire exactly the right ones.
+  static constexpr bool SPLIT = !W8 && NA < NTAP && IN != IN_INPUT;
+  static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
   static constexpr int CK = CKB / (int)sizeof(A);
   static constexpr int ICH = 16 / (int)sizeof(A);
   static constexpr int KSTEP_B = 16 * (int)sizeof(A);
   static constexpr int KSTEPS = CKB / KSTEP_B;
   static constexpr int PITEMS = PR * PC * SUBS;
   static constexpr int PPT = (PITEMS + 255) / 256;
-  static constexpr int EPI_ROW = 36;                     // floats per transposed row (9 slots: conflict-free)
-  static constexpr int EPI_BYTES = 4 * 32 * EPI_ROW * 4;
-  static constexpr int A_BYTES = PR * PC * POSB > EPI_BYTES ? PR * PC * POSB : EPI_BYTES;
+  static constexpr int A_BYTES = PR * PC * POSB;
   static constexpr int SMEM0 = A_BYTES + WBYTES + (3 * 256 + 128 + 64 + 16 + 128) * 4;
   // Workgroups per CU are capped by LDS where more resident tiles measured slower (cache/write
   // contention, not latency hiding, bounds them): CAP = 0 leaves occupancy to registers and LDS.
@@ -89,6 +97,7 @@ struct ConvCfg {
   static_assert(TF * RBT % WM == 0, "row blocks split evenly over the waves");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
   static_assert(WBYTES % 1024 == 0, "whole DMA pieces");
+  static_assert(!SPLIT || (HA % 4096 == 0 && (WBYTES - HA) % 4096 == 0 && PB + PPT <= 63), "wave-even halves");
   static_assert(!W8 || (sizeof(A) == 2 && KIND != CONV1), "fp8 weights: bf16 operands, 3x3 / 2x2 convs");
 };
 
@@ -137,7 +146,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int cout0 = ntile * NT;
   const int par = blockIdx.z, pf = par >> 1, pt = par & 1;
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) wave index
   const int wm = wv % C::WM, wn = wv / C::WM;
   const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
   const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
@@ -301,88 +311,150 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   }
   if (tid < NT) s_bias[tid] = c_bias;                 // all visible after the first chunk barrier
   if (W8 && tid < NT) s_wsc[tid] = c_wsc;
-  for (int ch = 0; ch < nchunk; ++ch) {
-    const int c0 = ch * C::CK;
-    cta_sync();                                        // previous chunk's fragments are consumed
-    dma_weights(ch);                                   // issued first: its latency overlaps the patch store
-    store_patch(c0);
-    // The weight DMA must have landed before any wave reads sW; the compiler does not track
-    // global_load_lds reliably (it was missing in the 1x1/128-wide instantiation: an intermittent,
-    // load-dependent race), so the wait is explicit.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    cta_sync();
-    if (ch + 1 < nchunk) {
-      if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && c0 + C::CK == p.C0) set_offsets(p.C1);
-      load_patch(c0 + C::CK);                          // in flight during this chunk's MFMAs
-    }
+
+  // MFMAs of taps [t0, t1) of the staged chunk (t0, t1 compile-time at every call site). Software-pipelined
+  // over the flattened (tap, row block) steps: the fragments of step i+1 (and the next tap's weight fragments)
+  // are read from LDS before step i's two MFMAs, so the LDS latency hides behind them (issued in the natural
+  // order, the compiler waited lgkmcnt(0) in front of every MFMA pair).
+  // Row block rb of wave wm is block rb * WM + wm (mel row rb * WM / RBT + wm / RBT, 32-frame block wm % RBT):
+  // a fragment's LDS address is one per-lane base plus a compile-time offset per (tap, rb), which the ds_read
+  // offset field absorbs (no address register per fragment).
+  static_assert(C::WM % C::RBT == 0, "row blocks interleave over the waves");
+  // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0, in[j+1] (k=0) & in[j]
+  // (k=2) for p=1; with the patch origin at (j0-1, j0'-1) tap (a, b) reads patch row 1 + pf - a, column
+  // 1 + pt - b. The parity part goes into the base.
+  const int a_base = ((wm / C::RBT) * C::S * C::PC + ((wm % C::RBT) * 32 + r) * C::S +
+                      (CONVT ? (1 + pf) * C::PC + 1 + pt : 0)) * C::POSB + h * (C::KSTEP_B / 2);
+  auto load_a = [&](int tap, int rb, int ks) {
+    const int dr = CONVT ? -(tap >> 1) : tap / C::KS;
+    const int dc = CONVT ? -(tap & 1) : tap % C::KS;
+    const int off = ((rb * (C::WM / C::RBT) * C::S + dr) * C::PC + dc) * C::POSB + ks * C::KSTEP_B;
+    return Mma<A>::load(sA + a_base + off);
+  };
+  auto load_b = [&](int tap, int cb, int ks) {
+    const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
+    const int row = wn * 64 + cb * 32 + r;
+    if constexpr (W8)   // 8-byte units swizzled per row (wimage.h conv8_swz; row base is a multiple of 32)
+      return w8_frag(sW + row * C::WROW + ((2 * tap + h) ^ conv8_swz(C::NTAP, r)) * 8);
+    else if (tap < C::NA)
+      return Mma<A>::load(sW + row * C::WROW + tap * C::CKB + koff);
+    else
+      return Mma<A>::load(sW + C::HA + row * C::WROWB + (tap - C::NA) * C::CKB + koff);
+  };
+  auto mma_taps = [&](int t0, int t1) {
+    constexpr int RB = C::RBW, KS = C::KSTEPS;
+    frag fa[2], fb[2][2];
+    fa[0] = load_a(t0, 0, 0);
+    fb[0][0] = load_b(t0, 0, 0);
+    fb[0][1] = load_b(t0, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, W8 ? 1 : 3, 0);   // LDS reads of the first step
 #pragma unroll
-    for (int tap = 0; tap < C::NTAP; ++tap) {
-      int dr, dc;
-      if (CONVT) {
-        // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0,
-        // in[j+1] (k=0) & in[j] (k=2) for p=1.  Patch origin is (j0-1, j0'-1).
-        const int a = tap >> 1, bb = tap & 1;
-        dr = 1 + (pf ? (a ? 0 : 1) : (a ? -1 : 0));
-        dc = 1 + (pt ? (bb ? 0 : 1) : (bb ? -1 : 0));
-      } else {
-        dr = tap / C::KS;
-        dc = tap - dr * C::KS;
-      }
-#pragma unroll
-      for (int ks = 0; ks < C::KSTEPS; ++ks) {
-        const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
-        frag af[C::RBW], bfr[2];
-#pragma unroll
-        for (int rb = 0; rb < C::RBW; ++rb) {
-          const int blk = wm * C::RBW + rb, lrow = blk / C::RBT, tblk = blk % C::RBT;
-          const int prow = lrow * C::S + dr;
-          const int pcol = (tblk * 32 + r) * C::S + dc;
-          af[rb] = Mma<A>::load(sA + (prow * C::PC + pcol) * C::POSB + koff);
+    for (int i = 0; i < C::NTAP * KS * RB; ++i) {
+      const int u = i / RB, rb = i % RB;          // u = tap-kstep unit
+      const int tap = t0 + u / KS, ks = u % KS;
+      if (tap >= t1) break;
+      const int n = i + 1, un = n / RB, rbn = n % RB;
+      const int tapn = t0 + un / KS, ksn = un % KS;
+      if (tapn < t1) {
+        if (rbn == 0) {                             // next unit: its weight fragments first
+          fb[un & 1][0] = load_b(tapn, 0, ksn);
+          fb[un & 1][1] = load_b(tapn, 1, ksn);
         }
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          if constexpr (W8)   // 8-byte units swizzled per row (wimage.h conv8_swz; row base is a multiple of 32)
-            bfr[cb] = w8_frag(sW + (wn * 64 + cb * 32 + r) * C::WROW + ((2 * tap + h) ^ conv8_swz(C::NTAP, r)) * 8);
-          else
-            bfr[cb] = Mma<A>::load(sW + (wn * 64 + cb * 32 + r) * C::WROW + tap * C::CKB + koff);
-#pragma unroll
-        for (int rb = 0; rb < C::RBW; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) Mma<A>::mma(af[rb], bfr[cb], acc[rb][cb]);
+        fa[n & 1] = load_a(tapn, rbn, ksn);
       }
+      // weights as the A operand, positions as B: the accumulator is channel x position (epilogue below)
+      Mma<A>::mma(fb[u & 1][0], fa[i & 1], acc[rb][0]);
+      Mma<A>::mma(fb[u & 1][1], fa[i & 1], acc[rb][1]);
+      // pin the order: step i+1's LDS reads, then step i's MFMAs (the compiler otherwise groups a tap's reads
+      // ahead of its MFMAs behind one lgkmcnt(0))
+      if constexpr (sizeof(A) == 2 && !W8) {
+        if (tapn < t1 && rbn == 0) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        if (tapn < t1 && rbn != 0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+    }
+  };
+  // patch loads of chunk k (channels k*CK..): switch to the second tensor's offsets at the concat boundary
+  auto issue_patch = [&](int k) {
+    const int ck0 = k * C::CK;
+    if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && ck0 == p.C0) set_offsets(p.C1);
+    load_patch(ck0);
+  };
+
+  if constexpr (C::SPLIT) {
+    // Per chunk ch (3 barriers): [A(ch) landed] taps of half A | [B(ch) landed, A free] stage A(ch+1), taps of
+    // half B | [B and patch free] patch ch+1 -> LDS, stage B(ch+1), patch loads of ch+2. VMEM issue order per
+    // wave: A(ch+1), B(ch+1), patch(ch+2) -- the counted waits below retire exactly the needed group (in-order
+    // vmcnt; the compiler's own waits cover the patch registers).
+    auto dma_half = [&](int ch, int half) {
+      const char* src = wimg + (long)ch * C::WBYTES + (half ? C::HA : 0) + lane * 16;
+      char* dst = sW + (half ? C::HA : 0);
+#pragma unroll
+      for (int k = 0; k < (half ? C::PB : C::PA); ++k) {
+        const int i = wv + 4 * k;
+        __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
+                                         (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+      }
+    };
+    lds_barrier();                                     // s_sc / s_sh / s_tb / s_bias visible; s_red (sA) free
+    dma_half(0, 0);
+    store_patch(0);
+    dma_half(0, 1);
+    if (nchunk > 1) issue_patch(1);
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const bool more = ch + 1 < nchunk;             // patch(ch+1) loads are in flight
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PB + C::PPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PB) : "memory");
+      cta_sync();                                      // A(ch) landed for every wave; patch(ch) stores visible
+      mma_taps(0, C::NA);
+      if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cta_sync();                                      // B(ch) landed; every wave is done with half A
+      if (more) dma_half(ch + 1, 0);
+      mma_taps(C::NA, C::NTAP);
+      if (more) {
+        cta_sync();                                    // half B and the patch are free
+        store_patch((ch + 1) * C::CK);
+        dma_half(ch + 1, 1);
+        if (ch + 2 < nchunk) issue_patch(ch + 2);
+      }
+    }
+  } else {
+    for (int ch = 0; ch < nchunk; ++ch) {
+      const int c0 = ch * C::CK;
+      cta_sync();                                        // previous chunk's fragments are consumed
+      dma_weights(ch);                                   // issued first: its latency overlaps the patch store
+      store_patch(c0);
+      // The weight DMA must have landed before any wave reads sW; the compiler does not track
+      // global_load_lds reliably (it was missing in the 1x1/128-wide instantiation: an intermittent,
+      // load-dependent race), so the wait is explicit.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cta_sync();
+      if (ch + 1 < nchunk) issue_patch(ch + 1);        // in flight during this chunk's MFMAs
+      mma_taps(0, C::NTAP);
     }
   }
 
-  // ---- epilogue: transpose each 32x32 block through the wave's own LDS scratch -> lane = (position,
-  // 8 channels); one workgroup barrier (patch/weights are dead), then wave-local ordering only
-  // LDS instructions of one wave execute in order, so the transposition only needs its own LDS traffic
-  // drained and the compiler kept from reordering memory operations. (A wavefront-scope release fence
-  // would also emit vmcnt(0) and serialise every block behind the previous block's global stores.)
-  auto wave_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-  __syncthreads();
-  float* scr = reinterpret_cast<float*>(sA) + wv * 32 * C::EPI_ROW;
-  const int g8 = lane & 3;                 // 8-channel group within the 32-channel block
-  float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+  // ---- epilogue straight from the accumulators. Lane (r, h) of block (rb, cb) holds channels
+  // cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r; one v_permlane32_swap per register pair leaves it
+  // with channels cb*32 + 16 pr + 8h + 0..7 (pr = 0, 1) of position r: bias, the ResnetBlock-output /
+  // residual fusion, 16-B stores and the GroupNorm partial sums (one 8-channel group per lane) with no LDS
+  // round trip. Stores never wait, but vmcnt is one in-order counter: a load waited on after a store waits for
+  // that store too, so the residual / pre-activation inputs are loaded ahead of the stores.
+  float gs[2][2] = {{0.f, 0.f}, {0.f, 0.f}}, gq[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
   A* out = reinterpret_cast<A*>(p.out);
-  // Per (row block, half): element offset of this lane's output position (channel cout0), -1 past T,
-  // and its mask. Stores never wait, but vmcnt is one in-order counter: a load waited on after a
-  // store waits for that store too. So no load may sit between the stores: bias and GroupNorm
-  // coefficients come from LDS, and the residual / pre-activation inputs are loaded up front.
-  long obase[C::RBW][2];
-  float om[C::RBW][2];
+  long obase[C::RBW];
+  float om[C::RBW];
 #pragma unroll
   for (int rb = 0; rb < C::RBW; ++rb) {
-    const int blk = wm * C::RBW + rb, lrow = blk / C::RBT, tblk = blk % C::RBT;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int tc = t0 + tblk * 32 + (lane >> 2) + 16 * half;
-      const int frow = f0 + lrow;
-      const int fo = CONVT ? 2 * frow + pf : frow;
-      const int to = CONVT ? 2 * tc + pt : tc;
-      const bool valid = tc < Tg;
-      obase[rb][half] = valid ? (((long)b * p.Fout + fo) * p.Tout + to) * p.Cout + cout0 : -1;
-      om[rb][half] = (OUT == OUT_RBOUT && valid) ? mask_at(p.mask, p.T0, b, to, p.lvl_out) : 0.f;
-    }
+    const int blk = rb * C::WM + wm, lrow = blk / C::RBT, tblk = blk % C::RBT;   // as load_a
+    const int tc = t0 + tblk * 32 + r;
+    const int frow = f0 + lrow;
+    const int fo = CONVT ? 2 * frow + pf : frow;
+    const int to = CONVT ? 2 * tc + pt : tc;
+    const bool valid = tc < Tg;
+    obase[rb] = valid ? (((long)b * p.Fout + fo) * p.Tout + to) * p.Cout + cout0 : -1;
+    om[rb] = (OUT == OUT_RBOUT && valid) ? mask_at(p.mask, p.T0, b, to, p.lvl_out) : 0.f;
   }
   constexpr bool EIN = OUT == OUT_RBOUT || OUT == OUT_RESID;
   constexpr int EIPI = (int)sizeof(A) / 2;                         // 16-B items per 8 channels
@@ -395,12 +467,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int half = 0; half < 2; ++half)
+      for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
         for (int q = 0; q < EIPI; ++q) {
-          const long ob = obase[rb][half];
-          const int cl = wn * 64 + cb * 32 + g8 * 8 + 4 * q;
-          ein[((slot * 2 + cb) * 2 + half) * EIPI + q] =
+          const long ob = obase[rb];
+          const int cl = wn * 64 + cb * 32 + pr * 16 + 8 * h + 4 * q;
+          ein[((slot * 2 + cb) * 2 + pr) * EIPI + q] =
               ob >= 0 ? *reinterpret_cast<const uint4*>(esrc + ob + cl) : make_uint4(0, 0, 0, 0);
         }
   };
@@ -413,77 +485,77 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 #pragma unroll
   for (int rb = 0; rb < C::RBW; ++rb) {
     if (EIN && !EALL && rb + 1 < C::RBW) load_ein(rb + 1, (rb + 1) & 1);
+    const long ob = obase[rb];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
+      float v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) scr[acc_row(j, h) * C::EPI_ROW + r] = acc[rb][cb][j];
-      wave_sync();
-      const int cl = wn * 64 + cb * 32 + g8 * 8;       // tile-local first channel of this lane
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
+      for (int q = 0; q < 16; ++q) v[q] = acc[rb][cb][q];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int pos = (lane >> 2) + 16 * half;
-        float v[8];
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(scr + pos * C::EPI_ROW + g8 * 8 + 4);
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]), __float_as_uint(v[8 * pr + 4 + q]),
+                                                           false, false);
+          v[8 * pr + q] = __uint_as_float(sw[0]);
+          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int cl = wn * 64 + cb * 32 + pr * 16 + 8 * h;   // tile-local first channel of this lane
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
+        float o[8];
         if (W8) {
           const f32x4 s0 = *reinterpret_cast<const f32x4*>(s_wsc + cl);
           const f32x4 s1 = *reinterpret_cast<const f32x4*>(s_wsc + cl + 4);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) { v[k] = lo[k] * s0[k] + b0[k]; v[4 + k] = hi[k] * s1[k] + b1[k]; }
+          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] * s0[k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] * s1[k] + b1[k]; }
         } else {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) { v[k] = lo[k] + b0[k]; v[4 + k] = hi[k] + b1[k]; }
+          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] + b1[k]; }
         }
-        const long ob = obase[rb][half];
         if (ob >= 0) {
           if (OUT == OUT_STATS) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) { gs[cb] += v[k]; gq[cb] += v[k] * v[k]; }
+            for (int k = 0; k < 8; ++k) { gs[cb][pr] += o[k]; gq[cb][pr] += o[k] * o[k]; }
           } else if (EIN) {
-            const int ei = (((EALL ? rb : (rb & 1)) * 2 + cb) * 2 + half) * EIPI;
+            const int ei = (((EALL ? rb : (rb & 1)) * 2 + cb) * 2 + pr) * EIPI;
             float e[8];
             item_to_f(ein[ei], e, A());
             if (EIPI == 2) item_to_f(ein[ei + (EIPI - 1)], e + 4, A());
             if (OUT == OUT_RBOUT) {
               // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
-              const float m = om[rb][half];
+              const float m = om[rb];
 #pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] = mish_act<A>(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + v[k];
+              for (int k = 0; k < 8; ++k) o[k] = mish_act<A>(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + o[k];
             } else {                                   // Residual: fn(x) + x   (diffusion.py:108)
 #pragma unroll
-              for (int k = 0; k < 8; ++k) v[k] += e[k];
+              for (int k = 0; k < 8; ++k) o[k] += e[k];
             }
           }
           if (sizeof(A) == 2) {
-            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(v, A());
+            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(o, A());
           } else {
-            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(v, A());
-            *reinterpret_cast<uint4*>(out + ob + cl + 4) = f_to_item(v + 4, A());
+            *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(o, A());
+            *reinterpret_cast<uint4*>(out + ob + cl + 4) = f_to_item(o + 4, A());
           }
         }
       }
-      wave_sync();
     }
   }
   if (OUT == OUT_STATS) {
-    // per 8-channel sub-group: reduce over the wave's positions (the 16 lanes with equal lane&3):
-    // rotations by 4 and 8 inside each 16-lane row (DPP), then across the four rows
-    auto ror4 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, false)); };
-    auto ror8 = [](float x) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false)); };
+    // per 8-channel group (cb, pr, h): sum over the half-wave's 32 positions, then over waves and groups
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      float s = gs[cb], q = gq[cb];
-      s += ror4(s); q += ror4(q);           // DPP row_ror:4 / row_ror:8
-      s += ror8(s); q += ror8(q);
-      s += __shfl_xor(s, 16); q += __shfl_xor(q, 16);
-      s += __shfl_xor(s, 32); q += __shfl_xor(q, 32);
-      if (lane < 4) {
-        s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 0] = s;
-        s_sub[((wv * 2 + cb) * 4 + lane) * 2 + 1] = q;
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const float s = half_sum32(gs[cb][pr]), q = half_sum32(gq[cb][pr]);
+        if (r == 0) {
+          s_sub[((wv * 2 + cb) * 4 + pr * 2 + h) * 2 + 0] = s;
+          s_sub[((wv * 2 + cb) * 4 + pr * 2 + h) * 2 + 1] = q;
+        }
       }
-    }
     __syncthreads();
     // ... then per GroupNorm group over waves / sub-groups in a fixed order, one slot per workgroup
     if (tid < 8) {

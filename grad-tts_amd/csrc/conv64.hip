@@ -54,22 +54,6 @@ constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
 
-// Sum of x over the 16-lane row (every lane, fixed order): DPP row rotations by 1, 2, 4, 8
-GT_DEV float row_sum16(float x) {
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xf, 0xf, false));
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xf, 0xf, false));
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, false));
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false));
-  return x;
-}
-// Sum over the 32 lanes of this half-wave, valid in lanes 0 and 32: row sums, then rows 1/3 brought down to
-// rows 0/2 by v_permlane16_swap
-GT_DEV float half_sum32(float x) {
-  const float s = row_sum16(x);
-  const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  return s + __uint_as_float(sw[1]);
-}
-
 // Mish(y) + tb for the bf16 operand path: tanh(softplus(y)) = 1 - 2 / ((e^y + 1)^2 + 1), so
 // Mish(y) + tb = y * (1 - 2 r) + tb with r = 1 / ((e^y + 1)^2 + 1): one v_exp_f32, one v_rcp_f32, five FMA-class
 // ops. e^y = inf for large y gives r = 0, i.e. y + tb (torch's softplus threshold). Absolute error

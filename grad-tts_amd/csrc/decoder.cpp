@@ -159,7 +159,9 @@ struct gt_decoder {
   size_t pool_used = 0;
   // captured sampler segments (gt_reverse_diffusion): HIP graphs of S Euler steps, keyed by everything the
   // captured kernels bake in (shapes, dtype, tensor / workspace / weight-arena addresses)
-  bool graphs = true;
+  // off by default: same-box A/B (tools/ab_graph.sh) measured no gain at B = 32 and a 7 % loss at B = 4 (every
+  // batch size is GPU-bound; graph replay adds inter-node gaps); GT_GRAPHS=1 or gt_decoder_set_graphs enables
+  bool graphs = false;
   hipStream_t cap_stream = nullptr;
   struct Graph { std::vector<uintptr_t> key; hipGraphExec_t exec; };
   std::vector<Graph> gcache;   // most recently used last

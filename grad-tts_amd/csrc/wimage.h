@@ -4,10 +4,13 @@
 // The image is laid out in exactly the order conv_kernel keeps the weight slab in LDS, so staging a
 // K-chunk is a straight, fully coalesced global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave
 // instruction) with no register round trip:
-//   image[n_tile][chunk] = WBYTES bytes = NT rows (output channels) x WROW bytes, zero padded;
-//   row n           = NTAP taps x CKB bytes (CK input channels of this chunk) + 16 B pad
-// The 16-byte row pad makes the row stride an odd number of 16-B LDS slots, so the 16 lanes of a
-// ds_read_b128 group (16 different output channels) hit 16 different slots.
+//   image[n_tile][chunk] = WBYTES bytes = half A, then half B (bf16 images with more than one tap):
+//   half A          = NT rows x WROWA bytes, taps [0, NA): NA x CKB bytes + 16 B pad, zero padded to 4 KiB
+//   half B          = NT rows x WROWB bytes, taps [NA, NTAP): (NTAP - NA) x CKB + 16 B pad, padded to 4 KiB
+// (fp32 and 1x1 images: one half with every tap). The 16-byte row pad makes the row stride an odd number of
+// 16-B LDS slots, so the 16 lanes of a ds_read_b128 group (16 different output channels) hit 16 different
+// slots. The two halves are staged separately: conv_kernel computes the taps of one half while the other
+// half of the next chunk lands (wave-even 1 KiB DMA pieces: each half is a multiple of 4 KiB).
 #pragma once
 
 namespace gt {
@@ -42,12 +45,18 @@ inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int c
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
 inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }
-inline __host__ __device__ constexpr int conv_wbytes(int nt, int ntap, int ckb) {
-  return ((nt * conv_wrow(ntap, ckb) + 4095) / 4096) * 4096;
+inline __host__ __device__ constexpr int round4k(int b) { return ((b + 4095) / 4096) * 4096; }
+// taps in half A: split images (bf16, more than one tap) put the first ceil(NTAP/2) taps there
+inline __host__ __device__ constexpr int conv_na(int act_bf16, int ntap) { return (act_bf16 && ntap > 1) ? (ntap + 1) / 2 : ntap; }
+inline __host__ __device__ constexpr int conv_habytes(int act_bf16, int nt, int ntap, int ckb) {
+  return round4k(nt * conv_wrow(conv_na(act_bf16, ntap), ckb));
+}
+inline __host__ __device__ constexpr int conv_hbbytes(int act_bf16, int nt, int ntap, int ckb) {
+  return conv_na(act_bf16, ntap) == ntap ? 0 : round4k(nt * conv_wrow(ntap - conv_na(act_bf16, ntap), ckb));
 }
 
 struct WImg {
-  int nt, ckb, ck, ntap, wrow, wbytes, nchunk, nntile;
+  int nt, ckb, ck, ntap, na, wrowa, wrowb, habytes, wbytes, nchunk, nntile;
   long total;   // bytes of the whole image
 };
 
@@ -57,8 +66,11 @@ inline __host__ __device__ WImg conv_wimg(int act_bf16, int ntap, int cin, int c
   w.ckb = conv_ckb(act_bf16);
   w.ck = w.ckb / (act_bf16 ? 2 : 4);
   w.ntap = ntap;
-  w.wrow = conv_wrow(ntap, w.ckb);
-  w.wbytes = conv_wbytes(w.nt, ntap, w.ckb);
+  w.na = conv_na(act_bf16, ntap);
+  w.wrowa = conv_wrow(w.na, w.ckb);
+  w.wrowb = conv_wrow(ntap - w.na, w.ckb);
+  w.habytes = conv_habytes(act_bf16, w.nt, ntap, w.ckb);
+  w.wbytes = w.habytes + conv_hbbytes(act_bf16, w.nt, ntap, w.ckb);
   w.nchunk = (cin + w.ck - 1) / w.ck;
   w.nntile = (cout + w.nt - 1) / w.nt;
   w.total = (long)w.nntile * w.nchunk * w.wbytes;
@@ -69,7 +81,9 @@ inline __host__ __device__ WImg conv_wimg(int act_bf16, int ntap, int cin, int c
 inline __host__ __device__ long conv_wimg_off(const WImg& w, int co, int tap, int ci, int esz) {
   const int tile = co / w.nt, n = co - tile * w.nt;
   const int ch = ci / w.ck, k = ci - ch * w.ck;
-  return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + (long)tap * w.ckb + (long)k * esz;
+  const long base = ((long)tile * w.nchunk + ch) * w.wbytes + (long)k * esz;
+  if (tap < w.na) return base + (long)n * w.wrowa + (long)tap * w.ckb;
+  return base + w.habytes + (long)n * w.wrowb + (long)(tap - w.na) * w.ckb;
 }
 
 // ---- fp8 weight image (GT_BF16_W8: e4m3 weights, bf16 activations) for the 3x3 / strided / transposed
@@ -90,8 +104,10 @@ inline __host__ __device__ WImg conv_wimg8(int ntap, int cin, int cout) {
   w.ckb = 16;
   w.ck = 16;
   w.ntap = ntap;
-  w.wrow = conv8_wrow(ntap);
-  w.wbytes = conv8_wbytes(w.nt, ntap);
+  w.na = ntap;
+  w.wrowa = conv8_wrow(ntap);
+  w.wrowb = 0;
+  w.wbytes = w.habytes = conv8_wbytes(w.nt, ntap);
   w.nchunk = (cin + w.ck - 1) / w.ck;
   w.nntile = (cout + w.nt - 1) / w.nt;
   w.total = (long)w.nntile * w.nchunk * w.wbytes;
@@ -102,7 +118,7 @@ inline __host__ __device__ long conv_wimg8_off(const WImg& w, int co, int tap, i
   const int tile = co / w.nt, n = co - tile * w.nt;
   const int ch = ci / 16, k = ci & 15;
   const int unit = (2 * tap + (k >> 3)) ^ conv8_swz(w.ntap, n);
-  return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrow + unit * 8 + (k & 7);
+  return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrowa + unit * 8 + (k & 7);
 }
 
 }  // namespace gt

@@ -83,7 +83,8 @@ int gt_reverse_diffusion(gt_decoder* dec, int dtype, const float* z, const float
                          const float* spk, int64_t B, int64_t T, int32_t n_timesteps, float* out, void* workspace,
                          size_t workspace_bytes, void* stream);
 
-/* HIP-graph replay of the sampler (default on; environment GT_GRAPHS=0 turns it off at creation).
+/* HIP-graph replay of the sampler (default off -- measured no faster, the sampler is GPU-bound at every batch
+ * size; environment GT_GRAPHS=1 turns it on at creation).
  * gt_reverse_diffusion captures its Euler steps once per (shape, dtype, tensor and workspace addresses) into
  * graphs of up to 100 steps (50-step segments plus a remainder beyond that; a device-side step index selects
  * each step's time-bias row and beta(t)) and replays them on the caller's stream. Captures are skipped while

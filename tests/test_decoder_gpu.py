@@ -213,6 +213,12 @@ def test_concurrent_streams_match_one_stream():
 # N = 100 sampler output by ~3e-2 relative to the fp32 weights (synthetic weights).
 W8 = "bf16_w8"
 W8_STAGE_TOL = 2e-2
+# One W8 estimator call: the max element may reach 1.5 x the reference's own bf16 envelope, and the 99.9th
+# percentile must stay under 1 x. Measured on estimator_s247: one sensitive element (b=1, f=58, t=25) is the
+# max in every build, at 1.39e-2 or 1.96e-2 depending only on the fp32 summation order of the GroupNorm
+# partials (two builds, same box), while the 2nd-largest (1.1-1.3e-2), p99.9 (1.01e-2) and mean (1.57e-3) are
+# unchanged (tools/diag_w8.py).
+W8_EST_MAX_X, W8_EST_P999_X = 1.5, 1.0
 
 
 @pytest.mark.parametrize("name", EST)
@@ -227,7 +233,10 @@ def test_w8_estimator_matches_oracle_dequantized(name):
                              torch.from_numpy(spk) if spk is not None else None, n_spks).numpy()
     y = dec.estimator(_cuda(g["x"]), _cuda(g["mask"]), _cuda(g["mu"]), _cuda(g["t"]),
                       _cuda(spk) if spk is not None else None).cpu().numpy()
-    report(f"w8 estimator {name} vs dequantized oracle", rel_err(y, ref), bf16_est_gate(name))
+    env = bf16_est_gate(name) / 1.25   # the reference's own bf16-autocast error on this fixture
+    d = np.abs(y.astype(np.float64) - ref) / np.abs(ref).max()
+    report(f"w8 estimator {name} vs dequantized oracle (p99.9)", float(np.quantile(d, 0.999)), W8_EST_P999_X * env)
+    report(f"w8 estimator {name} vs dequantized oracle", rel_err(y, ref), W8_EST_MAX_X * env)
 
 
 def test_w8_every_stage_matches_oracle_dequantized():

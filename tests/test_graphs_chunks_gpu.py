@@ -1,6 +1,6 @@
 """HIP-graph replay of the sampler and internal batch chunking (include/gradtts.h).
 
-* Graph segments (gt_reverse_diffusion captures up to 100 Euler steps per graph; beyond that 50-step segments
+* Graph segments (opt-in, gt_decoder_set_graphs; gt_reverse_diffusion captures up to 100 Euler steps per graph; beyond that 50-step segments
   plus a remainder, a device-side step index selecting each step's time-bias row and beta(t)) must give results
   bit-identical to the eager launch sequence, and a repeated call with the same buffers must replay, not
   re-capture.
@@ -61,6 +61,7 @@ def test_graph_reused_with_same_buffers():
     B, T, N = 2, 64, 30
     L = _lib.lib()
     h = dec.estimator._native()
+    _lib.check(L.gt_decoder_set_graphs(h, 1), "set_graphs")
     dcode = _dtype_code(torch.bfloat16)
     out = torch.empty((B, 80, T), dtype=torch.float32, device="cuda")
     ws = torch.empty(L.gt_decoder_workspace_bytes(h, dcode, B, T, N), dtype=torch.uint8, device="cuda")
