@@ -594,7 +594,7 @@ struct Run {
       // (GT_GN_APPLY_MIN_C, default 256 channels), where the operand-load transform of conv_kernel would be
       // recomputed by every 128-channel tile and halo row.
       const bool apply = Cout >= gn_apply_min_c() ||
-                         (dt && GT_L1_TF5 && Cout == 128 && Fl(lvl) == 40);   // level 1: plain 5-row tiles
+                         (dt && GT_L1_TF5 && !GT_L1_TF5_GN && Cout == 128 && Fl(lvl) == 40);   // level 1: plain 5-row tiles
       if (apply) {
         RbOutParams a{};
         a.pre = pre1; a.part = st1; a.nparts = np1; a.gamma = Fp(k + "block1.block.1.weight");

@@ -30,11 +30,12 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_L1_TF5
 #define GT_L1_TF5 0
 #endif
-// Option (off: the 5-row GroupNorm-input variant spills 51 VGPRs to scratch at 2 workgroups/CU and measured
-// 196 us vs 139 us per launch, same-box A/B tools/ab_variant.sh): the level-1 GroupNorm-input conv (128 -> 128,
-// 40 rows) on 5-row tiles with the in-register GroupNorm transform, 1024 tiles at B = 32 instead of 1280.
+// The level-1 GroupNorm-input conv (128 -> 128, 40 rows) on 5-row tiles with the in-register GroupNorm transform:
+// 1024 tiles at B = 32 (two whole rounds of 512 slots) instead of 1280. On since round 2: with the interleaved
+// row blocks it fits 247 VGPRs without spilling (round 1: 51 VGPRs spilled, 196 vs 139 us); same-box A/B
+// +0.7-0.9 % end to end (tools/ab_variants_full.sh).
 #ifndef GT_L1_TF5_GN
-#define GT_L1_TF5_GN 0
+#define GT_L1_TF5_GN 1
 #endif
 // mel rows per 3x3 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid rows)
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f) {
