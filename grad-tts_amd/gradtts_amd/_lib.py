@@ -70,6 +70,25 @@ def lib():
     return _lib
 
 
+OPS_PATH = os.path.join(_HERE, "libgradtts_ops.so")
+_ops = None
+
+
+def ops():
+    """torch.ops.gradtts (TORCH_LIBRARY(gradtts) in libgradtts_ops.so, bound to this process's libgradtts.so).
+    Raises if the op library has not been built (no fallback path)."""
+    global _ops
+    if _ops is None:
+        import torch
+        if not os.path.exists(OPS_PATH):
+            raise ImportError(f"{OPS_PATH} not found: build it with `python grad-tts_amd/build.py`")
+        lib()                                   # the C ABI first: the op library binds to the same file
+        torch.ops.load_library(OPS_PATH)
+        torch.ops.gradtts.bind(LIB_PATH)
+        _ops = torch.ops.gradtts
+    return _ops
+
+
 class GradTTSError(RuntimeError):
     pass
 

@@ -23,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import GT_BF16, GT_BF16_W8, GT_F32, check, lib
+from ._lib import GT_BF16, GT_BF16_W8, GT_F32, check, lib, ops
 
 
 class _ParamOnly(torch.nn.Module):
@@ -233,20 +233,14 @@ class GradLogPEstimator2d(torch.nn.Module):
         """s_theta(x_t, t) -> [B, n_feats, T]  (model/diffusion.py:174-216)."""
         device = _require_cuda(x, mu, mask)
         self._check_shapes(x, mask, mu)
-        B, _, T = x.shape
-        out_dtype = x.dtype
-        x32, m32, mu32 = _f32c(x, device), _f32c(mask, device), _f32c(mu, device)
-        t32 = _f32c(torch.as_tensor(t).reshape(-1).expand(B) if torch.as_tensor(t).numel() == 1 else t, device)
+        B = x.shape[0]
+        t = torch.as_tensor(t, device=device, dtype=torch.float32).reshape(-1)
         spk32 = self._spk(spk, B, device)
         dcode = _dtype_code(self.compute_dtype)
         with torch.cuda.device(device):
             h = self._native(*getattr(self, "_beta_override", (0.05, 20.0)))
-            out = torch.empty((B, self.n_feats, T), dtype=torch.float32, device=device)
-            ws = self._workspace(device, dcode, B, T, 0)
-            check(lib().gt_estimator_forward(h, dcode, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
-                                             spk32.data_ptr() if spk32 is not None else None, B, T, out.data_ptr(),
-                                             ws.data_ptr(), ws.numel(), _stream_ptr(device)), "gt_estimator_forward")
-        return out.to(out_dtype)
+            # torch.ops.gradtts.estimator (csrc/torch_ops.cpp) -> gt_estimator_forward on the current stream
+            return ops().estimator(h.value, dcode, x.to(device), mask.to(device), mu.to(device), t, spk32)
 
 
 def get_noise(t, beta_init, beta_term, cumulative=False):
@@ -287,20 +281,13 @@ class Diffusion(torch.nn.Module):
         est = self.estimator
         device = _require_cuda(z, mu, mask)
         est._check_shapes(z, mask, mu)
-        B, _, T = z.shape
-        out_dtype = z.dtype
-        z32, m32, mu32 = _f32c(z, device), _f32c(mask, device), _f32c(mu, device)
-        spk32 = est._spk(spk, B, device)
+        spk32 = est._spk(spk, z.shape[0], device)
         dcode = _dtype_code(est.compute_dtype)
-        N = int(n_timesteps)
         with torch.cuda.device(device):
             h = est._native(self.beta_min, self.beta_max)
-            out = torch.empty((B, self.n_feats, T), dtype=torch.float32, device=device)
-            ws = est._workspace(device, dcode, B, T, N)
-            check(lib().gt_reverse_diffusion(h, dcode, z32.data_ptr(), m32.data_ptr(), mu32.data_ptr(),
-                                             spk32.data_ptr() if spk32 is not None else None, B, T, N, out.data_ptr(),
-                                             ws.data_ptr(), ws.numel(), _stream_ptr(device)), "gt_reverse_diffusion")
-        return out.to(out_dtype)
+            # torch.ops.gradtts.reverse_diffusion (csrc/torch_ops.cpp) -> gt_reverse_diffusion on the current stream
+            return ops().reverse_diffusion(h.value, dcode, z.to(device), mask.to(device), mu.to(device),
+                                           int(n_timesteps), spk32)
 
     @torch.no_grad()
     def forward(self, z, mask, mu, n_timesteps, stoc=False, spk=None):

@@ -12,7 +12,7 @@ import ctypes
 
 import torch
 
-from ._lib import check, lib
+from ._lib import check, lib, ops
 
 
 def maximum_path_c(paths, values, t_xs, t_ys, max_neg_val=-1e9):
@@ -33,13 +33,8 @@ def maximum_path(value, mask):
         raise RuntimeError("gradtts_amd.maximum_path needs a HIP (MI355X) device; there is no CPU path")
     out_device, out_dtype = value.device, value.dtype
     device = value.device if value.is_cuda else torch.device("cuda", torch.cuda.current_device())
-    value = value.to(device)
-    mask = mask.to(device)
-    v = (value * mask).to(torch.float32).contiguous()       # __init__.py:13,16
-    t_x = mask.sum(1)[:, 0].to(torch.int32).contiguous()   # __init__.py:20
-    t_y = mask.sum(2)[:, 0].to(torch.int32).contiguous()   # __init__.py:21
-    path = torch.empty(v.shape, dtype=torch.int32, device=device)
-    if v.numel():
-        with torch.cuda.device(device):
-            maximum_path_c(path, v, t_x, t_y)
+    with torch.cuda.device(device):
+        # torch.ops.gradtts.maximum_path (csrc/torch_ops.cpp): value * mask (__init__.py:13), t_x / t_y from the
+        # mask (:20-21), the DP on device (:22), path as value.dtype (:23)
+        path = ops().maximum_path(value.to(device), mask.to(device))
     return path.to(device=out_device, dtype=out_dtype)

@@ -101,3 +101,29 @@ def test_product_path_fails_loudly_without_gpu():
     from gradtts_amd.monotonic_align import maximum_path
     with pytest.raises(RuntimeError, match="HIP"):
         maximum_path(torch.zeros(1, 3, 4), torch.ones(1, 3, 4))
+
+
+def test_torch_ops_registered_with_meta_kernels():
+    """torch.ops.gradtts.* (csrc/torch_ops.cpp) load and bind on a CPU-only host; their Meta kernels give
+    torch.compile's fake tensors the reference shapes and dtypes, and bad shapes raise like the C ABI."""
+    import torch
+    from gradtts_amd import _lib
+    ops = _lib.ops()
+    for name, schema in [
+        ("reverse_diffusion", "gradtts::reverse_diffusion(int decoder, int dtype, Tensor z, Tensor mask, Tensor mu, "
+                              "int n_timesteps, Tensor? spk) -> Tensor"),
+        ("estimator", "gradtts::estimator(int decoder, int dtype, Tensor x, Tensor mask, Tensor mu, Tensor t, "
+                      "Tensor? spk) -> Tensor"),
+        ("maximum_path", "gradtts::maximum_path(Tensor value, Tensor mask) -> Tensor"),
+    ]:
+        assert str(getattr(ops, name).default._schema) == schema
+    z = torch.empty(3, 80, 64, device="meta", dtype=torch.bfloat16)
+    m = torch.empty(3, 1, 64, device="meta")
+    y = ops.reverse_diffusion(0, _lib.GT_BF16, z, m, z, 10, None)
+    assert y.shape == (3, 80, 64) and y.dtype == torch.bfloat16 and y.device.type == "meta"
+    assert ops.estimator(0, _lib.GT_F32, z, m, z, torch.empty(3, device="meta"), None).shape == (3, 80, 64)
+    v = torch.empty(2, 7, 30, device="meta")
+    assert ops.maximum_path(v, v).shape == (2, 7, 30)
+    with pytest.raises(RuntimeError, match="multiple of 4"):
+        ops.reverse_diffusion(0, 0, torch.empty(1, 80, 30, device="meta"), torch.empty(1, 1, 30, device="meta"),
+                              torch.empty(1, 80, 30, device="meta"), 1, None)

@@ -5,7 +5,9 @@ set -e
 NAME=$1; shift
 R=$(cd $(dirname $0)/.. && pwd)
 D=$R/ab/$NAME; mkdir -p $D
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/include -I $R/grad-tts_amd/csrc -Wno-unused-result -Xclang -target-feature -Xclang -packed-fp32-ops"
+# PK="" builds with the compiler's packed-fp32 instructions (the product build disables them, build.py)
+PK=${PK--Xclang -target-feature -Xclang -packed-fp32-ops}
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/include -I $R/grad-tts_amd/csrc -Wno-unused-result $PK"
 for s in conv.hip conv64.hip attn.hip misc.hip mas.hip decoder.cpp; do
   L=""; case $s in *.cpp) L="-x hip";; esac
   /opt/rocm/bin/hipcc $F "$@" $L -c $R/grad-tts_amd/csrc/$s -o $D/$s.o 2>&1 | grep -v "packed-fp32-ops" || true &

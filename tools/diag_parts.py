@@ -16,7 +16,7 @@ dec, _ = make_decoder(1, 0, cdt)
 mu, z, mask, _ = synthetic_inputs(1234, B, T)
 t = np.full(B, 0.5, np.float32)
 args = [torch.from_numpy(a).cuda() for a in (z, mask, mu, t)]
-pmax = 20 * ((T + 63) // 64)
+pmax = 20 * ((T + 31) // 32)   # layout(): largest producer grid (level-0 conv64)
 for k in range(24):
     outs = []
     for rep in range(4):
