@@ -1025,7 +1025,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
       R.tb_bstride = 0; R.stepp = stepp;
       R.tb = tbuf; R.betas = betas;
       if (!use_graph) {
-        R.chk(hipMemsetD32Async((hipDeviceptr_t)stepp, 0, 1, R.s));
+        R.chk(launch_set_step(stepp, 0, R.s));
         for (int i = 0; i < n_timesteps && R.err == hipSuccess; ++i) {
           R.tb = tbuf + (size_t)i * kTbRow;
           R.betas = betas + i;
@@ -1045,7 +1045,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
         if (rem && (rc = run_segment_graph(d, R, key(rem), rem, xt, hf, st, &tail))) return rc;
         for (int k = 0; k <= q && R.err == hipSuccess; ++k) {
           if (k == q && !rem) break;
-          R.chk(hipMemsetD32Async((hipDeviceptr_t)stepp, k * S, 1, st));
+          R.chk(launch_set_step(stepp, k * S, st));
           R.chk(hipGraphLaunch(k < q ? seg : tail, st));
         }
       }

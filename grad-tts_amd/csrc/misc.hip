@@ -254,6 +254,15 @@ hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float*
   return hipGetLastError();
 }
 
+// device step index of the sampler (kernels.h tb_at): one lane stores it (a kernel node in every kind of capture)
+__global__ void set_step_kernel(int* stepp, int v) {
+  if (threadIdx.x == 0) stepp[0] = v;
+}
+hipError_t launch_set_step(int* stepp, int v, hipStream_t s) {
+  hipLaunchKernelGGL(set_step_kernel, dim3(1), dim3(64), 0, s, stepp, v);
+  return hipGetLastError();
+}
+
 hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s) {
   const long n = (long)B * F * T;
   hipLaunchKernelGGL(mask_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, mask, F, T, n, out);
