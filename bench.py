@@ -58,17 +58,20 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if one exists."""
+def pmc_traffic(kernel, args, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (tools/make_profiles.py), or None
+    when no summary exists or it was measured on another workload (batch per GPU, frames, dtype, speakers): a
+    kernel's per-launch average depends on the shape mix of its launches."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
+    with open(path) as f:
+        d = json.load(f)
+    cfg = d.get("config", {})
+    if (cfg.get("global_batch"), cfg.get("seq_len"), cfg.get("n_spks"), cfg.get("dtype")) != \
+            (args.batch, args.frames, args.n_spks, args.dtype):
         return None
+    return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(args, sd):
@@ -209,7 +212,7 @@ def main():
                          "achieved": achieved / 1e12, "peak": PEAK[args.dtype] / 1e12, "unit": "TFLOP/s",
                          "frac": achieved / PEAK[args.dtype], "avg_launch_us": avg_s * 1e6,
                          "flop_per_launch": dom["flop"] / dom["launches"],
-                         "traffic": pmc_traffic(dom["kernel"]),
+                         "traffic": pmc_traffic(dom["kernel"], args, world),
                          "algorithmic_bytes_per_launch": dom["bytes"] / dom["launches"],
                          "timing": "HIP event pair around each launch of this kernel during the timed steps"},
             "tables_from": ("the last warm-up step" if args.warmup else "the timed steps") + " with events on every launch",

@@ -186,11 +186,15 @@ namespace {
 int ck_of(int dt) { return dt ? 32 : 16; }
 size_t esize(int dt) { return dt ? 2 : 4; }
 
-// channel count from which block2's GroupNorm/Mish transform runs as a separate in-place pass
+// channel count from which block2's GroupNorm/Mish transform runs as a separate in-place pass (gn_apply_kernel)
+// instead of in the conv's operand load. Default: never (1024). Round 2: with the 256-channel GroupNorm-input conv
+// on 5-row tiles the in-register transform (recomputed by both 128-channel tiles and the halo rows) costs
+// 103 us per launch against 87 + 35 us for the plain conv plus the pass (same box, tools/ab_env.sh); the
+// knob (GT_GN_APPLY_MIN_C=256 restores the round-1 split) stays for A/B runs.
 static int gn_apply_min_c() {
   static const int v = [] {
     const char* e = getenv("GT_GN_APPLY_MIN_C");
-    return e ? atoi(e) : 256;
+    return e ? atoi(e) : 1024;
   }();
   return v;
 }

@@ -41,7 +41,7 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f) {
   return (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
           ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
-           (GT_L1_TF5_GN && im == 2 && cout == 128 && f == 40))) ? 5 : 4;
+           (im == 2 && (cout >= 256 || (GT_L1_TF5_GN && cout == 128 && f == 40))))) ? 5 : 4;
 }
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }

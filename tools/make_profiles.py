@@ -17,24 +17,60 @@ import json
 import os
 import re
 import shutil
+import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _demangle(name: str) -> str:
+    """Itanium names of this library's kernels (_ZN2gt<len><name>[I<template args>E]...) -> "gt::name<args>(";
+    template args DF16b (__bf16), f (float), Li<n>E (int), Lb<0|1>E (bool). Other names are returned as they are."""
+    m = re.match(r"_ZN2gt(\d+)(\w+)", name)
+    if not m:
+        return name
+    n = int(m.group(1))
+    base, rest = m.group(2)[:n], m.group(2)[n:]
+    args = []
+    if rest.startswith("I"):
+        for t in re.finditer(r"DF16b|f|Li(-?\d+)E|Lb([01])E", rest[1:]):
+            tok = t.group(0)
+            args.append("__bf16" if tok == "DF16b" else "float" if tok == "f" else
+                        t.group(1) if t.group(1) is not None else ("true" if t.group(2) == "1" else "false"))
+            if rest[1:].startswith("E", t.end()):
+                break
+    return f"void gt::{base}" + (f"<{', '.join(args)}>" if args else "") + "("
+
+
 def norm(name: str) -> str:
-    m = re.match(r"_ZN2gt(\d+)(\w+?)I(DF16b|f)((?:Li-?\d+E)*)E", name)
-    if m:
-        base = m.group(2)[: int(m.group(1))]
-        ty = "bf16" if m.group(3) == "DF16b" else "float"
-        ints = re.findall(r"Li(-?\d+)E", m.group(4))
-        if base == "conv_kernel" and len(ints) == 6:   # trailing W8 flag and tile rows: "...,w8,tf5>" / nothing
-            ints = ints[:4] + (["w8"] if ints[4] == "1" else []) + (["tf5"] if ints[5] == "5" else [])
-        return f"{base}<{','.join([ty] + ints)}>"
-    m = re.match(r"(?:void )?gt::(\w+)(<[^(]*>)?\(", name)
-    if m:
-        return m.group(1) + (m.group(2) or "").replace(" ", "")
-    return name.split("(")[0]
+    """rocprofv3 kernel name (mangled or demangled) -> the name decoder.cpp / bench.py use for the same kernel
+    instantiation ("conv_kernel<bf16,KIND,IN,OUT,NT[,w8][,tf5]>", "conv64_kernel<IN>", "attn_kv_kernel<bf16>",
+    "rbout_identity_kernel<bf16>", "gn_apply_kernel<bf16>", ...). Kernels outside namespace gt (the runtime's
+    copies / fills, torch's elementwise kernels) keep their base name; a gt:: kernel that does not parse raises."""
+    d = _demangle(name)
+    m = re.match(r"(?:void )?gt::(\w+)(?:<([^()]*)>)?\(", d)
+    if not m:
+        return d.split("(")[0]
+    base, args = m.group(1), [a.strip() for a in (m.group(2) or "").split(",") if a.strip()]
+    ty = lambda a: {"__bf16": "bf16", "bf16": "bf16", "float": "float"}[a]
+    try:
+        if base == "conv_kernel":            # <A, KIND, IN, OUT, NT, W8, TF>
+            A, kind, im, om, nt, w8, tf = args
+            return (f"conv_kernel<{ty(A)},{kind},{im},{om},{nt}" + (",w8" if w8 in ("1", "true") else "") +
+                    (",tf5" if tf == "5" else "") + ">")
+        if base == "conv64_kernel":          # <IN>
+            return f"conv64_kernel<{args[0]}>"
+        if base == "gn_mish_kernel":         # <A, APPLY>: the ResnetBlock output or block2's in-place input
+            return ("gn_apply_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
+        if base in ("attn_kv_kernel", "final_kernel", "to_nchw_kernel"):
+            return f"{base}<{ty(args[0])}>"
+        if base == "attn_fold_kernel" and args:
+            return f"{base}<{ty(args[0])}>"
+        if not args:
+            return base
+    except (KeyError, ValueError, IndexError):
+        pass
+    raise ValueError(f"unparsed gt:: kernel name: {d}")
 
 
 def pmc_sums(d):
@@ -81,10 +117,15 @@ def main():
         if "fetch_kb_per_launch_raw" in t and "write_kb_per_launch" in t:
             t["hbm_bytes_per_launch"] = (2 * t["fetch_kb_per_launch_raw"] + t["write_kb_per_launch"]) * 1024
     traffic = {k: v for k, v in traffic.items() if "hbm_bytes_per_launch" in v}
+    # the configuration the PMC passes ran (bench.py reads these bytes only for the same workload: the per-launch
+    # average of an instantiation depends on its shape mix, which depends on batch, frames, dtype and speakers)
+    cfg = json.load(open(os.path.join(dst, "bench.json")))["config"]
+    config = {k: cfg[k] for k in ("global_batch", "seq_len", "n_spks")}
+    config["dtype"] = json.load(open(os.path.join(dst, "bench.json")))["dtype"]
     with open(os.path.join(REPO, "profiles", "pmc_traffic.json"), "w") as f:
         json.dump({"source": f"profiles/{tag} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
                    "formula": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (gfx950 FETCH_SIZE halving)",
-                   **traffic}, f, indent=1, sort_keys=True)
+                   "config": config, "kernels": traffic}, f, indent=1, sort_keys=True)
     print(f"wrote {dst} and profiles/pmc_traffic.json ({len(traffic)} kernels)")
 
 
