@@ -22,6 +22,7 @@
 
 #include "gradtts.h"
 #include "kernels.h"
+#include "train.h"
 #include "wimage.h"
 
 using namespace gt;
@@ -927,6 +928,84 @@ int gt_estimator_forward(gt_decoder* d, int dtype, const float* x, const float* 
                          const float* spk, int64_t B, int64_t T, float* out, void* workspace, size_t workspace_bytes,
                          void* stream) {
   return estimator_impl(d, dtype, x, mask, mu, t, spk, B, T, out, workspace, workspace_bytes, stream, nullptr, nullptr);
+}
+
+// ---------------------------------------------------------------- training path (forward values)
+static size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+int gt_forward_diffusion(gt_decoder* d, const float* x0, const float* mask, const float* mu, const float* t,
+                         const float* z, int64_t B, int64_t T, float* xt, float* zm, void* stream) {
+  if (!d || !x0 || !mask || !mu || !t || !z || !xt) return fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || T <= 0 || B * 80 * T >= (int64_t(1) << 31)) return fail(GT_ERR_ARG, "bad B / T");
+  FwdDiffParams p;
+  p.x0 = x0; p.mu = mu; p.z = z; p.mask = mask; p.t = t; p.B = (int)B; p.F = 80; p.T = (int)T;
+  p.beta_min = d->beta_min;
+  p.half_delta = (float)(0.5 * ((double)d->beta_max - (double)d->beta_min));
+  p.xt = xt; p.zm = zm;
+  if (launch_fwd_diffusion(p, (hipStream_t)stream) != hipSuccess) return fail(GT_ERR_HIP, "forward_diffusion launch failed");
+  return GT_OK;
+}
+
+size_t gt_diffusion_loss_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int64_t T) {
+  if (B <= 0 || T <= 0) return 0;
+  const size_t n = (size_t)B * 80 * T * 4;
+  return align256(gt_decoder_workspace_bytes(d, dtype, B, T, 0)) + 2 * align256(n) +
+         align256((size_t)loss_blocks((long)B * 80 * T) * 8) + 256;
+}
+
+int gt_diffusion_loss_t(gt_decoder* d, int dtype, const float* x0, const float* mask, const float* mu, const float* t,
+                        const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, void* workspace,
+                        size_t workspace_bytes, void* stream) {
+  if (!d || !loss || !xt || !workspace) return fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || T <= 0 || B * 80 * T >= (int64_t(1) << 31)) return fail(GT_ERR_ARG, "bad B / T");
+  if (workspace_bytes < gt_diffusion_loss_workspace_bytes(d, dtype, B, T)) return fail(GT_ERR_WORKSPACE, "workspace too small");
+  uint8_t* ws = align_ws(workspace);
+  const size_t est_bytes = align256(gt_decoder_workspace_bytes(d, dtype, B, T, 0));
+  const size_t n = (size_t)B * 80 * T * 4;
+  float* zm = (float*)(ws + est_bytes);
+  float* score = (float*)(ws + est_bytes + align256(n));
+  float* part = (float*)(ws + est_bytes + 2 * align256(n));
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = gt_forward_diffusion(d, x0, mask, mu, t, z, B, T, xt, zm, stream);   // diffusion.py:275
+  if (rc) return rc;
+  rc = estimator_impl(d, dtype, xt, mask, mu, t, spk, B, T, score, ws, est_bytes, stream, nullptr, nullptr);  // :277
+  if (rc) return rc;
+  LossParams lp;
+  lp.score = score; lp.z = z; lp.mask = mask; lp.t = t; lp.B = (int)B; lp.F = 80; lp.T = (int)T;
+  lp.beta_min = d->beta_min;
+  lp.half_delta = (float)(0.5 * ((double)d->beta_max - (double)d->beta_min));
+  lp.part = part;
+  if (launch_loss(lp, loss, s) != hipSuccess) return fail(GT_ERR_HIP, "loss launch failed");   // :278-280
+  return GT_OK;
+}
+
+size_t gt_alignment_workspace_bytes(int64_t B, int64_t Tx, int64_t Ty) {
+  if (B <= 0 || Tx <= 0 || Ty <= 0) return 0;
+  return align256((size_t)B * Tx * Ty * 4) + align256((size_t)B * 8) + gt_maximum_path_workspace_bytes(B, Tx, Ty) + 256;
+}
+
+int gt_log_prior_maximum_path(const float* mu_x, const float* y, const float* x_mask, const float* y_mask, int64_t B,
+                              int64_t n_feats, int64_t Tx, int64_t Ty, int32_t* paths, float* log_prior,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (!mu_x || !y || !x_mask || !y_mask || !paths || !workspace) return fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || Tx <= 0 || Ty <= 0 || n_feats <= 0) return fail(GT_ERR_ARG, "bad shape");
+  if (n_feats > 128) return fail(GT_ERR_UNSUPPORTED, "n_feats > 128");
+  if (B > 65535 || B * Tx * Ty >= (int64_t(1) << 31)) return fail(GT_ERR_UNSUPPORTED, "alignment grid too large");
+  if (workspace_bytes < gt_alignment_workspace_bytes(B, Tx, Ty)) return fail(GT_ERR_WORKSPACE, "workspace too small");
+  uint8_t* ws = align_ws(workspace);
+  const size_t nlp = align256((size_t)B * Tx * Ty * 4);
+  float* lp = log_prior ? log_prior : (float*)ws;
+  int32_t* lens = (int32_t*)(ws + nlp);
+  void* mas_ws = ws + nlp + align256((size_t)B * 8);
+  const size_t mas_bytes = workspace_bytes - (size_t)((uint8_t*)mas_ws - (uint8_t*)workspace);
+  const hipStream_t s = (hipStream_t)stream;
+  const float cst = (float)(-0.5 * std::log(2.0 * M_PI) * (double)n_feats);   // tts.py:143 (Python float -> fp32 add)
+  if (launch_log_prior(mu_x, y, x_mask, y_mask, (int)B, (int)n_feats, (int)Tx, (int)Ty, cst, lp, s) != hipSuccess ||
+      launch_mask_len(x_mask, y_mask, (int)B, (int)Tx, (int)Ty, lens, lens + B, s) != hipSuccess)
+    return fail(GT_ERR_HIP, "log-prior launch failed");
+  const int rc = gt_maximum_path(paths, lp, lens, lens + B, B, Tx, Ty, -1e9f, mas_ws, mas_bytes, stream);
+  if (rc) return fail(rc, "maximum_path failed");
+  return GT_OK;
 }
 
 int gt_estimator_probe(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu, const float* t,

@@ -46,6 +46,16 @@ SIGNATURES = [
     ("gt_f32_to_e4m3", _c.c_uint8, [_c.c_float]),
     ("gt_quantize_e4m3", _c.c_int, [_c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p,
                                     _c.c_void_p]),
+    ("gt_forward_diffusion", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                        _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p, _c.c_void_p]),
+    ("gt_diffusion_loss_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int, _c.c_int64, _c.c_int64]),
+    ("gt_diffusion_loss_t", _c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                       _c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,
+                                       _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_alignment_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
+    ("gt_log_prior_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
+                                             _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,
+                                             _c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_maximum_path_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64,
                                    _c.c_int64, _c.c_float, _c.c_void_p, _c.c_size_t, _c.c_void_p]),

@@ -293,12 +293,69 @@ class Diffusion(torch.nn.Module):
     def forward(self, z, mask, mu, n_timesteps, stoc=False, spk=None):
         return self.reverse_diffusion(z, mask, mu, n_timesteps, stoc, spk)
 
-    def forward_diffusion(self, x0, mask, mu, t):
-        raise NotImplementedError("training path (forward_diffusion/loss_t/compute_loss, diffusion.py:244-287) is "
-                                  "outside this round's hot-path scope (SURVEY.md §8f row 1)")
+    # ---- training path: forward values on the HIP path; the U-Net backward is not built yet,
+    # so the loss carries a grad_fn whose backward raises (a training step fails loudly instead of silently
+    # training nothing).
+    def forward_diffusion(self, x0, mask, mu, t, z=None):
+        """``Diffusion.forward_diffusion`` (model/diffusion.py:244-252) -> (xt * mask, z * mask). ``z`` defaults to
+        ``torch.randn`` of x0's shape/dtype/device -- the reference's own draw (:249-250), same generator stream."""
+        device = _require_cuda(x0, mu, mask)
+        if z is None:
+            z = torch.randn(x0.shape, dtype=x0.dtype, device=x0.device, requires_grad=False)
+        x32, m32, mu32, z32 = (_f32c(a, device) for a in (x0, mask, mu, z))
+        t32 = _f32c(torch.as_tensor(t).reshape(-1), device)
+        B, _, T = x32.shape
+        xt = torch.empty_like(x32)
+        zm = torch.empty_like(x32)
+        with torch.cuda.device(device):
+            h = self.estimator._native(self.beta_min, self.beta_max)
+            check(lib().gt_forward_diffusion(h, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
+                                             z32.data_ptr(), B, T, xt.data_ptr(), zm.data_ptr(), _stream_ptr(device)),
+                  "gt_forward_diffusion")
+        return xt.to(x0.dtype), zm.to(x0.dtype)
 
-    def loss_t(self, x0, mask, mu, t, spk=None):
-        raise NotImplementedError("training path is outside this round's hot-path scope (SURVEY.md §8f row 1)")
+    def loss_t(self, x0, mask, mu, t, spk=None, z=None):
+        """``Diffusion.loss_t`` (diffusion.py:274-281) -> (loss, xt); ``z`` as in forward_diffusion."""
+        est = self.estimator
+        device = _require_cuda(x0, mu, mask)
+        est._check_shapes(x0, mask, mu)
+        if z is None:
+            z = torch.randn(x0.shape, dtype=x0.dtype, device=x0.device, requires_grad=False)
+        B, _, T = x0.shape
+        x32, m32, mu32, z32 = (_f32c(a, device) for a in (x0, mask, mu, z))
+        t32 = _f32c(torch.as_tensor(t).reshape(-1), device)
+        spk32 = est._spk(spk, B, device)
+        dcode = _dtype_code(est.compute_dtype)
+        loss = torch.empty((), dtype=torch.float32, device=device)
+        xt = torch.empty_like(x32)
+        with torch.cuda.device(device):
+            h = est._native(self.beta_min, self.beta_max)
+            ws = torch.empty(lib().gt_diffusion_loss_workspace_bytes(h, dcode, B, T), dtype=torch.uint8, device=device)
+            check(lib().gt_diffusion_loss_t(h, dcode, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
+                                            z32.data_ptr(), spk32.data_ptr() if spk32 is not None else None, B, T,
+                                            loss.data_ptr(), xt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                            _stream_ptr(device)), "gt_diffusion_loss_t")
+        params = [p for p in est.parameters() if p.requires_grad]
+        if torch.is_grad_enabled() and params:
+            loss = _NoUNetBackward.apply(loss, *params)
+        return loss.to(x0.dtype), xt.to(x0.dtype)
 
     def compute_loss(self, x0, mask, mu, spk=None, offset=1e-5):
-        raise NotImplementedError("training path is outside this round's hot-path scope (SURVEY.md §8f row 1)")
+        """``Diffusion.compute_loss`` (diffusion.py:283-287): t ~ U(0,1) clamped to [offset, 1 - offset]."""
+        t = torch.rand(x0.shape[0], dtype=x0.dtype, device=x0.device, requires_grad=False)
+        t = torch.clamp(t, offset, 1.0 - offset)
+        return self.loss_t(x0, mask, mu, t, spk)
+
+
+class _NoUNetBackward(torch.autograd.Function):
+    """Marks a loss computed by the HIP forward path as depending on the estimator parameters; its backward raises
+    until the HIP U-Net backward exists."""
+
+    @staticmethod
+    def forward(ctx, loss, *params):
+        return loss.clone()
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError("gradients of the HIP U-Net (training step backward, SURVEY.md §8f row 1) are "
+                                  "not implemented yet; the forward loss values are")

@@ -125,6 +125,30 @@ uint8_t gt_f32_to_e4m3(float x);
 int gt_quantize_e4m3(const float* w, int64_t rows, int64_t cols, int64_t row_stride, int64_t col_stride, uint8_t* q,
                      float* scale);
 
+/* ---- Training path, forward values ----
+ * Diffusion.forward_diffusion (model/diffusion.py:244-252) with the noise passed in: xt = (x0 e + mu (1 - e) +
+ * z sqrt(1 - e^2)) * mask, zm = z * mask, e = exp(-cum_noise(t) / 2). All [B,80,T] fp32, mask [B,1,T], t [B].
+ * zm may be NULL. No workspace. */
+int gt_forward_diffusion(gt_decoder* dec, const float* x0, const float* mask, const float* mu, const float* t,
+                         const float* z, int64_t B, int64_t T, float* xt, float* zm, void* stream);
+/* Diffusion.loss_t (diffusion.py:274-281) forward value with the noise passed in: loss[0] (device fp32) =
+ * sum((s_theta(xt) sqrt(1 - e^-cum) + z mask)^2) / (sum(mask) * 80), xt = the forward-diffused input (out,
+ * [B,80,T]). Deterministic (fixed-order reductions). Parameter gradients are not implemented (the U-Net backward
+ * is the next step of §8f row 1). */
+size_t gt_diffusion_loss_workspace_bytes(const gt_decoder* dec, int dtype, int64_t B, int64_t T);
+int gt_diffusion_loss_t(gt_decoder* dec, int dtype, const float* x0, const float* mask, const float* mu,
+                        const float* t, const float* z, const float* spk, int64_t B, int64_t T, float* loss,
+                        float* xt, void* workspace, size_t workspace_bytes, void* stream);
+/* The alignment step of GradTTS.compute_loss (model/tts.py:141-152) in one call: the log-prior of mu_x
+ * [B,n_feats,Tx] against y [B,n_feats,Ty] (three fp32 contractions + const, tts.py:143-149), masked with
+ * x_mask [B,Tx] (x) y_mask [B,Ty], then maximum_path on device (t_x, t_y from the masks). paths: [B,Tx,Ty]
+ * int32 (0/1); log_prior: optional [B,Tx,Ty] fp32 copy of the masked log-prior (NULL: kept in the workspace).
+ * n_feats <= 128. */
+size_t gt_alignment_workspace_bytes(int64_t B, int64_t Tx, int64_t Ty);
+int gt_log_prior_maximum_path(const float* mu_x, const float* y, const float* x_mask, const float* y_mask, int64_t B,
+                              int64_t n_feats, int64_t Tx, int64_t Ty, int32_t* paths, float* log_prior,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /* Monotonic alignment search.  values: [b, tx_max, ty_max] fp32 (already multiplied by the mask,
  * as maximum_path does before calling the Cython core); t_xs, t_ys: [b] int32 (device);
  * paths: [b, tx_max, ty_max] int32 output, fully written (0/1). `values` is not modified

@@ -153,6 +153,40 @@ def reverse_diffusion(p, z, mask, mu, n_timesteps, spk=None, n_spks=1, beta_min=
     return xt
 
 
+def forward_diffusion(x0, mask, mu, t, z, beta_min=0.05, beta_max=20.0):
+    """``Diffusion.forward_diffusion`` diffusion.py:244-252 with the noise ``z`` passed in (the reference draws it
+    with torch.randn at :249-250)."""
+    time = t.unsqueeze(-1).unsqueeze(-1)
+    cum_noise = get_noise(time, beta_min, beta_max, cumulative=True)
+    mean = x0 * torch.exp(-0.5 * cum_noise) + mu * (1.0 - torch.exp(-0.5 * cum_noise))
+    variance = 1.0 - torch.exp(-cum_noise)
+    xt = mean + z * torch.sqrt(variance)
+    return xt * mask, z * mask
+
+
+@torch.no_grad()
+def loss_t(p, x0, mask, mu, t, z, spk=None, n_spks=1, beta_min=0.05, beta_max=20.0, pe_scale=1000.0, dim=64,
+           n_feats=80):
+    """``Diffusion.loss_t`` diffusion.py:274-281 (forward value) with the noise passed in."""
+    xt, z = forward_diffusion(x0, mask, mu, t, z, beta_min, beta_max)
+    time = t.unsqueeze(-1).unsqueeze(-1)
+    cum_noise = get_noise(time, beta_min, beta_max, cumulative=True)
+    noise_estimation = estimator(p, xt, mask, mu, t, spk, n_spks, pe_scale, dim)
+    noise_estimation = noise_estimation * torch.sqrt(1.0 - torch.exp(-cum_noise))
+    loss = torch.sum((noise_estimation + z) ** 2) / (torch.sum(mask) * n_feats)
+    return loss, xt
+
+
+def log_prior(mu_x, y, n_feats=80):
+    """The log-prior that ``GradTTS.compute_loss`` aligns with MAS, model/tts.py:143-149 (three matmuls + const)."""
+    const = -0.5 * math.log(2 * math.pi) * n_feats
+    factor = -0.5 * torch.ones(mu_x.shape, dtype=mu_x.dtype)
+    y_square = torch.matmul(factor.transpose(1, 2), y ** 2)
+    y_mu_double = torch.matmul(2.0 * (factor * mu_x).transpose(1, 2), y)
+    mu_square = torch.sum(factor * (mu_x ** 2), 1).unsqueeze(-1)
+    return y_square - y_mu_double + mu_square + const
+
+
 def to_torch_params(sd, dtype=torch.float32):
     return {k: torch.as_tensor(v).to(dtype) for k, v in sd.items()}
 

@@ -16,9 +16,9 @@ run() {  # run <limit_s> <log> cmd...
 }
 BENCH="python3 bench.py $*"
 run 300 $OUT/bench.json $BENCH   # (stderr interleaved; make_profiles.py keeps the JSON line)
-run 400 $OUT/ktrace.log rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 $*
-run 300 $OUT/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
-run 300 $OUT/pmc_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
-run 300 $OUT/pmc_sq.log rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
-run 300 $OUT/pmc_sq2.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES --output-format csv -d $OUT/pmc_sq2 -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
+run 400 $OUT/ktrace.log rocprofv3 -M --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 $*
+run 300 $OUT/pmc_fetch.log rocprofv3 -M --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
+run 300 $OUT/pmc_write.log rocprofv3 -M --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
+run 300 $OUT/pmc_sq.log rocprofv3 -M --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
+run 300 $OUT/pmc_sq2.log rocprofv3 -M --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES --output-format csv -d $OUT/pmc_sq2 -o pmc -- python3 bench.py --no-cpu-baseline --steps 1 --warmup 0 --n-timesteps 2 $*
 echo done

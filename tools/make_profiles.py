@@ -89,7 +89,13 @@ def main():
     dst = os.path.join(REPO, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     for f in glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True):
-        shutil.copy(f, os.path.join(dst, "kernel_stats.csv"))
+        # rocprofv3 -M (mangled names: its demangler garbles __bf16 template arguments); add the bench's name
+        rows = list(csv.DictReader(open(f)))
+        with open(os.path.join(dst, "kernel_stats.csv"), "w", newline="") as out:
+            w = csv.DictWriter(out, fieldnames=["Kernel"] + list(rows[0].keys()) if rows else ["Kernel"])
+            w.writeheader()
+            for r in rows:
+                w.writerow({"Kernel": norm(r["Name"]), **r})
     if os.path.exists(os.path.join(src, "bench.json")):   # the JSON line (stderr may be interleaved)
         lines = [l for l in open(os.path.join(src, "bench.json")) if l.startswith("{")]
         if lines:
