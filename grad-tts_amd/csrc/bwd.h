@@ -1,0 +1,75 @@
+// U-Net backward building blocks (bwd.hip): parameter blocks and launchers. fp32, channels-last [B][F][T][C].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gt {
+
+// gather relation v = u*S - PAD + k over a KS x KS kernel (k = kh*KS + kw)
+struct GConvParams {
+  int B, Fi, Ti, Cin, Fo, To, Cout;   // in grid (Fi, Ti, Cin) -> out grid (Fo, To, Cout)
+  int KS, S, PAD;
+  int transposed;                     // 0: out[u] = sum W in[v(u,k)] (gconv);  1: out[v] = sum W in[u] (tconv)
+  int flip;                           // gconv: tap k reads weight KK-1-k (stride-1 dgrad)
+  const float* in; const float* w; long wsa, wsc;   // weight element (a = out channel, c = in channel, k) at a*wsa + c*wsc + k
+  const float* bias;
+  const float* mask; int T0, lvl_in;  // non-null: multiply the input by the level mask
+  const float* out_mask; int lvl_out; // non-null: multiply the output by the level mask
+  float* out; int out_cs, out_c0;     // output channel stride / first channel (writes into a wider tensor)
+  int accumulate;
+};
+// dW(a, b, k) = sum_u P[u][a] Q[v(u,k)][b]; U grid (Fu, Tu), V grid (Fv, Tv)
+struct WGradParams {
+  int B, Fu, Tu, A, Fv, Tv, Bc, KS, S, PAD;
+  const float* P; const float* pmask; int lvl_p;
+  const float* Q; const float* qmask; int lvl_q;
+  int T0;
+  float* part;
+};
+struct BlockBwdParams {
+  int B, npos, T, C;                  // npos = F * T of the level; T = frames of the level
+  const float* dA; const float* h; const float* stats; const float* gamma; const float* beta;
+  const float* mask; int T0, lvl;
+  float* gsum; float* dgb; float* dh;
+};
+struct EwParams {
+  int B, F, T, C;
+  const float* x; int xcs, xc0; float alpha;
+  const float* x2; float alpha2;      // optional second term (same channel count, dense)
+  const float* mask; int T0, lvl;
+  float* y; int ycs, yc0; int accumulate;
+};
+
+hipError_t launch_gconv(const GConvParams& p, hipStream_t s);
+// launchers of the single kernels (grid / block chosen by the caller)
+hipError_t launch_mish_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* pre, int n, float* dX);
+hipError_t launch_dmu(dim3 grid, dim3 block, hipStream_t strm, const float* dxin, int cin, const float* t,
+                      const float* mask, int B, int T, float bmin, float half_delta, float* dmu);
+hipError_t launch_spk_chan_sum(dim3 grid, dim3 block, hipStream_t strm, const float* dxin, int cin, int T, float* ds);
+hipError_t launch_mask_sum(dim3 grid, dim3 block, hipStream_t strm, const float* mask, long n, float* out);
+hipError_t launch_bsum(dim3 grid, dim3 block, hipStream_t strm, const float* x, const float* y, int npos, int C, float* out, int accumulate);
+hipError_t launch_colsum(dim3 grid, dim3 block, hipStream_t strm, const float* in, int B, int C, float* out, int accumulate);
+hipError_t launch_gn_stats(dim3 grid, dim3 block, hipStream_t strm, const float* h, int npos, int C, float* stats);
+hipError_t launch_block_bwd_reduce(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p);
+hipError_t launch_block_bwd_apply(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p);
+hipError_t launch_block_fwd(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p, const float* tb, float* out);
+hipError_t launch_ew(dim3 grid, dim3 block, hipStream_t strm, EwParams p);
+hipError_t launch_attn_kstats(dim3 grid, dim3 block, hipStream_t strm, const float* qkv, int npos, float* st);
+hipError_t launch_attn_ksoftmax(dim3 grid, dim3 block, hipStream_t strm, float* qkv, int B, int npos, const float* st);
+hipError_t launch_attn_outer(dim3 grid, dim3 block, hipStream_t strm, const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int npos, float* R);
+hipError_t launch_attn_headmm(dim3 grid, dim3 block, hipStream_t strm, const float* M, int trans, const float* X, int csx, int xo, int B, int npos, float* Y, int csy, int yo, int accumulate);
+hipError_t launch_attn_ksoftmax_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* qkv_s, float* dqkv, int B, int npos, const float* S);
+hipError_t launch_attn_rowdot(dim3 grid, dim3 block, hipStream_t strm, const float* a, int csa, int ao, const float* c, int csc, int co, int npos, float* S);
+hipError_t launch_dot(dim3 grid, dim3 block, hipStream_t strm, const float* x, const float* y, long n, float* out, int accumulate);
+hipError_t launch_linear_fwd(dim3 grid, dim3 block, hipStream_t strm, const float* X, int I, const float* W, const float* bias, int O, int act, float* Y);
+hipError_t launch_linear_wgrad(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* X, int B, int I, int O, float* dW, float* db);
+hipError_t launch_linear_dgrad(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* W, int I, int O, const float* pre, float* dX, int accumulate);
+hipError_t launch_posemb(dim3 grid, dim3 block, hipStream_t strm, const float* t, float scale, const float* freqs, float* out);
+hipError_t launch_loss_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* score, const float* z, const float* mask, const float* t, const float* tot, int B, int T, float bmin, float half_delta, float* ds);
+hipError_t launch_input_pack(dim3 grid, dim3 block, hipStream_t strm, const float* mu, const float* xt, const float* s, int B, int T, int cin, float* out);
+
+hipError_t launch_wgrad(const WGradParams& p, float* part, int splits, float* dw, long sa, long sb, int accumulate,
+                        hipStream_t s);
+
+
+}  // namespace gt

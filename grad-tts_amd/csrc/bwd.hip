@@ -1,0 +1,698 @@
+// Backward of the score U-Net for the training step (model/diffusion.py:16-216 through
+// Diffusion.loss_t :274-281), fp32, channels-last activations [B][F_l][T_l][C] as in the forward.
+//
+// Generic building blocks (every conv of the U-Net is one of three gather relations u -> v = u*S - PAD + k):
+//   gconv_kernel    out[u][a] (+)= sum_{k,c} W(a, c, k) in[v(u, k)][c] (* mask)   regular conv; with flipped taps
+//                   and transposed weight strides also the stride-1 dgrad (3x3 and 1x1)
+//   tconv_kernel    out[v][b] (+)= sum_{k,u: v(u,k) = v} W(a, b, k) in[u][a]        transposed relation: the dgrad of
+//                   the stride-2 Downsample conv, and ConvTranspose2d itself
+//   wgrad_kernel    dW(a, b, k) = sum_u P[u][a] Q[v(u, k)][b]                      every weight gradient (split over
+//                   positions, fixed-order reduction by wgrad_reduce_kernel)
+// plus GroupNorm/Mish (Block) backward, per-channel / per-utterance sums, the LinearAttention algebra, the small
+// MLPs and the loss. Weights are read in the reference layouts (Conv2d [out][in][kh][kw], ConvTranspose2d
+// [in][out][kh][kw]) through element strides. Deterministic: every reduction runs in a fixed order.
+//
+// This is the correctness-first version: LDS-tiled VALU fp32 (the MFMA versions of gconv / wgrad are the
+// next performance step).
+#include "bwd.h"
+#include "common.h"
+
+namespace gt {
+
+GT_DEV float mish_grad(float x) {   // d/dx x tanh(softplus(x)) (torch softplus threshold 20: x > 20 -> 1)
+  if (x > 20.f) return 1.f;
+  const float sp = log1pf(expf(x));
+  const float th = tanhf(sp);
+  const float sg = 1.f / (1.f + expf(-x));
+  return th + x * (1.f - th * th) * sg;
+}
+GT_DEV float mish_f(float x) { return x > 20.f ? x : x * tanhf(log1pf(expf(x))); }
+
+// ---------------------------------------------------------------- gconv: 64 output positions (one row) x 64
+// output channels per workgroup, 8-channel input chunks staged in LDS; thread = 4 positions x 4 channels
+constexpr int GC_CC = 8;
+__global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
+  __shared__ float s_in[4][64 * 2 + 4][GC_CC];   // KS <= 4 rows, (64 - 1) S + KS columns
+  __shared__ float s_w[64][GC_CC][16];
+  const int tid = threadIdx.x;
+  const int n_tt = (p.To + 63) / 64;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int fo = bid % p.Fo;
+  const int b = bid / p.Fo;
+  const int to0 = tt * 64, a0 = blockIdx.y * 64;
+  const int KK = p.KS * p.KS, PC = 63 * p.S + p.KS;
+  const int pl = tid & 15, al = tid >> 4;
+  float acc[4][4] = {};
+  for (int c0 = 0; c0 < p.Cin; c0 += GC_CC) {
+    __syncthreads();
+    for (int i = tid; i < p.KS * PC * GC_CC; i += 256) {
+      const int c = i % GC_CC, col = (i / GC_CC) % PC, row = i / (GC_CC * PC);
+      const int fi = fo * p.S - p.PAD + row, ti = to0 * p.S - p.PAD + col, ci = c0 + c;
+      float v = 0.f;
+      if (fi >= 0 && fi < p.Fi && ti >= 0 && ti < p.Ti && ci < p.Cin) {
+        v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
+        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+      }
+      s_in[row][col][c] = v;
+    }
+    for (int i = tid; i < 64 * GC_CC * KK; i += 256) {
+      const int k = i % KK, c = (i / KK) % GC_CC, a = i / (KK * GC_CC);
+      const int kk = p.flip ? KK - 1 - k : k;
+      s_w[a][c][k] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc + kk] : 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < KK; ++k) {
+      const int kh = k / p.KS, kw = k % p.KS;
+#pragma unroll
+      for (int c = 0; c < GC_CC; ++c) {
+        float x[4], w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = s_in[kh][(pl + 16 * i) * p.S + kw][c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = s_w[al * 4 + j][c][k];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(w[j], x[i], acc[i][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int to = to0 + pl + 16 * i;
+    if (to >= p.To) continue;
+    const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int a = a0 + al * 4 + j;
+      if (a >= p.Cout) continue;
+      const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
+      float v = acc[i][j] + (p.bias ? p.bias[a] : 0.f);
+      v *= om;
+      p.out[o] = p.accumulate ? p.out[o] + v : v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- tconv: out[v][b] = sum_{u*S-PAD+k = v} W in[u]
+// one workgroup per 64 output positions (one row) x 64 output channels; inputs read through L1 (the transposed
+// gather touches at most ceil(KS/S)^2 taps per output)
+__global__ __launch_bounds__(256) void tconv_kernel(GConvParams p) {
+  const int tid = threadIdx.x;
+  const int n_tt = (p.To + 63) / 64;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int fo = bid % p.Fo;
+  const int b = bid / p.Fo;
+  const int to0 = tt * 64, a0 = blockIdx.y * 64;
+  const int pl = tid & 15, al = tid >> 4;
+  float acc[4][4] = {};
+  for (int kh = 0; kh < p.KS; ++kh) {
+    const int nf = fo + p.PAD - kh;
+    if (nf < 0 || nf % p.S != 0 || nf / p.S >= p.Fi) continue;
+    const int fi = nf / p.S;
+    for (int kw = 0; kw < p.KS; ++kw) {
+      const int k = kh * p.KS + kw;
+      for (int c = 0; c < p.Cin; ++c) {
+        float w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int a = a0 + al * 4 + j;
+          w[j] = a < p.Cout ? p.w[(long)c * p.wsc + (long)a * p.wsa + k] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int nt = to0 + pl + 16 * i + p.PAD - kw;
+          if (to0 + pl + 16 * i >= p.To || nt < 0 || nt % p.S != 0 || nt / p.S >= p.Ti) continue;
+          const int ti = nt / p.S;
+          float x = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + c];
+          if (p.mask) x *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(w[j], x, acc[i][j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int to = to0 + pl + 16 * i;
+    if (to >= p.To) continue;
+    const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int a = a0 + al * 4 + j;
+      if (a >= p.Cout) continue;
+      const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
+      float v = acc[i][j] + (p.bias ? p.bias[a] : 0.f);
+      v *= om;
+      p.out[o] = p.accumulate ? p.out[o] + v : v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wgrad: dW(a, b, k) = sum_u P[u][a] Q[v(u,k)][b]
+// workgroup = 32 a x 32 b x all taps over its share of the U positions; thread = (a, b) pair x taps.
+// Grid (A/32, B/32, splits); partial[split][a][b][k] -> wgrad_reduce_kernel.
+constexpr int WG_U = 32;
+__global__ __launch_bounds__(256) void wgrad_kernel(WGradParams p) {
+  __shared__ float s_p[WG_U][33];
+  __shared__ float s_q[16][WG_U][33];
+  const int tid = threadIdx.x;
+  const int a0 = blockIdx.x * 32, b0 = blockIdx.y * 32, split = blockIdx.z;
+  const int KK = p.KS * p.KS;
+  const long nU = (long)p.B * p.Fu * p.Tu;
+  const long per = (nU + gridDim.z - 1) / gridDim.z;
+  const long u_lo = split * per, u_hi = u_lo + per < nU ? u_lo + per : nU;
+  const int ai = tid >> 3, bq = (tid & 7) * 4;   // thread: a = a0 + ai, b = b0 + bq .. bq+3
+  float acc[16][4] = {};
+  for (long u0 = u_lo; u0 < u_hi; u0 += WG_U) {
+    __syncthreads();
+    for (int i = tid; i < WG_U * 32; i += 256) {
+      const int uu = i / 32, a = i % 32;
+      const long u = u0 + uu;
+      float v = 0.f;
+      if (u < u_hi && a0 + a < p.A) {
+        const int b = (int)(u / ((long)p.Fu * p.Tu)), t = (int)(u % p.Tu);
+        v = p.P[u * p.A + a0 + a];
+        if (p.pmask) v *= mask_at(p.pmask, p.T0, b, t, p.lvl_p);
+      }
+      s_p[uu][a] = v;
+    }
+    for (int i = tid; i < KK * WG_U * 32; i += 256) {
+      const int bb = i % 32, uu = (i / 32) % WG_U, k = i / (32 * WG_U);
+      const long u = u0 + uu;
+      float v = 0.f;
+      if (u < u_hi && b0 + bb < p.Bc) {
+        const int b = (int)(u / ((long)p.Fu * p.Tu));
+        const int fu = (int)((u / p.Tu) % p.Fu), tu = (int)(u % p.Tu);
+        const int fv = fu * p.S - p.PAD + k / p.KS, tv = tu * p.S - p.PAD + k % p.KS;
+        if (fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv) {
+          v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + bb];
+          if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
+        }
+      }
+      s_q[k][uu][bb] = v;
+    }
+    __syncthreads();
+    for (int uu = 0; uu < WG_U; ++uu) {
+      const float pa = s_p[uu][ai];
+      for (int k = 0; k < KK; ++k) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[k][j] = fmaf(pa, s_q[k][uu][bq + j], acc[k][j]);
+      }
+    }
+  }
+  if (a0 + ai >= p.A) return;
+  for (int k = 0; k < KK; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + bq + j;
+      if (b < p.Bc) p.part[(((long)split * p.A + a0 + ai) * p.Bc + b) * KK + k] = acc[k][j];
+    }
+}
+
+// sum the splits in order; write dW in the reference layout through strides (a, b, k) -> a*sa + b*sb + k
+__global__ void wgrad_reduce_kernel(const float* part, int splits, int A, int Bc, int KK, long sa, long sb, float* dw,
+                                    int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)A * Bc * KK;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int q = 0; q < splits; ++q) s += part[(long)q * n + i];
+  const int k = (int)(i % KK), b = (int)((i / KK) % Bc), a = (int)(i / ((long)KK * Bc));
+  float* d = dw + a * sa + b * sb + k;
+  *d = accumulate ? *d + s : s;
+}
+
+// ---------------------------------------------------------------- per-utterance channel sums
+// out[b][c] (+)= sum over the utterance's positions of x[b][pos][c] (optionally x * y), one workgroup per (b, 256
+// channels); positions summed per thread in ascending order
+__global__ __launch_bounds__(256) void bsum_kernel(const float* x, const float* y, int npos, int C, float* out,
+                                                   int accumulate) {
+  const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float* xb = x + (long)b * npos * C + c;
+  const float* yb = y ? y + (long)b * npos * C + c : nullptr;
+  float s = 0.f;
+  for (int i = 0; i < npos; ++i) s += yb ? xb[(long)i * C] * yb[(long)i * C] : xb[(long)i * C];
+  float* o = out + (long)b * C + c;
+  *o = accumulate ? *o + s : s;
+}
+
+// out[c] (+)= sum_b in[b][c]
+__global__ void colsum_kernel(const float* in, int B, int C, float* out, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += in[(long)b * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---------------------------------------------------------------- GroupNorm statistics of a forward tensor
+// mean / rstd per (b, group) straight from the tensor (fp64 sums, fixed order): [B][8][2]
+__global__ __launch_bounds__(256) void gn_stats_kernel(const float* h, int npos, int C, float* stats) {
+  __shared__ double s[2][256];
+  const int b = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int cg = C / 8;
+  const float* hb = h + (long)b * npos * C + g * cg;
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = tid; i < (long)npos * cg; i += 256) {
+    const double v = hb[(i / cg) * C + i % cg];
+    s1 += v; s2 += v * v;
+  }
+  s[0][tid] = s1; s[1][tid] = s2;
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0, q = 0.0;
+    for (int i = 0; i < 256; ++i) { a += s[0][i]; q += s[1][i]; }
+    const double n = (double)npos * cg, mean = a / n;
+    double var = q / n - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    stats[(b * 8 + g) * 2] = (float)mean;
+    stats[(b * 8 + g) * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+  }
+}
+
+// ---------------------------------------------------------------- Block backward (Mish(GN(h)) * m)
+// dn = dA * m * mish'(n), n = xhat * gamma + beta; per (b, group): S1 = sum dn gamma, S2 = sum dn gamma xhat;
+// per (b, channel): dgamma = sum dn xhat, dbeta = sum dn. One workgroup per (b, group); fixed order.
+__global__ __launch_bounds__(256) void block_bwd_reduce_kernel(BlockBwdParams p) {
+  __shared__ double s[2][256];
+  const int b = blockIdx.x, g = blockIdx.y, tid = threadIdx.x;
+  const int cg = p.C / 8;
+  const float mean = p.stats[(b * 8 + g) * 2], rstd = p.stats[(b * 8 + g) * 2 + 1];
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = tid; i < (long)p.npos * cg; i += 256) {
+    const long pos = i / cg;
+    const int c = g * cg + (int)(i % cg);
+    const long o = ((long)b * p.npos + pos) * p.C + c;
+    const float xh = (p.h[o] - mean) * rstd;
+    const float n = xh * p.gamma[c] + p.beta[c];
+    const float m = mask_at(p.mask, p.T0, b, (int)(pos % p.T), p.lvl);
+    const float dn = p.dA[o] * m * mish_grad(n);
+    s1 += (double)(dn * p.gamma[c]);
+    s2 += (double)(dn * p.gamma[c] * xh);
+  }
+  s[0][tid] = s1; s[1][tid] = s2;
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0, q = 0.0;
+    for (int i = 0; i < 256; ++i) { a += s[0][i]; q += s[1][i]; }
+    p.gsum[(b * 8 + g) * 2] = (float)a;
+    p.gsum[(b * 8 + g) * 2 + 1] = (float)q;
+  }
+  // per-channel dgamma / dbeta of this utterance: thread c' of the group's channels
+  for (int cc = tid; cc < cg; cc += 256) {
+    const int c = g * cg + cc;
+    float dgm = 0.f, dbt = 0.f;
+    for (long pos = 0; pos < p.npos; ++pos) {
+      const long o = ((long)b * p.npos + pos) * p.C + c;
+      const float xh = (p.h[o] - mean) * rstd;
+      const float n = xh * p.gamma[c] + p.beta[c];
+      const float m = mask_at(p.mask, p.T0, b, (int)(pos % p.T), p.lvl);
+      const float dn = p.dA[o] * m * mish_grad(n);
+      dgm += dn * xh;
+      dbt += dn;
+    }
+    p.dgb[((long)b * p.C + c) * 2] = dgm;
+    p.dgb[((long)b * p.C + c) * 2 + 1] = dbt;
+  }
+}
+
+// dh = rstd (dn gamma - S1 / N - xhat S2 / N)
+__global__ __launch_bounds__(256) void block_bwd_apply_kernel(BlockBwdParams p) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)p.B * p.npos * p.C;
+  if (i >= n) return;
+  const int c = (int)(i % p.C);
+  const long pos = (i / p.C) % p.npos;
+  const int b = (int)(i / ((long)p.npos * p.C));
+  const int g = c / (p.C / 8);
+  const float mean = p.stats[(b * 8 + g) * 2], rstd = p.stats[(b * 8 + g) * 2 + 1];
+  const float N = (float)((double)p.npos * (p.C / 8));
+  const float xh = (p.h[i] - mean) * rstd;
+  const float nn = xh * p.gamma[c] + p.beta[c];
+  const float m = mask_at(p.mask, p.T0, b, (int)(pos % p.T), p.lvl);
+  const float dn = p.dA[i] * m * mish_grad(nn);
+  const float S1 = p.gsum[(b * 8 + g) * 2], S2 = p.gsum[(b * 8 + g) * 2 + 1];
+  p.dh[i] = rstd * (dn * p.gamma[c] - S1 / N - xh * S2 / N);
+}
+
+// Block forward output from the saved pre-activation: a = Mish(GN(h)) * m (+ tb) * m2 (recompute for the tape)
+__global__ __launch_bounds__(256) void block_fwd_kernel(BlockBwdParams p, const float* tb, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)p.B * p.npos * p.C;
+  if (i >= n) return;
+  const int c = (int)(i % p.C);
+  const long pos = (i / p.C) % p.npos;
+  const int b = (int)(i / ((long)p.npos * p.C));
+  const int g = c / (p.C / 8);
+  const float mean = p.stats[(b * 8 + g) * 2], rstd = p.stats[(b * 8 + g) * 2 + 1];
+  const float m = mask_at(p.mask, p.T0, b, (int)(pos % p.T), p.lvl);
+  float v = mish_f((p.h[i] - mean) * rstd * p.gamma[c] + p.beta[c]) * m;
+  if (tb) v = v + tb[(long)b * p.C + c];
+  out[i] = v;
+}
+
+// ---------------------------------------------------------------- elementwise helpers on [B][F][T][C]
+// y = alpha * x * (mask ? m : 1) (+ y if accumulate); channels [c0, c0 + C) of a tensor with cs channels
+__global__ void ew_kernel(EwParams p) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)p.B * p.F * p.T * p.C;
+  if (i >= n) return;
+  const int c = (int)(i % p.C);
+  const long pos = i / p.C;
+  const int t = (int)(pos % p.T);
+  const int b = (int)(pos / ((long)p.F * p.T));
+  float v = p.alpha * p.x[pos * p.xcs + p.xc0 + c];
+  if (p.mask) v *= mask_at(p.mask, p.T0, b, t, p.lvl);
+  if (p.x2) v += p.alpha2 * p.x2[pos * p.C + c];
+  float* o = p.y + pos * p.ycs + p.yc0 + c;
+  *o = p.accumulate ? *o + v : v;
+}
+
+// ---------------------------------------------------------------- LinearAttention pieces (4 heads x 32)
+// softmax statistics of k over the positions: per (b, row) max and sum of exp; k rows at channel offset 128 of qkv
+__global__ __launch_bounds__(256) void attn_kstats_kernel(const float* qkv, int npos, float* st) {
+  __shared__ float s_m[256];
+  __shared__ double s_l[256];
+  const int b = blockIdx.x, r = blockIdx.y, tid = threadIdx.x;
+  const float* kb = qkv + (long)b * npos * 384 + 128 + r;
+  float m = -__builtin_huge_valf();
+  for (long i = tid; i < npos; i += 256) m = fmaxf(m, kb[i * 384]);
+  s_m[tid] = m;
+  __syncthreads();
+  if (tid == 0) { float M = s_m[0]; for (int i = 1; i < 256; ++i) M = fmaxf(M, s_m[i]); s_m[0] = M; }
+  __syncthreads();
+  const float M = s_m[0];
+  double l = 0.0;
+  for (long i = tid; i < npos; i += 256) l += (double)expf(kb[i * 384] - M);
+  s_l[tid] = l;
+  __syncthreads();
+  if (tid == 0) {
+    double L = 0.0;
+    for (int i = 0; i < 256; ++i) L += s_l[i];
+    st[((long)b * 128 + r) * 2] = M;
+    st[((long)b * 128 + r) * 2 + 1] = (float)L;
+  }
+}
+
+// in place: k rows of qkv -> softmax(k) over the positions
+__global__ void attn_ksoftmax_kernel(float* qkv, int B, int npos, const float* st) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * npos * 128) return;
+  const int r = (int)(i % 128);
+  const long pos = i / 128;
+  const int b = (int)(pos / npos);
+  float* k = qkv + pos * 384 + 128 + r;
+  *k = expf(*k - st[((long)b * 128 + r) * 2]) / st[((long)b * 128 + r) * 2 + 1];
+}
+
+// R[b][h][d][e] = sum_pos X1[b][pos][x1o + 32h + d] X2[b][pos][x2o + 32h + e]   (grid (B, 4), 1024 threads)
+__global__ __launch_bounds__(1024) void attn_outer_kernel(const float* X1, int cs1, int x1o, const float* X2, int cs2,
+                                                          int x2o, int npos, float* R) {
+  const int b = blockIdx.x, h = blockIdx.y, d = threadIdx.x >> 5, e = threadIdx.x & 31;
+  const float* p1 = X1 + (long)b * npos * cs1 + x1o + 32 * h + d;
+  const float* p2 = X2 + (long)b * npos * cs2 + x2o + 32 * h + e;
+  float s = 0.f;
+  for (long i = 0; i < npos; ++i) s = fmaf(p1[i * cs1], p2[i * cs2], s);
+  R[(((long)b * 4 + h) * 32 + d) * 32 + e] = s;
+}
+
+// Y[b][pos][yo + 32h + j] (+)= sum_i M'[i][j] X[b][pos][xo + 32h + i], M' = M[b][h] (trans = 0: M[i][j]; 1: M[j][i])
+__global__ void attn_headmm_kernel(const float* M, int trans, const float* X, int csx, int xo, int B, int npos,
+                                   float* Y, int csy, int yo, int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * npos * 128) return;
+  const int hj = (int)(i % 128), h = hj >> 5, j = hj & 31;
+  const long pos = i / 128;
+  const int b = (int)(pos / npos);
+  const float* m = M + ((long)b * 4 + h) * 1024;
+  const float* x = X + pos * csx + xo + 32 * h;
+  float s = 0.f;
+  for (int ii = 0; ii < 32; ++ii) s = fmaf(trans ? m[j * 32 + ii] : m[ii * 32 + j], x[ii], s);
+  float* y = Y + pos * csy + yo + hj;
+  *y = accumulate ? *y + s : s;
+}
+
+// softmax backward of the k rows: dk = ks (dks - sum_pos ks dks), in place on the dk rows of dqkv (which hold dks)
+__global__ void attn_ksoftmax_bwd_kernel(const float* qkv_s, float* dqkv, int B, int npos, const float* S) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * npos * 128) return;
+  const int r = (int)(i % 128);
+  const long pos = i / 128;
+  const int b = (int)(pos / npos);
+  const float ks = qkv_s[pos * 384 + 128 + r];
+  float* d = dqkv + pos * 384 + 128 + r;
+  *d = ks * (*d - S[(long)b * 128 + r]);
+}
+
+// sum over positions (per b) of a[pos][ao + r] * c[pos][co + r], r < 128: S[b][r]
+__global__ void attn_rowdot_kernel(const float* a, int csa, int ao, const float* c, int csc, int co, int npos, float* S) {
+  const int b = blockIdx.x, r = threadIdx.x;
+  float s = 0.f;
+  for (long i = 0; i < npos; ++i) s = fmaf(a[((long)b * npos + i) * csa + ao + r], c[((long)b * npos + i) * csc + co + r], s);
+  S[(long)b * 128 + r] = s;
+}
+
+// scalar dot (fp64 sum, fixed order): out[0] (+)= sum_i x[i] y[i]
+__global__ __launch_bounds__(256) void dot_kernel(const float* x, const float* y, long n, float* out, int accumulate) {
+  __shared__ double s[256];
+  double a = 0.0;
+  for (long i = threadIdx.x; i < n; i += 256) a += (double)x[i] * (double)y[i];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += s[i];
+    out[0] = accumulate ? out[0] + (float)t : (float)t;
+  }
+}
+
+// ---------------------------------------------------------------- small dense layers ([B] rows)
+// Y[b][o] = act(sum_i W[o][i] X[b][i] + bias[o]); act 0: none, 1: Mish
+__global__ void linear_fwd_kernel(const float* X, int I, const float* W, const float* bias, int O, int act, float* Y) {
+  const int b = blockIdx.x;
+  for (int o = threadIdx.x; o < O; o += blockDim.x) {
+    float s = bias ? bias[o] : 0.f;
+    for (int i = 0; i < I; ++i) s += W[(long)o * I + i] * X[(long)b * I + i];
+    Y[(long)b * O + o] = act == 1 ? mish_f(s) : s;
+  }
+}
+// dW[o][i] (+)= sum_b dY[b][o] X[b][i]; db[o] (+)= sum_b dY[b][o]  (grid O rows)
+__global__ void linear_wgrad_kernel(const float* dY, const float* X, int B, int I, int O, float* dW, float* db) {
+  const int o = blockIdx.x;
+  for (int i = threadIdx.x; i < I; i += blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dY[(long)b * O + o] * X[(long)b * I + i];
+    dW[(long)o * I + i] += s;
+  }
+  if (threadIdx.x == 0 && db) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dY[(long)b * O + o];
+    db[o] += s;
+  }
+}
+// dX[b][i] (+)= (sum_o W[o][i] dY[b][o]) * (pre ? mish'(pre[b][i]) : 1)
+__global__ void linear_dgrad_kernel(const float* dY, const float* W, int I, int O, const float* pre, float* dX,
+                                    int accumulate) {
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < I; i += blockDim.x) {
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s += W[(long)o * I + i] * dY[(long)b * O + o];
+    if (pre) s *= mish_grad(pre[(long)b * I + i]);
+    dX[(long)b * I + i] = accumulate ? dX[(long)b * I + i] + s : s;
+  }
+}
+// SinusoidalPosEmb (diffusion.py:113-125) of t[b] -> [B][64]
+__global__ void posemb_kernel(const float* t, float scale, const float* freqs, float* out) {
+  const int b = blockIdx.x, j = threadIdx.x;
+  const float arg = (scale * t[b]) * freqs[j & 31];
+  out[b * 64 + j] = j < 32 ? sinf(arg) : cosf(arg);
+}
+
+// ---------------------------------------------------------------- loss / input layer / final layer
+// dL/ds = 2 (s sigma_b + z m) sigma_b / N, times mask (the score is (out * mask)); sigma_b = sqrt(1 - e^-cum)
+__global__ void loss_bwd_kernel(const float* score, const float* z, const float* mask, const float* t, const float* tot,
+                                int B, int T, float bmin, float half_delta, float* ds) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * 80 * T) return;
+  const int b = (int)(i / (80L * T)), tt = (int)(i % T);
+  const float tv = t[b];
+  const float cum = bmin * tv + half_delta * (tv * tv);
+  const float sg = sqrtf(1.f - expf(-cum));
+  const float m = mask[(long)b * T + tt];
+  const float N = tot[1] * 80.f;
+  ds[i] = 2.f * (score[i] * sg + z[i] * m) * sg / N * m;
+}
+// channels-last U-Net input [B][80][T][cin] = (mu, x_t, spk_mlp(spk) repeated over T)
+__global__ void input_pack_kernel(const float* mu, const float* xt, const float* s, int B, int T, int cin, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * 80 * T) return;
+  const int b = (int)(i / (80L * T)), f = (int)((i / T) % 80);
+  out[i * cin] = mu[i];
+  out[i * cin + 1] = xt[i];
+  if (cin == 3) out[i * cin + 2] = s[(long)b * 80 + f];
+}
+
+hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
+  if (p.KS > 4 || p.S > 2) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
+  if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad(const WGradParams& p, float* part, int splits, float* dw, long sa, long sb, int accumulate,
+                        hipStream_t s) {
+  if (p.KS > 4) return hipErrorInvalidValue;
+  WGradParams q = p;
+  q.part = part;
+  hipLaunchKernelGGL(wgrad_kernel, dim3((p.A + 31) / 32, (p.Bc + 31) / 32, splits), dim3(256), 0, s, q);
+  const long n = (long)p.A * p.Bc * p.KS * p.KS;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, splits, p.A, p.Bc,
+                     p.KS * p.KS, sa, sb, dw, accumulate);
+  return hipGetLastError();
+}
+
+
+// dX[b][i] = dY[b][i] * mish'(pre[b][i])   (grid B, block >= n)
+__global__ void mish_bwd_kernel(const float* dY, const float* pre, int n, float* dX) {
+  const int b = blockIdx.x, i = threadIdx.x;
+  if (i < n) dX[(long)b * n + i] = dY[(long)b * n + i] * mish_grad(pre[(long)b * n + i]);
+}
+// dmu = dx_in[.., 0] + dx_in[.., 1] (1 - e) m: mu enters the U-Net directly and through x_t (diffusion.py:247, 251)
+__global__ void dmu_kernel(const float* dxin, int cin, const float* t, const float* mask, int B, int T, float bmin,
+                           float half_delta, float* dmu) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * 80 * T) return;
+  const int b = (int)(i / (80L * T)), tt = (int)(i % T);
+  const float tv = t[b];
+  const float cum = __fadd_rn(__fmul_rn(bmin, tv), __fmul_rn(half_delta, __fmul_rn(tv, tv)));
+  const float e = expf(-0.5f * cum);
+  dmu[i] = dxin[i * cin] + dxin[i * cin + 1] * (1.f - e) * mask[(long)b * T + tt];
+}
+// ds[b][f] = sum_t dx_in[b][f][t][2]   (the speaker channel is spk_mlp(spk) repeated over T, diffusion.py:183-184)
+__global__ void spk_chan_sum_kernel(const float* dxin, int cin, int T, float* ds) {
+  const int b = blockIdx.x, f = threadIdx.x;
+  if (f >= 80) return;
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) s += dxin[(((long)b * 80 + f) * T + t) * cin + 2];
+  ds[b * 80 + f] = s;
+}
+// out[0] = sum of the mask (fp64, fixed order)
+__global__ void mask_sum_kernel(const float* mask, long n, float* out) {
+  __shared__ double s[256];
+  double a = 0.0;
+  for (long i = threadIdx.x; i < n; i += 256) a += mask[i];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += s[i];
+    out[0] = (float)t;
+  }
+}
+
+// ---- launchers
+hipError_t launch_bsum(dim3 grid, dim3 block, hipStream_t strm, const float* x, const float* y, int npos, int C, float* out, int accumulate) {
+  hipLaunchKernelGGL(bsum_kernel, grid, block, 0, strm, x, y, npos, C, out, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_colsum(dim3 grid, dim3 block, hipStream_t strm, const float* in, int B, int C, float* out, int accumulate) {
+  hipLaunchKernelGGL(colsum_kernel, grid, block, 0, strm, in, B, C, out, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_gn_stats(dim3 grid, dim3 block, hipStream_t strm, const float* h, int npos, int C, float* stats) {
+  hipLaunchKernelGGL(gn_stats_kernel, grid, block, 0, strm, h, npos, C, stats);
+  return hipGetLastError();
+}
+hipError_t launch_block_bwd_reduce(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p) {
+  hipLaunchKernelGGL(block_bwd_reduce_kernel, grid, block, 0, strm, p);
+  return hipGetLastError();
+}
+hipError_t launch_block_bwd_apply(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p) {
+  hipLaunchKernelGGL(block_bwd_apply_kernel, grid, block, 0, strm, p);
+  return hipGetLastError();
+}
+hipError_t launch_block_fwd(dim3 grid, dim3 block, hipStream_t strm, BlockBwdParams p, const float* tb, float* out) {
+  hipLaunchKernelGGL(block_fwd_kernel, grid, block, 0, strm, p, tb, out);
+  return hipGetLastError();
+}
+hipError_t launch_ew(dim3 grid, dim3 block, hipStream_t strm, EwParams p) {
+  hipLaunchKernelGGL(ew_kernel, grid, block, 0, strm, p);
+  return hipGetLastError();
+}
+hipError_t launch_attn_kstats(dim3 grid, dim3 block, hipStream_t strm, const float* qkv, int npos, float* st) {
+  hipLaunchKernelGGL(attn_kstats_kernel, grid, block, 0, strm, qkv, npos, st);
+  return hipGetLastError();
+}
+hipError_t launch_attn_ksoftmax(dim3 grid, dim3 block, hipStream_t strm, float* qkv, int B, int npos, const float* st) {
+  hipLaunchKernelGGL(attn_ksoftmax_kernel, grid, block, 0, strm, qkv, B, npos, st);
+  return hipGetLastError();
+}
+hipError_t launch_attn_outer(dim3 grid, dim3 block, hipStream_t strm, const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int npos, float* R) {
+  hipLaunchKernelGGL(attn_outer_kernel, grid, block, 0, strm, X1, cs1, x1o, X2, cs2, x2o, npos, R);
+  return hipGetLastError();
+}
+hipError_t launch_attn_headmm(dim3 grid, dim3 block, hipStream_t strm, const float* M, int trans, const float* X, int csx, int xo, int B, int npos, float* Y, int csy, int yo, int accumulate) {
+  hipLaunchKernelGGL(attn_headmm_kernel, grid, block, 0, strm, M, trans, X, csx, xo, B, npos, Y, csy, yo, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_attn_ksoftmax_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* qkv_s, float* dqkv, int B, int npos, const float* S) {
+  hipLaunchKernelGGL(attn_ksoftmax_bwd_kernel, grid, block, 0, strm, qkv_s, dqkv, B, npos, S);
+  return hipGetLastError();
+}
+hipError_t launch_attn_rowdot(dim3 grid, dim3 block, hipStream_t strm, const float* a, int csa, int ao, const float* c, int csc, int co, int npos, float* S) {
+  hipLaunchKernelGGL(attn_rowdot_kernel, grid, block, 0, strm, a, csa, ao, c, csc, co, npos, S);
+  return hipGetLastError();
+}
+hipError_t launch_dot(dim3 grid, dim3 block, hipStream_t strm, const float* x, const float* y, long n, float* out, int accumulate) {
+  hipLaunchKernelGGL(dot_kernel, grid, block, 0, strm, x, y, n, out, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_linear_fwd(dim3 grid, dim3 block, hipStream_t strm, const float* X, int I, const float* W, const float* bias, int O, int act, float* Y) {
+  hipLaunchKernelGGL(linear_fwd_kernel, grid, block, 0, strm, X, I, W, bias, O, act, Y);
+  return hipGetLastError();
+}
+hipError_t launch_linear_wgrad(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* X, int B, int I, int O, float* dW, float* db) {
+  hipLaunchKernelGGL(linear_wgrad_kernel, grid, block, 0, strm, dY, X, B, I, O, dW, db);
+  return hipGetLastError();
+}
+hipError_t launch_linear_dgrad(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* W, int I, int O, const float* pre, float* dX, int accumulate) {
+  hipLaunchKernelGGL(linear_dgrad_kernel, grid, block, 0, strm, dY, W, I, O, pre, dX, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_posemb(dim3 grid, dim3 block, hipStream_t strm, const float* t, float scale, const float* freqs, float* out) {
+  hipLaunchKernelGGL(posemb_kernel, grid, block, 0, strm, t, scale, freqs, out);
+  return hipGetLastError();
+}
+hipError_t launch_loss_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* score, const float* z, const float* mask, const float* t, const float* tot, int B, int T, float bmin, float half_delta, float* ds) {
+  hipLaunchKernelGGL(loss_bwd_kernel, grid, block, 0, strm, score, z, mask, t, tot, B, T, bmin, half_delta, ds);
+  return hipGetLastError();
+}
+hipError_t launch_input_pack(dim3 grid, dim3 block, hipStream_t strm, const float* mu, const float* xt, const float* s, int B, int T, int cin, float* out) {
+  hipLaunchKernelGGL(input_pack_kernel, grid, block, 0, strm, mu, xt, s, B, T, cin, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mish_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* pre, int n, float* dX) {
+  hipLaunchKernelGGL(mish_bwd_kernel, grid, block, 0, strm, dY, pre, n, dX);
+  return hipGetLastError();
+}
+hipError_t launch_dmu(dim3 grid, dim3 block, hipStream_t strm, const float* dxin, int cin, const float* t,
+                      const float* mask, int B, int T, float bmin, float half_delta, float* dmu) {
+  hipLaunchKernelGGL(dmu_kernel, grid, block, 0, strm, dxin, cin, t, mask, B, T, bmin, half_delta, dmu);
+  return hipGetLastError();
+}
+hipError_t launch_spk_chan_sum(dim3 grid, dim3 block, hipStream_t strm, const float* dxin, int cin, int T, float* ds) {
+  hipLaunchKernelGGL(spk_chan_sum_kernel, grid, block, 0, strm, dxin, cin, T, ds);
+  return hipGetLastError();
+}
+hipError_t launch_mask_sum(dim3 grid, dim3 block, hipStream_t strm, const float* mask, long n, float* out) {
+  hipLaunchKernelGGL(mask_sum_kernel, grid, block, 0, strm, mask, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace gt

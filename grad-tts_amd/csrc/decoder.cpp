@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "gradtts.h"
+#include "decoder_internal.h"
 #include "kernels.h"
 #include "train.h"
 #include "wimage.h"
@@ -168,6 +169,12 @@ struct gt_decoder {
   std::vector<Graph> gcache;   // most recently used last
   int64_t captures = 0;
   int64_t max_chunk = 0;       // > 0: cap on utterances per internal batch chunk (GT_MAX_CHUNK, tests)
+  // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
+  // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
+  bool raw_dirty = true;
+  float* raw = nullptr;
+  std::vector<int64_t> raw_off;
+  int64_t raw_numel = 0;
   void drop_graphs() {
     for (auto& g : gcache) (void)hipGraphExecDestroy(g.exec);
     gcache.clear();
@@ -807,6 +814,7 @@ void gt_decoder_destroy(gt_decoder* d) {
   if (!d) return;
   d->drop_graphs();
   if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
+  if (d->raw) (void)hipFree(d->raw);
   for (auto e : d->pool) (void)hipEventDestroy(e);
   for (int i = 0; i < 3; ++i)
     if (d->arena[i]) (void)hipFree(d->arena[i]);
@@ -870,6 +878,7 @@ int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int
   d->host[it->second].assign(data, data + numel);
   d->set[it->second] = true;
   d->dirty[0] = d->dirty[1] = d->dirty[2] = true;
+  d->raw_dirty = true;
   return GT_OK;
 }
 
@@ -929,6 +938,46 @@ int gt_estimator_forward(gt_decoder* d, int dtype, const float* x, const float* 
                          void* stream) {
   return estimator_impl(d, dtype, x, mask, mu, t, spk, B, T, out, workspace, workspace_bytes, stream, nullptr, nullptr);
 }
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- internal accessors (train_bwd.cpp, C++ linkage)
+int gt_internal_prepare_raw(gt_decoder* d) {
+  for (size_t i = 0; i < d->inv.size(); ++i)
+    if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
+  if (!d->raw_dirty) return GT_OK;
+  d->raw_off.clear();
+  int64_t n = 0;
+  for (auto& s : d->inv) { d->raw_off.push_back(n); n += s.numel(); }
+  d->raw_numel = n;
+  std::vector<float> h((size_t)n + 32);
+  for (size_t i = 0; i < d->inv.size(); ++i) memcpy(h.data() + d->raw_off[i], d->host[i].data(), d->host[i].size() * 4);
+  memcpy(h.data() + n, d->freqs, sizeof(d->freqs));
+  if (d->raw) { (void)hipFree(d->raw); d->raw = nullptr; }
+  if (hipMalloc(&d->raw, h.size() * 4) != hipSuccess) return fail(GT_ERR_HIP, "hipMalloc(raw params) failed");
+  if (hipMemcpy(d->raw, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipMemcpy(raw params) failed");
+  d->raw_dirty = false;
+  return GT_OK;
+}
+const float* gt_internal_param(gt_decoder* d, const std::string& name) {
+  auto it = d->index.find(name);
+  return it == d->index.end() ? nullptr : d->raw + d->raw_off[it->second];
+}
+int64_t gt_internal_param_offset(gt_decoder* d, const std::string& name) {
+  auto it = d->index.find(name);
+  return it == d->index.end() ? -1 : d->raw_off[it->second];
+}
+bool gt_internal_has_param(gt_decoder* d, const std::string& name) { return d->index.count(name) != 0; }
+float gt_internal_host_scalar(gt_decoder* d, const std::string& name) { return d->host[d->index.at(name)][0]; }
+const float* gt_internal_freqs(gt_decoder* d) { return d->raw + d->raw_numel; }
+int64_t gt_internal_numel(gt_decoder* d) { return d->raw_numel; }
+void gt_internal_consts(gt_decoder* d, int* n_spks, float* bmin, float* bmax, float* pe_scale) {
+  *n_spks = d->n_spks; *bmin = d->beta_min; *bmax = d->beta_max; *pe_scale = d->pe_scale;
+}
+int gt_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+
+extern "C" {
 
 // ---------------------------------------------------------------- training path (forward values)
 static size_t align256(size_t n) { return (n + 255) & ~size_t(255); }

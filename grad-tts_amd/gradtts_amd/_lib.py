@@ -52,6 +52,10 @@ SIGNATURES = [
     ("gt_diffusion_loss_t", _c.c_int, [_c.c_void_p, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                        _c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,
                                        _c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_train_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
+    ("gt_decoder_grad_numel", _c.c_int64, [_c.c_void_p]),
+    ("gt_diffusion_loss_grad", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 6 + [_c.c_int64, _c.c_int64] +
+     [_c.c_void_p] * 5 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_alignment_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_log_prior_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
                                              _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,

@@ -293,9 +293,9 @@ class Diffusion(torch.nn.Module):
     def forward(self, z, mask, mu, n_timesteps, stoc=False, spk=None):
         return self.reverse_diffusion(z, mask, mu, n_timesteps, stoc, spk)
 
-    # ---- training path: forward values on the HIP path; the U-Net backward is not built yet,
-    # so the loss carries a grad_fn whose backward raises (a training step fails loudly instead of silently
-    # training nothing).
+    # ---- training path: with gradients required, loss_t runs the fp32 training step of the
+    # library (taped forward + U-Net backward, gt_diffusion_loss_grad) and the loss carries the parameter / mu / spk
+    # gradients into autograd; otherwise the forward value only (gt_diffusion_loss_t, any compute dtype).
     def forward_diffusion(self, x0, mask, mu, t, z=None):
         """``Diffusion.forward_diffusion`` (model/diffusion.py:244-252) -> (xt * mask, z * mask). ``z`` defaults to
         ``torch.randn`` of x0's shape/dtype/device -- the reference's own draw (:249-250), same generator stream."""
@@ -325,6 +325,9 @@ class Diffusion(torch.nn.Module):
         x32, m32, mu32, z32 = (_f32c(a, device) for a in (x0, mask, mu, z))
         t32 = _f32c(torch.as_tensor(t).reshape(-1), device)
         spk32 = est._spk(spk, B, device)
+        if torch.is_grad_enabled() and (any(p.requires_grad for p in est.parameters()) or mu.requires_grad or
+                                        (spk is not None and spk.requires_grad)):
+            return self._loss_t_train(x32, m32, mu32, t32, z32, spk32, mu, spk, x0.dtype)
         dcode = _dtype_code(est.compute_dtype)
         loss = torch.empty((), dtype=torch.float32, device=device)
         xt = torch.empty_like(x32)
@@ -335,10 +338,31 @@ class Diffusion(torch.nn.Module):
                                             z32.data_ptr(), spk32.data_ptr() if spk32 is not None else None, B, T,
                                             loss.data_ptr(), xt.data_ptr(), ws.data_ptr(), ws.numel(),
                                             _stream_ptr(device)), "gt_diffusion_loss_t")
-        params = [p for p in est.parameters() if p.requires_grad]
-        if torch.is_grad_enabled() and params:
-            loss = _NoUNetBackward.apply(loss, *params)
         return loss.to(x0.dtype), xt.to(x0.dtype)
+
+    def _loss_t_train(self, x32, m32, mu32, t32, z32, spk32, mu, spk, out_dtype):
+        est = self.estimator
+        device = x32.device
+        B, _, T = x32.shape
+        L = lib()
+        with torch.cuda.device(device):
+            h = est._native(self.beta_min, self.beta_max)
+            names = [L.gt_decoder_param_name(h, i).decode() for i in range(L.gt_decoder_num_params(h))]
+            flat = torch.empty(L.gt_decoder_grad_numel(h), dtype=torch.float32, device=device)
+            dmu = torch.empty_like(x32)
+            dspk = torch.empty((B, est.spk_emb_dim), dtype=torch.float32, device=device) if spk32 is not None else None
+            loss = torch.empty(2, dtype=torch.float32, device=device)
+            xt = torch.empty_like(x32)
+            ws = torch.empty(L.gt_train_workspace_bytes(h, B, T), dtype=torch.uint8, device=device)
+            check(L.gt_diffusion_loss_grad(h, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
+                                           z32.data_ptr(), spk32.data_ptr() if spk32 is not None else None, B, T,
+                                           loss.data_ptr(), xt.data_ptr(), flat.data_ptr(), dmu.data_ptr(),
+                                           dspk.data_ptr() if dspk is not None else None, ws.data_ptr(), ws.numel(),
+                                           _stream_ptr(device)), "gt_diffusion_loss_grad")
+        params = dict(est.named_parameters())
+        plist = [params[n] for n in names]
+        out = _UNetLoss.apply(loss[0], flat, dmu, dspk, mu, spk, *plist)
+        return out.to(out_dtype), xt.to(out_dtype)
 
     def compute_loss(self, x0, mask, mu, spk=None, offset=1e-5):
         """``Diffusion.compute_loss`` (diffusion.py:283-287): t ~ U(0,1) clamped to [offset, 1 - offset]."""
@@ -347,15 +371,25 @@ class Diffusion(torch.nn.Module):
         return self.loss_t(x0, mask, mu, t, spk)
 
 
-class _NoUNetBackward(torch.autograd.Function):
-    """Marks a loss computed by the HIP forward path as depending on the estimator parameters; its backward raises
-    until the HIP U-Net backward exists."""
+class _UNetLoss(torch.autograd.Function):
+    """The loss of Diffusion.loss_t with the gradients the library computed in the same call (gt_diffusion_loss_grad):
+    backward scales them by the incoming gradient and hands them to the estimator parameters, mu and spk."""
 
     @staticmethod
-    def forward(ctx, loss, *params):
+    def forward(ctx, loss, flat, dmu, dspk, mu, spk, *params):
+        ctx.save_for_backward(flat, dmu, dspk if dspk is not None else flat.new_empty(0))
+        ctx.meta = ([p.shape for p in params], mu.dtype, spk.dtype if spk is not None else None, dspk is not None)
         return loss.clone()
 
     @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError("gradients of the HIP U-Net (training step backward, SURVEY.md §8f row 1) are "
-                                  "not implemented yet; the forward loss values are")
+    def backward(ctx, g):
+        flat, dmu, dspk = ctx.saved_tensors
+        shapes, mu_dtype, spk_dtype, has_spk = ctx.meta
+        grads, off = [], 0
+        for shp in shapes:
+            n = int(np.prod(shp)) if len(shp) else 1
+            grads.append(flat[off:off + n].view(shp) * g)
+            off += n
+        gmu = (dmu * g).to(mu_dtype)
+        gspk = (dspk * g).to(spk_dtype) if has_spk else None
+        return (None, None, None, None, gmu, gspk, *grads)

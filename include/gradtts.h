@@ -139,6 +139,17 @@ size_t gt_diffusion_loss_workspace_bytes(const gt_decoder* dec, int dtype, int64
 int gt_diffusion_loss_t(gt_decoder* dec, int dtype, const float* x0, const float* mask, const float* mu,
                         const float* t, const float* z, const float* spk, int64_t B, int64_t T, float* loss,
                         float* xt, void* workspace, size_t workspace_bytes, void* stream);
+/* Training step (fp32): loss_t forward with a tape and the backward of the U-Net. loss[0], xt as
+ * gt_diffusion_loss_t; grads: fp32 [gt_decoder_grad_numel] = d loss / d every estimator parameter, concatenated in
+ * state_dict inventory order (gt_decoder_param_name) in the reference layouts; dmu [B,80,T] = d loss / d mu
+ * (NULL: not written; mu enters the U-Net and x_t, diffusion.py:247/181); dspk [B,64] = d loss / d spk (n_spks > 1,
+ * NULL: not written). Deterministic. workspace: gt_train_workspace_bytes (the tape). */
+size_t gt_train_workspace_bytes(gt_decoder* dec, int64_t B, int64_t T);
+int64_t gt_decoder_grad_numel(gt_decoder* dec);
+int gt_diffusion_loss_grad(gt_decoder* dec, const float* x0, const float* mask, const float* mu, const float* t,
+                           const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, float* grads,
+                           float* dmu, float* dspk, void* workspace, size_t workspace_bytes, void* stream);
+
 /* The alignment step of GradTTS.compute_loss (model/tts.py:141-152) in one call: the log-prior of mu_x
  * [B,n_feats,Tx] against y [B,n_feats,Ty] (three fp32 contractions + const, tts.py:143-149), masked with
  * x_mask [B,Tx] (x) y_mask [B,Ty], then maximum_path on device (t_x, t_y from the masks). paths: [B,Tx,Ty]

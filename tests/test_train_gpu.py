@@ -5,6 +5,9 @@ and the C MAS oracle.
 Tolerances (written here): forward_diffusion fp32 elementwise 1e-6 x max|ref| (expf/sqrtf ulp differences);
 loss_t fp32 rel 1e-5, bf16 rel 1e-2 (the score's bf16 envelope, summed); log-prior fp32 1e-6 x max|ref|;
 alignment paths bit-exact against the C MAS oracle run on the same log-prior.
+Training step (gt_diffusion_loss_grad, fp32): loss rel 1e-5; every parameter gradient, d mu and d spk against
+torch.autograd through the oracle in fp64: max|g - ref| <= 2e-4 x (max|ref| of that tensor + 1e-3 x the largest
+max|ref| over all tensors) -- the floor covers the conv biases feeding a GroupNorm, whose exact gradient is 0.
 """
 import numpy as np
 import pytest
@@ -52,7 +55,8 @@ def test_loss_t_matches_oracle(cdt, tol, n_spks):
     dec, sd = make_decoder(n_spks, 0, cdt)
     c = lambda a: torch.from_numpy(a).cuda()
     s = c(spk) if n_spks > 1 else None
-    loss, xt = dec.loss_t(c(x0), c(mask), c(mu), c(t), s, z=c(z))
+    with torch.no_grad():   # forward value in the compute dtype (with gradients the fp32 training step runs)
+        loss, xt = dec.loss_t(c(x0), c(mask), c(mu), c(t), s, z=c(z))
     rloss, rxt = odec.loss_t(odec.to_torch_params(sd), *(torch.from_numpy(a) for a in (x0, mask, mu, t, z)),
                              torch.from_numpy(spk) if n_spks > 1 else None, n_spks)
     report(f"loss_t {cdt} n_spks={n_spks} (loss {float(loss):.5f} vs {float(rloss):.5f})",
@@ -60,9 +64,75 @@ def test_loss_t_matches_oracle(cdt, tol, n_spks):
     report(f"loss_t xt {cdt}", rel_err(xt.cpu().numpy(), rxt.numpy()), 1e-6)
 
 
-def test_compute_loss_seeded_deterministic_and_backward_raises():
+def _oracle_grads(sd, x0, mask, mu, t, z, spk, n_spks):
+    """torch.autograd through the oracle's loss_t in fp64 (oracle/decoder.py, diffusion.py:274-281)."""
+    from oracle import decoder as odec
+    d = lambda a: torch.from_numpy(a).double()
+    p = {k: v.double().requires_grad_() for k, v in odec.to_torch_params(sd).items()}
+    mu_t = d(mu).requires_grad_()
+    spk_t = d(spk).requires_grad_() if n_spks > 1 else None
+    x0_t, mask_t, t_t, z_t = d(x0), d(mask), d(t), d(z)
+    xt, zm = odec.forward_diffusion(x0_t, mask_t, mu_t, t_t, z_t)
+    cum = odec.get_noise(t_t[:, None, None], 0.05, 20.0, cumulative=True)
+    ne = odec.estimator(p, xt, mask_t, mu_t, t_t, spk_t, n_spks) * torch.sqrt(1.0 - torch.exp(-cum))
+    loss = torch.sum((ne + zm) ** 2) / (torch.sum(mask_t) * 80)
+    loss.backward()
+    return float(loss), {k: v.grad.numpy() for k, v in p.items()}, mu_t.grad.numpy(), \
+        (spk_t.grad.numpy() if spk_t is not None else None)
+
+
+@pytest.mark.parametrize("n_spks,B,T,lengths", [(1, 2, 64, [64, 44]), (247, 2, 32, [32, 21]), (1, 1, 40, [40])])
+def test_training_step_gradients_match_autograd(n_spks, B, T, lengths):
+    x0, mu, mask, z, t, spk = _data(9 + n_spks, B, T, lengths)
+    dec, sd = make_decoder(n_spks, 0, torch.float32)
+    c = lambda a: torch.from_numpy(a).cuda()
+    mu_d = c(mu).requires_grad_()
+    s = c(spk).requires_grad_() if n_spks > 1 else None
+    loss, _ = dec.loss_t(c(x0), c(mask), mu_d, c(t), s, z=c(z))
+    loss.backward()
+    rloss, rgrads, rdmu, rdspk = _oracle_grads(sd, x0, mask, mu, t, z, spk, n_spks)
+    report(f"train loss n_spks={n_spks} B={B} T={T}", abs(float(loss) - rloss) / abs(rloss), 1e-5)
+    gmax = max(float(np.abs(g).max()) for g in rgrads.values())
+    params = dict(dec.estimator.named_parameters())
+    worst, worst_name = 0.0, None
+    for name, rg in rgrads.items():
+        g = params[name].grad
+        assert g is not None, name
+        g = g.detach().cpu().numpy().astype(np.float64)
+        err = float(np.abs(g - rg).max()) / (float(np.abs(rg).max()) + 1e-3 * gmax)
+        if err > worst:
+            worst, worst_name = err, name
+    report(f"train param grads n_spks={n_spks} B={B} T={T} (worst {worst_name})", worst, 2e-4)
+    report(f"train d mu n_spks={n_spks}", rel_err(mu_d.grad.cpu().numpy(), rdmu), 2e-4)
+    if n_spks > 1:
+        report(f"train d spk n_spks={n_spks}", rel_err(s.grad.cpu().numpy(), rdspk), 2e-4)
+
+
+def test_training_step_deterministic_and_optimizer_step():
+    """Two identical calls give bit-identical gradients; an SGD step on them lowers the loss on the same draw and
+    the next call picks up the updated parameters (the handle re-syncs on the parameters' versions)."""
+    x0, mu, mask, z, t, _ = _data(13, 2, 64, [64, 50])
+    dec, _ = make_decoder(1, 0, torch.float32)
+    c = lambda a: torch.from_numpy(a).cuda()
+    args = (c(x0), c(mask), c(mu), c(t))
+    params = list(dec.estimator.parameters())
+    grads = []
+    for _ in range(2):
+        dec.zero_grad(set_to_none=True)
+        loss, _ = dec.loss_t(*args, z=c(z))
+        loss.backward()
+        grads.append([p.grad.clone() for p in params])
+    assert all(torch.equal(a, b) for a, b in zip(*grads))
+    opt = torch.optim.SGD(params, lr=1e-3)
+    opt.step()
+    with torch.no_grad():
+        loss2, _ = dec.loss_t(*args, z=c(z))
+    assert float(loss2) < float(loss), (float(loss2), float(loss))
+
+
+def test_compute_loss_seeded_deterministic_with_backward():
     x0, mu, mask, _, _, _ = _data(7, 2, 64, [64, 52])
-    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    dec, _ = make_decoder(1, 0, torch.float32)
     c = lambda a: torch.from_numpy(a).cuda()
     torch.manual_seed(11)
     l1, _ = dec.compute_loss(c(x0), c(mask), c(mu))
@@ -70,8 +140,8 @@ def test_compute_loss_seeded_deterministic_and_backward_raises():
     l2, _ = dec.compute_loss(c(x0), c(mask), c(mu))
     assert torch.isfinite(l1) and torch.equal(l1, l2)
     assert l1.requires_grad
-    with pytest.raises(NotImplementedError, match="backward"):
-        l1.backward()
+    l1.backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in dec.estimator.parameters())
 
 
 @pytest.mark.parametrize("B,Tx,Ty", [(3, 37, 150), (2, 130, 400), (4, 61, 1000)])
