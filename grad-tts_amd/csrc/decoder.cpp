@@ -942,14 +942,20 @@ int gt_estimator_forward(gt_decoder* d, int dtype, const float* x, const float* 
 }  // extern "C"
 
 // ---------------------------------------------------------------- internal accessors (train_bwd.cpp, C++ linkage)
-int gt_internal_prepare_raw(gt_decoder* d) {
-  for (size_t i = 0; i < d->inv.size(); ++i)
-    if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
-  if (!d->raw_dirty) return GT_OK;
+int gt_internal_layout(gt_decoder* d) {   // offsets of the raw block (the inventory's, fixed per decoder)
+  if (d->raw_off.size() == d->inv.size()) return GT_OK;
   d->raw_off.clear();
   int64_t n = 0;
   for (auto& s : d->inv) { d->raw_off.push_back(n); n += s.numel(); }
   d->raw_numel = n;
+  return GT_OK;
+}
+int gt_internal_prepare_raw(gt_decoder* d) {
+  for (size_t i = 0; i < d->inv.size(); ++i)
+    if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
+  if (!d->raw_dirty) return GT_OK;
+  gt_internal_layout(d);
+  const int64_t n = d->raw_numel;
   std::vector<float> h((size_t)n + 32);
   for (size_t i = 0; i < d->inv.size(); ++i) memcpy(h.data() + d->raw_off[i], d->host[i].data(), d->host[i].size() * 4);
   memcpy(h.data() + n, d->freqs, sizeof(d->freqs));

@@ -7,7 +7,8 @@
 
 #include "gradtts.h"
 
-int gt_internal_prepare_raw(gt_decoder* d);
+int gt_internal_layout(gt_decoder* d);         // raw-block offsets only (host; no device memory)
+int gt_internal_prepare_raw(gt_decoder* d);    // layout + upload of the raw parameter block
 const float* gt_internal_param(gt_decoder* d, const std::string& name);
 int64_t gt_internal_param_offset(gt_decoder* d, const std::string& name);
 bool gt_internal_has_param(gt_decoder* d, const std::string& name);

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -22,12 +23,16 @@ using namespace gt;
 
 namespace {
 
+using Regions = std::vector<std::pair<uintptr_t, size_t>>;
+
 struct Arena {   // bump allocator over the workspace; measure-only when base == nullptr
   uint8_t* base = nullptr;
   size_t off = 0;
+  Regions* rec = nullptr;   // extent checking (GT_TRAIN_DEBUG=2): every buffer handed out
   float* take(size_t floats) {
     const size_t o = off;
     off = (off + floats * 4 + 255) & ~size_t(255);
+    if (base && rec) rec->push_back({(uintptr_t)(base + o), floats * 4});
     return base ? reinterpret_cast<float*>(base + o) : nullptr;
   }
 };
@@ -46,7 +51,27 @@ struct Trainer {
   float* grads;             // flat [numel] in inventory order
   std::vector<float*> dtb;  // per ResnetBlock: [B][C] gradient of its time bias
 
-  void chk(hipError_t e) { if (err == hipSuccess && e != hipSuccess) err = e; }
+  int err_line = 0;
+  std::string err_cur;
+  bool debug = false;       // GT_TRAIN_DEBUG=1: synchronise after every launch and name the failing call site
+  // GT_TRAIN_DEBUG=2 (dry): no launches; every helper checks on the host that the extents its kernel will touch lie
+  // inside one buffer (arena allocation, caller buffer or the parameter block) and names the first that does not
+  bool dry = false;
+  Regions regions;
+  std::string bad;
+  bool live() const { return run && !dry; }
+  void need(const void* p, long elems, const char* what, int line) {
+    if (!dry || !bad.empty() || elems <= 0) return;
+    const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)elems * 4;
+    for (auto& r : regions)
+      if (a >= r.first && e <= r.first + r.second) return;
+    bad = std::string(what) + " out of range at train_bwd.cpp:" + std::to_string(line) + " (" + cur + ", " +
+          std::to_string(elems) + " elements)";
+  }
+  void chk(hipError_t e, int line = __builtin_LINE()) {
+    if (debug && e == hipSuccess && run) e = hipStreamSynchronize(s);
+    if (err == hipSuccess && e != hipSuccess) { err = e; err_line = line; err_cur = cur; }
+  }
   Lvl L(int l) const { return {80 >> l, T >> l}; }
   const float* P(const std::string& k) { return gt_internal_param(d, k); }
   float* G(const std::string& k) { return grads + gt_internal_param_offset(d, k); }
@@ -55,8 +80,16 @@ struct Trainer {
   // ------------------------------------------------------------ generic ops
   void gconv(const float* in, int Ci, int l_in, bool in_mask, const float* w, long wsa, long wsc, int KS, int S, int PAD,
              int flip, const float* bias, float* out, int Co, int l_out, bool out_mask, int out_cs, int out_c0, int acc,
-             bool transposed = false) {
+             bool transposed = false, int line = __builtin_LINE()) {
     if (!run) return;
+    {
+      const Lvl I = L(l_in), O = L(l_out);
+      need(in, (long)B * I.F * I.T * Ci, "gconv in", line);
+      need(out, ((long)B * O.F * O.T - 1) * out_cs + out_c0 + Co, "gconv out", line);
+      need(w, (long)(Co - 1) * wsa + (long)(Ci - 1) * wsc + KS * KS, "gconv weight", line);
+      if (bias) need(bias, Co, "gconv bias", line);
+    }
+    if (dry) return;
     GConvParams p{};
     p.B = B; p.Fi = L(l_in).F; p.Ti = L(l_in).T; p.Cin = Ci; p.Fo = L(l_out).F; p.To = L(l_out).T; p.Cout = Co;
     p.KS = KS; p.S = S; p.PAD = PAD; p.transposed = transposed; p.flip = flip;
@@ -64,36 +97,50 @@ struct Trainer {
     p.mask = in_mask ? mask : nullptr; p.T0 = T; p.lvl_in = l_in;
     p.out_mask = out_mask ? mask : nullptr; p.lvl_out = l_out;
     p.out = out; p.out_cs = out_cs; p.out_c0 = out_c0; p.accumulate = acc;
-    chk(launch_gconv(p, s));
+    chk(launch_gconv(p, s), line);
   }
   // dW(a, b, k) (+)= sum_u P[u][a] Q[v(u,k)][b]; written at dw + a*sa + b*sb + k
   void wgrad(const float* Pt, int Ad, int l_u, bool pmask, const float* Qt, int Bd, int l_v, bool qmask, int KS, int S,
-             int PAD, float* dw, long sa, long sb, int acc) {
+             int PAD, float* dw, long sa, long sb, int acc, int line = __builtin_LINE()) {
     const long nU = (long)B * L(l_u).F * L(l_u).T;
     const int splits = (int)std::max<long>(1, std::min<long>(256, nU / 512));
     float* part = A.take((size_t)splits * Ad * Bd * KS * KS);
     if (!run) return;
+    need(Pt, nU * Ad, "wgrad P", line);
+    need(Qt, (long)B * L(l_v).F * L(l_v).T * Bd, "wgrad Q", line);
+    need(dw, (long)(Ad - 1) * sa + (long)(Bd - 1) * sb + KS * KS, "wgrad dW", line);
+    if (dry) return;
     WGradParams p{};
     p.B = B; p.Fu = L(l_u).F; p.Tu = L(l_u).T; p.A = Ad; p.Fv = L(l_v).F; p.Tv = L(l_v).T; p.Bc = Bd;
     p.KS = KS; p.S = S; p.PAD = PAD; p.P = Pt; p.pmask = pmask ? mask : nullptr; p.lvl_p = l_u;
     p.Q = Qt; p.qmask = qmask ? mask : nullptr; p.lvl_q = l_v; p.T0 = T;
-    chk(launch_wgrad(p, part, splits, dw, sa, sb, acc, s));
+    chk(launch_wgrad(p, part, splits, dw, sa, sb, acc, s), line);
   }
   // out[c] (+)= sum_{b, pos} x   (bias gradients): per-utterance sums, then over the batch in order
-  void chansum(const float* x, int l, int C, float* out, int acc) {
+  void chansum(const float* x, int l, int C, float* out, int acc, int line = __builtin_LINE()) {
     float* tmp = A.take((size_t)B * C);
     if (!run) return;
-    chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, x, nullptr, L(l).F * L(l).T, C, tmp, 0));
-    chk(launch_colsum(dim3((C + 255) / 256), dim3(256), s, tmp, B, C, out, acc));
+    need(x, (long)B * L(l).F * L(l).T * C, "chansum x", line);
+    need(out, C, "chansum out", line);
+    if (dry) return;
+    chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, x, nullptr, L(l).F * L(l).T, C, tmp, 0), line);
+    chk(launch_colsum(dim3((C + 255) / 256), dim3(256), s, tmp, B, C, out, acc), line);
   }
   void ew(const float* x, int xcs, int xc0, float alpha, const float* x2, float alpha2, int l, int C, bool m, float* y,
-          int ycs, int yc0, int acc) {
+          int ycs, int yc0, int acc, int line = __builtin_LINE()) {
     if (!run) return;
+    {
+      const long np = (long)B * L(l).F * L(l).T;
+      need(x, (np - 1) * xcs + xc0 + C, "ew x", line);
+      if (x2) need(x2, np * C, "ew x2", line);
+      need(y, (np - 1) * ycs + yc0 + C, "ew y", line);
+    }
+    if (dry) return;
     EwParams p{};
     p.B = B; p.F = L(l).F; p.T = L(l).T; p.C = C; p.x = x; p.xcs = xcs; p.xc0 = xc0; p.alpha = alpha;
     p.x2 = x2; p.alpha2 = alpha2; p.mask = m ? mask : nullptr; p.T0 = T; p.lvl = l; p.y = y; p.ycs = ycs; p.yc0 = yc0;
     p.accumulate = acc;
-    chk(launch_ew(g1((long)B * L(l).F * L(l).T * C), dim3(256), s, p));
+    chk(launch_ew(g1((long)B * L(l).F * L(l).T * C), dim3(256), s, p), line);
   }
   BlockBwdParams bp(int l, int C, const float* h, const float* st, const std::string& gn) {
     BlockBwdParams p{};
@@ -103,27 +150,38 @@ struct Trainer {
   }
   float* gn_stats(const float* h, int l, int C) {
     float* st = A.take((size_t)B * 16);
-    if (run) chk(launch_gn_stats(dim3(B, 8), dim3(256), s, h, L(l).F * L(l).T, C, st));
+    if (live()) chk(launch_gn_stats(dim3(B, 8), dim3(256), s, h, L(l).F * L(l).T, C, st));
     return st;
   }
   float* block_fwd(int l, int C, const float* h, const float* st, const std::string& gn, const float* tb) {
     float* out = A.take((size_t)B * L(l).F * L(l).T * C);
-    if (run) chk(launch_block_fwd(g1((long)B * L(l).F * L(l).T * C), dim3(256), s, bp(l, C, h, st, gn), tb, out));
+    if (live()) chk(launch_block_fwd(g1((long)B * L(l).F * L(l).T * C), dim3(256), s, bp(l, C, h, st, gn), tb, out));
     return out;
   }
   // Block backward: dA -> dh, and the GroupNorm affine gradients
-  float* block_bwd(int l, int C, const float* dAv, const float* h, const float* st, const std::string& gn) {
+  float* block_bwd(int l, int C, const float* dAv, const float* h, const float* st, const std::string& gn,
+                   int line = __builtin_LINE()) {
     float* gsum = A.take((size_t)B * 16);
     float* dgb = A.take((size_t)B * C * 2);
     float* dh = A.take((size_t)B * L(l).F * L(l).T * C);
     float* tw = A.take((size_t)B * C);
     float* tb2 = A.take((size_t)B * C);
     if (!run) return dh;
+    {
+      const long n = (long)B * L(l).F * L(l).T * C;
+      need(dAv, n, "block_bwd dA", line);
+      need(h, n, "block_bwd h", line);
+      need(st, (long)B * 16, "block_bwd stats", line);
+      need(P(gn + ".weight"), C, "block_bwd gamma", line);
+      need(G(gn + ".weight"), C, "block_bwd dgamma", line);
+      need(G(gn + ".bias"), C, "block_bwd dbeta", line);
+    }
+    if (dry) return dh;
     BlockBwdParams p = bp(l, C, h, st, gn);
     p.dA = dAv; p.gsum = gsum; p.dgb = dgb; p.dh = dh;
-    chk(launch_block_bwd_reduce(dim3(B, 8), dim3(256), s, p));
-    chk(launch_block_bwd_apply(g1((long)B * p.npos * C), dim3(256), s, p));
-    chk(launch_colsum_strided(gn, dgb, C, tw, tb2));   // dgamma, dbeta = sums over the batch
+    chk(launch_block_bwd_reduce(dim3(B, 8), dim3(256), s, p), line);
+    chk(launch_block_bwd_apply(g1((long)B * p.npos * C), dim3(256), s, p), line);
+    chk(launch_colsum_strided(gn, dgb, C, tw, tb2), line);   // dgamma, dbeta = sums over the batch
     return dh;
   }
   // dgb [B][C][2] -> G(gn.weight)[c] += sum_b dgb[b][c][0]; G(gn.bias)[c] += sum_b dgb[b][c][1]
@@ -164,13 +222,14 @@ struct Trainer {
 
   // ResnetBlock forward (diffusion.py:61-79 / oracle resnet_block)
   float* resnet_fwd(const std::string& k, int r, int l, const float* x0, int C0, const float* x1, int C1, int C) {
+    cur = k + " fwd";
     RB b{k, l, C0, C1, C, x0, x1};
     const int Ci = C0 + C1;
     const long n = (long)B * L(l).F * L(l).T * C;
     b.h1 = A.take(n);
     const float* w1 = P(k + "block1.block.0.weight");
     gconv(x0, C0, l, true, w1, (long)Ci * 9, 9, 3, 1, 1, 0, P(k + "block1.block.0.bias"), b.h1, C, l, false, C, 0, 0);
-    if (x1) gconv(x1, C1, l, true, w1 + C0 * 9, (long)Ci * 9, 9, 3, 1, 1, 0, nullptr, b.h1, C, l, false, C, 0, 1);
+    if (C1 > 0) gconv(x1, C1, l, true, w1 + C0 * 9, (long)Ci * 9, 9, 3, 1, 1, 0, nullptr, b.h1, C, l, false, C, 0, 1);
     b.st1 = gn_stats(b.h1, l, C);
     b.tb = tbs[r]; b.r = r;
     b.u = block_fwd(l, C, b.h1, b.st1, k + "block1.block.1", b.tb);   // Mish(GN(h1)) m + tb
@@ -182,7 +241,7 @@ struct Trainer {
     if (gt_internal_has_param(d, k + "res_conv.weight")) {
       const float* wr = P(k + "res_conv.weight");
       gconv(x0, C0, l, true, wr, Ci, 1, 1, 1, 0, 0, P(k + "res_conv.bias"), b.out, C, l, false, C, 0, 1);
-      if (x1) gconv(x1, C1, l, true, wr + C0, Ci, 1, 1, 1, 0, 0, nullptr, b.out, C, l, false, C, 0, 1);
+      if (C1 > 0) gconv(x1, C1, l, true, wr + C0, Ci, 1, 1, 1, 0, 0, nullptr, b.out, C, l, false, C, 0, 1);
     } else {
       ew(x0, C, 0, 1.f, nullptr, 0.f, l, C, true, b.out, C, 0, 1);
     }
@@ -192,6 +251,7 @@ struct Trainer {
 
   // LinearAttention forward (diffusion.py:82-110 / oracle linear_attention)
   float* attn_fwd(const std::string& k, int l, const float* x, int C) {
+    cur = k + " fwd";
     AT a{k, l, C, x};
     const long np = (long)L(l).F * L(l).T;
     a.qkv = A.take((size_t)B * np * 384);
@@ -201,7 +261,7 @@ struct Trainer {
     a.o = A.take((size_t)B * np * 128);
     a.z = A.take((size_t)B * np * C);
     a.y = A.take((size_t)B * np * C);
-    if (run) {
+    if (live()) {
       chk(launch_attn_kstats(dim3(B, 128), dim3(256), s, a.qkv, (int)np, st));
       chk(launch_attn_ksoftmax(g1((long)B * np * 128), dim3(256), s, a.qkv, B, (int)np, st));
       chk(launch_attn_outer(dim3(B, 4), dim3(1024), s, a.qkv, 384, 128, a.qkv, 384, 256, (int)np, a.ctx));
@@ -220,7 +280,7 @@ struct Trainer {
     // time embedding (diffusion.py:113-125, 143-144, 177-178) and every ResnetBlock's mlp (64-65, 76)
     temb_s = A.take((size_t)B * 64); temb_pre0 = A.take((size_t)B * 256); temb_h = A.take((size_t)B * 256);
     temb = A.take((size_t)B * 64); temb_m = A.take((size_t)B * 64);
-    if (run) {
+    if (live()) {
       chk(launch_posemb(dim3(B), dim3(64), s, t, pe_scale, gt_internal_freqs(d), temb_s));
       chk(launch_linear_fwd(dim3(B), dim3(256), s, temb_s, 64, P("mlp.0.weight"), P("mlp.0.bias"), 256, 0, temb_pre0));
       chk(launch_linear_fwd(dim3(B), dim3(256), s, temb_s, 64, P("mlp.0.weight"), P("mlp.0.bias"), 256, 1, temb_h));
@@ -230,7 +290,7 @@ struct Trainer {
     const int Cs[12] = {64, 64, 128, 128, 256, 256, 256, 256, 128, 128, 64, 64};
     for (int r = 0; r < 12; ++r) {
       float* tb = A.take((size_t)B * Cs[r]);
-      if (run) chk(launch_linear_fwd(dim3(B), dim3(256), s, temb_m, 64, P(std::string(kRes[r]) + "mlp.1.weight"),
+      if (live()) chk(launch_linear_fwd(dim3(B), dim3(256), s, temb_m, 64, P(std::string(kRes[r]) + "mlp.1.weight"),
                                      P(std::string(kRes[r]) + "mlp.1.bias"), Cs[r], 0, tb));
       tbs.push_back(tb);
       dtb.push_back(A.take((size_t)B * Cs[r]));
@@ -239,14 +299,14 @@ struct Trainer {
     spk_pre = spk_h = spk_s = nullptr;
     if (n_spks > 1) {
       spk_pre = A.take((size_t)B * 256); spk_h = A.take((size_t)B * 256); spk_s = A.take((size_t)B * 80);
-      if (run) {
+      if (live()) {
         chk(launch_linear_fwd(dim3(B), dim3(256), s, spk, 64, P("spk_mlp.0.weight"), P("spk_mlp.0.bias"), 256, 0, spk_pre));
         chk(launch_linear_fwd(dim3(B), dim3(256), s, spk, 64, P("spk_mlp.0.weight"), P("spk_mlp.0.bias"), 256, 1, spk_h));
         chk(launch_linear_fwd(dim3(B), dim3(128), s, spk_h, 256, P("spk_mlp.2.weight"), P("spk_mlp.2.bias"), 80, 0, spk_s));
       }
     }
     xin = A.take((size_t)B * 80 * T * cin);
-    if (run) chk(launch_input_pack(g1((long)B * 80 * T), dim3(256), s, mu, xt, spk_s, B, T, cin, xin));
+    if (live()) chk(launch_input_pack(g1((long)B * 80 * T), dim3(256), s, mu, xt, spk_s, B, T, cin, xin));
     // down path
     float* h = resnet_fwd("downs.0.0.", 0, 0, xin, cin, nullptr, 0, 64);
     h = resnet_fwd("downs.0.1.", 1, 0, h, 64, nullptr, 0, 64);
@@ -297,16 +357,17 @@ struct Trainer {
   // ResnetBlock backward; dx0 / dx1 receive (accumulate) the input gradients
   void resnet_bwd(const RB& b, const float* dout, float* dx0, float* dx1) {
     const std::string& k = b.k;
+    cur = k + " bwd";
     const int l = b.l, C = b.C, Ci = b.C0 + b.C1;
     // residual branch
     if (gt_internal_has_param(d, k + "res_conv.weight")) {
       const float* wr = P(k + "res_conv.weight");
       float* gw = G(k + "res_conv.weight");
       wgrad(dout, C, l, false, b.x0, b.C0, l, true, 1, 1, 0, gw, Ci, 1, 1);
-      if (b.x1) wgrad(dout, C, l, false, b.x1, b.C1, l, true, 1, 1, 0, gw + b.C0, Ci, 1, 1);
+      if (b.C1 > 0) wgrad(dout, C, l, false, b.x1, b.C1, l, true, 1, 1, 0, gw + b.C0, Ci, 1, 1);
       chansum(dout, l, C, G(k + "res_conv.bias"), 1);
       gconv(dout, C, l, false, wr, 1, Ci, 1, 1, 0, 0, nullptr, dx0, b.C0, l, true, b.C0, 0, 1);
-      if (b.x1) gconv(dout, C, l, false, wr + b.C0, 1, Ci, 1, 1, 0, 0, nullptr, dx1, b.C1, l, true, b.C1, 0, 1);
+      if (b.C1 > 0) gconv(dout, C, l, false, wr + b.C0, 1, Ci, 1, 1, 0, 0, nullptr, dx1, b.C1, l, true, b.C1, 0, 1);
     } else {
       ew(dout, C, 0, 1.f, nullptr, 0.f, l, C, true, dx0, C, 0, 1);
     }
@@ -316,26 +377,27 @@ struct Trainer {
     chansum(dh2, l, C, G(k + "block2.block.0.bias"), 1);
     float* du = A.take((size_t)B * L(l).F * L(l).T * C);
     gconv(dh2, C, l, false, P(k + "block2.block.0.weight"), 9, (long)C * 9, 3, 1, 1, 1, nullptr, du, C, l, true, C, 0, 0);
-    if (run) chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, du, nullptr, L(l).F * L(l).T, C, dtb[b.r], 0));
+    if (live()) chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, du, nullptr, L(l).F * L(l).T, C, dtb[b.r], 0));
     // block1
     float* dh1 = block_bwd(l, C, du, b.h1, b.st1, k + "block1.block.1");
     const float* w1 = P(k + "block1.block.0.weight");
     float* gw1 = G(k + "block1.block.0.weight");
     wgrad(dh1, C, l, false, b.x0, b.C0, l, true, 3, 1, 1, gw1, (long)Ci * 9, 9, 1);
-    if (b.x1) wgrad(dh1, C, l, false, b.x1, b.C1, l, true, 3, 1, 1, gw1 + b.C0 * 9, (long)Ci * 9, 9, 1);
+    if (b.C1 > 0) wgrad(dh1, C, l, false, b.x1, b.C1, l, true, 3, 1, 1, gw1 + b.C0 * 9, (long)Ci * 9, 9, 1);
     chansum(dh1, l, C, G(k + "block1.block.0.bias"), 1);
     gconv(dh1, C, l, false, w1, 9, (long)Ci * 9, 3, 1, 1, 1, nullptr, dx0, b.C0, l, true, b.C0, 0, 1);
-    if (b.x1) gconv(dh1, C, l, false, w1 + b.C0 * 9, 9, (long)Ci * 9, 3, 1, 1, 1, nullptr, dx1, b.C1, l, true, b.C1, 0, 1);
+    if (b.C1 > 0) gconv(dh1, C, l, false, w1 + b.C0 * 9, 9, (long)Ci * 9, 3, 1, 1, 1, nullptr, dx1, b.C1, l, true, b.C1, 0, 1);
   }
 
   // LinearAttention backward; dx (accumulate) receives the input gradient
   void attn_bwd(const AT& a, const float* dy, float* dx) {
     const std::string& k = a.k;
+    cur = k + " bwd";
     const int l = a.l, C = a.C;
     const long np = (long)L(l).F * L(l).T, n = (long)B * np;
     const float g = gt_internal_host_scalar(d, k + "fn.g");
     ew(dy, C, 0, 1.f, nullptr, 0.f, l, C, false, dx, C, 0, 1);                 // residual
-    if (run) chk(launch_dot(dim3(1), dim3(256), s, dy, a.z, n * C, G(k + "fn.g"), 1));   // d g = sum dy . z
+    if (live()) chk(launch_dot(dim3(1), dim3(256), s, dy, a.z, n * C, G(k + "fn.g"), 1));   // d g = sum dy . z
     float* dz = A.take((size_t)n * C);
     ew(dy, C, 0, g, nullptr, 0.f, l, C, false, dz, C, 0, 0);
     wgrad(dz, C, l, false, a.o, 128, l, false, 1, 1, 0, G(k + "fn.fn.to_out.weight"), 128, 1, 1);
@@ -345,7 +407,7 @@ struct Trainer {
     float* dctx = A.take((size_t)B * 4096);
     float* dqkv = A.take((size_t)n * 384);
     float* S = A.take((size_t)B * 128);
-    if (run) {
+    if (live()) {
       chk(launch_attn_outer(dim3(B, 4), dim3(1024), s, a.qkv, 384, 0, dO, 128, 0, (int)np, dctx));      // q do^T
       chk(launch_attn_headmm(g1(n * 128), dim3(256), s, a.ctx, 1, dO, 128, 0, B, (int)np, dqkv, 384, 0, 0));     // dq
       chk(launch_attn_headmm(g1(n * 128), dim3(256), s, dctx, 1, a.qkv, 384, 256, B, (int)np, dqkv, 384, 128, 0));  // dks
@@ -361,7 +423,7 @@ struct Trainer {
     const long n0 = (long)B * 80 * T;
     // dL/dscore (diffusion.py:278-280)
     float* ds = A.take(n0);
-    if (run) chk(launch_loss_bwd(g1(n0), dim3(256), s, score, z, mask, t, lossp, B, T, bmin, half_delta, ds));
+    if (live()) chk(launch_loss_bwd(g1(n0), dim3(256), s, score, z, mask, t, lossp, B, T, bmin, half_delta, ds));
     // final conv (1x1, 64 -> 1) on af * m, output * m
     wgrad(ds, 1, 0, false, af, 64, 0, true, 1, 1, 0, G("final_conv.weight"), 64, 1, 1);
     chansum(ds, 0, 1, G("final_conv.bias"), 1);
@@ -455,7 +517,7 @@ struct Trainer {
     float* dtm = A.take((size_t)B * 64);
     float* dte = A.take((size_t)B * 64);
     float* dh0 = A.take((size_t)B * 256);
-    if (run) {
+    if (live()) {
       for (int r = 0; r < 12; ++r) {
         const std::string kr = std::string(kRes[r]) + "mlp.1.";
         chk(launch_linear_wgrad(dim3(Cs[r]), dim3(64), s, dtb[r], temb_m, B, 64, Cs[r], G(kr + "weight"), G(kr + "bias")));
@@ -467,11 +529,11 @@ struct Trainer {
       chk(launch_linear_wgrad(dim3(256), dim3(64), s, dh0, temb_s, B, 64, 256, G("mlp.0.weight"), G("mlp.0.bias")));
     }
     // inputs: dmu = dxin[..0] + dxin[..1] (1 - e) m (x_t = x0 e + mu (1 - e) + ..., masked); speaker channel
-    if (run && dmu) chk(launch_dmu(g1(n0), dim3(256), s, dxin, cin, t, mask, B, T, bmin, half_delta, dmu));
+    if (live() && dmu) chk(launch_dmu(g1(n0), dim3(256), s, dxin, cin, t, mask, B, T, bmin, half_delta, dmu));
     if (n_spks > 1) {
       float* dsv = A.take((size_t)B * 80);
       float* dsh = A.take((size_t)B * 256);
-      if (run) {
+      if (live()) {
         chk(launch_spk_chan_sum(dim3(B), dim3(128), s, dxin, cin, T, dsv));
         chk(launch_linear_wgrad(dim3(80), dim3(256), s, dsv, spk_h, B, 256, 80, G("spk_mlp.2.weight"), G("spk_mlp.2.bias")));
         chk(launch_linear_dgrad(dim3(B), dim3(256), s, dsv, P("spk_mlp.2.weight"), 256, 80, spk_pre, dsh, 0));
@@ -481,9 +543,13 @@ struct Trainer {
     }
     (void)xt_e;
   }
+  std::string cur;                // the ResnetBlock / attention being processed (error messages)
   const float* lossp = nullptr;   // device [2]: loss, sum(mask)
   const float* spkin = nullptr;
-  void zero(float* p, long n) { if (run) chk(hipMemsetAsync(p, 0, (size_t)n * 4, s)); }
+  void zero(float* p, long n, int line = __builtin_LINE()) {
+    if (run) need(p, n, "zero", line);
+    if (live()) chk(hipMemsetAsync(p, 0, (size_t)n * 4, s), line);
+  }
 };
 
 }  // namespace
@@ -491,17 +557,87 @@ struct Trainer {
 extern "C" {
 
 size_t gt_train_workspace_bytes(gt_decoder* d, int64_t B, int64_t T) {
-  if (!d || B <= 0 || T <= 0 || gt_internal_prepare_raw(d) != GT_OK) return 0;
+  if (!d || B <= 0 || T <= 0 || gt_internal_layout(d) != GT_OK) return 0;
   Trainer tr;
   tr.d = d; tr.B = (int)B; tr.T = (int)T; tr.run = false; tr.s = nullptr;
   float bmax;
   gt_internal_consts(d, &tr.n_spks, &tr.bmin, &bmax, &tr.pe_scale);
   tr.cin = tr.n_spks > 1 ? 3 : 2;
-  tr.A.take((size_t)B * 80 * T * 3);   // xt, zm, loss partials (see gt_diffusion_loss_grad)
+  tr.A.take((size_t)B * 80 * T);       // zm, loss partials, loss (as train_pass takes them)
+  tr.A.take((size_t)B * 80 * T * 2);
+  tr.A.take(2);
   tr.forward(nullptr, nullptr, nullptr, nullptr);
   tr.backward(nullptr, nullptr, nullptr, nullptr, nullptr);
   return tr.A.off + 4096;
 }
+
+}  // extern "C"
+
+// One pass of the training step. dry: no launches; every helper checks on the host that the extents its kernels will
+// touch lie inside one buffer (arena allocation, caller buffer, parameter block) -- run before every live pass, so a
+// host-side indexing error fails loudly instead of faulting the GPU.
+static int train_pass(gt_decoder* d, const float* x0, const float* mask, const float* mu, const float* t,
+                      const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, float* grads,
+                      float* dmu, float* dspk, void* workspace, size_t workspace_bytes, hipStream_t stream, bool dry,
+                      bool debug) {
+  Trainer tr;
+  tr.d = d; tr.B = (int)B; tr.T = (int)T; tr.run = true; tr.s = stream;
+  float bmax;
+  gt_internal_consts(d, &tr.n_spks, &tr.bmin, &bmax, &tr.pe_scale);
+  tr.half_delta = (float)(0.5 * ((double)bmax - (double)tr.bmin));
+  tr.cin = tr.n_spks > 1 ? 3 : 2;
+  tr.mask = mask; tr.grads = grads; tr.spkin = spk;
+  tr.debug = debug;
+  tr.dry = dry;
+  if (dry) {
+    const size_t n0b = (size_t)B * 80 * T * 4;
+    tr.regions = {{(uintptr_t)x0, n0b}, {(uintptr_t)mu, n0b}, {(uintptr_t)z, n0b}, {(uintptr_t)xt, n0b},
+                  {(uintptr_t)mask, (size_t)B * T * 4}, {(uintptr_t)t, (size_t)B * 4},
+                  {(uintptr_t)grads, (size_t)gt_internal_numel(d) * 4},
+                  {(uintptr_t)gt_internal_param(d, "mlp.0.weight") - (uintptr_t)gt_internal_param_offset(d, "mlp.0.weight") * 4,
+                   (size_t)(gt_internal_numel(d) + 32) * 4}};
+    if (dmu) tr.regions.push_back({(uintptr_t)dmu, n0b});
+    if (spk) tr.regions.push_back({(uintptr_t)spk, (size_t)B * 64 * 4});
+    if (dspk) tr.regions.push_back({(uintptr_t)dspk, (size_t)B * 64 * 4});
+    tr.A.rec = &tr.regions;
+  }
+  tr.A.base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  const long n0 = (long)B * 80 * T;
+  float* zm = tr.A.take((size_t)n0);
+  float* lpart = tr.A.take((size_t)n0 * 2);   // loss partials (generous)
+  float* lossv = tr.A.take(2);
+  if (!dry) tr.chk(hipMemsetAsync(grads, 0, (size_t)gt_internal_numel(d) * 4, tr.s));
+  // forward diffusion (diffusion.py:275), then the taped U-Net forward on x_t
+  FwdDiffParams fp;
+  fp.x0 = x0; fp.mu = mu; fp.z = z; fp.mask = mask; fp.t = t; fp.B = (int)B; fp.F = 80; fp.T = (int)T;
+  fp.beta_min = tr.bmin; fp.half_delta = tr.half_delta; fp.xt = xt; fp.zm = zm;
+  if (!dry) tr.chk(launch_fwd_diffusion(fp, tr.s));
+  tr.forward(mu, xt, spk, t);
+  // loss value and sum(mask) (for the gradient's normaliser)
+  LossParams lp;
+  lp.score = tr.score; lp.z = z; lp.mask = mask; lp.t = t; lp.B = (int)B; lp.F = 80; lp.T = (int)T;
+  lp.beta_min = tr.bmin; lp.half_delta = tr.half_delta; lp.part = lpart;
+  if (!dry) {
+    tr.chk(launch_loss(lp, lossv, tr.s));
+    tr.chk(launch_mask_sum(dim3(1), dim3(256), tr.s, mask, n0 / 80, lossv + 1));
+  }
+  tr.lossp = lossv;
+  tr.backward(z, t, xt, dmu, dspk);
+  if (dry) {
+    if (!tr.bad.empty()) return gt_internal_fail(GT_ERR_WORKSPACE, "training step extent check: " + tr.bad);
+    if (tr.A.off + 255 > workspace_bytes)
+      return gt_internal_fail(GT_ERR_WORKSPACE, "training step extent check: arena " + std::to_string(tr.A.off) +
+                                                   " B past the workspace " + std::to_string(workspace_bytes) + " B");
+    return GT_OK;
+  }
+  tr.chk(hipMemcpyAsync(loss, lossv, 4, hipMemcpyDeviceToDevice, tr.s));
+  if (tr.err != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(tr.err) +
+                                            " (train_bwd.cpp:" + std::to_string(tr.err_line) + ", block " + tr.err_cur + ")");
+  return GT_OK;
+}
+
+extern "C" {
 
 int gt_diffusion_loss_grad(gt_decoder* d, const float* x0, const float* mask, const float* mu, const float* t,
                            const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, float* grads,
@@ -509,45 +645,25 @@ int gt_diffusion_loss_grad(gt_decoder* d, const float* x0, const float* mask, co
   if (!d || !x0 || !mask || !mu || !t || !z || !loss || !xt || !grads || !workspace)
     return gt_internal_fail(GT_ERR_ARG, "null argument");
   if (B <= 0 || T <= 0 || T % 4 != 0) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
-  int rc = gt_internal_prepare_raw(d);
+  // GT_TRAIN_DEBUG=1: synchronise after every launch and name the failing call site; =2: the host extent check
+  // only (nothing touches the device: runs without a GPU, tests/test_train_cpu.py)
+  const char* dbg = getenv("GT_TRAIN_DEBUG");
+  const bool dry_only = dbg && dbg[0] == '2';
+  int rc = dry_only ? gt_internal_layout(d) : gt_internal_prepare_raw(d);
   if (rc) return rc;
   if (workspace_bytes < gt_train_workspace_bytes(d, B, T)) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
-  Trainer tr;
-  tr.d = d; tr.B = (int)B; tr.T = (int)T; tr.run = true; tr.s = (hipStream_t)stream;
-  float bmax;
-  gt_internal_consts(d, &tr.n_spks, &tr.bmin, &bmax, &tr.pe_scale);
-  if (tr.n_spks > 1 && !spk) return gt_internal_fail(GT_ERR_ARG, "n_spks > 1 needs spk");
-  tr.half_delta = (float)(0.5 * ((double)bmax - (double)tr.bmin));
-  tr.cin = tr.n_spks > 1 ? 3 : 2;
-  tr.mask = mask; tr.grads = grads; tr.spkin = spk;
-  tr.A.base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  const long n0 = (long)B * 80 * T;
-  float* zm = tr.A.take((size_t)n0);
-  float* lpart = tr.A.take((size_t)n0 * 2);   // loss partials (generous)
-  float* lossv = tr.A.take(2);
-  tr.chk(hipMemsetAsync(grads, 0, (size_t)gt_internal_numel(d) * 4, tr.s));
-  // forward diffusion (diffusion.py:275), then the taped U-Net forward on x_t
-  FwdDiffParams fp;
-  fp.x0 = x0; fp.mu = mu; fp.z = z; fp.mask = mask; fp.t = t; fp.B = (int)B; fp.F = 80; fp.T = (int)T;
-  fp.beta_min = tr.bmin; fp.half_delta = tr.half_delta; fp.xt = xt; fp.zm = zm;
-  tr.chk(launch_fwd_diffusion(fp, tr.s));
-  tr.forward(mu, xt, spk, t);
-  // loss value and sum(mask) (for the gradient's normaliser)
-  LossParams lp;
-  lp.score = tr.score; lp.z = z; lp.mask = mask; lp.t = t; lp.B = (int)B; lp.F = 80; lp.T = (int)T;
-  lp.beta_min = tr.bmin; lp.half_delta = tr.half_delta; lp.part = lpart;
-  tr.chk(launch_loss(lp, lossv, tr.s));
-  tr.chk(launch_mask_sum(dim3(1), dim3(256), tr.s, mask, n0 / 80, lossv + 1));
-  tr.lossp = lossv;
-  tr.backward(z, t, xt, dmu, dspk);
-  tr.chk(hipMemcpyAsync(loss, lossv, 4, hipMemcpyDeviceToDevice, tr.s));
-  if (tr.err != hipSuccess)
-    return gt_internal_fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(tr.err));
-  return GT_OK;
+  int n_spks; float bmin, bmax, pe;
+  gt_internal_consts(d, &n_spks, &bmin, &bmax, &pe);
+  if (n_spks > 1 && !spk) return gt_internal_fail(GT_ERR_ARG, "n_spks > 1 needs spk");
+  rc = train_pass(d, x0, mask, mu, t, z, spk, B, T, loss, xt, grads, dmu, dspk, workspace, workspace_bytes,
+                  (hipStream_t)stream, true, false);
+  if (rc || dry_only) return rc;
+  return train_pass(d, x0, mask, mu, t, z, spk, B, T, loss, xt, grads, dmu, dspk, workspace, workspace_bytes,
+                    (hipStream_t)stream, false, dbg && dbg[0] == '1');
 }
 
 int64_t gt_decoder_grad_numel(gt_decoder* d) {
-  if (!d || gt_internal_prepare_raw(d) != GT_OK) return -1;
+  if (!d || gt_internal_layout(d) != GT_OK) return -1;
   return gt_internal_numel(d);
 }
 
