@@ -68,6 +68,30 @@ hipError_t launch_posemb(dim3 grid, dim3 block, hipStream_t strm, const float* t
 hipError_t launch_loss_bwd(dim3 grid, dim3 block, hipStream_t strm, const float* score, const float* z, const float* mask, const float* t, const float* tot, int B, int T, float bmin, float half_delta, float* ds);
 hipError_t launch_input_pack(dim3 grid, dim3 block, hipStream_t strm, const float* mu, const float* xt, const float* s, int B, int T, int cin, float* out);
 
+// split position reductions (fixed order; part sizes from pos_splits)
+constexpr int kDotBlocks = 256;
+int pos_splits(long npos);
+// part: B * pos_splits(npos) * C floats; out[b][c] (per_b) or out[c]
+hipError_t launch_chan_sums(const float* x, const float* y, int B, int npos, int C, float* part, float* out, int per_b,
+                            int accumulate, hipStream_t strm);
+// part: B * pos_splits(npos) * C * 2 floats; writes p.dgb [B][C][2] and p.gsum [B][8][2]
+hipError_t launch_block_bwd_sums(const BlockBwdParams& p, float* part, hipStream_t strm);
+// part: kDotBlocks doubles
+hipError_t launch_dot_sum(const float* x, const float* y, long n, double* part, float* out, int accumulate,
+                          hipStream_t strm);
+// part: pos_splits(npos) * B * 4096 floats
+hipError_t launch_attn_outer_split(const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int B, int npos,
+                                   float* part, float* R, hipStream_t strm);
+// part: pos_splits(npos) * B * 128 floats
+hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float* c, int csc, int co, int B, int npos,
+                                    float* part, float* S_out, hipStream_t strm);
+
+// fp32-MFMA weight gradient: part holds mwgrad_splits(p) * KS^2 * A * Bc floats (<= kWPartCap, one shared buffer)
+constexpr long kWPartCap = 8L << 20;
+int mwgrad_splits(const WGradParams& p);
+hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm);
+bool train_valu();
+
 hipError_t launch_wgrad(const WGradParams& p, float* part, int splits, float* dw, long sa, long sb, int accumulate,
                         hipStream_t s);
 

@@ -14,10 +14,15 @@
 //
 // This is the correctness-first version: LDS-tiled VALU fp32 (the MFMA versions of gconv / wgrad are the
 // next performance step).
+#include <algorithm>
+#include <cstdlib>
+
 #include "bwd.h"
 #include "common.h"
 
 namespace gt {
+
+static const bool kValu = getenv("GT_TRAIN_VALU") != nullptr;   // A/B switch: the VALU gconv / wgrad kernels
 
 GT_DEV float mish_grad(float x) {   // d/dx x tanh(softplus(x)) (torch softplus threshold 20: x > 20 -> 1)
   if (x > 20.f) return 1.f;
@@ -93,6 +98,181 @@ __global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
       p.out[o] = p.accumulate ? p.out[o] + v : v;
     }
   }
+}
+
+// ---------------------------------------------------------------- mconv: the gconv relation on fp32 MFMA
+// Implicit GEMM on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains): M = 64 output positions of one row, N = 64 output
+// channels, K = input channels x taps in chunks of MC_KC channels staged in LDS (input patch [row][col][c], weights
+// [c][tap][a]); wave w owns the 32 x 32 block (positions (w & 1) * 32, channels (w >> 1) * 32).
+constexpr int MC_KC = 8;
+__global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
+  __shared__ float s_in[4][130][MC_KC + 1];
+  __shared__ float s_w[MC_KC][16][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_tt = (p.To + 63) / 64;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int fo = bid % p.Fo;
+  const int b = bid / p.Fo;
+  const int to0 = tt * 64, a0 = blockIdx.y * 64;
+  const int KK = p.KS * p.KS, PC = 63 * p.S + p.KS;
+  const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int c0 = 0; c0 < p.Cin; c0 += MC_KC) {
+    __syncthreads();
+    for (int i = tid; i < p.KS * PC * MC_KC; i += 256) {
+      const int c = i % MC_KC, col = (i / MC_KC) % PC, row = i / (MC_KC * PC);
+      const int fi = fo * p.S - p.PAD + row, ti = to0 * p.S - p.PAD + col, ci = c0 + c;
+      float v = 0.f;
+      if (fi >= 0 && fi < p.Fi && ti >= 0 && ti < p.Ti && ci < p.Cin) {
+        v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
+        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+      }
+      s_in[row][col][c] = v;
+    }
+    for (int i = tid; i < 64 * MC_KC * KK; i += 256) {
+      const int a = i % 64, k = (i / 64) % KK, c = i / (64 * KK);
+      const int kk = p.flip ? KK - 1 - k : k;
+      s_w[c][k][a] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc + kk] : 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < KK; ++k) {
+      const int kh = k / p.KS, kw = k % p.KS;
+      const float* ip = &s_in[kh][(pb + r) * p.S + kw][hh];
+      const float* wp = &s_w[hh][k][cb + r];
+#pragma unroll
+      for (int cp = 0; cp < MC_KC / 2; ++cp)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ip[2 * cp], wp[2 * cp * 16 * 65], acc, 0, 0, 0);
+    }
+  }
+  const int a = a0 + cb + r;
+  if (a >= p.Cout) return;
+  const float bias = p.bias ? p.bias[a] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int to = to0 + pb + acc_row(j, hh);
+    if (to >= p.To) continue;
+    const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
+    const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
+    const float v = (acc[j] + bias) * om;
+    p.out[o] = p.accumulate ? p.out[o] + v : v;
+  }
+}
+
+// ---------------------------------------------------------------- mwgrad: weight gradients on fp32 MFMA
+// dW(a, b, k) = sum_u P[u][a] Q[v(u, k)][b] as a GEMM with M = 64 a, N = 64 b, K = positions: each workgroup walks
+// its share of 32-position row segments, staging P [32][64] and the KS-row patch of Q the segment's taps touch;
+// wave w owns the 32 x 32 (a, b) block ((w & 1) * 32, (w >> 1) * 32) for the KG taps of its group.
+// part[split][k][a][b] -> mwgrad_reduce_kernel (splits in order).
+constexpr int MW_QC = 68;   // patch columns: 31 * S + KS <= 66
+template <int KG>
+__global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, float* part) {
+  constexpr int NR = KG == 1 ? 1 : (KG == 8 ? 2 : 3);   // patch rows of a tap group (KS = 1 / 4 / 3)
+  __shared__ float s_p[32][65];
+  __shared__ float s_q[NR][MW_QC][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
+  const int split = blockIdx.z % splits, k0 = (blockIdx.z / splits) * KG;
+  const int KK = p.KS * p.KS, kh0 = k0 / p.KS;
+  const int ncol = 31 * p.S + p.KS;
+  const int n_tt = (p.Tu + 31) / 32;
+  const long nseg = (long)p.B * p.Fu * n_tt;
+  const long per = (nseg + splits - 1) / splits;
+  const long s_lo = split * per, s_hi = s_lo + per < nseg ? s_lo + per : nseg;
+  const int ab = (wv & 1) * 32, bb = (wv >> 1) * 32;
+  f32x16 acc[KG];
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[g][j] = 0.f;
+  for (long sg = s_lo; sg < s_hi; ++sg) {
+    const int tt = (int)(sg % n_tt);
+    const int fu = (int)((sg / n_tt) % p.Fu);
+    const int b = (int)(sg / ((long)n_tt * p.Fu));
+    const int t0 = tt * 32;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j, u = i >> 6, a = i & 63;
+      float v = 0.f;
+      if (t0 + u < p.Tu && a0 + a < p.A) {
+        v = p.P[(((long)b * p.Fu + fu) * p.Tu + t0 + u) * p.A + a0 + a];
+        if (p.pmask) v *= mask_at(p.pmask, p.T0, b, t0 + u, p.lvl_p);
+      }
+      s_p[u][a] = v;
+    }
+    for (int i = tid; i < NR * ncol * 64; i += 256) {
+      const int c = i & 63, col = (i >> 6) % ncol, rr = (i >> 6) / ncol;
+      const int fv = fu * p.S - p.PAD + kh0 + rr, tv = t0 * p.S - p.PAD + col;
+      float v = 0.f;
+      if (fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + c < p.Bc) {
+        v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + c];
+        if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
+      }
+      s_q[rr][col][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int k = k0 + g, kh = k / p.KS - kh0, kw = k % p.KS;
+#pragma unroll 4
+      for (int up = 0; up < 16; ++up) {
+        const int u = 2 * up + hh;
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(s_p[u][ab + r], s_q[kh][u * p.S + kw][bb + r], acc[g], 0, 0, 0);
+      }
+    }
+  }
+  const int bc = b0 + bb + r;
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    const int k = k0 + g;
+    if (k >= KK) break;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int a = a0 + ab + acc_row(j, hh);
+      if (a < p.A && bc < p.Bc) part[(((long)split * KK + k) * p.A + a) * p.Bc + bc] = acc[g][j];
+    }
+  }
+}
+
+__global__ void mwgrad_reduce_kernel(const float* part, int splits, int A, int Bc, int KK, long sa, long sb, float* dw,
+                                     int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)KK * A * Bc;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int q = 0; q < splits; ++q) s += part[(long)q * n + i];
+  const int bc = (int)(i % Bc), a = (int)((i / Bc) % A), k = (int)(i / ((long)A * Bc));
+  float* d = dw + a * sa + bc * sb + k;
+  *d = accumulate ? *d + s : s;
+}
+
+int mwgrad_splits(const WGradParams& p) {
+  const int groups = p.KS == 4 ? 2 : 1;
+  const long tiles = (long)((p.A + 63) / 64) * ((p.Bc + 63) / 64) * groups;
+  const long nseg = (long)p.B * p.Fu * ((p.Tu + 31) / 32);
+  long s = std::max<long>(1, 1024 / tiles);
+  s = std::min<long>(s, nseg);
+  s = std::min<long>(s, kWPartCap / ((long)p.KS * p.KS * p.A * p.Bc));
+  return (int)std::max<long>(1, s);
+}
+
+bool train_valu() { return kValu; }
+
+hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm) {
+  if (!(p.KS == 1 || p.KS == 3 || p.KS == 4) || 31 * p.S + p.KS > MW_QC) return hipErrorInvalidValue;
+  const int splits = mwgrad_splits(p);
+  const int groups = p.KS == 4 ? 2 : 1;
+  const dim3 grid((p.A + 63) / 64, (p.Bc + 63) / 64, splits * groups);
+  if (p.KS == 1) hipLaunchKernelGGL(mwgrad_kernel<1>, grid, dim3(256), 0, strm, p, splits, part);
+  else if (p.KS == 3) hipLaunchKernelGGL(mwgrad_kernel<9>, grid, dim3(256), 0, strm, p, splits, part);
+  else hipLaunchKernelGGL(mwgrad_kernel<8>, grid, dim3(256), 0, strm, p, splits, part);
+  const long n = (long)p.KS * p.KS * p.A * p.Bc;
+  hipLaunchKernelGGL(mwgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, strm, part, splits, p.A,
+                     p.Bc, p.KS * p.KS, sa, sb, dw, accumulate);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- tconv: out[v][b] = sum_{u*S-PAD+k = v} W in[u]
@@ -540,7 +720,8 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   if (p.KS > 4 || p.S > 2) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
   if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
+  else if (kValu) hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(mconv_kernel, grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -593,6 +774,193 @@ __global__ void mask_sum_kernel(const float* mask, long n, float* out) {
     for (int i = 0; i < 256; ++i) t += s[i];
     out[0] = (float)t;
   }
+}
+
+// ---------------------------------------------------------------- split reductions over the positions
+// Every position sum below runs in two fixed-order levels: S splits of each utterance's positions (pos_splits), then
+// the splits in order (sum_splits_kernel). Deterministic, and the grid fills the chip at every level.
+int pos_splits(long npos) { return (int)std::max<long>(1, std::min<long>(64, npos / 512)); }
+
+GT_DEV void split_range(long n, int S, int s, long* lo, long* hi) {
+  const long per = (n + S - 1) / S;
+  *lo = (long)s * per;
+  *hi = *lo + per < n ? *lo + per : n;
+}
+
+// out[g][j] (+)= sum_q part[g][q][j], q ascending
+__global__ void sum_splits_kernel(const float* part, int G, int S, long n, float* out, int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)G * n) return;
+  const long g = i / n, j = i % n;
+  float s = 0.f;
+  for (int q = 0; q < S; ++q) s += part[(g * S + q) * n + j];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+// part[b][s][c] = sum over split s of utterance b's positions of x[b][pos][c] (* y): grid (C/64, S, B), 64 channels
+// x 4 position lanes per workgroup (each wave reads 64 consecutive channels of one position)
+__global__ __launch_bounds__(256) void chan_partial_kernel(const float* x, const float* y, int npos, int C, float* part) {
+  __shared__ float s_r[4][64];
+  const int tid = threadIdx.x, cl = tid & 63, pl = tid >> 6;
+  const int c = blockIdx.x * 64 + cl, s = blockIdx.y, b = blockIdx.z, S = gridDim.y;
+  long lo, hi;
+  split_range(npos, S, s, &lo, &hi);
+  float acc = 0.f;
+  if (c < C) {
+    const float* xb = x + (long)b * npos * C + c;
+    const float* yb = y ? y + (long)b * npos * C + c : nullptr;
+    for (long i = lo + pl; i < hi; i += 4) acc += yb ? xb[i * C] * yb[i * C] : xb[i * C];
+  }
+  s_r[pl][cl] = acc;
+  __syncthreads();
+  if (pl == 0 && c < C) part[((long)b * S + s) * C + c] = ((s_r[0][cl] + s_r[1][cl]) + s_r[2][cl]) + s_r[3][cl];
+}
+
+// Block backward sums: part[b][s][c] = (sum dn xhat, sum dn) over split s (dn = dA m mish'(n), as block_bwd_apply)
+__global__ __launch_bounds__(256) void block_bwd_partial_kernel(BlockBwdParams p, float* part) {
+  __shared__ float s_r[2][4][64];
+  const int tid = threadIdx.x, cl = tid & 63, pl = tid >> 6;
+  const int c = blockIdx.x * 64 + cl, s = blockIdx.y, b = blockIdx.z, S = gridDim.y;
+  long lo, hi;
+  split_range(p.npos, S, s, &lo, &hi);
+  float a1 = 0.f, a2 = 0.f;
+  if (c < p.C) {
+    const int g = c / (p.C / 8);
+    const float mean = p.stats[(b * 8 + g) * 2], rstd = p.stats[(b * 8 + g) * 2 + 1];
+    const float gm = p.gamma[c], bt = p.beta[c];
+    for (long pos = lo + pl; pos < hi; pos += 4) {
+      const long o = ((long)b * p.npos + pos) * p.C + c;
+      const float xh = (p.h[o] - mean) * rstd;
+      const float m = mask_at(p.mask, p.T0, b, (int)(pos % p.T), p.lvl);
+      const float dn = p.dA[o] * m * mish_grad(xh * gm + bt);
+      a1 += dn * xh;
+      a2 += dn;
+    }
+  }
+  s_r[0][pl][cl] = a1;
+  s_r[1][pl][cl] = a2;
+  __syncthreads();
+  if (pl == 0 && c < p.C) {
+    float* o = part + (((long)b * S + s) * p.C + c) * 2;
+    o[0] = ((s_r[0][0][cl] + s_r[0][1][cl]) + s_r[0][2][cl]) + s_r[0][3][cl];
+    o[1] = ((s_r[1][0][cl] + s_r[1][1][cl]) + s_r[1][2][cl]) + s_r[1][3][cl];
+  }
+}
+
+// per utterance (one workgroup, C <= 256): dgb[b][c] = splits summed in order (fp64); gsum[b][g] = (S1, S2) with
+// S1 = sum_c gamma_c sum dn = sum dn gamma, S2 = sum_c gamma_c sum dn xhat
+__global__ __launch_bounds__(256) void block_bwd_final_kernel(BlockBwdParams p, const float* part, int S) {
+  __shared__ double s_g[2][256];
+  const int b = blockIdx.x, c = threadIdx.x;
+  if (c < p.C) {
+    double d1 = 0.0, d2 = 0.0;
+    for (int q = 0; q < S; ++q) {
+      const float* o = part + (((long)b * S + q) * p.C + c) * 2;
+      d1 += (double)o[0];
+      d2 += (double)o[1];
+    }
+    p.dgb[((long)b * p.C + c) * 2] = (float)d1;
+    p.dgb[((long)b * p.C + c) * 2 + 1] = (float)d2;
+    s_g[0][c] = (double)p.gamma[c] * d2;
+    s_g[1][c] = (double)p.gamma[c] * d1;
+  }
+  __syncthreads();
+  if (c < 8) {
+    const int cg = p.C / 8;
+    double S1 = 0.0, S2 = 0.0;
+    for (int i = 0; i < cg; ++i) { S1 += s_g[0][c * cg + i]; S2 += s_g[1][c * cg + i]; }
+    p.gsum[(b * 8 + c) * 2] = (float)S1;
+    p.gsum[(b * 8 + c) * 2 + 1] = (float)S2;
+  }
+}
+
+// dot product: 256 workgroups of fp64 partials, then one thread in order
+__global__ __launch_bounds__(256) void dot_partial_kernel(const float* x, const float* y, long n, double* part) {
+  __shared__ double s[256];
+  long lo, hi;
+  split_range(n, gridDim.x, blockIdx.x, &lo, &hi);
+  double a = 0.0;
+  for (long i = lo + threadIdx.x; i < hi; i += 256) a += (double)x[i] * (double)y[i];
+  s[threadIdx.x] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < 256; ++i) t += s[i];
+    part[blockIdx.x] = t;
+  }
+}
+__global__ void dot_final_kernel(const double* part, int nblk, float* out, int accumulate) {
+  if (threadIdx.x != 0) return;
+  double t = 0.0;
+  for (int i = 0; i < nblk; ++i) t += part[i];
+  out[0] = accumulate ? out[0] + (float)t : (float)t;
+}
+
+// attn_outer over a split of the positions: part[s][b][h][d][e]   (grid (B, 4, S), 1024 threads)
+__global__ __launch_bounds__(1024) void attn_outer_split_kernel(const float* X1, int cs1, int x1o, const float* X2,
+                                                                int cs2, int x2o, int npos, float* part) {
+  const int b = blockIdx.x, h = blockIdx.y, s = blockIdx.z, B = gridDim.x, d = threadIdx.x >> 5, e = threadIdx.x & 31;
+  long lo, hi;
+  split_range(npos, gridDim.z, s, &lo, &hi);
+  const float* p1 = X1 + (long)b * npos * cs1 + x1o + 32 * h + d;
+  const float* p2 = X2 + (long)b * npos * cs2 + x2o + 32 * h + e;
+  float acc = 0.f;
+  for (long i = lo; i < hi; ++i) acc = fmaf(p1[i * cs1], p2[i * cs2], acc);
+  part[((((long)s * B + b) * 4 + h) * 32 + d) * 32 + e] = acc;
+}
+
+// attn_rowdot over a split: part[s][b][r]   (grid (B, S), 128 threads)
+__global__ void attn_rowdot_split_kernel(const float* a, int csa, int ao, const float* c, int csc, int co, int npos,
+                                         float* part) {
+  const int b = blockIdx.x, s = blockIdx.y, B = gridDim.x, r = threadIdx.x;
+  long lo, hi;
+  split_range(npos, gridDim.y, s, &lo, &hi);
+  float acc = 0.f;
+  for (long i = lo; i < hi; ++i)
+    acc = fmaf(a[((long)b * npos + i) * csa + ao + r], c[((long)b * npos + i) * csc + co + r], acc);
+  part[((long)s * B + b) * 128 + r] = acc;
+}
+
+static hipError_t sum_splits(const float* part, int G, int S, long n, float* out, int accumulate, hipStream_t strm) {
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)(((long)G * n + 255) / 256)), dim3(256), 0, strm, part, G, S, n,
+                     out, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_chan_sums(const float* x, const float* y, int B, int npos, int C, float* part, float* out, int per_b,
+                            int accumulate, hipStream_t strm) {
+  const int S = pos_splits(npos);
+  hipLaunchKernelGGL(chan_partial_kernel, dim3((C + 63) / 64, S, B), dim3(256), 0, strm, x, y, npos, C, part);
+  return per_b ? sum_splits(part, B, S, C, out, accumulate, strm) : sum_splits(part, 1, B * S, C, out, accumulate, strm);
+}
+
+hipError_t launch_block_bwd_sums(const BlockBwdParams& p, float* part, hipStream_t strm) {
+  if (p.C > 256) return hipErrorInvalidValue;
+  const int S = pos_splits(p.npos);
+  hipLaunchKernelGGL(block_bwd_partial_kernel, dim3((p.C + 63) / 64, S, p.B), dim3(256), 0, strm, p, part);
+  hipLaunchKernelGGL(block_bwd_final_kernel, dim3(p.B), dim3(256), 0, strm, p, part, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_dot_sum(const float* x, const float* y, long n, double* part, float* out, int accumulate,
+                          hipStream_t strm) {
+  hipLaunchKernelGGL(dot_partial_kernel, dim3(kDotBlocks), dim3(256), 0, strm, x, y, n, part);
+  hipLaunchKernelGGL(dot_final_kernel, dim3(1), dim3(64), 0, strm, part, kDotBlocks, out, accumulate);
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_outer_split(const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int B, int npos,
+                                   float* part, float* R, hipStream_t strm) {
+  const int S = pos_splits(npos);
+  hipLaunchKernelGGL(attn_outer_split_kernel, dim3(B, 4, S), dim3(1024), 0, strm, X1, cs1, x1o, X2, cs2, x2o, npos, part);
+  return sum_splits(part, 1, S, (long)B * 4096, R, 0, strm);
+}
+
+hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float* c, int csc, int co, int B, int npos,
+                                    float* part, float* S_out, hipStream_t strm) {
+  const int S = pos_splits(npos);
+  hipLaunchKernelGGL(attn_rowdot_split_kernel, dim3(B, S), dim3(128), 0, strm, a, csa, ao, c, csc, co, npos, part);
+  return sum_splits(part, 1, S, (long)B * 128, S_out, 0, strm);
 }
 
 // ---- launchers

@@ -7,6 +7,7 @@
 // sizes the workspace (gt_train_workspace_bytes).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -104,7 +105,7 @@ struct Trainer {
              int PAD, float* dw, long sa, long sb, int acc, int line = __builtin_LINE()) {
     const long nU = (long)B * L(l_u).F * L(l_u).T;
     const int splits = (int)std::max<long>(1, std::min<long>(256, nU / 512));
-    float* part = A.take((size_t)splits * Ad * Bd * KS * KS);
+    float* part = train_valu() ? A.take((size_t)splits * Ad * Bd * KS * KS) : wpart;
     if (!run) return;
     need(Pt, nU * Ad, "wgrad P", line);
     need(Qt, (long)B * L(l_v).F * L(l_v).T * Bd, "wgrad Q", line);
@@ -114,17 +115,18 @@ struct Trainer {
     p.B = B; p.Fu = L(l_u).F; p.Tu = L(l_u).T; p.A = Ad; p.Fv = L(l_v).F; p.Tv = L(l_v).T; p.Bc = Bd;
     p.KS = KS; p.S = S; p.PAD = PAD; p.P = Pt; p.pmask = pmask ? mask : nullptr; p.lvl_p = l_u;
     p.Q = Qt; p.qmask = qmask ? mask : nullptr; p.lvl_q = l_v; p.T0 = T;
-    chk(launch_wgrad(p, part, splits, dw, sa, sb, acc, s), line);
+    if (train_valu()) chk(launch_wgrad(p, part, splits, dw, sa, sb, acc, s), line);
+    else chk(launch_mwgrad(p, part, dw, sa, sb, acc, s), line);
   }
   // out[c] (+)= sum_{b, pos} x   (bias gradients): per-utterance sums, then over the batch in order
   void chansum(const float* x, int l, int C, float* out, int acc, int line = __builtin_LINE()) {
-    float* tmp = A.take((size_t)B * C);
+    const int npos = L(l).F * L(l).T;
+    float* part = A.take((size_t)B * pos_splits(npos) * C);
     if (!run) return;
-    need(x, (long)B * L(l).F * L(l).T * C, "chansum x", line);
+    need(x, (long)B * npos * C, "chansum x", line);
     need(out, C, "chansum out", line);
     if (dry) return;
-    chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, x, nullptr, L(l).F * L(l).T, C, tmp, 0), line);
-    chk(launch_colsum(dim3((C + 255) / 256), dim3(256), s, tmp, B, C, out, acc), line);
+    chk(launch_chan_sums(x, nullptr, B, npos, C, part, out, 0, acc, s), line);
   }
   void ew(const float* x, int xcs, int xc0, float alpha, const float* x2, float alpha2, int l, int C, bool m, float* y,
           int ycs, int yc0, int acc, int line = __builtin_LINE()) {
@@ -166,6 +168,7 @@ struct Trainer {
     float* dh = A.take((size_t)B * L(l).F * L(l).T * C);
     float* tw = A.take((size_t)B * C);
     float* tb2 = A.take((size_t)B * C);
+    float* part = A.take((size_t)B * pos_splits((long)L(l).F * L(l).T) * C * 2);
     if (!run) return dh;
     {
       const long n = (long)B * L(l).F * L(l).T * C;
@@ -179,7 +182,7 @@ struct Trainer {
     if (dry) return dh;
     BlockBwdParams p = bp(l, C, h, st, gn);
     p.dA = dAv; p.gsum = gsum; p.dgb = dgb; p.dh = dh;
-    chk(launch_block_bwd_reduce(dim3(B, 8), dim3(256), s, p), line);
+    chk(launch_block_bwd_sums(p, part, s), line);
     chk(launch_block_bwd_apply(g1((long)B * p.npos * C), dim3(256), s, p), line);
     chk(launch_colsum_strided(gn, dgb, C, tw, tb2), line);   // dgamma, dbeta = sums over the batch
     return dh;
@@ -261,10 +264,11 @@ struct Trainer {
     a.o = A.take((size_t)B * np * 128);
     a.z = A.take((size_t)B * np * C);
     a.y = A.take((size_t)B * np * C);
+    float* opart = A.take((size_t)pos_splits(np) * B * 4096);
     if (live()) {
       chk(launch_attn_kstats(dim3(B, 128), dim3(256), s, a.qkv, (int)np, st));
       chk(launch_attn_ksoftmax(g1((long)B * np * 128), dim3(256), s, a.qkv, B, (int)np, st));
-      chk(launch_attn_outer(dim3(B, 4), dim3(1024), s, a.qkv, 384, 128, a.qkv, 384, 256, (int)np, a.ctx));
+      chk(launch_attn_outer_split(a.qkv, 384, 128, a.qkv, 384, 256, B, (int)np, opart, a.ctx, s));
       chk(launch_attn_headmm(g1((long)B * np * 128), dim3(256), s, a.ctx, 0, a.qkv, 384, 0, B, (int)np, a.o, 128, 0, 0));
     }
     gconv(a.o, 128, l, false, P(k + "fn.fn.to_out.weight"), 128, 1, 1, 1, 0, 0, P(k + "fn.fn.to_out.bias"), a.z, C, l,
@@ -276,7 +280,9 @@ struct Trainer {
   }
 
   // ------------------------------------------------------------ forward (oracle estimator order)
+  float* wpart = nullptr;   // weight-gradient partials, one buffer reused by every wgrad (stream-ordered)
   void forward(const float* mu, const float* xt, const float* spk, const float* t) {
+    wpart = A.take((size_t)kWPartCap);
     // time embedding (diffusion.py:113-125, 143-144, 177-178) and every ResnetBlock's mlp (64-65, 76)
     temb_s = A.take((size_t)B * 64); temb_pre0 = A.take((size_t)B * 256); temb_h = A.take((size_t)B * 256);
     temb = A.take((size_t)B * 64); temb_m = A.take((size_t)B * 64);
@@ -377,7 +383,11 @@ struct Trainer {
     chansum(dh2, l, C, G(k + "block2.block.0.bias"), 1);
     float* du = A.take((size_t)B * L(l).F * L(l).T * C);
     gconv(dh2, C, l, false, P(k + "block2.block.0.weight"), 9, (long)C * 9, 3, 1, 1, 1, nullptr, du, C, l, true, C, 0, 0);
-    if (live()) chk(launch_bsum(dim3(B, (C + 255) / 256), dim3(256), s, du, nullptr, L(l).F * L(l).T, C, dtb[b.r], 0));
+    {
+      const int npos = L(l).F * L(l).T;
+      float* part = A.take((size_t)B * pos_splits(npos) * C);
+      if (live()) chk(launch_chan_sums(du, nullptr, B, npos, C, part, dtb[b.r], 1, 0, s));
+    }
     // block1
     float* dh1 = block_bwd(l, C, du, b.h1, b.st1, k + "block1.block.1");
     const float* w1 = P(k + "block1.block.0.weight");
@@ -397,7 +407,8 @@ struct Trainer {
     const long np = (long)L(l).F * L(l).T, n = (long)B * np;
     const float g = gt_internal_host_scalar(d, k + "fn.g");
     ew(dy, C, 0, 1.f, nullptr, 0.f, l, C, false, dx, C, 0, 1);                 // residual
-    if (live()) chk(launch_dot(dim3(1), dim3(256), s, dy, a.z, n * C, G(k + "fn.g"), 1));   // d g = sum dy . z
+    double* dpart = reinterpret_cast<double*>(A.take(2 * kDotBlocks));
+    if (live()) chk(launch_dot_sum(dy, a.z, n * C, dpart, G(k + "fn.g"), 1, s));   // d g = sum dy . z
     float* dz = A.take((size_t)n * C);
     ew(dy, C, 0, g, nullptr, 0.f, l, C, false, dz, C, 0, 0);
     wgrad(dz, C, l, false, a.o, 128, l, false, 1, 1, 0, G(k + "fn.fn.to_out.weight"), 128, 1, 1);
@@ -407,12 +418,14 @@ struct Trainer {
     float* dctx = A.take((size_t)B * 4096);
     float* dqkv = A.take((size_t)n * 384);
     float* S = A.take((size_t)B * 128);
+    float* opart = A.take((size_t)pos_splits(np) * B * 4096);
+    float* rpart = A.take((size_t)pos_splits(np) * B * 128);
     if (live()) {
-      chk(launch_attn_outer(dim3(B, 4), dim3(1024), s, a.qkv, 384, 0, dO, 128, 0, (int)np, dctx));      // q do^T
+      chk(launch_attn_outer_split(a.qkv, 384, 0, dO, 128, 0, B, (int)np, opart, dctx, s));      // q do^T
       chk(launch_attn_headmm(g1(n * 128), dim3(256), s, a.ctx, 1, dO, 128, 0, B, (int)np, dqkv, 384, 0, 0));     // dq
       chk(launch_attn_headmm(g1(n * 128), dim3(256), s, dctx, 1, a.qkv, 384, 256, B, (int)np, dqkv, 384, 128, 0));  // dks
       chk(launch_attn_headmm(g1(n * 128), dim3(256), s, dctx, 0, a.qkv, 384, 128, B, (int)np, dqkv, 384, 256, 0));  // dv
-      chk(launch_attn_rowdot(dim3(B), dim3(128), s, a.qkv, 384, 128, dqkv, 384, 128, (int)np, S));
+      chk(launch_attn_rowdot_split(a.qkv, 384, 128, dqkv, 384, 128, B, (int)np, rpart, S, s));
       chk(launch_attn_ksoftmax_bwd(g1(n * 128), dim3(256), s, a.qkv, dqkv, B, (int)np, S));
     }
     wgrad(dqkv, 384, l, false, a.x, C, l, false, 1, 1, 0, G(k + "fn.fn.to_qkv.weight"), C, 1, 1);

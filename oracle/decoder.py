@@ -31,7 +31,7 @@ def sinusoidal_pos_emb(t, dim, scale):
     """``SinusoidalPosEmb`` diffusion.py:113-125."""
     half = dim // 2
     emb = math.log(10000) / (half - 1)
-    emb = torch.exp(torch.arange(half, dtype=torch.float32) * -emb).to(t.dtype)
+    emb = torch.exp(torch.arange(half, dtype=torch.float32) * -emb).to(t.device, t.dtype)
     emb = scale * t.unsqueeze(1) * emb.unsqueeze(0)
     return torch.cat((emb.sin(), emb.cos()), dim=-1)
 

@@ -168,3 +168,48 @@ def test_log_prior_alignment(B, Tx, Ty, mas_oracle):
     path_ref_lp, _ = mas_oracle(ref_lp, tx, ty)                 # ... and on the oracle's own log-prior
     agree = float((path_ref_lp == path_same_lp).mean())
     report(f"alignment B={B} Tx={Tx} Ty={Ty} path agreement with the oracle log-prior", 1.0 - agree, 1e-3)
+
+
+def test_training_step_speed_vs_torch_eager():
+    """Report (no gate) the training-step time at the reference's training shape (params.py: batch 16, out_size
+    2 s = 172 frames) against torch eager autograd of the same loss on the same GPU (MIOpen convs, fp32)."""
+    import time
+    from oracle import decoder as odec
+    B, T = 16, 172
+    x0, mu, mask, z, t, _ = _data(21, B, T, None)
+    dec, sd = make_decoder(1, 0, torch.float32)
+    c = lambda a: torch.from_numpy(a).cuda()
+    args = (c(x0), c(mask), c(mu), c(t))
+    zz = c(z)
+
+    def ours():
+        dec.zero_grad(set_to_none=True)
+        loss, _ = dec.loss_t(*args, z=zz)
+        loss.backward()
+
+    p = {k: v.cuda().requires_grad_() for k, v in odec.to_torch_params(sd).items()}
+    x0_t, mask_t, mu_t, t_t = args
+
+    def eager():
+        for v in p.values():
+            v.grad = None
+        xt, zm = odec.forward_diffusion(x0_t, mask_t, mu_t, t_t, zz)
+        cum = odec.get_noise(t_t[:, None, None], 0.05, 20.0, cumulative=True)
+        ne = odec.estimator(p, xt, mask_t, mu_t, t_t) * torch.sqrt(1.0 - torch.exp(-cum))
+        loss = torch.sum((ne + zm) ** 2) / (torch.sum(mask_t) * 80)
+        loss.backward()
+
+    def timed(fn, n=5):
+        fn(); fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
+
+    ms_ours, ms_eager = timed(ours), timed(eager)
+    frames = B * T
+    report(f"training step B={B} T={T}: ours {ms_ours:.2f} ms ({frames / ms_ours * 1e3:.0f} frames/s), torch eager "
+           f"{ms_eager:.2f} ms ({frames / ms_eager * 1e3:.0f} frames/s); ratio eager/ours", ms_eager / ms_ours, 0.0,
+           gate=False, ms_ours=ms_ours, ms_eager=ms_eager)
