@@ -74,6 +74,13 @@ int pos_splits(long npos);
 // part: B * pos_splits(npos) * C floats; out[b][c] (per_b) or out[c]
 hipError_t launch_chan_sums(const float* x, const float* y, int B, int npos, int C, float* part, float* out, int per_b,
                             int accumulate, hipStream_t strm);
+hipError_t launch_chan_sums_strided(const float* x, int xcs, int xo, const float* y, int ycs, int yo, int B, int npos,
+                                    int C, float* part, float* out, int per_b, int accumulate, hipStream_t strm);
+// GroupNorm (mean, rstd) per (b, group) [B][8][2]; part: B * 8 * gn_splits(npos) * 2 doubles
+int gn_splits(long npos);
+hipError_t launch_gn_stats_split(const float* h, int B, int npos, int C, double* part, float* stats, hipStream_t strm);
+hipError_t launch_attn_headmm_mfma(const float* M, int trans, const float* X, int csx, int xo, int B, int npos, float* Y,
+                                   int csy, int yo, int accumulate, hipStream_t strm);
 // part: B * pos_splits(npos) * C * 2 floats; writes p.dgb [B][C][2] and p.gsum [B][8][2]
 hipError_t launch_block_bwd_sums(const BlockBwdParams& p, float* part, hipStream_t strm);
 // part: kDotBlocks doubles
@@ -82,7 +89,7 @@ hipError_t launch_dot_sum(const float* x, const float* y, long n, double* part, 
 // part: pos_splits(npos) * B * 4096 floats
 hipError_t launch_attn_outer_split(const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int B, int npos,
                                    float* part, float* R, hipStream_t strm);
-// part: pos_splits(npos) * B * 128 floats
+// part: B * pos_splits(npos) * 128 floats
 hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float* c, int csc, int co, int B, int npos,
                                     float* part, float* S_out, hipStream_t strm);
 

@@ -24,14 +24,25 @@ namespace gt {
 
 static const bool kValu = getenv("GT_TRAIN_VALU") != nullptr;   // A/B switch: the VALU gconv / wgrad kernels
 
-GT_DEV float mish_grad(float x) {   // d/dx x tanh(softplus(x)) (torch softplus threshold 20: x > 20 -> 1)
+// tanh(softplus(x)) = n / (n + 2) with n = e (e + 2), e = exp(x): one exponential per element (softplus threshold
+// 20 as torch: x > 20 -> mish = x, mish' = 1)
+GT_DEV float mish_grad(float x) {   // d/dx x tanh(softplus(x)) = th + x (1 - th^2) sigmoid(x)
   if (x > 20.f) return 1.f;
-  const float sp = log1pf(expf(x));
-  const float th = tanhf(sp);
-  const float sg = 1.f / (1.f + expf(-x));
+  const float e = __expf(x), n = e * (e + 2.f);
+  const float th = __fdividef(n, n + 2.f), sg = __fdividef(e, 1.f + e);
   return th + x * (1.f - th * th) * sg;
 }
-GT_DEV float mish_f(float x) { return x > 20.f ? x : x * tanhf(log1pf(expf(x))); }
+GT_DEV float mish_f(float x) {
+  if (x > 20.f) return x;
+  const float e = __expf(x), n = e * (e + 2.f);
+  return x * __fdividef(n, n + 2.f);
+}
+
+GT_DEV void split_range(long n, int S, int s, long* lo, long* hi) {
+  const long per = (n + S - 1) / S;
+  *lo = (long)s * per;
+  *hi = *lo + per < n ? *lo + per : n;
+}
 
 // ---------------------------------------------------------------- gconv: 64 output positions (one row) x 64
 // output channels per workgroup, 8-channel input chunks staged in LDS; thread = 4 positions x 4 channels
@@ -105,9 +116,12 @@ __global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
 // channels, K = input channels x taps in chunks of MC_KC channels staged in LDS (input patch [row][col][c], weights
 // [c][tap][a]); wave w owns the 32 x 32 block (positions (w & 1) * 32, channels (w >> 1) * 32).
 constexpr int MC_KC = 8;
+template <int KS, int SE>
 __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
-  __shared__ float s_in[4][130][MC_KC + 1];
-  __shared__ float s_w[MC_KC][16][65];
+  constexpr int KK = KS * KS, PC = 63 * SE + KS, NCOL = (PC + 31) / 32;
+  constexpr int NW = 64 * MC_KC * KK, NWJ = (NW + 255) / 256;
+  __shared__ float s_in[KS][PC][MC_KC + 1];
+  __shared__ float s_w[MC_KC][KK][65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int n_tt = (p.To + 63) / 64;
   int bid = blockIdx.x;
@@ -115,36 +129,80 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   const int fo = bid % p.Fo;
   const int b = bid / p.Fo;
   const int to0 = tt * 64, a0 = blockIdx.y * 64;
-  const int KK = p.KS * p.KS, PC = 63 * p.S + p.KS;
+  // transposed relation (ConvTranspose2d, strided-conv dgrad): a stride-1 conv over the S-dilated input with the
+  // taps flipped and padding KS - 1 - PAD
+  const bool dil = p.transposed != 0;
+  const int pad = dil ? KS - 1 - p.PAD : p.PAD;
+  const bool flip = dil ? !p.flip : p.flip != 0;
+  const bool a_fast = p.wsa < p.wsc;   // stage weights along their contiguous axis
   const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
+  const int ic = tid & 7, iq = tid >> 3;   // input staging: channel, column lane (32 columns per pass)
+  float rin[KS][NCOL], rw[NWJ];
+  auto load = [&](int c0) {   // next chunk into registers (in flight during the MFMAs of the current one)
+    const int ci = c0 + ic;
+#pragma unroll
+    for (int row = 0; row < KS; ++row) {
+      const int fd = fo * SE - pad + row;
+#pragma unroll
+      for (int q = 0; q < NCOL; ++q) {
+        const int col = iq + 32 * q;
+        const int td = to0 * SE - pad + col;
+        float v = 0.f;
+        bool ok = col < PC && fd >= 0 && td >= 0 && ci < p.Cin;
+        int fi = fd, ti = td;
+        if (dil) { ok = ok && fd % p.S == 0 && td % p.S == 0; fi = fd / p.S; ti = td / p.S; }
+        if (ok && fi < p.Fi && ti < p.Ti) {
+          v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
+          if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+        }
+        rin[row][q] = v;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j) {
+      const int i = tid + 256 * j;
+      float v = 0.f;
+      if (i < NW) {
+        const int k = i % KK, rest = i / KK;
+        const int a = a_fast ? rest % 64 : rest / MC_KC, c = a_fast ? rest / 64 : rest % MC_KC;
+        const int kk = flip ? KK - 1 - k : k;
+        if (a0 + a < p.Cout && c0 + c < p.Cin) v = p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc + kk];
+      }
+      rw[j] = v;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int row = 0; row < KS; ++row)
+#pragma unroll
+      for (int q = 0; q < NCOL; ++q)
+        if (iq + 32 * q < PC) s_in[row][iq + 32 * q][ic] = rin[row][q];
+#pragma unroll
+    for (int j = 0; j < NWJ; ++j) {
+      const int i = tid + 256 * j;
+      if (i < NW) {
+        const int k = i % KK, rest = i / KK;
+        const int a = a_fast ? rest % 64 : rest / MC_KC, c = a_fast ? rest / 64 : rest % MC_KC;
+        s_w[c][k][a] = rw[j];
+      }
+    }
+  };
   f32x16 acc;
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  load(0);
   for (int c0 = 0; c0 < p.Cin; c0 += MC_KC) {
     __syncthreads();
-    for (int i = tid; i < p.KS * PC * MC_KC; i += 256) {
-      const int c = i % MC_KC, col = (i / MC_KC) % PC, row = i / (MC_KC * PC);
-      const int fi = fo * p.S - p.PAD + row, ti = to0 * p.S - p.PAD + col, ci = c0 + c;
-      float v = 0.f;
-      if (fi >= 0 && fi < p.Fi && ti >= 0 && ti < p.Ti && ci < p.Cin) {
-        v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
-        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
-      }
-      s_in[row][col][c] = v;
-    }
-    for (int i = tid; i < 64 * MC_KC * KK; i += 256) {
-      const int a = i % 64, k = (i / 64) % KK, c = i / (64 * KK);
-      const int kk = p.flip ? KK - 1 - k : k;
-      s_w[c][k][a] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc + kk] : 0.f;
-    }
+    store();
     __syncthreads();
+    if (c0 + MC_KC < p.Cin) load(c0 + MC_KC);
+#pragma unroll
     for (int k = 0; k < KK; ++k) {
-      const int kh = k / p.KS, kw = k % p.KS;
-      const float* ip = &s_in[kh][(pb + r) * p.S + kw][hh];
-      const float* wp = &s_w[hh][k][cb + r];
+      const int kh = k / KS, kw = k % KS;
 #pragma unroll
       for (int cp = 0; cp < MC_KC / 2; ++cp)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ip[2 * cp], wp[2 * cp * 16 * 65], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[kh][(pb + r) * SE + kw][2 * cp + hh], s_w[2 * cp + hh][k][cb + r],
+                                                   acc, 0, 0, 0);
     }
   }
   const int a = a0 + cb + r;
@@ -163,20 +221,22 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
 
 // ---------------------------------------------------------------- mwgrad: weight gradients on fp32 MFMA
 // dW(a, b, k) = sum_u P[u][a] Q[v(u, k)][b] as a GEMM with M = 64 a, N = 64 b, K = positions: each workgroup walks
-// its share of 32-position row segments, staging P [32][64] and the KS-row patch of Q the segment's taps touch;
-// wave w owns the 32 x 32 (a, b) block ((w & 1) * 32, (w >> 1) * 32) for the KG taps of its group.
-// part[split][k][a][b] -> mwgrad_reduce_kernel (splits in order).
-constexpr int MW_QC = 68;   // patch columns: 31 * S + KS <= 66
-template <int KG>
+// its share of 32-position row segments, staging P [32][64] and the KS-row patch of Q the segment's taps touch (the
+// next segment's loads in flight during the current MFMAs); wave w owns the 32 x 32 (a, b) block
+// ((w & 1) * 32, (w >> 1) * 32) for the KG taps of its group. LDS row strides put the two half-waves' rows 32 banks
+// apart. part[split][k][a][b] -> mwgrad_reduce_kernel (splits in order).
+template <int KS, int S>
 __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, float* part) {
-  constexpr int NR = KG == 1 ? 1 : (KG == 8 ? 2 : 3);   // patch rows of a tap group (KS = 1 / 4 / 3)
-  __shared__ float s_p[32][65];
-  __shared__ float s_q[NR][MW_QC][65];
+  constexpr int KG = KS == 4 ? 8 : KS * KS, NR = KG / KS;                    // taps / patch rows of a group
+  constexpr int NCOL = 31 * S + KS, QS = S == 1 ? 96 : 80, PS = 96;          // patch columns, LDS row strides
+  constexpr int NQ = (NCOL + 3) / 4;                                         // columns per staging lane
+  __shared__ float s_p[32 * PS];
+  __shared__ float s_q[NR * NCOL * QS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int sc = tid & 63, sl = tid >> 6;   // staging: channel, row lane
   const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
   const int split = blockIdx.z % splits, k0 = (blockIdx.z / splits) * KG;
-  const int KK = p.KS * p.KS, kh0 = k0 / p.KS;
-  const int ncol = 31 * p.S + p.KS;
+  const int kh0 = k0 / KS;
   const int n_tt = (p.Tu + 31) / 32;
   const long nseg = (long)p.B * p.Fu * n_tt;
   const long per = (nseg + splits - 1) / splits;
@@ -187,52 +247,69 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
   for (int g = 0; g < KG; ++g)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[g][j] = 0.f;
-  for (long sg = s_lo; sg < s_hi; ++sg) {
+  float rp[8], rq[NR][NQ];
+  auto load = [&](long sg) {
     const int tt = (int)(sg % n_tt);
     const int fu = (int)((sg / n_tt) % p.Fu);
     const int b = (int)(sg / ((long)n_tt * p.Fu));
     const int t0 = tt * 32;
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int i = tid + 256 * j, u = i >> 6, a = i & 63;
+      const int u = sl + 4 * j;
       float v = 0.f;
-      if (t0 + u < p.Tu && a0 + a < p.A) {
-        v = p.P[(((long)b * p.Fu + fu) * p.Tu + t0 + u) * p.A + a0 + a];
+      if (t0 + u < p.Tu && a0 + sc < p.A) {
+        v = p.P[(((long)b * p.Fu + fu) * p.Tu + t0 + u) * p.A + a0 + sc];
         if (p.pmask) v *= mask_at(p.pmask, p.T0, b, t0 + u, p.lvl_p);
       }
-      s_p[u][a] = v;
+      rp[j] = v;
     }
-    for (int i = tid; i < NR * ncol * 64; i += 256) {
-      const int c = i & 63, col = (i >> 6) % ncol, rr = (i >> 6) / ncol;
-      const int fv = fu * p.S - p.PAD + kh0 + rr, tv = t0 * p.S - p.PAD + col;
-      float v = 0.f;
-      if (fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + c < p.Bc) {
-        v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + c];
-        if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      const int fv = fu * S - p.PAD + kh0 + rr;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int col = sl + 4 * q, tv = t0 * S - p.PAD + col;
+        float v = 0.f;
+        if (col < NCOL && fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + sc < p.Bc) {
+          v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + sc];
+          if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
+        }
+        rq[rr][q] = v;
       }
-      s_q[rr][col][c] = v;
     }
+  };
+  if (s_lo < s_hi) load(s_lo);
+  for (long sg = s_lo; sg < s_hi; ++sg) {
     __syncthreads();
 #pragma unroll
+    for (int j = 0; j < 8; ++j) s_p[(sl + 4 * j) * PS + sc] = rp[j];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        if (sl + 4 * q < NCOL) s_q[(rr * NCOL + sl + 4 * q) * QS + sc] = rq[rr][q];
+    __syncthreads();
+    if (sg + 1 < s_hi) load(sg + 1);
+#pragma unroll
     for (int g = 0; g < KG; ++g) {
-      const int k = k0 + g, kh = k / p.KS - kh0, kw = k % p.KS;
+      const int kh = g / KS, kw = g % KS;
 #pragma unroll 4
       for (int up = 0; up < 16; ++up) {
         const int u = 2 * up + hh;
-        acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(s_p[u][ab + r], s_q[kh][u * p.S + kw][bb + r], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(s_p[u * PS + ab + r], s_q[(kh * NCOL + u * S + kw) * QS + bb + r],
+                                                      acc[g], 0, 0, 0);
       }
     }
   }
   const int bc = b0 + bb + r;
+  constexpr int KKt = KS * KS;
 #pragma unroll
   for (int g = 0; g < KG; ++g) {
     const int k = k0 + g;
-    if (k >= KK) break;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int a = a0 + ab + acc_row(j, hh);
-      if (a < p.A && bc < p.Bc) part[(((long)split * KK + k) * p.A + a) * p.Bc + bc] = acc[g][j];
+      if (a < p.A && bc < p.Bc) part[(((long)split * KKt + k) * p.A + a) * p.Bc + bc] = acc[g][j];
     }
   }
 }
@@ -243,6 +320,7 @@ __global__ void mwgrad_reduce_kernel(const float* part, int splits, int A, int B
   const long n = (long)KK * A * Bc;
   if (i >= n) return;
   float s = 0.f;
+#pragma unroll 8
   for (int q = 0; q < splits; ++q) s += part[(long)q * n + i];
   const int bc = (int)(i % Bc), a = (int)((i / Bc) % A), k = (int)(i / ((long)A * Bc));
   float* d = dw + a * sa + bc * sb + k;
@@ -253,7 +331,7 @@ int mwgrad_splits(const WGradParams& p) {
   const int groups = p.KS == 4 ? 2 : 1;
   const long tiles = (long)((p.A + 63) / 64) * ((p.Bc + 63) / 64) * groups;
   const long nseg = (long)p.B * p.Fu * ((p.Tu + 31) / 32);
-  long s = std::max<long>(1, 1024 / tiles);
+  long s = std::max<long>(1, 512 / tiles);
   s = std::min<long>(s, nseg);
   s = std::min<long>(s, kWPartCap / ((long)p.KS * p.KS * p.A * p.Bc));
   return (int)std::max<long>(1, s);
@@ -262,13 +340,15 @@ int mwgrad_splits(const WGradParams& p) {
 bool train_valu() { return kValu; }
 
 hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm) {
-  if (!(p.KS == 1 || p.KS == 3 || p.KS == 4) || 31 * p.S + p.KS > MW_QC) return hipErrorInvalidValue;
+  const int cfg = p.KS * 10 + p.S;
+  if (!(cfg == 11 || cfg == 31 || cfg == 32 || cfg == 42)) return hipErrorInvalidValue;
   const int splits = mwgrad_splits(p);
   const int groups = p.KS == 4 ? 2 : 1;
   const dim3 grid((p.A + 63) / 64, (p.Bc + 63) / 64, splits * groups);
-  if (p.KS == 1) hipLaunchKernelGGL(mwgrad_kernel<1>, grid, dim3(256), 0, strm, p, splits, part);
-  else if (p.KS == 3) hipLaunchKernelGGL(mwgrad_kernel<9>, grid, dim3(256), 0, strm, p, splits, part);
-  else hipLaunchKernelGGL(mwgrad_kernel<8>, grid, dim3(256), 0, strm, p, splits, part);
+  if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 31) hipLaunchKernelGGL((mwgrad_kernel<3, 1>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 32) hipLaunchKernelGGL((mwgrad_kernel<3, 2>), grid, dim3(256), 0, strm, p, splits, part);
+  else hipLaunchKernelGGL((mwgrad_kernel<4, 2>), grid, dim3(256), 0, strm, p, splits, part);
   const long n = (long)p.KS * p.KS * p.A * p.Bc;
   hipLaunchKernelGGL(mwgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, strm, part, splits, p.A,
                      p.Bc, p.KS * p.KS, sa, sb, dw, accumulate);
@@ -427,6 +507,48 @@ __global__ void colsum_kernel(const float* in, int B, int C, float* out, int acc
   float s = 0.f;
   for (int b = 0; b < B; ++b) s += in[(long)b * C + c];
   out[c] = accumulate ? out[c] + s : s;
+}
+
+// GroupNorm statistics in two levels: fp64 (sum, sum of squares) per (b, group, split), then the splits in order
+__global__ __launch_bounds__(256) void gn_partial_kernel(const float* h, int npos, int C, double* part) {
+  __shared__ double s[2][256];
+  const int b = blockIdx.x, g = blockIdx.y, sp = blockIdx.z, S = gridDim.z, tid = threadIdx.x;
+  const int cg = C / 8;
+  long lo, hi;
+  split_range((long)npos * cg, S, sp, &lo, &hi);
+  const float* hb = h + (long)b * npos * C + g * cg;
+  double s1 = 0.0, s2 = 0.0;
+  for (long i = lo + tid; i < hi; i += 256) {
+    const double v = hb[(i / cg) * C + i % cg];
+    s1 += v; s2 += v * v;
+  }
+  s[0][tid] = s1; s[1][tid] = s2;
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0, q = 0.0;
+    for (int i = 0; i < 256; ++i) { a += s[0][i]; q += s[1][i]; }
+    part[(((long)b * 8 + g) * S + sp) * 2] = a;
+    part[(((long)b * 8 + g) * S + sp) * 2 + 1] = q;
+  }
+}
+__global__ void gn_final_kernel(const double* part, int S, int nbg, double n, float* stats) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // b * 8 + g
+  if (i >= nbg) return;
+  double a = 0.0, q = 0.0;
+  for (int sp = 0; sp < S; ++sp) { a += part[((long)i * S + sp) * 2]; q += part[((long)i * S + sp) * 2 + 1]; }
+  const double mean = a / n;
+  double var = q / n - mean * mean;
+  var = var > 0.0 ? var : 0.0;
+  stats[i * 2] = (float)mean;
+  stats[i * 2 + 1] = (float)(1.0 / sqrt(var + 1e-5));
+}
+int gn_splits(long npos) { return (int)std::max<long>(1, std::min<long>(32, npos / 512)); }
+hipError_t launch_gn_stats_split(const float* h, int B, int npos, int C, double* part, float* stats, hipStream_t strm) {
+  const int S = gn_splits(npos);
+  hipLaunchKernelGGL(gn_partial_kernel, dim3(B, 8, S), dim3(256), 0, strm, h, npos, C, part);
+  hipLaunchKernelGGL(gn_final_kernel, dim3((B * 8 + 255) / 256), dim3(256), 0, strm, part, S, B * 8,
+                     (double)npos * (C / 8), stats);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- GroupNorm statistics of a forward tensor
@@ -719,9 +841,18 @@ __global__ void input_pack_kernel(const float* mu, const float* xt, const float*
 hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   if (p.KS > 4 || p.S > 2) return hipErrorInvalidValue;
   const dim3 grid((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
-  if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
-  else if (kValu) hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(mconv_kernel, grid, dim3(256), 0, s, p);
+  if (kValu) {
+    if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
+  } else {
+    const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
+    if (cfg == 11) hipLaunchKernelGGL((mconv_kernel<1, 1>), grid, dim3(256), 0, s, p);
+    else if (cfg == 31) hipLaunchKernelGGL((mconv_kernel<3, 1>), grid, dim3(256), 0, s, p);
+    else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2>), grid, dim3(256), 0, s, p);
+    else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1>), grid, dim3(256), 0, s, p);
+    else if (cfg == 42) hipLaunchKernelGGL((mconv_kernel<4, 2>), grid, dim3(256), 0, s, p);
+    else return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -779,13 +910,8 @@ __global__ void mask_sum_kernel(const float* mask, long n, float* out) {
 // ---------------------------------------------------------------- split reductions over the positions
 // Every position sum below runs in two fixed-order levels: S splits of each utterance's positions (pos_splits), then
 // the splits in order (sum_splits_kernel). Deterministic, and the grid fills the chip at every level.
-int pos_splits(long npos) { return (int)std::max<long>(1, std::min<long>(64, npos / 512)); }
+int pos_splits(long npos) { return (int)std::max<long>(1, std::min<long>(128, npos / 128)); }
 
-GT_DEV void split_range(long n, int S, int s, long* lo, long* hi) {
-  const long per = (n + S - 1) / S;
-  *lo = (long)s * per;
-  *hi = *lo + per < n ? *lo + per : n;
-}
 
 // out[g][j] (+)= sum_q part[g][q][j], q ascending
 __global__ void sum_splits_kernel(const float* part, int G, int S, long n, float* out, int accumulate) {
@@ -799,7 +925,8 @@ __global__ void sum_splits_kernel(const float* part, int G, int S, long n, float
 
 // part[b][s][c] = sum over split s of utterance b's positions of x[b][pos][c] (* y): grid (C/64, S, B), 64 channels
 // x 4 position lanes per workgroup (each wave reads 64 consecutive channels of one position)
-__global__ __launch_bounds__(256) void chan_partial_kernel(const float* x, const float* y, int npos, int C, float* part) {
+__global__ __launch_bounds__(256) void chan_partial_kernel(const float* x, int xcs, int xo, const float* y, int ycs,
+                                                           int yo, int npos, int C, float* part) {
   __shared__ float s_r[4][64];
   const int tid = threadIdx.x, cl = tid & 63, pl = tid >> 6;
   const int c = blockIdx.x * 64 + cl, s = blockIdx.y, b = blockIdx.z, S = gridDim.y;
@@ -807,9 +934,9 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(const float* x, const
   split_range(npos, S, s, &lo, &hi);
   float acc = 0.f;
   if (c < C) {
-    const float* xb = x + (long)b * npos * C + c;
-    const float* yb = y ? y + (long)b * npos * C + c : nullptr;
-    for (long i = lo + pl; i < hi; i += 4) acc += yb ? xb[i * C] * yb[i * C] : xb[i * C];
+    const float* xb = x + (long)b * npos * xcs + xo + c;
+    const float* yb = y ? y + (long)b * npos * ycs + yo + c : nullptr;
+    for (long i = lo + pl; i < hi; i += 4) acc += yb ? xb[i * xcs] * yb[i * ycs] : xb[i * xcs];
   }
   s_r[pl][cl] = acc;
   __syncthreads();
@@ -921,6 +1048,86 @@ __global__ void attn_rowdot_split_kernel(const float* a, int csa, int ao, const 
   part[((long)s * B + b) * 128 + r] = acc;
 }
 
+// Y[b][pos][yo + 32h + j] (+)= sum_i M'[i][j] X[b][pos][xo + 32h + i] on fp32 MFMA: 64 positions x 4 heads per
+// workgroup (wave = head), X slice and M staged in LDS
+__global__ __launch_bounds__(256) void attn_headmm_mfma_kernel(const float* M, int trans, const float* X, int csx, int xo,
+                                                               int npos, float* Y, int csy, int yo, int accumulate) {
+  __shared__ float s_x[64][129];
+  __shared__ float s_m[4][32][33];
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int p0 = blockIdx.x * 64, b = blockIdx.y;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int i = tid + 256 * j, pp = i >> 7, ch = i & 127;
+    s_x[pp][ch] = p0 + pp < npos ? X[((long)b * npos + p0 + pp) * csx + xo + ch] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int i = tid + 256 * j, hd = i >> 10, ii = (i >> 5) & 31, jj = i & 31;
+    s_m[hd][ii][jj] = M[(long)b * 4096 + i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int pbk = 0; pbk < 2; ++pbk) {
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int i = 2 * ks + hh;
+      const float bv = trans ? s_m[h][r][i] : s_m[h][i][r];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_x[pbk * 32 + r][32 * h + i], bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int pos = p0 + pbk * 32 + acc_row(j, hh);
+      if (pos >= npos) continue;
+      float* y = Y + ((long)b * npos + pos) * csy + yo + 32 * h + r;
+      *y = accumulate ? *y + acc[j] : acc[j];
+    }
+  }
+}
+
+// R_part[s][b][h][d][e] = sum over split s of X1[pos][x1o + 32h + d] X2[pos][x2o + 32h + e] on fp32 MFMA
+// (grid (S, B), wave = head, 32-position segments staged in LDS)
+__global__ __launch_bounds__(256) void attn_outer_mfma_kernel(const float* X1, int cs1, int x1o, const float* X2, int cs2,
+                                                              int x2o, int npos, float* part) {
+  __shared__ float s1[32][129], s2[32][129];
+  const int tid = threadIdx.x, lane = tid & 63, h = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int sp = blockIdx.x, b = blockIdx.y, S = gridDim.x, B = gridDim.y;
+  long lo, hi;
+  split_range(npos, S, sp, &lo, &hi);
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (long p0 = lo; p0 < hi; p0 += 32) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int i = tid + 256 * j, pp = i >> 7, ch = i & 127;
+      const bool ok = p0 + pp < hi;
+      s1[pp][ch] = ok ? X1[((long)b * npos + p0 + pp) * cs1 + x1o + ch] : 0.f;
+      s2[pp][ch] = ok ? X2[((long)b * npos + p0 + pp) * cs2 + x2o + ch] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int pp = 2 * ks + hh;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s1[pp][32 * h + r], s2[pp][32 * h + r], acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    part[((((long)sp * B + b) * 4 + h) * 32 + acc_row(j, hh)) * 32 + r] = acc[j];
+}
+
+hipError_t launch_attn_headmm_mfma(const float* M, int trans, const float* X, int csx, int xo, int B, int npos, float* Y,
+                                   int csy, int yo, int accumulate, hipStream_t strm) {
+  hipLaunchKernelGGL(attn_headmm_mfma_kernel, dim3((npos + 63) / 64, B), dim3(256), 0, strm, M, trans, X, csx, xo, npos, Y,
+                     csy, yo, accumulate);
+  return hipGetLastError();
+}
+
 static hipError_t sum_splits(const float* part, int G, int S, long n, float* out, int accumulate, hipStream_t strm) {
   hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)(((long)G * n + 255) / 256)), dim3(256), 0, strm, part, G, S, n,
                      out, accumulate);
@@ -929,8 +1136,13 @@ static hipError_t sum_splits(const float* part, int G, int S, long n, float* out
 
 hipError_t launch_chan_sums(const float* x, const float* y, int B, int npos, int C, float* part, float* out, int per_b,
                             int accumulate, hipStream_t strm) {
+  return launch_chan_sums_strided(x, C, 0, y, C, 0, B, npos, C, part, out, per_b, accumulate, strm);
+}
+hipError_t launch_chan_sums_strided(const float* x, int xcs, int xo, const float* y, int ycs, int yo, int B, int npos,
+                                    int C, float* part, float* out, int per_b, int accumulate, hipStream_t strm) {
   const int S = pos_splits(npos);
-  hipLaunchKernelGGL(chan_partial_kernel, dim3((C + 63) / 64, S, B), dim3(256), 0, strm, x, y, npos, C, part);
+  hipLaunchKernelGGL(chan_partial_kernel, dim3((C + 63) / 64, S, B), dim3(256), 0, strm, x, xcs, xo, y, ycs, yo, npos, C,
+                     part);
   return per_b ? sum_splits(part, B, S, C, out, accumulate, strm) : sum_splits(part, 1, B * S, C, out, accumulate, strm);
 }
 
@@ -952,15 +1164,13 @@ hipError_t launch_dot_sum(const float* x, const float* y, long n, double* part, 
 hipError_t launch_attn_outer_split(const float* X1, int cs1, int x1o, const float* X2, int cs2, int x2o, int B, int npos,
                                    float* part, float* R, hipStream_t strm) {
   const int S = pos_splits(npos);
-  hipLaunchKernelGGL(attn_outer_split_kernel, dim3(B, 4, S), dim3(1024), 0, strm, X1, cs1, x1o, X2, cs2, x2o, npos, part);
+  hipLaunchKernelGGL(attn_outer_mfma_kernel, dim3(S, B), dim3(256), 0, strm, X1, cs1, x1o, X2, cs2, x2o, npos, part);
   return sum_splits(part, 1, S, (long)B * 4096, R, 0, strm);
 }
 
 hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float* c, int csc, int co, int B, int npos,
                                     float* part, float* S_out, hipStream_t strm) {
-  const int S = pos_splits(npos);
-  hipLaunchKernelGGL(attn_rowdot_split_kernel, dim3(B, S), dim3(128), 0, strm, a, csa, ao, c, csc, co, npos, part);
-  return sum_splits(part, 1, S, (long)B * 128, S_out, 0, strm);
+  return launch_chan_sums_strided(a, csa, ao, c, csc, co, B, npos, 128, part, S_out, 1, 0, strm);
 }
 
 // ---- launchers

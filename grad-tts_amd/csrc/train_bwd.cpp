@@ -152,7 +152,9 @@ struct Trainer {
   }
   float* gn_stats(const float* h, int l, int C) {
     float* st = A.take((size_t)B * 16);
-    if (live()) chk(launch_gn_stats(dim3(B, 8), dim3(256), s, h, L(l).F * L(l).T, C, st));
+    const int npos = L(l).F * L(l).T;
+    double* part = reinterpret_cast<double*>(A.take((size_t)B * 8 * gn_splits(npos) * 4));
+    if (live()) chk(launch_gn_stats_split(h, B, npos, C, part, st, s));
     return st;
   }
   float* block_fwd(int l, int C, const float* h, const float* st, const std::string& gn, const float* tb) {
@@ -269,7 +271,7 @@ struct Trainer {
       chk(launch_attn_kstats(dim3(B, 128), dim3(256), s, a.qkv, (int)np, st));
       chk(launch_attn_ksoftmax(g1((long)B * np * 128), dim3(256), s, a.qkv, B, (int)np, st));
       chk(launch_attn_outer_split(a.qkv, 384, 128, a.qkv, 384, 256, B, (int)np, opart, a.ctx, s));
-      chk(launch_attn_headmm(g1((long)B * np * 128), dim3(256), s, a.ctx, 0, a.qkv, 384, 0, B, (int)np, a.o, 128, 0, 0));
+      chk(launch_attn_headmm_mfma(a.ctx, 0, a.qkv, 384, 0, B, (int)np, a.o, 128, 0, 0, s));
     }
     gconv(a.o, 128, l, false, P(k + "fn.fn.to_out.weight"), 128, 1, 1, 1, 0, 0, P(k + "fn.fn.to_out.bias"), a.z, C, l,
           false, C, 0, 0);
@@ -419,12 +421,12 @@ struct Trainer {
     float* dqkv = A.take((size_t)n * 384);
     float* S = A.take((size_t)B * 128);
     float* opart = A.take((size_t)pos_splits(np) * B * 4096);
-    float* rpart = A.take((size_t)pos_splits(np) * B * 128);
+    float* rpart = A.take((size_t)B * pos_splits(np) * 128);
     if (live()) {
       chk(launch_attn_outer_split(a.qkv, 384, 0, dO, 128, 0, B, (int)np, opart, dctx, s));      // q do^T
-      chk(launch_attn_headmm(g1(n * 128), dim3(256), s, a.ctx, 1, dO, 128, 0, B, (int)np, dqkv, 384, 0, 0));     // dq
-      chk(launch_attn_headmm(g1(n * 128), dim3(256), s, dctx, 1, a.qkv, 384, 256, B, (int)np, dqkv, 384, 128, 0));  // dks
-      chk(launch_attn_headmm(g1(n * 128), dim3(256), s, dctx, 0, a.qkv, 384, 128, B, (int)np, dqkv, 384, 256, 0));  // dv
+      chk(launch_attn_headmm_mfma(a.ctx, 1, dO, 128, 0, B, (int)np, dqkv, 384, 0, 0, s));     // dq
+      chk(launch_attn_headmm_mfma(dctx, 1, a.qkv, 384, 256, B, (int)np, dqkv, 384, 128, 0, s));  // dks
+      chk(launch_attn_headmm_mfma(dctx, 0, a.qkv, 384, 128, B, (int)np, dqkv, 384, 256, 0, s));  // dv
       chk(launch_attn_rowdot_split(a.qkv, 384, 128, dqkv, 384, 128, B, (int)np, rpart, S, s));
       chk(launch_attn_ksoftmax_bwd(g1(n * 128), dim3(256), s, a.qkv, dqkv, B, (int)np, S));
     }

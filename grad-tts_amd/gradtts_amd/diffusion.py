@@ -385,10 +385,11 @@ class _UNetLoss(torch.autograd.Function):
     def backward(ctx, g):
         flat, dmu, dspk = ctx.saved_tensors
         shapes, mu_dtype, spk_dtype, has_spk = ctx.meta
+        scaled = flat * g   # one kernel; the parameter gradients are views of it
         grads, off = [], 0
         for shp in shapes:
             n = int(np.prod(shp)) if len(shp) else 1
-            grads.append(flat[off:off + n].view(shp) * g)
+            grads.append(scaled[off:off + n].view(shp))
             off += n
         gmu = (dmu * g).to(mu_dtype)
         gspk = (dspk * g).to(spk_dtype) if has_spk else None
