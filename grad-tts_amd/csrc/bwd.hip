@@ -115,19 +115,23 @@ __global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
 // Implicit GEMM on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains): M = 64 output positions of one row, N = 64 output
 // channels, K = input channels x taps in chunks of MC_KC channels staged in LDS (input patch [row][col][c], weights
 // [c][tap][a]); wave w owns the 32 x 32 block (positions (w & 1) * 32, channels (w >> 1) * 32).
-constexpr int MC_KC = 8;
+constexpr int MC_ROWS = 4;
+// Tile: MC_ROWS output rows x 64 positions x 64 output channels; wave w owns row w (2 x 2 blocks of 32 x 32). The
+// input patch ((MC_ROWS - 1) * SE + KS rows) and the weight chunk are staged once per 8-channel chunk and reused by
+// the four rows; the next chunk's global loads are in flight during the current chunk's MFMAs.
 template <int KS, int SE>
 __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
-  constexpr int KK = KS * KS, PC = 63 * SE + KS, NCOL = (PC + 31) / 32;
+  constexpr int MC_KC = 8, NCL = 32;   // input channels per staged chunk, staging column lanes per pass
+  constexpr int KK = KS * KS, PC = 63 * SE + KS, PR = (MC_ROWS - 1) * SE + KS, NCOL = (PC + NCL - 1) / NCL;
   constexpr int NW = 64 * MC_KC * KK, NWJ = (NW + 255) / 256;
-  __shared__ float s_in[KS][PC][MC_KC + 1];
+  __shared__ float s_in[PR][PC][MC_KC + 1];
   __shared__ float s_w[MC_KC][KK][65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
-  const int n_tt = (p.To + 63) / 64;
+  const int n_tt = (p.To + 63) / 64, n_f4 = (p.Fo + MC_ROWS - 1) / MC_ROWS;
   int bid = blockIdx.x;
   const int tt = bid % n_tt; bid /= n_tt;
-  const int fo = bid % p.Fo;
-  const int b = bid / p.Fo;
+  const int fo0 = (bid % n_f4) * MC_ROWS;
+  const int b = bid / n_f4;
   const int to0 = tt * 64, a0 = blockIdx.y * 64;
   // transposed relation (ConvTranspose2d, strided-conv dgrad): a stride-1 conv over the S-dilated input with the
   // taps flipped and padding KS - 1 - PAD
@@ -135,17 +139,16 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   const int pad = dil ? KS - 1 - p.PAD : p.PAD;
   const bool flip = dil ? !p.flip : p.flip != 0;
   const bool a_fast = p.wsa < p.wsc;   // stage weights along their contiguous axis
-  const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
-  const int ic = tid & 7, iq = tid >> 3;   // input staging: channel, column lane (32 columns per pass)
-  float rin[KS][NCOL], rw[NWJ];
+  const int ic = tid % MC_KC, iq = tid / MC_KC;   // input staging: channel, column lane (NCL columns per pass)
+  float rin[PR][NCOL], rw[NWJ];
   auto load = [&](int c0) {   // next chunk into registers (in flight during the MFMAs of the current one)
     const int ci = c0 + ic;
 #pragma unroll
-    for (int row = 0; row < KS; ++row) {
-      const int fd = fo * SE - pad + row;
+    for (int row = 0; row < PR; ++row) {
+      const int fd = fo0 * SE - pad + row;
 #pragma unroll
       for (int q = 0; q < NCOL; ++q) {
-        const int col = iq + 32 * q;
+        const int col = iq + NCL * q;
         const int td = to0 * SE - pad + col;
         float v = 0.f;
         bool ok = col < PC && fd >= 0 && td >= 0 && ci < p.Cin;
@@ -173,10 +176,10 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   };
   auto store = [&]() {
 #pragma unroll
-    for (int row = 0; row < KS; ++row)
+    for (int row = 0; row < PR; ++row)
 #pragma unroll
       for (int q = 0; q < NCOL; ++q)
-        if (iq + 32 * q < PC) s_in[row][iq + 32 * q][ic] = rin[row][q];
+        if (iq + NCL * q < PC) s_in[row][iq + NCL * q][ic] = rin[row][q];
 #pragma unroll
     for (int j = 0; j < NWJ; ++j) {
       const int i = tid + 256 * j;
@@ -187,9 +190,13 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
       }
     }
   };
-  f32x16 acc;
+  f32x16 acc[2][2];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[x][y][j] = 0.f;
   load(0);
   for (int c0 = 0; c0 < p.Cin; c0 += MC_KC) {
     __syncthreads();
@@ -200,10 +207,91 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
     for (int k = 0; k < KK; ++k) {
       const int kh = k / KS, kw = k % KS;
 #pragma unroll
-      for (int cp = 0; cp < MC_KC / 2; ++cp)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[kh][(pb + r) * SE + kw][2 * cp + hh], s_w[2 * cp + hh][k][cb + r],
-                                                   acc, 0, 0, 0);
+      for (int cp = 0; cp < MC_KC / 2; ++cp) {
+        const int c = 2 * cp + hh;
+        const float x0 = s_in[wv * SE + kh][r * SE + kw][c], x1 = s_in[wv * SE + kh][(32 + r) * SE + kw][c];
+        const float w0 = s_w[c][k][r], w1 = s_w[c][k][32 + r];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, w0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, w1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, w0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, w1, acc[1][1], 0, 0, 0);
+      }
     }
+  }
+  const int fo = fo0 + wv;
+  if (fo >= p.Fo) return;
+#pragma unroll
+  for (int y = 0; y < 2; ++y) {
+    const int a = a0 + 32 * y + r;
+    if (a >= p.Cout) continue;
+    const float bias = p.bias ? p.bias[a] : 0.f;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int to = to0 + 32 * x + acc_row(j, hh);
+        if (to >= p.To) continue;
+        const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
+        const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
+        const float v = (acc[x][y][j] + bias) * om;
+        p.out[o] = p.accumulate ? p.out[o] + v : v;
+      }
+  }
+}
+
+// 1x1 convs (qkv / to_out / res_conv / final_conv and their dgrads): one row of 64 positions x 64 channels per
+// workgroup, 32-channel chunks (128-byte input rows), waves 2 x 2 over (positions, channels)
+__global__ __launch_bounds__(256) void mconv1_kernel(GConvParams p) {
+  constexpr int KC = 32;
+  __shared__ float s_in[64][KC + 1];
+  __shared__ float s_w[KC][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_tt = (p.To + 63) / 64;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int fo = bid % p.Fo;
+  const int b = bid / p.Fo;
+  const int to0 = tt * 64, a0 = blockIdx.y * 64;
+  const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
+  const bool a_fast = p.wsa < p.wsc;
+  float rin[8], rw[8];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // input: 32 channels x 64 positions
+      const int i = tid + 256 * j, c = i & 31, pp = i >> 5;
+      const int ti = to0 + pp, ci = c0 + c;
+      float v = 0.f;
+      if (ti < p.Ti && ci < p.Cin) {
+        v = p.in[(((long)b * p.Fi + fo) * p.Ti + ti) * p.Cin + ci];
+        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+      }
+      rin[j] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {   // weights: 64 a x 32 c
+      const int i = tid + 256 * j;
+      const int a = a_fast ? (i & 63) : (i >> 5), c = a_fast ? (i >> 6) : (i & 31);
+      rw[j] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc] : 0.f;
+    }
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  load(0);
+  for (int c0 = 0; c0 < p.Cin; c0 += KC) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j;
+      s_in[i >> 5][i & 31] = rin[j];
+      const int a = a_fast ? (i & 63) : (i >> 5), c = a_fast ? (i >> 6) : (i & 31);
+      s_w[c][a] = rw[j];
+    }
+    __syncthreads();
+    if (c0 + KC < p.Cin) load(c0 + KC);
+#pragma unroll
+    for (int cp = 0; cp < KC / 2; ++cp)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[pb + r][2 * cp + hh], s_w[2 * cp + hh][cb + r], acc, 0, 0, 0);
   }
   const int a = a0 + cb + r;
   if (a >= p.Cout) return;
@@ -845,8 +933,12 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
     if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
   } else {
+    const dim3 mgrid((unsigned)((long)p.B * ((p.Fo + MC_ROWS - 1) / MC_ROWS) * ((p.To + 63) / 64)),
+                     (unsigned)((p.Cout + 63) / 64));
+    const dim3& grid = mgrid;
     const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
-    if (cfg == 11) hipLaunchKernelGGL((mconv_kernel<1, 1>), grid, dim3(256), 0, s, p);
+    if (cfg == 11) hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
+                                                   (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);
     else if (cfg == 31) hipLaunchKernelGGL((mconv_kernel<3, 1>), grid, dim3(256), 0, s, p);
     else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2>), grid, dim3(256), 0, s, p);
     else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1>), grid, dim3(256), 0, s, p);
@@ -919,6 +1011,7 @@ __global__ void sum_splits_kernel(const float* part, int G, int S, long n, float
   if (i >= (long)G * n) return;
   const long g = i / n, j = i % n;
   float s = 0.f;
+#pragma unroll 8
   for (int q = 0; q < S; ++q) s += part[(g * S + q) * n + j];
   out[i] = accumulate ? out[i] + s : s;
 }
