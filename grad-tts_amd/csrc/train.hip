@@ -11,6 +11,8 @@
 // Layouts are the reference's: mu_x [B][F][Tx], y / x0 / mu / z [B][F][T], masks [B][T] (0/1), output
 // log-prior [B][Tx][Ty] fp32. Bound: HBM (every kernel streams its operands once; the log-prior contraction is
 // 2*F FLOP per output against 4 B written).
+#include <algorithm>
+
 #include "common.h"
 #include "gradtts.h"
 #include "train.h"
@@ -137,6 +139,114 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const float* part, int 
     for (int i = 0; i < 256; ++i) { A += s[0][i]; M += s[1][i]; }
     loss[0] = (float)(A / (M * (double)F));   // (:280)
   }
+}
+
+// ---------------------------------------------------------------- likelihood (n_best/likelihood, §8 f3)
+// Probability-flow drift of SPEECHSDE and its Hutchinson divergence (likelihood.py:27-38, 61-68;
+// sde_lib.py:278-282, reverse :93-100): with x1 = x m, beta = beta_0 + t (beta_1 - beta_0), g2 = sqrt(beta)^2,
+//   drift = (0.5 beta (mu - x1) - g2 s(x1) 0.5) m
+//   div   = sum eps . d(sum drift . eps)/dx = sum eps m (-0.5 beta m eps - 0.5 g2 u),  u = J_s(x1)^T (m eps)
+GT_DEV float lik_beta(float t, float bmin, float delta) { return __fadd_rn(bmin, __fmul_rn(t, delta)); }
+
+__global__ void lik_prep_kernel(const float* x, const float* mask, const float* eps, int B, int T, float* xm, float* v) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * 80 * T) return;
+  const float m = mask[(i / (80L * T)) * T + i % T];
+  xm[i] = __fmul_rn(x[i], m);
+  v[i] = __fmul_rn(eps[i], m);
+}
+
+// grid (nblk, B): drift per element; part[b][blk] = this block's sum of eps m (-0.5 beta m eps - 0.5 g2 u)
+__global__ __launch_bounds__(256) void lik_partial_kernel(LikParams p) {
+  __shared__ float s_w[4];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const long n = 80L * p.T, base = (long)b * n;
+  const float tb = p.t[b];
+  const float beta = lik_beta(tb, p.beta_min, p.delta);
+  const float sq = sqrtf(beta), g2 = __fmul_rn(sq, sq), hb = __fmul_rn(0.5f, beta);
+  float acc = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const long j = ((long)blockIdx.x * 4 + k) * 256 + tid;
+    if (j >= n) continue;
+    const long i = base + j;
+    const float m = p.mask[(long)b * p.T + j % p.T];
+    const float x1 = p.xm[i], e = p.eps[i];
+    const float d = __fsub_rn(__fmul_rn(hb, __fsub_rn(p.mu[i], x1)), __fmul_rn(__fmul_rn(g2, p.score[i]), 0.5f));
+    p.drift[i] = __fmul_rn(d, m);
+    const float gr = __fmul_rn(m, __fsub_rn(__fmul_rn(-hb, __fmul_rn(m, e)), __fmul_rn(__fmul_rn(0.5f, g2), p.u[i])));
+    acc = __fadd_rn(acc, __fmul_rn(gr, e));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((tid & 63) == 0) s_w[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) p.part[(long)b * gridDim.x + blockIdx.x] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
+}
+
+__global__ void lik_final_kernel(const float* part, int nblk, int B, float* div) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  double a = 0.0;
+  for (int i = 0; i < nblk; ++i) a += (double)part[(long)b * nblk + i];
+  div[b] = (float)a;
+}
+
+int lik_blocks(int T) { return (int)((80L * T + 1023) / 1024); }
+
+hipError_t launch_lik_prep(const float* x, const float* mask, const float* eps, int B, int T, float* xm, float* v,
+                           hipStream_t s) {
+  const long n = (long)B * 80 * T;
+  hipLaunchKernelGGL(lik_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, mask, eps, B, T, xm, v);
+  return hipGetLastError();
+}
+
+hipError_t launch_lik_drift_div(const LikParams& p, float* div, hipStream_t s) {
+  const int nblk = lik_blocks(p.T);
+  hipLaunchKernelGGL(lik_partial_kernel, dim3(nblk, p.B), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(lik_final_kernel, dim3((p.B + 63) / 64), dim3(64), 0, s, p.part, nblk, p.B, div);
+  return hipGetLastError();
+}
+
+// Euler integration state (likelihood.py:99-107): fp64 as the reference's numpy state, cast to fp32 per evaluation
+__global__ void lik_init_kernel(const float* data, const float* mask, int B, int T, double* y, double* logp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < B) logp[i] = 0.0;
+  if (i >= (long)B * 80 * T) return;
+  y[i] = (double)__fmul_rn(data[i], mask[(i / (80L * T)) * T + i % T]);
+}
+__global__ void lik_cast_kernel(const double* y, long n, float* x, float* tbuf, int B, float tval) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < B) tbuf[i] = tval;
+  if (i < n) x[i] = (float)y[i];
+}
+__global__ void lik_step_kernel(double* y, const float* drift, long n, double h, double* logp, const float* div, int B) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = y[i] + (double)drift[i] * h;
+  if (i < B) logp[i] = logp[i] + (double)div[i] * h;
+}
+__global__ void lik_out_kernel(const double* y, long n, const double* logp, int B, float* z, float* dlogp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) z[i] = (float)y[i];
+  if (i < B) dlogp[i] = (float)logp[i];
+}
+
+static dim3 lik_grid(long n, int B) { return dim3((unsigned)((std::max<long>(n, B) + 255) / 256)); }
+hipError_t launch_lik_init(const float* data, const float* mask, int B, int T, double* y, double* logp, hipStream_t s) {
+  hipLaunchKernelGGL(lik_init_kernel, lik_grid((long)B * 80 * T, B), dim3(256), 0, s, data, mask, B, T, y, logp);
+  return hipGetLastError();
+}
+hipError_t launch_lik_cast(const double* y, long n, float* x, float* tbuf, int B, float tval, hipStream_t s) {
+  hipLaunchKernelGGL(lik_cast_kernel, lik_grid(n, B), dim3(256), 0, s, y, n, x, tbuf, B, tval);
+  return hipGetLastError();
+}
+hipError_t launch_lik_step(double* y, const float* drift, long n, double h, double* logp, const float* div, int B,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(lik_step_kernel, lik_grid(n, B), dim3(256), 0, s, y, drift, n, h, logp, div, B);
+  return hipGetLastError();
+}
+hipError_t launch_lik_out(const double* y, long n, const double* logp, int B, float* z, float* dlogp, hipStream_t s) {
+  hipLaunchKernelGGL(lik_out_kernel, lik_grid(n, B), dim3(256), 0, s, y, n, logp, B, z, dlogp);
+  return hipGetLastError();
 }
 
 hipError_t launch_log_prior(const float* mu_x, const float* y, const float* x_mask, const float* y_mask, int B, int F,

@@ -61,6 +61,7 @@ struct Trainer {
   Regions regions;
   std::string bad;
   bool live() const { return run && !dry; }
+  bool pgrads = true;       // false (estimator VJP): no parameter-gradient work, only the input cotangents
   void need(const void* p, long elems, const char* what, int line) {
     if (!dry || !bad.empty() || elems <= 0) return;
     const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)elems * 4;
@@ -109,6 +110,7 @@ struct Trainer {
     if (!run) return;
     need(Pt, nU * Ad, "wgrad P", line);
     need(Qt, (long)B * L(l_v).F * L(l_v).T * Bd, "wgrad Q", line);
+    if (!pgrads) return;
     need(dw, (long)(Ad - 1) * sa + (long)(Bd - 1) * sb + KS * KS, "wgrad dW", line);
     if (dry) return;
     WGradParams p{};
@@ -124,6 +126,7 @@ struct Trainer {
     float* part = A.take((size_t)B * pos_splits(npos) * C);
     if (!run) return;
     need(x, (long)B * npos * C, "chansum x", line);
+    if (!pgrads) return;
     need(out, C, "chansum out", line);
     if (dry) return;
     chk(launch_chan_sums(x, nullptr, B, npos, C, part, out, 0, acc, s), line);
@@ -178,15 +181,17 @@ struct Trainer {
       need(h, n, "block_bwd h", line);
       need(st, (long)B * 16, "block_bwd stats", line);
       need(P(gn + ".weight"), C, "block_bwd gamma", line);
-      need(G(gn + ".weight"), C, "block_bwd dgamma", line);
-      need(G(gn + ".bias"), C, "block_bwd dbeta", line);
+      if (pgrads) {
+        need(G(gn + ".weight"), C, "block_bwd dgamma", line);
+        need(G(gn + ".bias"), C, "block_bwd dbeta", line);
+      }
     }
     if (dry) return dh;
     BlockBwdParams p = bp(l, C, h, st, gn);
     p.dA = dAv; p.gsum = gsum; p.dgb = dgb; p.dh = dh;
     chk(launch_block_bwd_sums(p, part, s), line);
     chk(launch_block_bwd_apply(g1((long)B * p.npos * C), dim3(256), s, p), line);
-    chk(launch_colsum_strided(gn, dgb, C, tw, tb2), line);   // dgamma, dbeta = sums over the batch
+    if (pgrads) chk(launch_colsum_strided(gn, dgb, C, tw, tb2), line);   // dgamma, dbeta = sums over the batch
     return dh;
   }
   // dgb [B][C][2] -> G(gn.weight)[c] += sum_b dgb[b][c][0]; G(gn.bias)[c] += sum_b dgb[b][c][1]
@@ -388,7 +393,7 @@ struct Trainer {
     {
       const int npos = L(l).F * L(l).T;
       float* part = A.take((size_t)B * pos_splits(npos) * C);
-      if (live()) chk(launch_chan_sums(du, nullptr, B, npos, C, part, dtb[b.r], 1, 0, s));
+      if (live() && pgrads) chk(launch_chan_sums(du, nullptr, B, npos, C, part, dtb[b.r], 1, 0, s));
     }
     // block1
     float* dh1 = block_bwd(l, C, du, b.h1, b.st1, k + "block1.block.1");
@@ -410,7 +415,7 @@ struct Trainer {
     const float g = gt_internal_host_scalar(d, k + "fn.g");
     ew(dy, C, 0, 1.f, nullptr, 0.f, l, C, false, dx, C, 0, 1);                 // residual
     double* dpart = reinterpret_cast<double*>(A.take(2 * kDotBlocks));
-    if (live()) chk(launch_dot_sum(dy, a.z, n * C, dpart, G(k + "fn.g"), 1, s));   // d g = sum dy . z
+    if (live() && pgrads) chk(launch_dot_sum(dy, a.z, n * C, dpart, G(k + "fn.g"), 1, s));   // d g = sum dy . z
     float* dz = A.take((size_t)n * C);
     ew(dy, C, 0, g, nullptr, 0.f, l, C, false, dz, C, 0, 0);
     wgrad(dz, C, l, false, a.o, 128, l, false, 1, 1, 0, G(k + "fn.fn.to_out.weight"), 128, 1, 1);
@@ -439,6 +444,13 @@ struct Trainer {
     // dL/dscore (diffusion.py:278-280)
     float* ds = A.take(n0);
     if (live()) chk(launch_loss_bwd(g1(n0), dim3(256), s, score, z, mask, t, lossp, B, T, bmin, half_delta, ds));
+    (void)xt_e;
+    backward_core(ds, t, dmu, dspk);
+  }
+  float* dxin = nullptr;   // d / d(U-Net input channels (mu, x_t[, s])), [B][80][T][cin]
+  // backward from ds = d/d(pre-mask estimator output) (the output mask already applied)
+  void backward_core(const float* ds, const float* t, float* dmu, float* dspk) {
+    const long n0 = (long)B * 80 * T;
     // final conv (1x1, 64 -> 1) on af * m, output * m
     wgrad(ds, 1, 0, false, af, 64, 0, true, 1, 1, 0, G("final_conv.weight"), 64, 1, 1);
     chansum(ds, 0, 1, G("final_conv.bias"), 1);
@@ -524,7 +536,7 @@ struct Trainer {
     float* dx12 = A.take(n0 * 64);
     zero(dx12, n0 * 64);
     resnet_bwd(rbs[1], dx11, dx12, nullptr);                             // downs.0.1
-    float* dxin = A.take(n0 * cin);
+    dxin = A.take(n0 * cin);
     zero(dxin, n0 * cin);
     resnet_bwd(rbs[0], dx12, dxin, nullptr);                             // downs.0.0 (input channels mu, x_t[, s])
     // time MLPs: dtb_r -> mlp.1 of every block, d Mish(t_emb) -> mlp.2 -> Mish -> mlp.0
@@ -532,7 +544,7 @@ struct Trainer {
     float* dtm = A.take((size_t)B * 64);
     float* dte = A.take((size_t)B * 64);
     float* dh0 = A.take((size_t)B * 256);
-    if (live()) {
+    if (live() && pgrads) {
       for (int r = 0; r < 12; ++r) {
         const std::string kr = std::string(kRes[r]) + "mlp.1.";
         chk(launch_linear_wgrad(dim3(Cs[r]), dim3(64), s, dtb[r], temb_m, B, 64, Cs[r], G(kr + "weight"), G(kr + "bias")));
@@ -548,7 +560,7 @@ struct Trainer {
     if (n_spks > 1) {
       float* dsv = A.take((size_t)B * 80);
       float* dsh = A.take((size_t)B * 256);
-      if (live()) {
+      if (live() && pgrads) {
         chk(launch_spk_chan_sum(dim3(B), dim3(128), s, dxin, cin, T, dsv));
         chk(launch_linear_wgrad(dim3(80), dim3(256), s, dsv, spk_h, B, 256, 80, G("spk_mlp.2.weight"), G("spk_mlp.2.bias")));
         chk(launch_linear_dgrad(dim3(B), dim3(256), s, dsv, P("spk_mlp.2.weight"), 256, 80, spk_pre, dsh, 0));
@@ -556,7 +568,6 @@ struct Trainer {
         if (dspk) chk(launch_linear_dgrad(dim3(B), dim3(64), s, dsh, P("spk_mlp.0.weight"), 64, 256, nullptr, dspk, 0));
       }
     }
-    (void)xt_e;
   }
   std::string cur;                // the ResnetBlock / attention being processed (error messages)
   const float* lossp = nullptr;   // device [2]: loss, sum(mask)
@@ -680,6 +691,190 @@ int gt_diffusion_loss_grad(gt_decoder* d, const float* x0, const float* mask, co
 int64_t gt_decoder_grad_numel(gt_decoder* d) {
   if (!d || gt_internal_layout(d) != GT_OK) return -1;
   return gt_internal_numel(d);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- estimator VJP and likelihood (§8 f3)
+static size_t al256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// score = estimator(x, mask, mu, t, spk); vjp = (d score / d x)^T v. The training tape and backward without the
+// parameter-gradient work (Trainer::pgrads = false), started from the output cotangent v (times the output mask).
+static int vjp_pass(gt_decoder* d, const float* x, const float* mask, const float* mu, const float* t, const float* spk,
+                    const float* v, int64_t B, int64_t T, float* score, float* vjp, void* workspace,
+                    size_t workspace_bytes, hipStream_t stream, bool dry, bool debug) {
+  Trainer tr;
+  tr.d = d; tr.B = (int)B; tr.T = (int)T; tr.run = true; tr.s = stream;
+  float bmax;
+  gt_internal_consts(d, &tr.n_spks, &tr.bmin, &bmax, &tr.pe_scale);
+  tr.half_delta = (float)(0.5 * ((double)bmax - (double)tr.bmin));
+  tr.cin = tr.n_spks > 1 ? 3 : 2;
+  tr.mask = mask; tr.grads = nullptr; tr.spkin = spk; tr.pgrads = false;
+  tr.debug = debug; tr.dry = dry;
+  const long n0 = (long)B * 80 * T;
+  if (dry) {
+    const size_t n0b = (size_t)n0 * 4;
+    tr.regions = {{(uintptr_t)x, n0b}, {(uintptr_t)mu, n0b}, {(uintptr_t)v, n0b}, {(uintptr_t)vjp, n0b},
+                  {(uintptr_t)mask, (size_t)B * T * 4}, {(uintptr_t)t, (size_t)B * 4},
+                  {(uintptr_t)gt_internal_param(d, "mlp.0.weight") - (uintptr_t)gt_internal_param_offset(d, "mlp.0.weight") * 4,
+                   (size_t)(gt_internal_numel(d) + 32) * 4}};
+    if (score) tr.regions.push_back({(uintptr_t)score, n0b});
+    if (spk) tr.regions.push_back({(uintptr_t)spk, (size_t)B * 64 * 4});
+    tr.A.rec = &tr.regions;
+  }
+  tr.A.base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  float* ds = tr.A.take((size_t)n0);   // the same leading takes as train_pass (one workspace size for both)
+  tr.A.take((size_t)n0 * 2);
+  tr.A.take(2);
+  tr.forward(mu, x, spk, t);
+  tr.cur = "vjp cotangent";
+  tr.ew(v, 1, 0, 1.f, nullptr, 0.f, 0, 1, true, ds, 1, 0, 0);   // d/d(pre-mask output) = v m
+  tr.backward_core(ds, t, nullptr, nullptr);
+  tr.cur = "vjp input channel";
+  tr.ew(tr.dxin, tr.cin, 1, 1.f, nullptr, 0.f, 0, 1, false, vjp, 1, 0, 0);   // channel 1 of the U-Net input = x
+  if (dry) {
+    if (!tr.bad.empty()) return gt_internal_fail(GT_ERR_WORKSPACE, "estimator VJP extent check: " + tr.bad);
+    if (tr.A.off + 255 > workspace_bytes)
+      return gt_internal_fail(GT_ERR_WORKSPACE, "estimator VJP extent check: arena past the workspace");
+    return GT_OK;
+  }
+  if (score) tr.chk(hipMemcpyAsync(score, tr.score, (size_t)n0 * 4, hipMemcpyDeviceToDevice, tr.s));
+  if (tr.err != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(tr.err) +
+                                            " (train_bwd.cpp:" + std::to_string(tr.err_line) + ", " + tr.err_cur + ")");
+  return GT_OK;
+}
+
+namespace {
+struct LikWs { size_t xm, vv, u, score, part, y, logp, x32, tbuf, drift, div, total; };
+LikWs lik_ws(gt_decoder* d, int64_t B, int64_t T) {
+  const size_t n0 = (size_t)B * 80 * T;
+  LikWs w{};
+  size_t off = al256(gt_train_workspace_bytes(d, B, T));
+  auto put = [&](size_t bytes) { const size_t o = off; off = al256(off + bytes); return o; };
+  w.xm = put(n0 * 4); w.vv = put(n0 * 4); w.u = put(n0 * 4); w.score = put(n0 * 4);
+  w.part = put((size_t)B * lik_blocks((int)T) * 4);
+  w.y = put(n0 * 8); w.logp = put((size_t)B * 8); w.x32 = put(n0 * 4); w.tbuf = put((size_t)B * 4);
+  w.drift = put(n0 * 4); w.div = put((size_t)B * 4);
+  w.total = off + 256;
+  return w;
+}
+}  // namespace
+
+// drift and divergence of one probability-flow evaluation; base = 256-aligned workspace laid out by lik_ws
+static int drift_div_pass(gt_decoder* d, const float* x, const float* mask, const float* mu, const float* t,
+                          const float* spk, const float* eps, int64_t B, int64_t T, float* drift, float* div,
+                          uint8_t* base, const LikWs& w, hipStream_t stream, bool dry, bool debug) {
+  float* xm = (float*)(base + w.xm);
+  float* vv = (float*)(base + w.vv);
+  float* u = (float*)(base + w.u);
+  float* sc = (float*)(base + w.score);
+  if (!dry) {
+    const hipError_t e = launch_lik_prep(x, mask, eps, (int)B, (int)T, xm, vv, stream);
+    if (e != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("lik_prep: ") + hipGetErrorString(e));
+  }
+  int rc = vjp_pass(d, xm, mask, mu, t, spk, vv, B, T, sc, u, base, w.xm, stream, dry, debug);
+  if (rc || dry) return rc;
+  int n_spks; float bmin, bmax, pe;
+  gt_internal_consts(d, &n_spks, &bmin, &bmax, &pe);
+  LikParams lp;
+  lp.xm = xm; lp.mu = mu; lp.mask = mask; lp.eps = eps; lp.score = sc; lp.u = u; lp.t = t;
+  lp.B = (int)B; lp.T = (int)T; lp.beta_min = bmin; lp.delta = (float)((double)bmax - (double)bmin);
+  lp.drift = drift; lp.part = (float*)(base + w.part);
+  const hipError_t e = launch_lik_drift_div(lp, div, stream);
+  if (e != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("lik_drift_div: ") + hipGetErrorString(e));
+  return GT_OK;
+}
+
+extern "C" {
+
+size_t gt_estimator_vjp_workspace_bytes(gt_decoder* d, int64_t B, int64_t T) { return gt_train_workspace_bytes(d, B, T); }
+
+int gt_estimator_vjp(gt_decoder* d, const float* x, const float* mask, const float* mu, const float* t, const float* spk,
+                     const float* v, int64_t B, int64_t T, float* score, float* vjp_x, void* workspace,
+                     size_t workspace_bytes, void* stream) {
+  if (!d || !x || !mask || !mu || !t || !v || !vjp_x || !workspace) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || T <= 0 || T % 4 != 0) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
+  const char* dbg = getenv("GT_TRAIN_DEBUG");
+  const bool dry_only = dbg && dbg[0] == '2';
+  int rc = dry_only ? gt_internal_layout(d) : gt_internal_prepare_raw(d);
+  if (rc) return rc;
+  if (workspace_bytes < gt_train_workspace_bytes(d, B, T)) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
+  int n_spks; float bmin, bmax, pe;
+  gt_internal_consts(d, &n_spks, &bmin, &bmax, &pe);
+  if (n_spks > 1 && !spk) return gt_internal_fail(GT_ERR_ARG, "n_spks > 1 needs spk");
+  rc = vjp_pass(d, x, mask, mu, t, spk, v, B, T, score, vjp_x, workspace, workspace_bytes, (hipStream_t)stream, true, false);
+  if (rc || dry_only) return rc;
+  return vjp_pass(d, x, mask, mu, t, spk, v, B, T, score, vjp_x, workspace, workspace_bytes, (hipStream_t)stream, false,
+                  dbg && dbg[0] == '1');
+}
+
+size_t gt_likelihood_workspace_bytes(gt_decoder* d, int64_t B, int64_t T) {
+  if (!d || B <= 0 || T <= 0 || gt_internal_layout(d) != GT_OK) return 0;
+  return lik_ws(d, B, T).total;
+}
+
+static int lik_common(gt_decoder* d, const float* mask, const float* mu, const float* spk, const float* eps, int64_t B,
+                      int64_t T, size_t workspace_bytes, bool* dry_only, bool* debug) {
+  if (!d || !mask || !mu || !eps) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || T <= 0 || T % 4 != 0) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
+  const char* dbg = getenv("GT_TRAIN_DEBUG");
+  *dry_only = dbg && dbg[0] == '2';
+  *debug = dbg && dbg[0] == '1';
+  int rc = *dry_only ? gt_internal_layout(d) : gt_internal_prepare_raw(d);
+  if (rc) return rc;
+  if (workspace_bytes < lik_ws(d, B, T).total) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
+  int n_spks; float bmin, bmax, pe;
+  gt_internal_consts(d, &n_spks, &bmin, &bmax, &pe);
+  if (n_spks > 1 && !spk) return gt_internal_fail(GT_ERR_ARG, "n_spks > 1 needs spk");
+  return GT_OK;
+}
+
+int gt_likelihood_drift_div(gt_decoder* d, const float* x, const float* mask, const float* mu, const float* t,
+                            const float* spk, const float* eps, int64_t B, int64_t T, float* drift, float* div,
+                            void* workspace, size_t workspace_bytes, void* stream) {
+  if (!x || !t || !drift || !div || !workspace) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  bool dry_only, debug;
+  int rc = lik_common(d, mask, mu, spk, eps, B, T, workspace_bytes, &dry_only, &debug);
+  if (rc) return rc;
+  const LikWs w = lik_ws(d, B, T);
+  uint8_t* base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  rc = drift_div_pass(d, x, mask, mu, t, spk, eps, B, T, drift, div, base, w, (hipStream_t)stream, true, false);
+  if (rc || dry_only) return rc;
+  return drift_div_pass(d, x, mask, mu, t, spk, eps, B, T, drift, div, base, w, (hipStream_t)stream, false, debug);
+}
+
+int gt_likelihood_euler(gt_decoder* d, const float* data, const float* mask, const float* mu, const float* spk,
+                        const float* eps, int64_t B, int64_t T, int32_t n_steps, float* z, float* delta_logp,
+                        void* workspace, size_t workspace_bytes, void* stream) {
+  if (!data || !z || !delta_logp || !workspace || n_steps <= 0) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  bool dry_only, debug;
+  int rc = lik_common(d, mask, mu, spk, eps, B, T, workspace_bytes, &dry_only, &debug);
+  if (rc) return rc;
+  const LikWs w = lik_ws(d, B, T);
+  uint8_t* base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  double* y = (double*)(base + w.y);
+  double* logp = (double*)(base + w.logp);
+  float* x32 = (float*)(base + w.x32);
+  float* tbuf = (float*)(base + w.tbuf);
+  float* drift = (float*)(base + w.drift);
+  float* div = (float*)(base + w.div);
+  rc = drift_div_pass(d, x32, mask, mu, tbuf, spk, eps, B, T, drift, div, base, w, (hipStream_t)stream, true, false);
+  if (rc || dry_only) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const long n0 = (long)B * 80 * T;
+  const double h = 1.0 / n_steps;
+  hipError_t e = launch_lik_init(data, mask, (int)B, (int)T, y, logp, s);
+  for (int i = 0; i < n_steps && e == hipSuccess; ++i) {
+    e = launch_lik_cast(y, n0, x32, tbuf, (int)B, (float)((i + 0.5) * h), s);   // t = (i + 0.5) h (likelihood.py:104)
+    if (e != hipSuccess) break;
+    rc = drift_div_pass(d, x32, mask, mu, tbuf, spk, eps, B, T, drift, div, base, w, s, false, debug);
+    if (rc) return rc;
+    e = launch_lik_step(y, drift, n0, h, logp, div, (int)B, s);
+  }
+  if (e == hipSuccess) e = launch_lik_out(y, n0, logp, (int)B, z, delta_logp, s);
+  if (e != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("likelihood Euler: ") + hipGetErrorString(e));
+  return GT_OK;
 }
 
 }  // extern "C"

@@ -56,6 +56,14 @@ SIGNATURES = [
     ("gt_decoder_grad_numel", _c.c_int64, [_c.c_void_p]),
     ("gt_diffusion_loss_grad", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 6 + [_c.c_int64, _c.c_int64] +
      [_c.c_void_p] * 5 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_estimator_vjp_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
+    ("gt_estimator_vjp", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 6 + [_c.c_int64, _c.c_int64] +
+     [_c.c_void_p] * 2 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_likelihood_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
+    ("gt_likelihood_drift_div", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 6 + [_c.c_int64, _c.c_int64] +
+     [_c.c_void_p] * 2 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_likelihood_euler", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 5 + [_c.c_int64, _c.c_int64, _c.c_int32] +
+     [_c.c_void_p] * 2 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_alignment_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_log_prior_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
                                              _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,

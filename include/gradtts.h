@@ -150,6 +150,30 @@ int gt_diffusion_loss_grad(gt_decoder* dec, const float* x0, const float* mask, 
                            const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, float* grads,
                            float* dmu, float* dspk, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Estimator VJP (fp32), the building block of the likelihood's Hutchinson divergence (SURVEY §8 f3;
+ * n_best/likelihood/likelihood.py:27-38 takes it with torch.autograd.grad): score [B,80,T] = the estimator
+ * output on (x, mask, mu, t, spk) (NULL: not written); vjp_x [B,80,T] = (d score / d x)^T v.
+ * workspace: gt_estimator_vjp_workspace_bytes. */
+size_t gt_estimator_vjp_workspace_bytes(gt_decoder* dec, int64_t B, int64_t T);
+int gt_estimator_vjp(gt_decoder* dec, const float* x, const float* mask, const float* mu, const float* t,
+                     const float* spk, const float* v, int64_t B, int64_t T, float* score, float* vjp_x,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Likelihood of a mel under SPEECHSDE's probability-flow ODE (n_best/likelihood/likelihood.py:41-133,
+ * sde_lib.py:256-297), fp32 evaluations:
+ * gt_likelihood_drift_div: one ODE evaluation = likelihood_fn's ode_func (likelihood.py:92-97): drift [B,80,T]
+ *   = drift_fn(x, t) (:61-65) and div [B] = the Hutchinson divergence of drift_fn with probe eps (:27-38, 67-68).
+ * gt_likelihood_euler: the euler > 0 branch (:99-115) on the device: state in fp64 as the reference's numpy
+ *   state, t_i = (i + 0.5) / n_steps, from data * mask; returns z [B,80,T] and delta_logp [B] (fp32).
+ * workspace (both): gt_likelihood_workspace_bytes. */
+size_t gt_likelihood_workspace_bytes(gt_decoder* dec, int64_t B, int64_t T);
+int gt_likelihood_drift_div(gt_decoder* dec, const float* x, const float* mask, const float* mu, const float* t,
+                            const float* spk, const float* eps, int64_t B, int64_t T, float* drift, float* div,
+                            void* workspace, size_t workspace_bytes, void* stream);
+int gt_likelihood_euler(gt_decoder* dec, const float* data, const float* mask, const float* mu, const float* spk,
+                        const float* eps, int64_t B, int64_t T, int32_t n_steps, float* z, float* delta_logp,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
 /* The alignment step of GradTTS.compute_loss (model/tts.py:141-152) in one call: the log-prior of mu_x
  * [B,n_feats,Tx] against y [B,n_feats,Ty] (three fp32 contractions + const, tts.py:143-149), masked with
  * x_mask [B,Tx] (x) y_mask [B,Ty], then maximum_path on device (t_x, t_y from the masks). paths: [B,Tx,Ty]

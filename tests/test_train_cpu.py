@@ -55,3 +55,34 @@ def test_grad_numel_matches_state_dict():
         assert L.gt_decoder_grad_numel(h) == n
     finally:
         L.gt_decoder_destroy(h)
+
+
+@pytest.mark.parametrize("n_spks,B,T", [(1, 2, 32), (247, 3, 24)])
+def test_vjp_and_likelihood_extents(monkeypatch, n_spks, B, T):
+    monkeypatch.setenv("GT_TRAIN_DEBUG", "2")
+    L, h = _decoder(n_spks)
+    try:
+        n0 = B * 80 * T
+        x, mu, v, out1, out2 = (np.zeros(n0, np.float32) for _ in range(5))
+        mask, t = np.ones(B * T, np.float32), np.full(B, 0.5, np.float32)
+        spk, div = np.zeros(B * 64, np.float32), np.zeros(B, np.float32)
+        p = lambda a: a.ctypes.data
+        sp = p(spk) if n_spks > 1 else None
+        ws = L.gt_estimator_vjp_workspace_bytes(h, B, T)
+        work = np.zeros(ws, np.uint8)
+        rc = L.gt_estimator_vjp(h, p(x), p(mask), p(mu), p(t), sp, p(v), B, T, p(out1), p(out2), p(work), ws, None)
+        msg = L.gt_last_error()
+        assert rc == 0, msg.decode() if msg else rc
+        ws = L.gt_likelihood_workspace_bytes(h, B, T)
+        work = np.zeros(ws, np.uint8)
+        rc = L.gt_likelihood_drift_div(h, p(x), p(mask), p(mu), p(t), sp, p(v), B, T, p(out1), p(div), p(work), ws,
+                                       None)
+        msg = L.gt_last_error()
+        assert rc == 0, msg.decode() if msg else rc
+        rc = L.gt_likelihood_euler(h, p(x), p(mask), p(mu), sp, p(v), B, T, 4, p(out1), p(div), p(work), ws, None)
+        msg = L.gt_last_error()
+        assert rc == 0, msg.decode() if msg else rc
+        assert L.gt_likelihood_euler(h, p(x), p(mask), p(mu), sp, p(v), B, T, 4, p(out1), p(div), p(work), ws - 1,
+                                     None) == 5
+    finally:
+        L.gt_decoder_destroy(h)
