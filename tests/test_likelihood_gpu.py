@@ -113,3 +113,44 @@ def test_likelihood_blackbox_rk45_runs_and_agrees_with_euler():
     bpd_eu, _, dl_eu, _ = get_likelihood_fn(sde, euler=200)(dec.estimator, c(x), epsilon=c(eps))
     assert torch.isfinite(bpd_rk).all()
     report("likelihood RK45 vs Euler-200 bpd", float(abs(bpd_rk - bpd_eu).max() / abs(bpd_eu).max()), 2e-2)
+
+
+def test_likelihood_speed_vs_torch_eager():
+    """Report (no gate) the n-best rescoring workload of the reference (n_best/config/generate_scores.yaml:
+    n_euler = 10; a batch of 16 hypotheses of 172 frames) against the reference's own algorithm run eagerly on the
+    same GPU (torch autograd for the divergence, numpy fp64 state between steps as likelihood.py:92-107)."""
+    import time
+    from oracle import decoder as odec, likelihood as olik
+    B, T, N = 16, 172, 10
+    x, mu, mask, eps, _, _ = _case(13, B, T, None, 1)
+    dec, sd = make_decoder(1, 0, torch.float32)
+    c = lambda a: torch.from_numpy(a).cuda()
+    sde = SPEECHSDE(0.05, 20.0, 1000, c(mu), None, c(mask))
+    fn = get_likelihood_fn(sde, euler=N)
+    ours = lambda: fn(dec.estimator, c(x), epsilon=c(eps))
+    p = {k: v_.cuda() for k, v_ in odec.to_torch_params(sd).items()}
+    mu_d, mask_d, eps_d = c(mu), c(mask), c(eps)
+
+    def eager():
+        y = np.concatenate([(x * mask).reshape(-1).astype(np.float64), np.zeros((B,))])
+        for i in range(N):
+            t = (i + 0.5) / N
+            sample = torch.from_numpy(y[:-B].reshape(x.shape)).cuda().float()
+            vt = torch.ones(B, device="cuda") * t
+            dr = olik.drift_fn(p, sample, mask_d, mu_d, vt)
+            dv = olik.div_fn(p, sample, mask_d, mu_d, vt, eps_d)
+            y = y + np.concatenate([dr.detach().cpu().numpy().reshape(-1), dv.cpu().numpy()]) * (1 / N)
+        return y
+
+    def timed(f, n=3):
+        f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            f()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
+
+    ms_ours, ms_eager = timed(ours), timed(eager)
+    report(f"likelihood B={B} T={T} n_euler={N}: ours {ms_ours:.1f} ms, torch eager {ms_eager:.1f} ms; "
+           f"ratio eager/ours", ms_eager / ms_ours, 0.0, gate=False, ms_ours=ms_ours, ms_eager=ms_eager)
