@@ -1,0 +1,41 @@
+// Text encoder kernels (textenc.hip): parameter blocks and launchers. fp32, channels-last [B][T][C].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gt {
+
+// conv1d (Conv1d, weight [Cout][Cin][K], padding pad) on fp32 MFMA; epilogue: + bias, ReLU, + residual, * mask
+struct C1dParams {
+  const float* in; int in_cs;          // input [B][T][in_cs], channels [0, Cin)
+  const float* in_mask;                // multiply the input by mask[b][t] (null: no mask)
+  const float* w; const float* bias;
+  int B, T, Cin, Cout, K, pad;
+  float* out; int out_cs, out_c0;      // channels-last output, or channel-major [B][Cout][T] if chan_major
+  int chan_major, relu;
+  const float* res; int res_cs;        // out = res + conv (after bias / ReLU)
+  const float* out_mask;
+};
+hipError_t launch_c1d(const C1dParams& p, hipStream_t s);
+
+// LayerNorm over channels (text_encoder.py:11-29): out = LN(x (+ res)) * gamma + beta, then ReLU, then * mask
+hipError_t launch_te_ln(const float* x, int x_cs, const float* res, int res_cs, const float* gamma, const float* beta,
+                        long npos, int C, float eps, int relu_after, const float* mask, float* out, int out_cs,
+                        hipStream_t s);
+
+// tokens outside [0, n_vocab) embed as NaN (the reference raises an index error) instead of reading out of range
+hipError_t launch_te_embed(const int64_t* tokens, const int64_t* lengths, const float* emb, int n_vocab, int B, int T,
+                           int C, float scale, float* x, float* x_mask, hipStream_t s);
+
+// relative-position multi-head self-attention core (text_encoder.py:145-174), head dim 96, window <= 8:
+// qkv [B][T][3C] (q | k | v), out [B][T][C]
+hipError_t launch_te_attn(const float* qkv, const float* x_mask, const float* erk, const float* erv, int B, int T, int C,
+                          int H, int W, float* out, hipStream_t s);
+
+// GradTTS.forward front-end (tts.py:86-101)
+hipError_t launch_te_durations(const float* logw, const float* x_mask, int B, int Tx, float length_scale, float* w_ceil,
+                               float* cum, int64_t* y_lengths, hipStream_t s);
+hipError_t launch_te_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int B,
+                            int Tx, int Ty, int F, float* mu_y, float* y_mask, float* attn, hipStream_t s);
+
+}  // namespace gt

@@ -1,0 +1,302 @@
+// Text encoder of GradTTS (model/text_encoder.py:285-335) and the front-end of GradTTS.forward
+// (model/tts.py:86-101, utils.py:6-39) for gfx950. fp32 (the reference's inference precision), activations
+// channels-last [B][T][C]:
+//
+//   c1d_kernel      every Conv1d (prenet k5, FFN k3, duration predictor k3, the 1x1 q/k/v/o and projections) as an
+//                   implicit GEMM on v_mfma_f32_32x32x2_f32: 64 frames x 64 output channels per workgroup, 16-channel
+//                   chunks of the input (+ K - 1 halo frames) and of the weights in LDS; the epilogue adds the bias,
+//                   ReLU, the residual and the mask, and writes channels-last or channel-major (mu_x, logw)
+//   te_ln_kernel    LayerNorm over channels (+ residual, + ReLU, * mask), one wave per frame
+//   te_attn_kernel  relative-position attention: 16 query frames per workgroup, 64-frame key/value tiles in LDS,
+//                   online softmax; the relative key logits and value terms (|j - i| <= window) from LDS copies
+//                   of emb_rel_k / emb_rel_v; masked_fill(-1e4) semantics kept (padded rows average all keys)
+//   te_durations / te_expand   durations, y_lengths, generate_path and mu_y = attn^T mu_x as a gather
+#include <math.h>
+
+#include "common.h"
+#include "textenc.h"
+
+namespace gt {
+
+GT_DEV float wave_sum(float x) {   // butterfly over the 64 lanes (every lane gets the total)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+constexpr int C1_KC = 16;
+__global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
+  __shared__ float s_in[64 + 4][C1_KC + 1];
+  __shared__ float s_w[C1_KC][5][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_tt = (p.T + 63) / 64;
+  const int tt = blockIdx.x % n_tt, b = blockIdx.x / n_tt;
+  const int t0 = tt * 64, a0 = blockIdx.y * 64;
+  const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
+  const int K = p.K, NP = 64 + K - 1;
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int c0 = 0; c0 < p.Cin; c0 += C1_KC) {
+    __syncthreads();
+    for (int i = tid; i < NP * C1_KC; i += 256) {
+      const int c = i & (C1_KC - 1), pp = i / C1_KC;
+      const int t = t0 - p.pad + pp, ci = c0 + c;
+      float v = 0.f;
+      if (t >= 0 && t < p.T && ci < p.Cin) {
+        v = p.in[((long)b * p.T + t) * p.in_cs + ci];
+        if (p.in_mask) v *= p.in_mask[(long)b * p.T + t];
+      }
+      s_in[pp][c] = v;
+    }
+    for (int i = tid; i < 64 * C1_KC * K; i += 256) {   // contiguous along (c, k) for a fixed output channel
+      const int k = i % K, rest = i / K, c = rest % C1_KC, a = rest / C1_KC;
+      s_w[c][k][a] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[((long)(a0 + a) * p.Cin + c0 + c) * K + k] : 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int cp = 0; cp < C1_KC / 2; ++cp) {
+        const int c = 2 * cp + hh;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[pb + r + k][c], s_w[c][k][cb + r], acc, 0, 0, 0);
+      }
+  }
+  const int o = a0 + cb + r;
+  if (o >= p.Cout) return;
+  const float bias = p.bias ? p.bias[o] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int t = t0 + pb + acc_row(j, hh);
+    if (t >= p.T) continue;
+    float v = acc[j] + bias;
+    if (p.relu) v = fmaxf(v, 0.f);
+    if (p.res) v = p.res[((long)b * p.T + t) * p.res_cs + o] + v;
+    if (p.out_mask) v *= p.out_mask[(long)b * p.T + t];
+    if (p.chan_major) p.out[((long)b * p.Cout + o) * p.T + t] = v;
+    else p.out[((long)b * p.T + t) * p.out_cs + p.out_c0 + o] = v;
+  }
+}
+
+hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
+  if (p.K < 1 || p.K > 5) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(p.B * ((p.T + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
+  hipLaunchKernelGGL(c1d_kernel, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- LayerNorm
+__global__ __launch_bounds__(256) void te_ln_kernel(const float* x, int x_cs, const float* res, int res_cs,
+                                                    const float* gamma, const float* beta, long npos, int C, float eps,
+                                                    int relu_after, const float* mask, float* out, int out_cs) {
+  const long pos = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pos >= npos) return;
+  float v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = lane + 64 * k;
+    v[k] = 0.f;
+    if (c < C) {
+      v[k] = x[pos * x_cs + c];
+      if (res) v[k] = v[k] + res[pos * res_cs + c];
+      s += v[k];
+    }
+  }
+  s = wave_sum(s);
+  const float mean = s / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (lane + 64 * k < C) q += (v[k] - mean) * (v[k] - mean);
+  q = wave_sum(q);
+  const float rs = rsqrtf(q / (float)C + eps);
+  const float m = mask ? mask[pos] : 1.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = lane + 64 * k;
+    if (c >= C) continue;
+    float y = (v[k] - mean) * rs * gamma[c] + beta[c];
+    if (relu_after) y = fmaxf(y, 0.f);
+    out[pos * out_cs + c] = y * m;
+  }
+}
+
+hipError_t launch_te_ln(const float* x, int x_cs, const float* res, int res_cs, const float* gamma, const float* beta,
+                        long npos, int C, float eps, int relu_after, const float* mask, float* out, int out_cs,
+                        hipStream_t s) {
+  if (C > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(te_ln_kernel, dim3((unsigned)((npos + 3) / 4)), dim3(256), 0, s, x, x_cs, res, res_cs, gamma, beta,
+                     npos, C, eps, relu_after, mask, out, out_cs);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- embedding + x_mask (text_encoder.py:322-324)
+__global__ void te_embed_kernel(const int64_t* tokens, const int64_t* lengths, const float* emb, int n_vocab, int B,
+                                int T, int C, float scale, float* x, float* x_mask) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)B * T * C) return;
+  const long pos = i / C;
+  const int c = (int)(i % C);
+  const int b = (int)(pos / T), t = (int)(pos % T);
+  const int64_t tok = tokens[pos];
+  x[i] = (tok >= 0 && tok < n_vocab) ? emb[tok * C + c] * scale : __builtin_nanf("");   // out of range: NaN, no read
+  if (c == 0) x_mask[pos] = t < lengths[b] ? 1.f : 0.f;
+}
+
+hipError_t launch_te_embed(const int64_t* tokens, const int64_t* lengths, const float* emb, int n_vocab, int B, int T,
+                           int C, float scale, float* x, float* x_mask, hipStream_t s) {
+  const long n = (long)B * T * C;
+  hipLaunchKernelGGL(te_embed_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tokens, lengths, emb, n_vocab,
+                     B, T, C, scale, x, x_mask);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- attention
+constexpr int TA_Q = 16, TA_KT = 64, TA_D = 96, TA_WMAX = 17;
+__global__ __launch_bounds__(256) void te_attn_kernel(const float* qkv, const float* x_mask, const float* erk,
+                                                      const float* erv, int T, int C, int W, float* out) {
+  __shared__ float s_q[TA_Q][TA_D + 1], s_k[TA_KT][TA_D + 1], s_v[TA_KT][TA_D];
+  __shared__ float s_ek[TA_WMAX][TA_D + 1], s_ev[TA_WMAX][TA_D];
+  __shared__ float s_s[TA_Q][TA_KT + 1], s_win[TA_Q][TA_WMAX];
+  const int tid = threadIdx.x, i0 = blockIdx.x * TA_Q, h = blockIdx.y, b = blockIdx.z;
+  const int row = tid >> 4, g = tid & 15;   // query row of this thread; 6 output dims / 4 keys per thread
+  const int i = i0 + row, nw = 2 * W + 1, C3 = 3 * C;
+  const float* base = qkv + (long)b * T * C3;
+  const float sq = sqrtf((float)TA_D);
+  for (int e = tid; e < TA_Q * TA_D; e += 256) {
+    const int rr = e / TA_D, d = e % TA_D;
+    s_q[rr][d] = i0 + rr < T ? base[(long)(i0 + rr) * C3 + h * TA_D + d] : 0.f;
+  }
+  for (int e = tid; e < nw * TA_D; e += 256) {
+    s_ek[e / TA_D][e % TA_D] = erk[e];
+    s_ev[e / TA_D][e % TA_D] = erv[e];
+  }
+  for (int e = tid; e < TA_Q * TA_WMAX; e += 256) s_win[e / TA_WMAX][e % TA_WMAX] = -INFINITY;
+  const float xi = i < T ? x_mask[(long)b * T + i] : 0.f;
+  float m = -INFINITY, l = 0.f, o[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < T; j0 += TA_KT) {
+    __syncthreads();
+    for (int e = tid; e < TA_KT * TA_D; e += 256) {
+      const int jj = e / TA_D, d = e % TA_D;
+      const bool ok = j0 + jj < T;
+      s_k[jj][d] = ok ? base[(long)(j0 + jj) * C3 + C + h * TA_D + d] : 0.f;
+      s_v[jj][d] = ok ? base[(long)(j0 + jj) * C3 + 2 * C + h * TA_D + d] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int jj = g * 4 + e, j = j0 + jj;
+      float sc = -INFINITY;   // frames past T are not keys
+      if (j < T) {
+        float dot = 0.f;
+        for (int d = 0; d < TA_D; ++d) dot = fmaf(s_q[row][d], s_k[jj][d], dot);
+        sc = dot / sq;
+        const int rel = j - i;
+        if (rel >= -W && rel <= W) {
+          float dr = 0.f;
+          for (int d = 0; d < TA_D; ++d) dr = fmaf(s_q[row][d], s_ek[rel + W][d], dr);
+          sc = sc + dr / sq;
+        }
+        if (!(xi != 0.f && x_mask[(long)b * T + j] != 0.f)) sc = -1e4f;   // masked_fill(mask == 0, -1e4)
+        if (rel >= -W && rel <= W) s_win[row][rel + W] = sc;
+      }
+      s_s[row][jj] = sc;
+    }
+    __syncthreads();
+    float mt = m;
+    for (int jj = 0; jj < TA_KT; ++jj) mt = fmaxf(mt, s_s[row][jj]);
+    const float corr = __expf(m - mt);   // m = -inf on the first tile: corr = 0, l = o = 0 anyway
+    float lt = 0.f, ot[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int jj = 0; jj < TA_KT; ++jj) {
+      const float pj = __expf(s_s[row][jj] - mt);
+      lt += pj;
+#pragma unroll
+      for (int dd = 0; dd < 6; ++dd) ot[dd] = fmaf(pj, s_v[jj][g * 6 + dd], ot[dd]);
+    }
+    l = l * corr + lt;
+#pragma unroll
+    for (int dd = 0; dd < 6; ++dd) o[dd] = o[dd] * corr + ot[dd];
+    m = mt;
+  }
+  if (i >= T) return;
+  const float il = 1.f / l;
+#pragma unroll
+  for (int dd = 0; dd < 6; ++dd) o[dd] *= il;
+  for (int w = 0; w < nw; ++w) {
+    const float sw = s_win[row][w];
+    if (sw == -INFINITY) continue;
+    const float pw = __expf(sw - m) * il;
+#pragma unroll
+    for (int dd = 0; dd < 6; ++dd) o[dd] = fmaf(pw, s_ev[w][g * 6 + dd], o[dd]);
+  }
+#pragma unroll
+  for (int dd = 0; dd < 6; ++dd) out[((long)b * T + i) * C + h * TA_D + g * 6 + dd] = o[dd];
+}
+
+hipError_t launch_te_attn(const float* qkv, const float* x_mask, const float* erk, const float* erv, int B, int T, int C,
+                          int H, int W, float* out, hipStream_t s) {
+  if (C != H * TA_D || 2 * W + 1 > TA_WMAX) return hipErrorInvalidValue;
+  // erk / erv: [2W + 1][96] per layer (heads share them, text_encoder.py:119-124)
+  hipLaunchKernelGGL(te_attn_kernel, dim3((unsigned)((T + TA_Q - 1) / TA_Q), H, B), dim3(256), 0, s, qkv, x_mask, erk, erv,
+                     T, C, W, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- durations, generate_path, mu_y
+// per utterance, in frame order: w = exp(logw) m; w_ceil = ceil(w) * length_scale; cum = cumsum(w_ceil);
+// y_length = max(1, (long) sum(w_ceil))   (tts.py:86-89, utils.py:29)
+__global__ void te_durations_kernel(const float* logw, const float* x_mask, int B, int Tx, float ls, float* w_ceil,
+                                    float* cum, int64_t* y_lengths) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  float c = 0.f;
+  for (int t = 0; t < Tx; ++t) {
+    const long i = (long)b * Tx + t;
+    const float w = __expf(logw[i]) * x_mask[i];
+    const float wc = ceilf(w) * ls;
+    w_ceil[i] = wc;
+    c += wc;
+    cum[i] = c;
+  }
+  y_lengths[b] = (int64_t)fmaxf(c, 1.f);
+}
+
+// per output frame j: the token i* with cum[i*-1] <= j < cum[i*] (generate_path's one nonzero in column j), if
+// x_mask[i*] y_mask[j]; mu_y[:, j] = mu_x[:, i*] (the matmul with a 0/1 column is exact), y_mask, attn
+__global__ void te_expand_kernel(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths,
+                                 int B, int Tx, int Ty, int F, float* mu_y, float* y_mask, float* attn) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)B * Ty) return;
+  const int b = (int)(e / Ty), j = (int)(e % Ty);
+  const float* cb = cum + (long)b * Tx;
+  const float jf = (float)j;
+  int lo = 0, hi = Tx;   // first i with jf < cum[i]
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (jf < cb[mid]) hi = mid; else lo = mid + 1;
+  }
+  const float ym = j < y_lengths[b] ? 1.f : 0.f;
+  y_mask[e] = ym;
+  const bool on = lo < Tx && ym != 0.f && x_mask[(long)b * Tx + lo] != 0.f;
+  for (int f = 0; f < F; ++f) mu_y[((long)b * F + f) * Ty + j] = on ? mu_x[((long)b * F + f) * Tx + lo] : 0.f;
+  if (attn)
+    for (int t = 0; t < Tx; ++t) attn[((long)b * Tx + t) * Ty + j] = (on && t == lo) ? 1.f : 0.f;
+}
+
+hipError_t launch_te_durations(const float* logw, const float* x_mask, int B, int Tx, float length_scale, float* w_ceil,
+                               float* cum, int64_t* y_lengths, hipStream_t s) {
+  hipLaunchKernelGGL(te_durations_kernel, dim3((B + 63) / 64), dim3(64), 0, s, logw, x_mask, B, Tx, length_scale, w_ceil,
+                     cum, y_lengths);
+  return hipGetLastError();
+}
+
+hipError_t launch_te_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int B,
+                            int Tx, int Ty, int F, float* mu_y, float* y_mask, float* attn, hipStream_t s) {
+  const long n = (long)B * Ty;
+  hipLaunchKernelGGL(te_expand_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mu_x, cum, x_mask, y_lengths, B,
+                     Tx, Ty, F, mu_y, y_mask, attn);
+  return hipGetLastError();
+}
+
+}  // namespace gt

@@ -64,6 +64,17 @@ SIGNATURES = [
      [_c.c_void_p] * 2 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_likelihood_euler", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 5 + [_c.c_int64, _c.c_int64, _c.c_int32] +
      [_c.c_void_p] * 2 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_text_encoder_create", _c.c_int, [_c.c_int] * 9 + [_c.c_void_p]),
+    ("gt_text_encoder_destroy", None, [_c.c_void_p]),
+    ("gt_text_encoder_num_params", _c.c_int, [_c.c_void_p]),
+    ("gt_text_encoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),
+    ("gt_text_encoder_param_numel", _c.c_int64, [_c.c_void_p, _c.c_int]),
+    ("gt_text_encoder_set_param", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_void_p, _c.c_int64]),
+    ("gt_text_encoder_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
+    ("gt_text_encoder_forward", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 2 + [_c.c_int64, _c.c_int64] +
+     [_c.c_void_p] * 3 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+    ("gt_durations", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_float] + [_c.c_void_p] * 4),
+    ("gt_expand", _c.c_int, [_c.c_void_p] * 4 + [_c.c_int64] * 3 + [_c.c_int32] + [_c.c_void_p] * 4),
     ("gt_alignment_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_log_prior_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
                                              _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,

@@ -177,3 +177,83 @@ def estimator_flops(B: int, T: int, n_spks: int = 1) -> int:
     if n_spks > 1:
         return B * (134_256_640 * T + 368_640)
     return B * (134_154_240 * T + 294_912)
+
+
+# ---- text encoder (model/text_encoder.py:285-335; GradTTS builds it speaker-agnostic, tts.py:49-51) ----------
+def text_encoder_param_shapes(n_vocab: int = 149, n_feats: int = 80, n_channels: int = 192,
+                              filter_channels: int = 768, filter_channels_dp: int = 256, n_heads: int = 2,
+                              n_layers: int = 6, kernel_size: int = 3, window_size: int = 4):
+    """state_dict keys and shapes of the reference TextEncoder, in its registration order (the order
+    tests/golden/gradtts_layout.json records from the real module, without the ``encoder.`` prefix)."""
+    C, kc = n_channels, n_channels // n_heads
+    out = OrderedDict()
+    out["emb.weight"] = (n_vocab, C)
+    for i in range(3):
+        out[f"prenet.conv_layers.{i}.weight"] = (C, C, 5)
+        out[f"prenet.conv_layers.{i}.bias"] = (C,)
+    for i in range(3):
+        out[f"prenet.norm_layers.{i}.gamma"] = (C,)
+        out[f"prenet.norm_layers.{i}.beta"] = (C,)
+    out["prenet.proj.weight"] = (C, C, 1)
+    out["prenet.proj.bias"] = (C,)
+    for l in range(n_layers):
+        p = f"encoder.attn_layers.{l}."
+        out[p + "emb_rel_k"] = (1, 2 * window_size + 1, kc)
+        out[p + "emb_rel_v"] = (1, 2 * window_size + 1, kc)
+        for n in ("conv_q", "conv_k", "conv_v", "conv_o"):
+            out[p + n + ".weight"] = (C, C, 1)
+            out[p + n + ".bias"] = (C,)
+    for l in range(n_layers):
+        out[f"encoder.norm_layers_1.{l}.gamma"] = (C,)
+        out[f"encoder.norm_layers_1.{l}.beta"] = (C,)
+    for l in range(n_layers):
+        p = f"encoder.ffn_layers.{l}."
+        out[p + "conv_1.weight"] = (filter_channels, C, kernel_size)
+        out[p + "conv_1.bias"] = (filter_channels,)
+        out[p + "conv_2.weight"] = (C, filter_channels, kernel_size)
+        out[p + "conv_2.bias"] = (C,)
+    for l in range(n_layers):
+        out[f"encoder.norm_layers_2.{l}.gamma"] = (C,)
+        out[f"encoder.norm_layers_2.{l}.beta"] = (C,)
+    out["proj_m.weight"] = (n_feats, C, 1)
+    out["proj_m.bias"] = (n_feats,)
+    Fd = filter_channels_dp
+    out["proj_w.conv_1.weight"] = (Fd, C, kernel_size)
+    out["proj_w.conv_1.bias"] = (Fd,)
+    out["proj_w.norm_1.gamma"] = (Fd,)
+    out["proj_w.norm_1.beta"] = (Fd,)
+    out["proj_w.conv_2.weight"] = (Fd, Fd, kernel_size)
+    out["proj_w.conv_2.bias"] = (Fd,)
+    out["proj_w.norm_2.gamma"] = (Fd,)
+    out["proj_w.norm_2.beta"] = (Fd,)
+    out["proj_w.proj.weight"] = (1, Fd, 1)
+    out["proj_w.proj.bias"] = (1,)
+    return out
+
+
+def synthetic_text_encoder_state_dict(seed: int = 0, **kw) -> "OrderedDict[str, np.ndarray]":
+    """Deterministic synthetic TextEncoder weights (float32), one PCG64 stream in key order:
+    convs U(-1/sqrt(fan_in), +) (torch's default bound; the prenet projection too, which the reference zero-inits,
+    so the path is exercised); LayerNorm gamma = 1 + 0.1 U(-1,1), beta = 0.1 U(-1,1); the embedding
+    U(-sqrt(3/C), +) (the variance of the reference's N(0, 1/C)); relative embeddings U(-1/sqrt(k_c), +)."""
+    rng = np.random.default_rng(seed)
+    out: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    last_fan = 1
+    for key, shape in text_encoder_param_shapes(**kw).items():
+        if key.endswith((".gamma", ".beta")):
+            u = rng.uniform(-1.0, 1.0, size=shape)
+            arr = (1.0 + 0.1 * u) if key.endswith("gamma") else 0.1 * u
+        elif key == "emb.weight":
+            arr = rng.uniform(-1.0, 1.0, size=shape) * np.sqrt(3.0 / shape[1])
+        elif "emb_rel" in key:
+            b = 1.0 / np.sqrt(shape[-1])
+            arr = rng.uniform(-b, b, size=shape)
+        elif key.endswith("weight"):
+            last_fan = _fan_in(shape)
+            b = 1.0 / np.sqrt(last_fan)
+            arr = rng.uniform(-b, b, size=shape)
+        else:
+            b = 1.0 / np.sqrt(last_fan)
+            arr = rng.uniform(-b, b, size=shape)
+        out[key] = np.ascontiguousarray(arr.astype(np.float32))
+    return out

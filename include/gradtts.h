@@ -174,6 +174,31 @@ int gt_likelihood_euler(gt_decoder* dec, const float* data, const float* mask, c
                         const float* eps, int64_t B, int64_t T, int32_t n_steps, float* z, float* delta_logp,
                         void* workspace, size_t workspace_bytes, void* stream);
 
+/* Text encoder of GradTTS (model/text_encoder.py:285-335; speaker-agnostic as GradTTS builds it, tts.py:49-51) and
+ * the front-end of GradTTS.forward (tts.py:84-101). fp32. Parameters by the reference TextEncoder's state_dict
+ * names (host data, uploaded on the next forward after a change). gt_text_encoder_forward = TextEncoder.forward:
+ * tokens / x_lengths int64 [B,Tx] / [B]; outputs mu_x [B,n_feats,Tx], logw [B,1,Tx], x_mask [B,1,Tx].
+ * gt_durations: w_ceil = ceil(exp(logw) x_mask) * length_scale, cum = cumsum(w_ceil), y_lengths =
+ * max(1, (long) sum w_ceil) (tts.py:86-89). gt_expand: y_mask, generate_path's alignment (attn [B,Tx,Ty] fp32, NULL:
+ * not written) and mu_y = attn^T mu_x [B,n_feats,Ty] (tts.py:93-99, utils.py:26-39); Ty = fix_len_compatibility(max
+ * y_lengths) is the caller's (it needs y_lengths on the host, as the reference's int(y_lengths.max()) does). */
+typedef struct gt_text_encoder gt_text_encoder;
+int gt_text_encoder_create(int n_vocab, int n_feats, int n_channels, int filter_channels, int filter_channels_dp,
+                           int n_heads, int n_layers, int kernel_size, int window_size, gt_text_encoder** out);
+void gt_text_encoder_destroy(gt_text_encoder* enc);
+int gt_text_encoder_num_params(gt_text_encoder* enc);
+const char* gt_text_encoder_param_name(gt_text_encoder* enc, int i);
+int64_t gt_text_encoder_param_numel(gt_text_encoder* enc, int i);
+int gt_text_encoder_set_param(gt_text_encoder* enc, const char* name, const float* data, int64_t numel);
+size_t gt_text_encoder_workspace_bytes(gt_text_encoder* enc, int64_t B, int64_t Tx);
+int gt_text_encoder_forward(gt_text_encoder* enc, const int64_t* tokens, const int64_t* x_lengths, int64_t B,
+                            int64_t Tx, float* mu_x, float* logw, float* x_mask, void* workspace,
+                            size_t workspace_bytes, void* stream);
+int gt_durations(const float* logw, const float* x_mask, int64_t B, int64_t Tx, float length_scale, float* w_ceil,
+                 float* cum, int64_t* y_lengths, void* stream);
+int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int64_t B,
+              int64_t Tx, int64_t Ty, int32_t n_feats, float* mu_y, float* y_mask, float* attn, void* stream);
+
 /* The alignment step of GradTTS.compute_loss (model/tts.py:141-152) in one call: the log-prior of mu_x
  * [B,n_feats,Tx] against y [B,n_feats,Ty] (three fp32 contractions + const, tts.py:143-149), masked with
  * x_mask [B,Tx] (x) y_mask [B,Ty], then maximum_path on device (t_x, t_y from the masks). paths: [B,Tx,Ty]
