@@ -23,7 +23,7 @@ OPS_OUT = os.path.join(HERE, "gradtts_amd", "libgradtts_ops.so")   # torch.ops.g
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GRADTTS_ARCH", "gfx950")
 SOURCES = ["conv.hip", "conv64.hip", "attn.hip", "misc.hip", "mas.hip", "train.hip", "bwd.hip", "textenc.hip",
-           "decoder.cpp", "train_bwd.cpp", "textenc.cpp"]
+           "decoder.cpp", "train_bwd.cpp", "textenc.cpp", "vocoder.cpp"]
 # -packed-fp32-ops: keep the compiler from emitting v_pk_{fma,add,mul}_f32. Round 1: with them the GroupNorm
 # sum-of-squares chain of the old LDS-transposing epilogue gave timing-dependent results. Round 2 (register
 # epilogue): the bf16 / fp32 paths are bit-reproducible with them (tools/diag_pk.sh, diag_pk2.sh: 30/30 stages

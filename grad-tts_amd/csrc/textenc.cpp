@@ -168,9 +168,10 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
   const long npos = (long)B * T;
   auto conv = [&](const float* in, int cin, int in_cs, const float* in_mask, const std::string& key, int cout, int k,
                   float* out, int out_cs, int out_c0, int relu, const float* res, const float* out_mask, int chan_major) {
-    C1dParams p{};
+    C1dParams p = c1d_defaults();
     p.in = in; p.in_cs = in_cs; p.in_mask = in_mask; p.w = P(key + ".weight"); p.bias = P(key + ".bias");
-    p.B = Bi; p.T = Ti; p.Cin = cin; p.Cout = cout; p.K = k; p.pad = k / 2;
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = cin; p.Cout = cout; p.K = k; p.pad = k / 2;
+    p.wso = (long)cin * k; p.wsc = k;
     p.out = out; p.out_cs = out_cs; p.out_c0 = out_c0; p.chan_major = chan_major; p.relu = relu;
     p.res = res; p.res_cs = C; p.out_mask = out_mask;
     chk(launch_c1d(p, s));
@@ -201,9 +202,10 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
     ln(x, xa, "encoder.norm_layers_1." + std::to_string(l), C, 0, nullptr, xb);          // x = LN(x + y)
     const std::string f = "encoder.ffn_layers." + std::to_string(l) + ".";
     conv(xb, C, C, x_mask, f + "conv_1", e->Fc, e->K, hid, e->Fc, 0, 1, nullptr, nullptr, 0);
-    C1dParams p{};
+    C1dParams p = c1d_defaults();
     p.in = hid; p.in_cs = e->Fc; p.in_mask = x_mask; p.w = P(f + "conv_2.weight"); p.bias = P(f + "conv_2.bias");
-    p.B = Bi; p.T = Ti; p.Cin = e->Fc; p.Cout = C; p.K = e->K; p.pad = e->K / 2;
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fc; p.Cout = C; p.K = e->K; p.pad = e->K / 2;
+    p.wso = (long)e->Fc * e->K; p.wsc = e->K;
     p.out = xa; p.out_cs = C; p.out_mask = x_mask;
     chk(launch_c1d(p, s));
     ln(xb, xa, "encoder.norm_layers_2." + std::to_string(l), C, 0, x_mask, x);         // LN(x + y), * mask
@@ -214,17 +216,19 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
   conv(x, C, C, x_mask, "proj_w.conv_1", e->Fdp, e->K, d1, e->Fdp, 0, 1, nullptr, nullptr, 0);
   ln(d1, nullptr, "proj_w.norm_1", e->Fdp, 0, nullptr, d2);
   {
-    C1dParams p{};
+    C1dParams p = c1d_defaults();
     p.in = d2; p.in_cs = e->Fdp; p.in_mask = x_mask; p.w = P("proj_w.conv_2.weight"); p.bias = P("proj_w.conv_2.bias");
-    p.B = Bi; p.T = Ti; p.Cin = e->Fdp; p.Cout = e->Fdp; p.K = e->K; p.pad = e->K / 2;
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fdp; p.Cout = e->Fdp; p.K = e->K; p.pad = e->K / 2;
+    p.wso = (long)e->Fdp * e->K; p.wsc = e->K;
     p.out = d1; p.out_cs = e->Fdp; p.relu = 1;
     chk(launch_c1d(p, s));
   }
   ln(d1, nullptr, "proj_w.norm_2", e->Fdp, 0, nullptr, d2);
   {
-    C1dParams p{};
+    C1dParams p = c1d_defaults();
     p.in = d2; p.in_cs = e->Fdp; p.in_mask = x_mask; p.w = P("proj_w.proj.weight"); p.bias = P("proj_w.proj.bias");
-    p.B = Bi; p.T = Ti; p.Cin = e->Fdp; p.Cout = 1; p.K = 1; p.pad = 0;
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fdp; p.Cout = 1; p.K = 1; p.pad = 0;
+    p.wso = e->Fdp; p.wsc = 1;
     p.out = logw; p.chan_major = 1; p.out_mask = x_mask;
     chk(launch_c1d(p, s));
   }

@@ -5,17 +5,31 @@
 
 namespace gt {
 
-// conv1d (Conv1d, weight [Cout][Cin][K], padding pad) on fp32 MFMA; epilogue: + bias, ReLU, + residual, * mask
+// conv1d on fp32 MFMA, general enough for the text encoder and the HiFi-GAN generator:
+//   out[row(q)][o] = epi( sum_{j < K, c} W(o, c, j) act(in[q + j dil - pad][c]) ),  row(q) = q out_stride + out_off
+// W(o, c, j) = w[o wso + c wsc + tap0 + j tap_step] (Conv1d [Cout][Cin][K]: wso = Cin K, wsc = K, tap0 = 0,
+// tap_step = 1; one phase r of ConvTranspose1d [Cin][Cout][k]: wso = k, wsc = Cout k, tap0 = r, tap_step = u,
+// dil = -1). act = identity or leaky ReLU(in_slope) (* in_mask). epi: + bias, ReLU, + res, out (+)= ..., / div,
+// tanh, * out_mask.
 struct C1dParams {
-  const float* in; int in_cs;          // input [B][T][in_cs], channels [0, Cin)
+  const float* in; int in_cs;          // input [B][Tin][in_cs] channels [0, Cin) (in_chan_major: [B][Cin][Tin])
+  int in_chan_major;
   const float* in_mask;                // multiply the input by mask[b][t] (null: no mask)
+  int in_act; float in_slope;          // 1: leaky ReLU with in_slope
   const float* w; const float* bias;
-  int B, T, Cin, Cout, K, pad;
-  float* out; int out_cs, out_c0;      // channels-last output, or channel-major [B][Cout][T] if chan_major
+  long wso, wsc; int tap0, tap_step;
+  int B, T, Cin, Cout, K, pad, dil;    // T = input frames; q runs over [0, Q)
+  int Q, Tout, out_stride, out_off;    // output frames Tout; rows outside [0, Tout) are skipped
+  float* out; int out_cs, out_c0;      // channels-last output, or channel-major [B][Cout][Tout] if chan_major
   int chan_major, relu;
   const float* res; int res_cs;        // out = res + conv (after bias / ReLU)
+  int accumulate;                      // out = out + (...)
+  float div;                           // 0: none; else out = (...) / div
+  int out_tanh;
   const float* out_mask;
 };
+// Conv1d defaults (wso = Cin K, wsc = K, tap_step = 1, dil = 1, Q = Tout = T, out_stride = 1)
+C1dParams c1d_defaults();
 hipError_t launch_c1d(const C1dParams& p, hipStream_t s);
 
 // LayerNorm over channels (text_encoder.py:11-29): out = LN(x (+ res)) * gamma + beta, then ReLU, then * mask

@@ -24,16 +24,26 @@ GT_DEV float wave_sum(float x) {   // butterfly over the 64 lanes (every lane ge
   return x;
 }
 
-constexpr int C1_KC = 16;
+constexpr int C1_KC = 16, C1_KMAX = 11, C1_NP = 64 + 50;   // taps, patch rows (64 + (K - 1) |dil| <= 114)
+C1dParams c1d_defaults() {
+  C1dParams p{};
+  p.tap_step = 1;
+  p.dil = 1;
+  p.out_stride = 1;
+  return p;
+}
+
 __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
-  __shared__ float s_in[64 + 4][C1_KC + 1];
-  __shared__ float s_w[C1_KC][5][65];
+  __shared__ float s_in[C1_NP][C1_KC + 1];
+  __shared__ float s_w[C1_KC][C1_KMAX][65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
-  const int n_tt = (p.T + 63) / 64;
-  const int tt = blockIdx.x % n_tt, b = blockIdx.x / n_tt;
-  const int t0 = tt * 64, a0 = blockIdx.y * 64;
+  const int n_qt = (p.Q + 63) / 64;
+  const int qt = blockIdx.x % n_qt, b = blockIdx.x / n_qt;
+  const int q0 = qt * 64, a0 = blockIdx.y * 64;
   const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
-  const int K = p.K, NP = 64 + K - 1;
+  const int K = p.K, span = (K - 1) * p.dil;
+  const int lo = span < 0 ? span : 0, NP = 64 + (span < 0 ? -span : span);
+  const int start = q0 - p.pad + lo;   // input frame of patch row 0
   f32x16 acc;
 #pragma unroll
   for (int j = 0; j < 16; ++j) acc[j] = 0.f;
@@ -41,45 +51,55 @@ __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
     __syncthreads();
     for (int i = tid; i < NP * C1_KC; i += 256) {
       const int c = i & (C1_KC - 1), pp = i / C1_KC;
-      const int t = t0 - p.pad + pp, ci = c0 + c;
+      const int t = start + pp, ci = c0 + c;
       float v = 0.f;
       if (t >= 0 && t < p.T && ci < p.Cin) {
-        v = p.in[((long)b * p.T + t) * p.in_cs + ci];
+        v = p.in_chan_major ? p.in[((long)b * p.Cin + ci) * p.T + t] : p.in[((long)b * p.T + t) * p.in_cs + ci];
+        if (p.in_act && v < 0.f) v *= p.in_slope;
         if (p.in_mask) v *= p.in_mask[(long)b * p.T + t];
       }
       s_in[pp][c] = v;
     }
-    for (int i = tid; i < 64 * C1_KC * K; i += 256) {   // contiguous along (c, k) for a fixed output channel
+    for (int i = tid; i < 64 * C1_KC * K; i += 256) {
       const int k = i % K, rest = i / K, c = rest % C1_KC, a = rest / C1_KC;
-      s_w[c][k][a] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[((long)(a0 + a) * p.Cin + c0 + c) * K + k] : 0.f;
+      s_w[c][k][a] = (a0 + a < p.Cout && c0 + c < p.Cin)
+                         ? p.w[(long)(a0 + a) * p.wso + (long)(c0 + c) * p.wsc + p.tap0 + k * p.tap_step] : 0.f;
     }
     __syncthreads();
-    for (int k = 0; k < K; ++k)
+    for (int k = 0; k < K; ++k) {
+      const int row = pb + r + k * p.dil - lo;
 #pragma unroll
       for (int cp = 0; cp < C1_KC / 2; ++cp) {
         const int c = 2 * cp + hh;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[pb + r + k][c], s_w[c][k][cb + r], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_in[row][c], s_w[c][k][cb + r], acc, 0, 0, 0);
       }
+    }
   }
   const int o = a0 + cb + r;
   if (o >= p.Cout) return;
   const float bias = p.bias ? p.bias[o] : 0.f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int t = t0 + pb + acc_row(j, hh);
-    if (t >= p.T) continue;
+    const int q = q0 + pb + acc_row(j, hh);
+    if (q >= p.Q) continue;
+    const int t = q * p.out_stride + p.out_off;
+    if (t < 0 || t >= p.Tout) continue;
     float v = acc[j] + bias;
     if (p.relu) v = fmaxf(v, 0.f);
-    if (p.res) v = p.res[((long)b * p.T + t) * p.res_cs + o] + v;
-    if (p.out_mask) v *= p.out_mask[(long)b * p.T + t];
-    if (p.chan_major) p.out[((long)b * p.Cout + o) * p.T + t] = v;
-    else p.out[((long)b * p.T + t) * p.out_cs + p.out_c0 + o] = v;
+    if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
+    const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
+    if (p.accumulate) v = p.out[oi] + v;
+    if (p.div != 0.f) v = v / p.div;
+    if (p.out_tanh) v = tanhf(v);
+    if (p.out_mask) v *= p.out_mask[(long)b * p.Tout + t];
+    p.out[oi] = v;
   }
 }
 
 hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
-  if (p.K < 1 || p.K > 5) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)(p.B * ((p.T + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
+  const int span = (p.K - 1) * (p.dil < 0 ? -p.dil : p.dil);
+  if (p.K < 1 || p.K > C1_KMAX || 64 + span > C1_NP || p.Q <= 0) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)(p.B * ((p.Q + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
   hipLaunchKernelGGL(c1d_kernel, grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }

@@ -75,6 +75,17 @@ SIGNATURES = [
      [_c.c_void_p] * 3 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_durations", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_float] + [_c.c_void_p] * 4),
     ("gt_expand", _c.c_int, [_c.c_void_p] * 4 + [_c.c_int64] * 3 + [_c.c_int32] + [_c.c_void_p] * 4),
+    ("gt_vocoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
+                                     _c.c_void_p, _c.c_void_p]),
+    ("gt_vocoder_destroy", None, [_c.c_void_p]),
+    ("gt_vocoder_num_params", _c.c_int, [_c.c_void_p]),
+    ("gt_vocoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),
+    ("gt_vocoder_param_numel", _c.c_int64, [_c.c_void_p, _c.c_int]),
+    ("gt_vocoder_set_param", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_void_p, _c.c_int64]),
+    ("gt_vocoder_hop", _c.c_int64, [_c.c_void_p]),
+    ("gt_vocoder_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
+    ("gt_vocoder_forward", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,
+                                      _c.c_size_t, _c.c_void_p]),
     ("gt_alignment_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64, _c.c_int64]),
     ("gt_log_prior_maximum_path", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int64,
                                              _c.c_int64, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,

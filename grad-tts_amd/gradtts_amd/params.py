@@ -257,3 +257,57 @@ def synthetic_text_encoder_state_dict(seed: int = 0, **kw) -> "OrderedDict[str, 
             arr = rng.uniform(-b, b, size=shape)
         out[key] = np.ascontiguousarray(arr.astype(np.float32))
     return out
+
+
+# ---- HiFi-GAN generator (hifi-gan/models.py:77-128; checkpts/hifigan-config.json, V1) -------------------------
+HIFIGAN_V1 = {"resblock": "1", "upsample_rates": [8, 8, 2, 2], "upsample_kernel_sizes": [16, 16, 4, 4],
+              "upsample_initial_channel": 512, "resblock_kernel_sizes": [3, 7, 11],
+              "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]], "num_mels": 80}
+
+
+def _wn(out, key, w_shape, g_dim0):
+    out[key + ".bias"] = (w_shape[1] if key.startswith("ups.") else w_shape[0],)
+    out[key + ".weight_g"] = (g_dim0, 1, 1)
+    out[key + ".weight_v"] = tuple(w_shape)
+
+
+def vocoder_param_shapes(h=None):
+    """Generator state_dict keys and shapes in registration order (weight_norm puts bias, weight_g, weight_v)."""
+    h = h or HIFIGAN_V1
+    out = OrderedDict()
+    c0 = h["upsample_initial_channel"]
+    _wn(out, "conv_pre", (c0, h.get("num_mels", 80), 7), c0)
+    for i, (u, k) in enumerate(zip(h["upsample_rates"], h["upsample_kernel_sizes"])):
+        cin, cout = c0 // 2 ** i, c0 // 2 ** (i + 1)
+        _wn(out, f"ups.{i}", (cin, cout, k), cin)   # ConvTranspose1d weight [in][out][k]; weight_norm dim 0 = in
+    n = 0
+    for i in range(len(h["upsample_rates"])):
+        ch = c0 // 2 ** (i + 1)
+        for k, d in zip(h["resblock_kernel_sizes"], h["resblock_dilation_sizes"]):
+            for part in ("convs1", "convs2"):
+                for m in range(len(d)):
+                    _wn(out, f"resblocks.{n}.{part}.{m}", (ch, ch, k), ch)
+            n += 1
+    _wn(out, "conv_post", (1, c0 // 2 ** len(h["upsample_rates"]), 7), 1)
+    return out
+
+
+def synthetic_vocoder_state_dict(seed: int = 0, h=None) -> "OrderedDict[str, np.ndarray]":
+    """Deterministic synthetic Generator weights (float32), one PCG64 stream in key order: weight_v
+    U(-1/sqrt(fan_in), +), weight_g = ||v|| over all but dim 0 times 1 + 0.1 U(-1,1) (so the weight-norm scale is
+    exercised), bias U(-1/sqrt(fan_in), +)."""
+    rng = np.random.default_rng(seed)
+    shapes = vocoder_param_shapes(h)
+    out: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    keys = list(shapes)
+    for i in range(0, len(keys), 3):
+        kb, kg, kv = keys[i], keys[i + 1], keys[i + 2]
+        vs = shapes[kv]
+        fan = vs[0] * vs[2] if kb.startswith("ups.") else vs[1] * vs[2]
+        bnd = 1.0 / np.sqrt(fan)
+        bias = rng.uniform(-bnd, bnd, size=shapes[kb])
+        v = rng.uniform(-bnd, bnd, size=vs)
+        norm = np.sqrt((v.reshape(vs[0], -1) ** 2).sum(1)).reshape(vs[0], 1, 1)
+        g = norm * (1.0 + 0.1 * rng.uniform(-1.0, 1.0, size=norm.shape))
+        out[kb], out[kg], out[kv] = (np.ascontiguousarray(a.astype(np.float32)) for a in (bias, g, v))
+    return out

@@ -199,6 +199,24 @@ int gt_durations(const float* logw, const float* x_mask, int64_t B, int64_t Tx, 
 int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int64_t B,
               int64_t Tx, int64_t Ty, int32_t n_feats, float* mu_y, float* y_mask, float* attn, void* stream);
 
+/* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1; the vocoder of inference.py:73-97). fp32. Parameters by
+ * the reference Generator's state_dict names (bias, weight_g, weight_v per conv); weight norm baked on upload as
+ * remove_weight_norm() does. gt_vocoder_forward: mel [B,n_mels,T] -> audio [B,1,T*hop], hop = prod(upsample_rates).
+ * Implemented: ResBlock1 with 3 dilations per resblock, upsampling kernel = 2 x rate (V1 / V2). */
+typedef struct gt_vocoder gt_vocoder;
+int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
+                      const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes,
+                      const int* resblock_dilations, gt_vocoder** out);
+void gt_vocoder_destroy(gt_vocoder* voc);
+int gt_vocoder_num_params(gt_vocoder* voc);
+const char* gt_vocoder_param_name(gt_vocoder* voc, int i);
+int64_t gt_vocoder_param_numel(gt_vocoder* voc, int i);
+int gt_vocoder_set_param(gt_vocoder* voc, const char* name, const float* data, int64_t numel);
+int64_t gt_vocoder_hop(gt_vocoder* voc);
+size_t gt_vocoder_workspace_bytes(gt_vocoder* voc, int64_t B, int64_t T);
+int gt_vocoder_forward(gt_vocoder* voc, const float* mel, int64_t B, int64_t T, float* audio, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
 /* The alignment step of GradTTS.compute_loss (model/tts.py:141-152) in one call: the log-prior of mu_x
  * [B,n_feats,Tx] against y [B,n_feats,Ty] (three fp32 contractions + const, tts.py:143-149), masked with
  * x_mask [B,Tx] (x) y_mask [B,Ty], then maximum_path on device (t_x, t_y from the masks). paths: [B,Tx,Ty]

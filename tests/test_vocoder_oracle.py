@@ -1,0 +1,29 @@
+"""The HiFi-GAN oracle (oracle/vocoder.py) against the reference Generator's own outputs (tests/golden/voc_*.npz)
+and its recorded state_dict layout. Gates: fp64 restatement vs fp64 reference 1e-10 x max|ref|; fp32 1e-5."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gradtts_amd.params import state_dict_sha256, synthetic_vocoder_state_dict, vocoder_param_shapes
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_layout_matches_reference_generator():
+    layout = json.load(open(os.path.join(GOLD, "hifigan_layout.json")))
+    assert [(k, tuple(s)) for k, s in layout] == list(vocoder_param_shapes().items())
+
+
+@pytest.mark.parametrize("name", ["voc_B2_T6", "voc_B1_T13"])
+def test_oracle_matches_reference_golden(name):
+    from oracle import vocoder as ov
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    sd = synthetic_vocoder_state_dict(int(g["weights_seed"]))
+    assert state_dict_sha256(sd) == str(g["weights_sha256"])
+    for tag, dt, tol in (("f64", torch.float64, 1e-10), ("f32", torch.float32, 1e-5)):
+        a = ov.generator(ov.to_torch_params(sd, dt), torch.from_numpy(g["mel"]).to(dt)).numpy()
+        ref = g[f"audio_{tag}"]
+        assert np.max(np.abs(a - ref)) / np.max(np.abs(ref)) <= tol, tag
