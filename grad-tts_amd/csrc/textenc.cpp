@@ -253,4 +253,11 @@ int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const in
   return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
 }
 
+int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats, float* mu_y,
+                   void* stream) {
+  if (!attn || !mu_x || !mu_y || B <= 0 || Tx <= 0 || Ty <= 0) return gt_internal_fail(GT_ERR_ARG, "bad argument");
+  const hipError_t e = launch_te_path_gather(attn, mu_x, (int)B, (int)Tx, (int)Ty, n_feats, mu_y, (hipStream_t)stream);
+  return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
+}
+
 }  // extern "C"

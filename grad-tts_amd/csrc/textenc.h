@@ -52,4 +52,8 @@ hipError_t launch_te_durations(const float* logw, const float* x_mask, int B, in
 hipError_t launch_te_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int B,
                             int Tx, int Ty, int F, float* mu_y, float* y_mask, float* attn, hipStream_t s);
 
+// mu_y = attn^T mu_x for a 0/1 alignment attn [B][Tx][Ty] (GradTTS.get_score_model, tts.py:233-234)
+hipError_t launch_te_path_gather(const float* attn, const float* mu_x, int B, int Tx, int Ty, int F, float* mu_y,
+                                 hipStream_t s);
+
 }  // namespace gt

@@ -304,6 +304,36 @@ __global__ void te_expand_kernel(const float* mu_x, const float* cum, const floa
     for (int t = 0; t < Tx; ++t) attn[((long)b * Tx + t) * Ty + j] = (on && t == lo) ? 1.f : 0.f;
 }
 
+// mu_y[b][f][j] = sum_i attn[b][i][j] mu_x[b][f][i]  (tts.py:233-234, with the MAS path of get_score_model); a 0/1
+// monotonic path has at most one nonzero per column, so the sum is that single product (exact)
+__global__ __launch_bounds__(256) void te_path_gather_kernel(const float* attn, const float* mu_x, int Tx, int Ty, int F,
+                                                             float* mu_y) {
+  const int b = blockIdx.y, j = blockIdx.x * 64 + (threadIdx.x & 63), fg = threadIdx.x >> 6;
+  if (j >= Ty) return;
+  const int f0 = fg * ((F + 3) / 4), f1 = min(F, f0 + (F + 3) / 4);
+  float acc[32];
+#pragma unroll
+  for (int f = 0; f < 32; ++f) acc[f] = 0.f;
+  for (int i = 0; i < Tx; ++i) {
+    const float a = attn[((long)b * Tx + i) * Ty + j];
+    if (a == 0.f) continue;
+#pragma unroll
+    for (int f = 0; f < 32; ++f)
+      if (f0 + f < f1) acc[f] += a * mu_x[((long)b * F + f0 + f) * Tx + i];
+  }
+#pragma unroll
+  for (int f = 0; f < 32; ++f)
+    if (f0 + f < f1) mu_y[((long)b * F + f0 + f) * Ty + j] = acc[f];
+}
+
+hipError_t launch_te_path_gather(const float* attn, const float* mu_x, int B, int Tx, int Ty, int F, float* mu_y,
+                                 hipStream_t s) {
+  if ((F + 3) / 4 > 32) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(te_path_gather_kernel, dim3((unsigned)((Ty + 63) / 64), B), dim3(256), 0, s, attn, mu_x, Tx, Ty, F,
+                     mu_y);
+  return hipGetLastError();
+}
+
 hipError_t launch_te_durations(const float* logw, const float* x_mask, int B, int Tx, float length_scale, float* w_ceil,
                                float* cum, int64_t* y_lengths, hipStream_t s) {
   hipLaunchKernelGGL(te_durations_kernel, dim3((B + 63) / 64), dim3(64), 0, s, logw, x_mask, B, Tx, length_scale, w_ceil,

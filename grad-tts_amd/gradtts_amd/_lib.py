@@ -75,6 +75,8 @@ SIGNATURES = [
      [_c.c_void_p] * 3 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_durations", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_float] + [_c.c_void_p] * 4),
     ("gt_expand", _c.c_int, [_c.c_void_p] * 4 + [_c.c_int64] * 3 + [_c.c_int32] + [_c.c_void_p] * 4),
+    ("gt_path_gather", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int32,
+                                  _c.c_void_p, _c.c_void_p]),
     ("gt_vocoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                      _c.c_void_p, _c.c_void_p]),
     ("gt_vocoder_destroy", None, [_c.c_void_p]),

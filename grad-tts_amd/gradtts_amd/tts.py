@@ -42,7 +42,44 @@ class GradTTS(torch.nn.Module):
         decoder_outputs = decoder_outputs[:, :, :y_max_length]
         return encoder_outputs, decoder_outputs, attn[:, :, :y_max_length]
 
+    @torch.no_grad()
+    def get_score_model(self, x, x_lengths, y, y_lengths, spk=None):
+        """tts.py:196-254: the score model of one text / mel pair for likelihood rescoring -- encoder, log-prior +
+        MAS alignment (one device call, gradtts_amd.alignment) and mu_y = attn^T mu_x (gt_path_gather). Returns
+        (ScoreModel(estimator, y_mask, mu_y, spk), mu_y, spk, y_mask) as the reference does."""
+        from ._lib import check, lib
+        from .alignment import mas_alignment
+        from .diffusion import _stream_ptr
+        device = self.encoder.emb.weight.device
+        x, x_lengths, y, y_lengths = (a.to(device) for a in (x, x_lengths, y, y_lengths))
+        if self.n_spks > 1:
+            spk = self.spk_emb.weight.index_select(0, spk.to(device))
+        mu_x, logw, x_mask = self.encoder(x, x_lengths, spk)
+        Ty = y.shape[-1]
+        y_mask = (torch.arange(Ty, device=device)[None] < y_lengths[:, None]).unsqueeze(1).to(x_mask.dtype)
+        attn = mas_alignment(mu_x, y, x_mask, y_mask)
+        B, F, Tx = mu_x.shape
+        mu_y = torch.empty(B, F, Ty, dtype=torch.float32, device=device)
+        with torch.cuda.device(device):
+            check(lib().gt_path_gather(attn.contiguous().data_ptr(), mu_x.data_ptr(), B, Tx, Ty, F, mu_y.data_ptr(),
+                                       _stream_ptr(device)), "gt_path_gather")
+        return ScoreModel(self.decoder.estimator, y_mask, mu_y, spk), mu_y, spk, y_mask
+
     def compute_loss(self, *args, **kwargs):
         raise NotImplementedError("training the text encoder (GradTTS.compute_loss's encoder gradients) is not "
                                   "implemented on the HIP path; the decoder's training step is "
                                   "(gradtts_amd.diffusion.Diffusion.compute_loss)")
+
+
+class ScoreModel(torch.nn.Module):
+    """The score model of get_score_model (tts.py:239-252): forward(x, t) = estimator(x, y_mask, mu_y, t, spk)."""
+
+    def __init__(self, estimator, y_mask, mu_y, spk):
+        super().__init__()
+        self.y_mask = y_mask
+        self.mu_y = mu_y
+        self.spk = spk
+        self.estimator = estimator
+
+    def forward(self, x, t):
+        return self.estimator(x=x, mask=self.y_mask, mu=self.mu_y, t=t, spk=self.spk)

@@ -198,6 +198,9 @@ int gt_durations(const float* logw, const float* x_mask, int64_t B, int64_t Tx, 
                  float* cum, int64_t* y_lengths, void* stream);
 int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const int64_t* y_lengths, int64_t B,
               int64_t Tx, int64_t Ty, int32_t n_feats, float* mu_y, float* y_mask, float* attn, void* stream);
+/* mu_y [B,n_feats,Ty] = attn^T mu_x for a 0/1 alignment attn [B,Tx,Ty] (GradTTS.get_score_model, tts.py:233-234) */
+int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
+                   float* mu_y, void* stream);
 
 /* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1; the vocoder of inference.py:73-97). fp32. Parameters by
  * the reference Generator's state_dict names (bias, weight_g, weight_v per conv); weight norm baked on upload as

@@ -154,3 +154,38 @@ def test_likelihood_speed_vs_torch_eager():
     ms_ours, ms_eager = timed(ours), timed(eager)
     report(f"likelihood B={B} T={T} n_euler={N}: ours {ms_ours:.1f} ms, torch eager {ms_eager:.1f} ms; "
            f"ratio eager/ours", ms_eager / ms_ours, 0.0, gate=False, ms_ours=ms_ours, ms_eager=ms_eager)
+
+
+def test_get_score_model_and_rescoring_chain(mas_oracle):
+    """GradTTS.get_score_model (tts.py:196-254: encoder, log-prior + MAS, mu_y = attn^T mu_x) and the rescoring
+    call of n_best (get_score_parallel.py:68-85: SPEECHSDE + get_likelihood_fn(euler) on the score model) against
+    the oracle chain (oracle text encoder -> log-prior -> C MAS oracle -> oracle likelihood, fp64)."""
+    from oracle import decoder as odec, likelihood as olik, text_encoder as ote
+    from gradtts_amd.params import synthetic_text_encoder_state_dict
+    from gradtts_amd.tts import GradTTS
+    m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+    esd, dsd = synthetic_text_encoder_state_dict(2), None
+    dec, dsd = make_decoder(1, 0, torch.float32)
+    m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)
+    m.decoder.estimator.load_state_dict(dec.estimator.state_dict(), strict=True)
+    m = m.cuda()
+    rng = np.random.default_rng(31)
+    B, Tx, Ty = 2, 15, 40
+    tokens = torch.from_numpy(rng.integers(0, 149, (B, Tx)))
+    x_lengths, y_lengths = torch.tensor([15, 11]), torch.tensor([40, 32])
+    y = torch.from_numpy((rng.standard_normal((B, 80, Ty)) * 0.5).astype(np.float32))
+    score_model, mu_y, spk, y_mask = m.get_score_model(tokens.cuda(), x_lengths.cuda(), y.cuda(), y_lengths.cuda())
+    mu_x, _, xm = ote.text_encoder(ote.to_torch_params(esd), tokens, x_lengths)
+    ym = (torch.arange(Ty)[None] < y_lengths[:, None]).unsqueeze(1).float()
+    lp = (odec.log_prior(mu_x, y) * (xm.transpose(1, 2) * ym)).numpy()
+    path, _ = mas_oracle(lp, x_lengths.numpy(), y_lengths.numpy())
+    r_mu_y = torch.matmul(torch.from_numpy(path).float().transpose(1, 2), mu_x.transpose(1, 2)).transpose(1, 2)
+    report("get_score_model mu_y", rel_err(mu_y.cpu().numpy(), r_mu_y.numpy()), 2e-5)
+    eps = torch.from_numpy((rng.integers(0, 2, (B, 80, Ty)) * 2 - 1).astype(np.float32))
+    sde = SPEECHSDE(0.05, 20.0, 1000, mu_y, spk, y_mask)
+    bpd, _, dl, _ = get_likelihood_fn(sde, lambda x: x, rtol=1e-3, atol=1e-3, euler=2)(score_model, y.cuda(),
+                                                                                      epsilon=eps.cuda())
+    p = {k: v_.double() for k, v_ in odec.to_torch_params(dsd).items()}
+    rbpd, _, rdl, _ = olik.likelihood_euler(p, y, ym, r_mu_y, eps, 2)
+    report("rescoring bpd (get_score_model + euler 2)", float(np.max(np.abs(bpd.cpu().numpy() - rbpd.numpy()) /
+                                                                      np.abs(rbpd.numpy()))), 1e-4)
