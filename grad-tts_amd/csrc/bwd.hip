@@ -115,24 +115,26 @@ __global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
 // Implicit GEMM on v_mfma_f32_32x32x2_f32 (exact fp32 fma chains): M = 64 output positions of one row, N = 64 output
 // channels, K = input channels x taps in chunks of MC_KC channels staged in LDS (input patch [row][col][c], weights
 // [c][tap][a]); wave w owns the 32 x 32 block (positions (w & 1) * 32, channels (w >> 1) * 32).
-constexpr int MC_ROWS = 4;
-// Tile: MC_ROWS output rows x 64 positions x 64 output channels; wave w owns row w (2 x 2 blocks of 32 x 32). The
-// input patch ((MC_ROWS - 1) * SE + KS rows) and the weight chunk are staged once per 8-channel chunk and reused by
-// the four rows; the next chunk's global loads are in flight during the current chunk's MFMAs.
-template <int KS, int SE>
+// Tile: RH output rows x TW frames (RH TW <= 256 positions, flattened q = row TW + col) x 64 output channels; wave w
+// owns positions q in [64 w, 64 w + 64) (2 x 2 blocks of 32 x 32 with the channel halves). The input patch
+// ((RH - 1) SE + KS rows x (TW - 1) SE + KS columns) and the weight chunk are staged once per 8-channel chunk and
+// shared by the whole tile; the next chunk's global loads are in flight during the current chunk's MFMAs. The tile
+// shape is picked per launch to fit the level's mel rows x frames (4 x 64, 8 x 32, 5 x 48: level 1 / 2 frame
+// counts like 86 / 43 waste 12-19 % instead of 49 % on 64-frame tiles).
+template <int KS, int SE, int RH, int TW>
 __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   constexpr int MC_KC = 8, NCL = 32;   // input channels per staged chunk, staging column lanes per pass
-  constexpr int KK = KS * KS, PC = 63 * SE + KS, PR = (MC_ROWS - 1) * SE + KS, NCOL = (PC + NCL - 1) / NCL;
+  constexpr int KK = KS * KS, PC = (TW - 1) * SE + KS, PR = (RH - 1) * SE + KS, NCOL = (PC + NCL - 1) / NCL;
   constexpr int NW = 64 * MC_KC * KK, NWJ = (NW + 255) / 256;
   __shared__ float s_in[PR][PC][MC_KC + 1];
   __shared__ float s_w[MC_KC][KK][65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
-  const int n_tt = (p.To + 63) / 64, n_f4 = (p.Fo + MC_ROWS - 1) / MC_ROWS;
+  const int n_tt = (p.To + TW - 1) / TW, n_fr = (p.Fo + RH - 1) / RH;
   int bid = blockIdx.x;
   const int tt = bid % n_tt; bid /= n_tt;
-  const int fo0 = (bid % n_f4) * MC_ROWS;
-  const int b = bid / n_f4;
-  const int to0 = tt * 64, a0 = blockIdx.y * 64;
+  const int fo0 = (bid % n_fr) * RH;
+  const int b = bid / n_fr;
+  const int to0 = tt * TW, a0 = blockIdx.y * 64;
   // transposed relation (ConvTranspose2d, strided-conv dgrad): a stride-1 conv over the S-dilated input with the
   // taps flipped and padding KS - 1 - PAD
   const bool dil = p.transposed != 0;
@@ -197,6 +199,14 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
     for (int y = 0; y < 2; ++y)
 #pragma unroll
       for (int j = 0; j < 16; ++j) acc[x][y][j] = 0.f;
+  // this lane's A-operand positions (one per 32-position block)
+  int prow[2], pcol[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int q = 64 * wv + 32 * x + r;
+    prow[x] = q / TW < RH ? (q / TW) * SE : 0;   // positions past RH rows read row 0; their outputs are dropped
+    pcol[x] = (q % TW) * SE;
+  }
   load(0);
   for (int c0 = 0; c0 < p.Cin; c0 += MC_KC) {
     __syncthreads();
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
 #pragma unroll
       for (int cp = 0; cp < MC_KC / 2; ++cp) {
         const int c = 2 * cp + hh;
-        const float x0 = s_in[wv * SE + kh][r * SE + kw][c], x1 = s_in[wv * SE + kh][(32 + r) * SE + kw][c];
+        const float x0 = s_in[prow[0] + kh][pcol[0] + kw][c], x1 = s_in[prow[1] + kh][pcol[1] + kw][c];
         const float w0 = s_w[c][k][r], w1 = s_w[c][k][32 + r];
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, w0, acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, w1, acc[0][1], 0, 0, 0);
@@ -218,8 +228,6 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
       }
     }
   }
-  const int fo = fo0 + wv;
-  if (fo >= p.Fo) return;
 #pragma unroll
   for (int y = 0; y < 2; ++y) {
     const int a = a0 + 32 * y + r;
@@ -229,8 +237,9 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const int to = to0 + 32 * x + acc_row(j, hh);
-        if (to >= p.To) continue;
+        const int q = 64 * wv + 32 * x + acc_row(j, hh);
+        const int fo = fo0 + q / TW, to = to0 + q % TW;
+        if (q / TW >= RH || fo >= p.Fo || to >= p.To) continue;
         const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
         const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
         const float v = (acc[x][y][j] + bias) * om;
@@ -313,19 +322,19 @@ __global__ __launch_bounds__(256) void mconv1_kernel(GConvParams p) {
 // next segment's loads in flight during the current MFMAs); wave w owns the 32 x 32 (a, b) block
 // ((w & 1) * 32, (w >> 1) * 32) for the KG taps of its group. LDS row strides put the two half-waves' rows 32 banks
 // apart. part[split][k][a][b] -> mwgrad_reduce_kernel (splits in order).
-template <int KS, int S>
+template <int KS, int S, int SEG>
 __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, float* part) {
   constexpr int KG = KS == 4 ? 8 : KS * KS, NR = KG / KS;                    // taps / patch rows of a group
-  constexpr int NCOL = 31 * S + KS, QS = S == 1 ? 96 : 80, PS = 96;          // patch columns, LDS row strides
-  constexpr int NQ = (NCOL + 3) / 4;                                         // columns per staging lane
-  __shared__ float s_p[32 * PS];
+  constexpr int NCOL = (SEG - 1) * S + KS, QS = S == 1 ? 96 : 80, PS = 96;   // patch columns, LDS row strides
+  constexpr int NQ = (NCOL + 3) / 4, NPJ = SEG / 4;                          // staging per lane: Q columns, P rows
+  __shared__ float s_p[SEG * PS];
   __shared__ float s_q[NR * NCOL * QS];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int sc = tid & 63, sl = tid >> 6;   // staging: channel, row lane
   const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 64;
   const int split = blockIdx.z % splits, k0 = (blockIdx.z / splits) * KG;
   const int kh0 = k0 / KS;
-  const int n_tt = (p.Tu + 31) / 32;
+  const int n_tt = (p.Tu + SEG - 1) / SEG;
   const long nseg = (long)p.B * p.Fu * n_tt;
   const long per = (nseg + splits - 1) / splits;
   const long s_lo = split * per, s_hi = s_lo + per < nseg ? s_lo + per : nseg;
@@ -335,14 +344,14 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
   for (int g = 0; g < KG; ++g)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[g][j] = 0.f;
-  float rp[8], rq[NR][NQ];
+  float rp[NPJ], rq[NR][NQ];
   auto load = [&](long sg) {
     const int tt = (int)(sg % n_tt);
     const int fu = (int)((sg / n_tt) % p.Fu);
     const int b = (int)(sg / ((long)n_tt * p.Fu));
-    const int t0 = tt * 32;
+    const int t0 = tt * SEG;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < NPJ; ++j) {
       const int u = sl + 4 * j;
       float v = 0.f;
       if (t0 + u < p.Tu && a0 + sc < p.A) {
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
   for (long sg = s_lo; sg < s_hi; ++sg) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s_p[(sl + 4 * j) * PS + sc] = rp[j];
+    for (int j = 0; j < NPJ; ++j) s_p[(sl + 4 * j) * PS + sc] = rp[j];
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr)
 #pragma unroll
@@ -382,7 +391,7 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
     for (int g = 0; g < KG; ++g) {
       const int kh = g / KS, kw = g % KS;
 #pragma unroll 4
-      for (int up = 0; up < 16; ++up) {
+      for (int up = 0; up < SEG / 2; ++up) {
         const int u = 2 * up + hh;
         acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(s_p[u * PS + ab + r], s_q[(kh * NCOL + u * S + kw) * QS + bb + r],
                                                       acc[g], 0, 0, 0);
@@ -415,10 +424,16 @@ __global__ void mwgrad_reduce_kernel(const float* part, int splits, int A, int B
   *d = accumulate ? *d + s : s;
 }
 
+// 48-position segments where they cut the padded frames (a level-2 row of 43 frames: 48 instead of 64)
+static int mwgrad_seg(const WGradParams& p) {
+  return (p.KS == 3 && p.S == 1 && (p.Tu + 47) / 48 * 48 < (p.Tu + 31) / 32 * 32) ? 48 : 32;
+}
+
 int mwgrad_splits(const WGradParams& p) {
   const int groups = p.KS == 4 ? 2 : 1;
   const long tiles = (long)((p.A + 63) / 64) * ((p.Bc + 63) / 64) * groups;
-  const long nseg = (long)p.B * p.Fu * ((p.Tu + 31) / 32);
+  const int seg = mwgrad_seg(p);
+  const long nseg = (long)p.B * p.Fu * ((p.Tu + seg - 1) / seg);
   long s = std::max<long>(1, 512 / tiles);
   s = std::min<long>(s, nseg);
   s = std::min<long>(s, kWPartCap / ((long)p.KS * p.KS * p.A * p.Bc));
@@ -433,10 +448,12 @@ hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, 
   const int splits = mwgrad_splits(p);
   const int groups = p.KS == 4 ? 2 : 1;
   const dim3 grid((p.A + 63) / 64, (p.Bc + 63) / 64, splits * groups);
-  if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1>), grid, dim3(256), 0, strm, p, splits, part);
-  else if (cfg == 31) hipLaunchKernelGGL((mwgrad_kernel<3, 1>), grid, dim3(256), 0, strm, p, splits, part);
-  else if (cfg == 32) hipLaunchKernelGGL((mwgrad_kernel<3, 2>), grid, dim3(256), 0, strm, p, splits, part);
-  else hipLaunchKernelGGL((mwgrad_kernel<4, 2>), grid, dim3(256), 0, strm, p, splits, part);
+  if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 31 && mwgrad_seg(p) == 48)
+    hipLaunchKernelGGL((mwgrad_kernel<3, 1, 48>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 31) hipLaunchKernelGGL((mwgrad_kernel<3, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 32) hipLaunchKernelGGL((mwgrad_kernel<3, 2, 32>), grid, dim3(256), 0, strm, p, splits, part);
+  else hipLaunchKernelGGL((mwgrad_kernel<4, 2, 32>), grid, dim3(256), 0, strm, p, splits, part);
   const long n = (long)p.KS * p.KS * p.A * p.Bc;
   hipLaunchKernelGGL(mwgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, strm, part, splits, p.A,
                      p.Bc, p.KS * p.KS, sa, sb, dw, accumulate);
@@ -933,16 +950,23 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
     if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
   } else {
-    const dim3 mgrid((unsigned)((long)p.B * ((p.Fo + MC_ROWS - 1) / MC_ROWS) * ((p.To + 63) / 64)),
-                     (unsigned)((p.Cout + 63) / 64));
-    const dim3& grid = mgrid;
+    auto mgrid = [&](int rh, int tw) {
+      return dim3((unsigned)((long)p.B * ((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw)), (unsigned)((p.Cout + 63) / 64));
+    };
+    auto slots = [&](int rh, int tw) { return (long)((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw); };
     const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
-    if (cfg == 11) hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
-                                                   (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);
-    else if (cfg == 31) hipLaunchKernelGGL((mconv_kernel<3, 1>), grid, dim3(256), 0, s, p);
-    else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2>), grid, dim3(256), 0, s, p);
-    else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1>), grid, dim3(256), 0, s, p);
-    else if (cfg == 42) hipLaunchKernelGGL((mconv_kernel<4, 2>), grid, dim3(256), 0, s, p);
+    if (cfg == 11) {
+      hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
+                                             (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);
+    } else if (cfg == 31) {   // the 3x3 stride-1 convs: tile shape with the fewest 256-position tiles
+      const long s4 = slots(4, 64), s8 = slots(8, 32), s5 = slots(5, 48);
+      if (s4 <= s8 && s4 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+      else if (s8 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 8, 32>), mgrid(8, 32), dim3(256), 0, s, p);
+      else hipLaunchKernelGGL((mconv_kernel<3, 1, 5, 48>), mgrid(5, 48), dim3(256), 0, s, p);
+    }
+    else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+    else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+    else if (cfg == 42) hipLaunchKernelGGL((mconv_kernel<4, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
     else return hipErrorInvalidValue;
   }
   return hipGetLastError();
