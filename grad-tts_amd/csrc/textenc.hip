@@ -24,7 +24,7 @@ GT_DEV float wave_sum(float x) {   // butterfly over the 64 lanes (every lane ge
   return x;
 }
 
-constexpr int C1_KC = 16, C1_KMAX = 11, C1_NP = 64 + 50;   // taps, patch rows (64 + (K - 1) |dil| <= 114)
+constexpr int C1_KMAX = 11, C1_SPAN = 50;   // taps, (K - 1) |dilation|
 C1dParams c1d_defaults() {
   C1dParams p{};
   p.tap_step = 1;
@@ -33,9 +33,13 @@ C1dParams c1d_defaults() {
   return p;
 }
 
+// LDS sized per kernel-size class: KM taps at most, KC input channels per chunk, patch rows 64 + SP (short kernels
+// take 32-channel chunks: a 3-tap conv has too few MFMAs per chunk to hide two barriers on 16)
+template <int KM, int KC, int SP>
 __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
-  __shared__ float s_in[C1_NP][C1_KC + 1];
-  __shared__ float s_w[C1_KC][C1_KMAX][65];
+  constexpr int C1_KC = KC;
+  __shared__ float s_in[64 + SP][C1_KC + 1];
+  __shared__ float s_w[C1_KC][KM][65];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
   const int n_qt = (p.Q + 63) / 64;
   const int qt = blockIdx.x % n_qt, b = blockIdx.x / n_qt;
@@ -96,11 +100,96 @@ __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
   }
 }
 
+// bf16 variant (HiFi-GAN throughput mode): operands rounded to bf16 when staged, fp32 accumulation on
+// v_mfma_f32_32x32x16_bf16; 32-channel chunks = two 16-deep MFMA steps per tap; same tile, epilogue and semantics
+template <int KM, int SP>
+__global__ __launch_bounds__(256) void c1d_bf16_kernel(C1dParams p) {
+  constexpr int KC = 32, LD = KC + 8;   // row of 40 bf16 = 80 bytes: 16-byte aligned fragments
+  __shared__ __attribute__((aligned(16))) bf16 s_in[64 + SP][LD];
+  __shared__ __attribute__((aligned(16))) bf16 s_w[KM][64][LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_qt = (p.Q + 63) / 64;
+  const int qt = blockIdx.x % n_qt, b = blockIdx.x / n_qt;
+  const int q0 = qt * 64, a0 = blockIdx.y * 64;
+  const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
+  const int K = p.K, span = (K - 1) * p.dil;
+  const int lo = span < 0 ? span : 0, NP = 64 + (span < 0 ? -span : span);
+  const int start = q0 - p.pad + lo;
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  for (int c0 = 0; c0 < p.Cin; c0 += KC) {
+    __syncthreads();
+    for (int i = tid; i < NP * 4; i += 256) {   // 8-channel groups of the input patch
+      const int g = i & 3, pp = i >> 2;
+      const int t = start + pp, cg = c0 + 8 * g;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+      if (t >= 0 && t < p.T && cg < p.Cin) {
+        const float m = p.in_mask ? p.in_mask[(long)b * p.T + t] : 1.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = p.in_chan_major ? p.in[((long)b * p.Cin + cg + e) * p.T + t] : p.in[((long)b * p.T + t) * p.in_cs + cg + e];
+          if (p.in_act && x < 0.f) x *= p.in_slope;
+          v[e] = x * m;
+        }
+      }
+      *reinterpret_cast<uint4*>(&s_in[pp][8 * g]) = f_to_item(v, bf16());
+    }
+    for (int i = tid; i < 64 * K * 4; i += 256) {   // weights [o][k][c]: 16-byte groups of 8 input channels
+      const int g = i & 3, rest = i >> 2, k = rest % K, o = rest / K;
+      uint4 w = make_uint4(0, 0, 0, 0);
+      if (a0 + o < p.Cout && c0 + 8 * g < p.Cin)
+        w = *reinterpret_cast<const uint4*>(p.wbf + ((long)(a0 + o) * K + k) * p.Cin + c0 + 8 * g);
+      *reinterpret_cast<uint4*>(&s_w[k][o][8 * g]) = w;
+    }
+    __syncthreads();
+    for (int k = 0; k < K; ++k) {
+      const int row = pb + r + k * p.dil - lo;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(&s_in[row][16 * ks + 8 * hh]);
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&s_w[k][cb + r][16 * ks + 8 * hh]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+      }
+    }
+  }
+  const int o = a0 + cb + r;
+  if (o >= p.Cout) return;
+  const float bias = p.bias ? p.bias[o] : 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int q = q0 + pb + acc_row(j, hh);
+    if (q >= p.Q) continue;
+    const int t = q * p.out_stride + p.out_off;
+    if (t < 0 || t >= p.Tout) continue;
+    float v = acc[j] + bias;
+    if (p.relu) v = fmaxf(v, 0.f);
+    if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
+    const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
+    if (p.accumulate) v = p.out[oi] + v;
+    if (p.div != 0.f) v = v / p.div;
+    if (p.out_tanh) v = tanhf(v);
+    if (p.out_mask) v *= p.out_mask[(long)b * p.Tout + t];
+    p.out[oi] = v;
+  }
+}
+
 hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
   const int span = (p.K - 1) * (p.dil < 0 ? -p.dil : p.dil);
-  if (p.K < 1 || p.K > C1_KMAX || 64 + span > C1_NP || p.Q <= 0) return hipErrorInvalidValue;
+  if (p.K < 1 || p.K > C1_KMAX || span > C1_SPAN || p.Q <= 0) return hipErrorInvalidValue;
   const dim3 grid((unsigned)(p.B * ((p.Q + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
-  hipLaunchKernelGGL(c1d_kernel, grid, dim3(256), 0, s, p);
+  if (p.bf16) {
+    if (!p.wbf || p.Cin % 8) return hipErrorInvalidValue;
+    if (p.K <= 3 && span <= 10) hipLaunchKernelGGL((c1d_bf16_kernel<3, 10>), grid, dim3(256), 0, s, p);
+    else if (p.K <= 7 && span <= 30) hipLaunchKernelGGL((c1d_bf16_kernel<7, 30>), grid, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((c1d_bf16_kernel<C1_KMAX, C1_SPAN>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
+  if (p.K <= 3 && span <= 10) hipLaunchKernelGGL((c1d_kernel<3, 32, 10>), grid, dim3(256), 0, s, p);
+  else if (p.K <= 7 && span <= 30) hipLaunchKernelGGL((c1d_kernel<7, 16, 30>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((c1d_kernel<C1_KMAX, 16, C1_SPAN>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

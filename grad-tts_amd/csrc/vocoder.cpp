@@ -35,11 +35,21 @@ struct gt_vocoder {
   float* dev = nullptr;
   int64_t dev_numel = 0;
   bool dirty = true;
+  int bf16 = 0;                          // compute dtype: 0 fp32, 1 bf16 operands (fp32 accumulation)
+  std::map<std::string, int64_t> bfoff;  // bf16 weights [o][k][c] (ups: [phase][o][2][c]) in devbf
+  uint16_t* devbf = nullptr;
+  int64_t devbf_numel = 0;
 };
 
 namespace {
 
 int64_t prod(const std::vector<int64_t>& d) { int64_t n = 1; for (auto v : d) n *= v; return n; }
+
+uint16_t to_bf16(float f) {   // round to nearest even (finite weights)
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
 
 void add_wn(gt_vocoder* v, const std::string& k, std::vector<int64_t> w, int64_t bias_n) {
   v->inv.push_back({k + ".bias", {bias_n}});
@@ -69,6 +79,33 @@ int upload(gt_vocoder* v) {
     v->woff[key + ".bias"] = (int64_t)h.size();
     h.insert(h.end(), b.begin(), b.end());
   }
+  // bf16 copies of the effective weights in the operand layout of c1d_bf16_kernel
+  std::vector<uint16_t> hb;
+  v->bfoff.clear();
+  for (size_t i = 0; i < v->inv.size(); i += 3) {
+    const std::string key = v->inv[i].first.substr(0, v->inv[i].first.size() - 5);
+    const std::vector<int64_t>& d = v->inv[i + 2].second;
+    const float* w = h.data() + v->woff[key + ".weight"];
+    v->bfoff[key] = (int64_t)hb.size();
+    if (key.rfind("ups.", 0) == 0) {   // ConvTranspose1d [Cin][Cout][k], k = 2u: per phase r, [o][j][c] = w[c][o][r + u j]
+      const int64_t ci = d[0], co = d[1], kk = d[2], u = kk / 2;
+      for (int64_t r = 0; r < u; ++r)
+        for (int64_t o = 0; o < co; ++o)
+          for (int64_t j = 0; j < 2; ++j)
+            for (int64_t c = 0; c < ci; ++c) hb.push_back(to_bf16(w[(c * co + o) * kk + r + u * j]));
+    } else {                             // Conv1d [Cout][Cin][k] -> [o][k][c]
+      const int64_t co = d[0], ci = d[1], kk = d[2];
+      for (int64_t o = 0; o < co; ++o)
+        for (int64_t k = 0; k < kk; ++k)
+          for (int64_t c = 0; c < ci; ++c) hb.push_back(to_bf16(w[(o * ci + c) * kk + k]));
+    }
+    while (hb.size() % 8) hb.push_back(0);   // 16-byte aligned starts
+  }
+  if (v->devbf && (int64_t)hb.size() != v->devbf_numel) { (void)hipFree(v->devbf); v->devbf = nullptr; }
+  if (!v->devbf && hipMalloc(&v->devbf, hb.size() * 2) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
+  v->devbf_numel = (int64_t)hb.size();
+  if (hipMemcpy(v->devbf, hb.data(), hb.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
   if (v->dev && (int64_t)h.size() != v->dev_numel) { (void)hipFree(v->dev); v->dev = nullptr; }
   if (!v->dev && hipMalloc(&v->dev, h.size() * 4) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
   v->dev_numel = (int64_t)h.size();
@@ -132,6 +169,7 @@ int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const 
 void gt_vocoder_destroy(gt_vocoder* v) {
   if (!v) return;
   if (v->dev) (void)hipFree(v->dev);
+  if (v->devbf) (void)hipFree(v->devbf);
   delete v;
 }
 
@@ -150,6 +188,12 @@ int gt_vocoder_set_param(gt_vocoder* v, const char* name, const float* data, int
   v->host[it->second].assign(data, data + numel);
   v->set[it->second] = true;
   v->dirty = true;
+  return GT_OK;
+}
+
+int gt_vocoder_set_compute_dtype(gt_vocoder* v, int dtype) {
+  if (!v || (dtype != 0 && dtype != 1)) return gt_internal_fail(GT_ERR_ARG, "dtype must be 0 (fp32) or 1 (bf16)");
+  v->bf16 = dtype;
   return GT_OK;
 }
 
@@ -181,6 +225,14 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
   hipError_t err = hipSuccess;
   auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
   const int Bi = (int)B;
+  auto BF = [&](const std::string& k) { return v->devbf + v->bfoff.at(k); };
+  auto launch = [&](C1dParams& p, const std::string& key, int phase) {   // fp32 or bf16 operands per the handle
+    if (v->bf16) {
+      p.bf16 = 1;
+      p.wbf = BF(key) + (int64_t)phase * p.Cout * p.K * p.Cin;
+    }
+    chk(launch_c1d(p, s));
+  };
   // conv_pre: channel-major mel [B][n_mels][T] -> [B][T][c0]
   float* x = buf[0];
   {
@@ -189,7 +241,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
     p.wso = (long)v->n_mels * 7; p.wsc = 7;
     p.B = Bi; p.T = (int)T; p.Q = (int)T; p.Tout = (int)T; p.Cin = v->n_mels; p.Cout = v->c0; p.K = 7; p.pad = 3;
     p.out = x; p.out_cs = v->c0;
-    chk(launch_c1d(p, s));
+    launch(p, "conv_pre", 0);
   }
   int Tin = (int)T, cin = v->c0, n = 0;
   for (int i = 0; i < v->n_up; ++i) {
@@ -203,7 +255,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
       p.B = Bi; p.T = Tin; p.Cin = cin; p.Cout = cout; p.K = 2; p.pad = 0; p.dil = -1;
       p.Q = Tin + 1; p.Tout = Tout; p.out_stride = u; p.out_off = r - P;
       p.out = xu; p.out_cs = cout;
-      chk(launch_c1d(p, s));
+      launch(p, key, r);
     }
     float* cur = buf[2];
     float* t1 = buf[3];
@@ -220,7 +272,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
         p.w = W(c1); p.bias = Bs(c1); p.wso = (long)cout * kk; p.wsc = kk;
         p.B = Bi; p.T = Tout; p.Q = Tout; p.Tout = Tout; p.Cin = cout; p.Cout = cout; p.K = kk; p.dil = d;
         p.pad = (kk * d - d) / 2; p.out = t1; p.out_cs = cout;
-        chk(launch_c1d(p, s));
+        launch(p, c1, 0);
         C1dParams q = c1d_defaults();   // y = c2(leaky_relu(xt, 0.1)) + y
         q.in = t1; q.in_cs = cout; q.in_act = 1; q.in_slope = 0.1f;
         q.w = W(c2); q.bias = Bs(c2); q.wso = (long)cout * kk; q.wsc = kk;
@@ -232,7 +284,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
           q.out = xs; q.accumulate = j > 0;
           if (j == v->nk - 1) q.div = (float)v->nk;
         }
-        chk(launch_c1d(q, s));
+        launch(q, c2, 0);
         y = cur;
       }
     }
@@ -245,7 +297,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
     p.w = W("conv_post"); p.bias = Bs("conv_post"); p.wso = (long)cin * 7; p.wsc = 7;
     p.B = Bi; p.T = Tin; p.Q = Tin; p.Tout = Tin; p.Cin = cin; p.Cout = 1; p.K = 7; p.pad = 3;
     p.out = audio; p.out_cs = 1; p.out_tanh = 1;
-    chk(launch_c1d(p, s));
+    launch(p, "conv_post", 0);
   }
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("vocoder launch failed: ") + hipGetErrorString(err));
   return GT_OK;

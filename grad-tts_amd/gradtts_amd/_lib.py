@@ -85,6 +85,7 @@ SIGNATURES = [
     ("gt_vocoder_param_numel", _c.c_int64, [_c.c_void_p, _c.c_int]),
     ("gt_vocoder_set_param", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_void_p, _c.c_int64]),
     ("gt_vocoder_hop", _c.c_int64, [_c.c_void_p]),
+    ("gt_vocoder_set_compute_dtype", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_vocoder_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
     ("gt_vocoder_forward", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_void_p, _c.c_void_p,
                                       _c.c_size_t, _c.c_void_p]),

@@ -34,11 +34,16 @@ class ResBlock1(torch.nn.Module):
 
 
 class Generator(torch.nn.Module):
-    """``Generator(h)`` with h the HiFi-GAN config (AttrDict or dict: resblock '1', upsample_rates,
-    upsample_kernel_sizes, upsample_initial_channel, resblock_kernel_sizes, resblock_dilation_sizes)."""
+    """``Generator(h, compute_dtype=torch.float32)`` with h the HiFi-GAN config (AttrDict or dict: resblock '1',
+    upsample_rates, upsample_kernel_sizes, upsample_initial_channel, resblock_kernel_sizes,
+    resblock_dilation_sizes). compute_dtype=torch.bfloat16 rounds the conv operands to bf16 (fp32 accumulation,
+    fp32 activations in memory): the throughput mode; fp32 is the parity path."""
 
-    def __init__(self, h):
+    def __init__(self, h, compute_dtype=torch.float32):
         super().__init__()
+        if compute_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("compute_dtype must be torch.float32 (parity path) or torch.bfloat16 (throughput)")
+        self.compute_dtype = compute_dtype
         g = (lambda k: h[k]) if isinstance(h, dict) else (lambda k: getattr(h, k))
         if str(g("resblock")) != "1":
             raise ValueError("the HIP vocoder implements ResBlock1 (HiFi-GAN V1 / V2)")
@@ -76,6 +81,8 @@ class Generator(torch.nn.Module):
             check(L.gt_vocoder_create(self.n_mels, self.c0, self.num_upsamples, ia(self.rates), ia(self.kernels),
                                       self.num_kernels, ia(self.rb_k), ia(dil), ctypes.byref(h)), "gt_vocoder_create")
             self._handle = h
+        check(L.gt_vocoder_set_compute_dtype(self._handle, 1 if self.compute_dtype == torch.bfloat16 else 0),
+              "gt_vocoder_set_compute_dtype")
         sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
         if sig != self._synced:
             params = dict(self.named_parameters())

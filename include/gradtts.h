@@ -216,6 +216,8 @@ const char* gt_vocoder_param_name(gt_vocoder* voc, int i);
 int64_t gt_vocoder_param_numel(gt_vocoder* voc, int i);
 int gt_vocoder_set_param(gt_vocoder* voc, const char* name, const float* data, int64_t numel);
 int64_t gt_vocoder_hop(gt_vocoder* voc);
+/* 0: fp32 (default, the parity path); 1: bf16 operands with fp32 accumulation (throughput mode) */
+int gt_vocoder_set_compute_dtype(gt_vocoder* voc, int dtype);
 size_t gt_vocoder_workspace_bytes(gt_vocoder* voc, int64_t B, int64_t T);
 int gt_vocoder_forward(gt_vocoder* voc, const float* mel, int64_t B, int64_t T, float* audio, void* workspace,
                        size_t workspace_bytes, void* stream);

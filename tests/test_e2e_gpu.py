@@ -20,14 +20,14 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def build(compute_dtype=torch.float32):
+def build(compute_dtype=torch.float32, vocoder_dtype=torch.float32):
     from gradtts_amd.tts import GradTTS
     from gradtts_amd.vocoder import Generator
     m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000, compute_dtype=compute_dtype)
     esd, dsd, vsd = synthetic_text_encoder_state_dict(2), synthetic_state_dict(seed=0), synthetic_vocoder_state_dict(7)
     m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)
     m.decoder.estimator.load_state_dict({k: torch.from_numpy(v) for k, v in dsd.items()}, strict=True)
-    voc = Generator(HIFIGAN_V1)
+    voc = Generator(HIFIGAN_V1, compute_dtype=vocoder_dtype)
     voc.load_state_dict({k: torch.from_numpy(v) for k, v in vsd.items()}, strict=True)
     voc.remove_weight_norm()
     return m.cuda(), voc.cuda().eval(), (esd, dsd, vsd)
@@ -69,7 +69,7 @@ def test_end_to_end_rtf(B, Tx, N, dtype):
     """Report (no gate): wall time per stage and the real-time factor (wall / seconds of audio at 22.05 kHz)."""
     import time
     from gradtts_amd.text_encoder import align_durations
-    m, voc, _ = build(dtype)
+    m, voc, _ = build(dtype, dtype)
     rng = np.random.default_rng(22)
     tokens = torch.from_numpy(rng.integers(0, 149, (B, Tx))).cuda()
     lengths = torch.full((B,), Tx, dtype=torch.int64).cuda()
@@ -93,6 +93,6 @@ def test_end_to_end_rtf(B, Tx, N, dtype):
     times, n_samples = once()
     total = sum(times)
     sec = B * n_samples / 22050
-    report(f"end-to-end B={B} Tx={Tx} N={N} {str(dtype)[6:]}: encoder+align {times[0] * 1e3:.1f} ms, decoder "
+    report(f"end-to-end B={B} Tx={Tx} N={N} decoder + vocoder {str(dtype)[6:]}: encoder+align {times[0] * 1e3:.1f} ms, decoder "
            f"{times[1] * 1e3:.1f} ms, vocoder {times[2] * 1e3:.1f} ms; {sec:.1f} s of audio, RTF", total / sec, 0.0,
            gate=False, ms=[t * 1e3 for t in times], audio_s=sec)

@@ -2,7 +2,8 @@
 (tests/golden/voc_*.npz, made by make_golden_vocoder.py from the real hifi-gan/models.py) and the pinned oracle.
 
 Tolerances (written here): audio fp32 vs the reference's fp64 1e-5 x max|ref| (fp32 MFMA convs in a different
-summation order through 4 stages x 18 resblock convs); larger random shapes vs the fp32 oracle 1e-5."""
+summation order through 4 stages x 18 resblock convs); larger random shapes vs the fp32 oracle 1e-5. The bf16
+throughput mode (operands rounded to bf16, fp32 accumulation): 2e-2 x max|ref| against fp64, error printed."""
 import os
 
 import numpy as np
@@ -24,8 +25,8 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def make_vocoder(seed):
-    g = Generator(HIFIGAN_V1)
+def make_vocoder(seed, compute_dtype=torch.float32):
+    g = Generator(HIFIGAN_V1, compute_dtype=compute_dtype)
     sd = synthetic_vocoder_state_dict(seed)
     g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     g.remove_weight_norm()
@@ -41,6 +42,14 @@ def test_vocoder_matches_reference_golden(name):
     assert audio.shape == g["audio_f64"].shape
     report(f"vocoder audio {name} vs fp64 reference", rel_err(audio.cpu().numpy(), g["audio_f64"]), 1e-5)
     report(f"vocoder audio {name} vs fp32 reference", rel_err(audio.cpu().numpy(), g["audio_f32"]), 1e-5)
+
+
+@pytest.mark.parametrize("name", ["voc_B2_T6", "voc_B1_T13"])
+def test_vocoder_bf16_mode_within_envelope(name):
+    g = np.load(os.path.join(GOLD, name + ".npz"))
+    voc, _ = make_vocoder(int(g["weights_seed"]), torch.bfloat16)
+    audio = voc(torch.from_numpy(g["mel"]).cuda())
+    report(f"vocoder bf16 mode audio {name} vs fp64 reference", rel_err(audio.cpu().numpy(), g["audio_f64"]), 2e-2)
 
 
 def test_vocoder_matches_oracle_longer():
@@ -72,10 +81,13 @@ def test_vocoder_speed_vs_torch_eager():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
+    voc16, _ = make_vocoder(4, torch.bfloat16)
     with torch.no_grad():
         ms_ours = timed(lambda: voc(mel))
+        ms_bf16 = timed(lambda: voc16(mel))
         ms_eager = timed(lambda: ov.generator(p, mel))
     sec = B * T * 256 / 22050
-    report(f"vocoder B={B} T={T} ({sec:.1f} s of audio): ours {ms_ours:.1f} ms (RTF {ms_ours / 1e3 / sec:.5f}), "
-           f"torch eager {ms_eager:.1f} ms; ratio eager/ours", ms_eager / ms_ours, 0.0, gate=False, ms_ours=ms_ours,
+    report(f"vocoder B={B} T={T} ({sec:.1f} s of audio): ours fp32 {ms_ours:.1f} ms (RTF {ms_ours / 1e3 / sec:.5f}), "
+           f"ours bf16 {ms_bf16:.1f} ms (RTF {ms_bf16 / 1e3 / sec:.5f}), torch eager fp32 {ms_eager:.1f} ms; "
+           f"ratio eager/ours-fp32", ms_eager / ms_ours, 0.0, gate=False, ms_ours=ms_ours, ms_bf16=ms_bf16,
            ms_eager=ms_eager)
