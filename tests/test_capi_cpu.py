@@ -127,3 +127,45 @@ def test_torch_ops_registered_with_meta_kernels():
     with pytest.raises(RuntimeError, match="multiple of 4"):
         ops.reverse_diffusion(0, 0, torch.empty(1, 80, 30, device="meta"), torch.empty(1, 1, 30, device="meta"),
                               torch.empty(1, 80, 30, device="meta"), 1, None)
+
+
+def test_text_encoder_and_vocoder_registries_match_reference_layouts():
+    """The C-ABI parameter registries of the text encoder and the HiFi-GAN generator list exactly the reference
+    modules' state_dict keys and sizes (tests/golden/gradtts_layout.json, hifigan_layout.json, recorded from the
+    real modules); unknown names and wrong sizes are rejected (no GPU needed)."""
+    import json
+    from gradtts_amd.params import HIFIGAN_V1
+    L = _lib.lib()
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    enc_ref = [(k[len("encoder."):], int(np.prod(s))) for k, s in json.load(open(os.path.join(gold, "gradtts_layout.json")))["1"]
+               if k.startswith("encoder.")]
+    h = ctypes.c_void_p()
+    assert L.gt_text_encoder_create(149, 80, 192, 768, 256, 2, 6, 3, 4, ctypes.byref(h)) == 0
+    try:
+        got = [(L.gt_text_encoder_param_name(h, i).decode(), L.gt_text_encoder_param_numel(h, i))
+               for i in range(L.gt_text_encoder_num_params(h))]
+        assert got == enc_ref
+        x = np.zeros(4, np.float32)
+        assert L.gt_text_encoder_set_param(h, b"no.such.param", x.ctypes.data, 4) == 3
+        assert L.gt_text_encoder_set_param(h, b"proj_w.proj.bias", x.ctypes.data, 4) == 3
+        assert L.gt_text_encoder_set_param(h, b"proj_w.proj.bias", x.ctypes.data, 1) == 0
+        assert L.gt_text_encoder_workspace_bytes(h, 2, 10) > 0
+    finally:
+        L.gt_text_encoder_destroy(h)
+    voc_ref = [(k, int(np.prod(s))) for k, s in json.load(open(os.path.join(gold, "hifigan_layout.json")))]
+    ia = lambda xs: (ctypes.c_int * len(xs))(*xs)
+    v = ctypes.c_void_p()
+    dil = [d for ds in HIFIGAN_V1["resblock_dilation_sizes"] for d in ds]
+    assert L.gt_vocoder_create(80, 512, 4, ia([8, 8, 2, 2]), ia([16, 16, 4, 4]), 3, ia([3, 7, 11]), ia(dil),
+                               ctypes.byref(v)) == 0
+    try:
+        got = [(L.gt_vocoder_param_name(v, i).decode(), L.gt_vocoder_param_numel(v, i))
+               for i in range(L.gt_vocoder_num_params(v))]
+        assert got == voc_ref
+        assert L.gt_vocoder_hop(v) == 256
+        assert L.gt_vocoder_set_compute_dtype(v, 1) == 0 and L.gt_vocoder_set_compute_dtype(v, 2) == 1
+        assert L.gt_vocoder_workspace_bytes(v, 1, 10) > 0
+    finally:
+        L.gt_vocoder_destroy(v)
+    # an unsupported configuration (upsampling kernel != 2 x rate) is refused at creation
+    assert L.gt_vocoder_create(80, 512, 1, ia([8]), ia([15]), 3, ia([3, 7, 11]), ia(dil), ctypes.byref(v)) == 4
