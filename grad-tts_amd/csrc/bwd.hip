@@ -387,14 +387,14 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
         if (sl + 4 * q < NCOL) s_q[(rr * NCOL + sl + 4 * q) * QS + sc] = rq[rr][q];
     __syncthreads();
     if (sg + 1 < s_hi) load(sg + 1);
+#pragma unroll 2
+    for (int up = 0; up < SEG / 2; ++up) {   // one P read feeds the KG taps: independent accumulator chains
+      const int u = 2 * up + hh;
+      const float pa = s_p[u * PS + ab + r];
 #pragma unroll
-    for (int g = 0; g < KG; ++g) {
-      const int kh = g / KS, kw = g % KS;
-#pragma unroll 4
-      for (int up = 0; up < SEG / 2; ++up) {
-        const int u = 2 * up + hh;
-        acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(s_p[u * PS + ab + r], s_q[(kh * NCOL + u * S + kw) * QS + bb + r],
-                                                      acc[g], 0, 0, 0);
+      for (int g = 0; g < KG; ++g) {
+        const int kh = g / KS, kw = g % KS;
+        acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(pa, s_q[(kh * NCOL + u * S + kw) * QS + bb + r], acc[g], 0, 0, 0);
       }
     }
   }
