@@ -63,14 +63,21 @@ def test_front_end_exact_on_reference_encoder_outputs(name, ls):
     assert np.array_equal(mu_y.cpu().numpy(), g[f"{k}_mu_y"])
 
 
-def test_gradtts_forward_matches_oracle_chain():
+@pytest.mark.parametrize("n_spks", [1, 247])
+def test_gradtts_forward_matches_oracle_chain(n_spks):
     from oracle import decoder as odec, text_encoder as ote
     from gradtts_amd.tts import GradTTS
-    m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+    m = GradTTS(149, n_spks, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
     esd = synthetic_text_encoder_state_dict(2)
-    dsd = synthetic_state_dict(seed=0, n_spks=1)
+    dsd = synthetic_state_dict(seed=0, n_spks=n_spks)
     m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)
     m.decoder.estimator.load_state_dict({k: torch.from_numpy(v) for k, v in dsd.items()}, strict=True)
+    spk_ids, spk_vec = None, None
+    if n_spks > 1:   # speaker embedding table (tts.py:46) with seeded values; ids looked up as tts.py:78 does
+        table = torch.from_numpy(np.random.default_rng(5).standard_normal((n_spks, 64)).astype(np.float32))
+        m.spk_emb.weight.data.copy_(table)
+        spk_ids = torch.tensor([3, 200])
+        spk_vec = table[spk_ids]
     m = m.cuda()
     rng = np.random.default_rng(4)
     B, Tx = 2, 29
@@ -85,7 +92,8 @@ def test_gradtts_forward_matches_oracle_chain():
 
     torch.randn_like = record
     try:
-        enc_out, dec_out, attn = m(tokens.cuda(), lengths.cuda(), n_timesteps=5)
+        enc_out, dec_out, attn = m(tokens.cuda(), lengths.cuda(), n_timesteps=5,
+                                   spk=spk_ids.cuda() if spk_ids is not None else None)
     finally:
         torch.randn_like = randn_like
     assert len(drawn) == 1
@@ -93,12 +101,14 @@ def test_gradtts_forward_matches_oracle_chain():
     mu_x, logw, xm = ote.text_encoder(ote.to_torch_params(esd), tokens, lengths)
     w_ceil, y_len, y_max, y_mask, r_attn, mu_y = ote.front_end(mu_x, logw, xm)
     z = mu_y + drawn[0].cpu()
-    r_dec = odec.reverse_diffusion(odec.to_torch_params(dsd), z, y_mask, mu_y, 5)
+    r_dec = odec.reverse_diffusion(odec.to_torch_params(dsd), z, y_mask, mu_y, 5, spk_vec, n_spks)
     # the reference slices attn's TEXT axis with y_max_length (tts.py:108): kept as is
     assert enc_out.shape[-1] == y_max and attn.shape == r_attn[:, :, :y_max].shape
     assert np.array_equal(attn.cpu().numpy(), r_attn[:, :, :y_max].numpy())
-    report("GradTTS.forward encoder outputs", rel_err(enc_out.cpu().numpy(), mu_y[:, :, :y_max].numpy()), 2e-5)
-    report("GradTTS.forward decoder outputs (N=5)", rel_err(dec_out.cpu().numpy(), r_dec[:, :, :y_max].numpy()), 1e-4)
+    report(f"GradTTS.forward encoder outputs n_spks={n_spks}", rel_err(enc_out.cpu().numpy(),
+                                                                       mu_y[:, :, :y_max].numpy()), 2e-5)
+    report(f"GradTTS.forward decoder outputs (N=5) n_spks={n_spks}",
+           rel_err(dec_out.cpu().numpy(), r_dec[:, :, :y_max].numpy()), 1e-4)
 
 
 def test_text_encoder_speed_vs_torch_eager():
