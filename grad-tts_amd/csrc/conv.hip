@@ -585,12 +585,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0, int TF_ = 4>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 
-// 3x3 launch with the tile height conv_tf picks (5 rows only exists for 128-wide tiles)
+// 3x3 launch with the tile height conv_tf picks (5 rows only exists for 128-wide tiles; the small-batch plan's
+// 1-row (128-wide) / 2-row (64-wide) tiles only for bf16 weights)
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
+  if constexpr (!W8 && sizeof(A) == 2)
+    if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, 0, NT == 128 ? 1 : 2>(p, s);
   if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
+}
+template <class A, int IN, int OUT, int NT>
+static hipError_t launch_c1(const ConvParams& p, hipStream_t s) {
+  if constexpr (sizeof(A) == 2)
+    if (p.small) return launch_t<A, CONV1, IN, OUT, NT, 0, NT == 128 ? 1 : 2>(p, s);
+  return launch_t<A, CONV1, IN, OUT, NT>(p, s);
 }
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
@@ -612,13 +621,13 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
 template <class A, int NT>
 static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   // Instantiated combinations (the U-Net uses exactly these):
-  if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_t<A, CONV3, IN_INPUT, OUT_STATS, NT>(p, s);
+  if (kind == CONV3 && im == IN_INPUT && om == OUT_STATS) return launch_c3<A, IN_INPUT, NT, 0>(p, s);
   if (kind == CONV3 && im == IN_MASK && om == OUT_STATS) return launch_c3<A, IN_MASK, NT, 0>(p, s);
   if (kind == CONV3 && im == IN_GN && om == OUT_STATS) return launch_c3<A, IN_GN, NT, 0>(p, s);
   if (kind == CONV3 && im == IN_PLAIN && om == OUT_STATS) return launch_c3<A, IN_PLAIN, NT, 0>(p, s);
-  if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_t<A, CONV1, IN_INPUT, OUT_RBOUT, NT>(p, s);
-  if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_t<A, CONV1, IN_MASK, OUT_RBOUT, NT>(p, s);
-  if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_t<A, CONV1, IN_PLAIN, OUT_RESID, NT>(p, s);
+  if (kind == CONV1 && im == IN_INPUT && om == OUT_RBOUT) return launch_c1<A, IN_INPUT, OUT_RBOUT, NT>(p, s);
+  if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_c1<A, IN_MASK, OUT_RBOUT, NT>(p, s);
+  if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_c1<A, IN_PLAIN, OUT_RESID, NT>(p, s);
   if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONV3_S2, IN_MASK, OUT_PLAIN, NT>(p, s);
   if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT>(p, s);
   return hipErrorNotSupported;
@@ -638,14 +647,15 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
   return hipErrorNotSupported;
 }
 
-int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout) {   // CONV3 tiles: TF rows x 64 frames x NT
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small) {   // CONV3 tiles: TF rows x 64 frames x NT
   const int nt = conv_nt(act_bf16, Cout);
-  return (F / conv_tf(CONV3, im, nt, Cout, F)) * ((T + 63) / 64) * (Cout / nt);
+  return (F / conv_tf(CONV3, im, nt, Cout, F, small)) * ((T + 63) / 64) * (Cout / nt);
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
+  if (p.small && !act_bf16) return hipErrorNotSupported;   // small-batch plan: bf16 weights and activations only
   if (p.wscale) {   // fp8 weight image
-    if (!act_bf16) return hipErrorNotSupported;
+    if (!act_bf16 || p.small) return hipErrorNotSupported;
     return conv_nt(1, p.Cout) == 128 ? dispatch_w8<128>(kind, im, om, p, s) : dispatch_w8<64>(kind, im, om, p, s);
   }
   if (!act_bf16) return dispatch<float, 64>(kind, im, om, p, s);

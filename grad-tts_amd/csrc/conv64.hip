@@ -324,16 +324,19 @@ bool conv64_eligible(const ConvParams& p) {
 // segment -- and with them every rounding are the same in any batch or GPU shard. 80 rows: the whole column (20
 // tiles; 512 workgroups at B = 32, T = 512); 40 rows: half a column (5 tiles), which keeps two workgroups per CU
 // at level 1.
-static int conv64_seg(int F) {
+// The small-batch plan (decoder.cpp) walks one tile per segment: at B = 1 the throughput plan launches 16
+// workgroups at level 0.
+static int conv64_seg(int F, int small) {
   const int n_ft = F / 4;
+  if (small) return 1;
   return (n_ft >= 20 || n_ft % 2) ? n_ft : n_ft / 2;
 }
 
-int conv64_nparts(int F, int T) { return ((T + 31) / 32) * ((F / 4) / conv64_seg(F)); }
+int conv64_nparts(int F, int T, int small) { return ((T + 31) / 32) * ((F / 4) / conv64_seg(F, small)); }
 
 hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
-  const int L = conv64_seg(p.Fout);
+  const int L = conv64_seg(p.Fout, p.small);
   const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
   if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK>), dim3(grid), dim3(256), 0, s, p, L);
   else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN>), dim3(grid), dim3(256), 0, s, p, L);

@@ -136,6 +136,10 @@ struct Blob {   // host staging of one packed device arena
   }
 };
 
+// largest call batch on the small-batch tile plan (small_plan). Measured (50-step decodes, T = 512, one box):
+// B = 1 47.3 vs 78.9 ms, B = 2 50.7 vs 80.6, B = 4 61.0 vs 82.7, B = 8 94.9 vs 94.3, B = 16 152.9 vs 116.3
+constexpr int64_t kSmallB = 4;
+
 }  // namespace
 
 struct gt_decoder {
@@ -169,6 +173,9 @@ struct gt_decoder {
   std::vector<Graph> gcache;   // most recently used last
   int64_t captures = 0;
   int64_t max_chunk = 0;       // > 0: cap on utterances per internal batch chunk (GT_MAX_CHUNK, tests)
+  // bf16 calls on at most small_b utterances run the small-batch tile plan (small_plan below);
+  // GT_SMALL_B at creation or gt_decoder_set_small_batch
+  int64_t small_b = kSmallB;
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -483,6 +490,7 @@ struct Run {
   const float* tb; long tb_bstride;
   const int* stepp = nullptr;     // device step index of graph segments (kernels.h tb_at); null = 0
   const float* betas = nullptr;   // per-step beta(t) table (sampler), indexed by *stepp
+  int small = 0;                  // small-batch tile plan (small_plan)
   int stat_slot = 0;
   hipError_t err = hipSuccess;
   const char* probe = nullptr;   // diagnostics: copy the activation named `probe` to probe_out (NCHW fp32)
@@ -513,9 +521,10 @@ struct Run {
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
     // "<instantiation as rocprof names it>@<shape>": bench.py aggregates per instantiation
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
+    const int tf = dt ? conv_tf(kind, im, nt, p.Cout, p.Fout, p.small) : 4;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
-                             (p.wscale ? ",w8" : "") + (dt && conv_tf(kind, im, nt, p.Cout, p.Fout) == 5 ? ",tf5" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+                             (p.wscale ? ",w8" : "") + (tf != 4 ? ",tf" + std::to_string(tf) : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
@@ -528,10 +537,10 @@ struct Run {
       const double pos = (double)p.B * p.Fout * p.Tout;
       timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
-      return conv64_nparts(p.Fout, p.Tout);
+      return conv64_nparts(p.Fout, p.Tout, p.small);
     }
     conv(CONV3, im, OUT_STATS, p);
-    return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout);
+    return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small);
   }
 
   // diagnostics: "gnpart.<k>" copies GroupNorm partial slot k (B x pmax x 16 floats) after the launch that
@@ -571,6 +580,7 @@ struct Run {
     p.B = B; p.T0 = T; p.mask = mask; p.stepp = stepp;
     p.Fin = Fl(lvl_in); p.Tin = Tl(lvl_in); p.Fout = Fl(lvl_out); p.Tout = Tl(lvl_out);
     p.lvl_in = lvl_in; p.lvl_out = lvl_out;
+    p.small = small;
     return p;
   }
 
@@ -594,7 +604,7 @@ struct Run {
       p.out = pre1; p.out_part = st1;
       if (input) {
         conv(CONV3, IN_INPUT, OUT_STATS, p);
-        np1 = conv_gn_nparts(dt, IN_INPUT, Fl(lvl), Tl(lvl), Cout);
+        np1 = conv_gn_nparts(dt, IN_INPUT, Fl(lvl), Tl(lvl), Cout, small);
       } else {
         np1 = conv3_stats(IN_MASK, p, k + "block1.block.0.weight");
       }
@@ -752,6 +762,13 @@ struct Run {
   }
 };
 
+// Small-batch tile plan: bf16 (not fp8-weight) calls on at most d->small_b utterances take 1-row (128-wide)
+// and 2-row (64-wide) conv tiles and one-tile conv64 segments -- at B = 1 the throughput tiles fill 16-40 of the 256
+// CUs at levels 1-2 and 16 at level 0. Every utterance's arithmetic is the same within a plan (batch-invariant
+// for any B on either side of the threshold); the two plans partition the GroupNorm partial sums differently, so
+// results across plans agree to fp32 rounding of those sums (GPU test: plan agreement within the bf16 gate).
+int small_plan(const gt_decoder* d, int dtype, int64_t nb) { return (dtype == GT_BF16 && nb <= d->small_b) ? 1 : 0; }
+
 uint8_t* align_ws(void* ws) { return (uint8_t*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
 
 // Utterances per internal batch chunk. The conv kernels address an activation tensor through a raw buffer
@@ -806,6 +823,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   for (int k = 0; k < 32; ++k) d->freqs[k] = expf((float)k * negc);
   if (const char* e = getenv("GT_GRAPHS")) d->graphs = atoi(e) != 0;
   if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
+  if (const char* e = getenv("GT_SMALL_B")) d->small_b = atoll(e);
   *out = d;
   return GT_OK;
 }
@@ -906,7 +924,7 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
     const int64_t nb = std::min(Bc, B - b0);
     const size_t fo = (size_t)b0 * 80 * T;
     Run R;
-    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.s = (hipStream_t)stream;
+    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = (hipStream_t)stream;
     R.ws = align_ws(workspace);
     R.L = layout(R.dt, nb, T, 0);
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = x + fo; R.spk_s = nullptr;
@@ -1134,7 +1152,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
     const int64_t nb = std::min(Bc, B - b0);
     const size_t fo = (size_t)b0 * 80 * T;
     Run R;
-    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.s = st;
+    R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = st;
     R.ws = align_ws(workspace);
     R.L = layout(R.dt, nb, T, n_timesteps);
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = out + fo; R.spk_s = nullptr;
@@ -1174,7 +1192,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
         const int S = n_timesteps <= 100 ? n_timesteps : 50;
         const int q = n_timesteps / S, rem = n_timesteps % S;
         auto key = [&](int steps) {
-          return std::vector<uintptr_t>{(uintptr_t)dtype, (uintptr_t)nb, (uintptr_t)T, (uintptr_t)steps,
+          return std::vector<uintptr_t>{(uintptr_t)dtype, (uintptr_t)nb, (uintptr_t)R.small, (uintptr_t)T, (uintptr_t)steps,
                                         (uintptr_t)n_timesteps, (uintptr_t)R.ws, (uintptr_t)xt, (uintptr_t)R.mask,
                                         (uintptr_t)R.mu, (uintptr_t)d->arena[dtype]};
         };
@@ -1201,5 +1219,13 @@ int gt_decoder_set_graphs(gt_decoder* d, int on) {
 }
 
 int64_t gt_decoder_graph_captures(const gt_decoder* d) { return d ? d->captures : -1; }
+
+int gt_decoder_set_small_batch(gt_decoder* d, int64_t max_b) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  if (max_b < 0) return fail(GT_ERR_ARG, "max_b must be >= 0");
+  d->small_b = max_b;
+  d->drop_graphs();
+  return GT_OK;
+}
 
 }  // extern "C"

@@ -40,11 +40,12 @@ struct ConvParams {
   // ---- output
   void* out; float* out_part;                         // OUT_STATS: GroupNorm partials of the output (common.h)
   const void* pre; const float* pre_part; int pre_nparts; const float* pre_gamma; const float* pre_beta; long pre_count;  // OUT_RBOUT
+  int small;                     // small-batch tile plan (wimage.h conv_tf; conv64 one-tile segments)
 };
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid
-int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout);
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small);
 
 struct AttnKVParams {
   const void* x; int B, n, C, Cpad;   // x: [B][n][C] (n = F*T)
@@ -95,7 +96,7 @@ hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, in
 
 // weight-resident 3x3 conv for Cin = Cout = 64, bf16 (conv64.hip); GroupNorm partial slots: one per 4 x 32 tile
 // (conv64_nparts). conv64_eligible: shape/layout preconditions (no concat, no fp8 image).
-int conv64_nparts(int F, int T);
+int conv64_nparts(int F, int T, int small);
 bool conv64_eligible(const ConvParams& p);
 hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s);
 

@@ -1,0 +1,99 @@
+"""Small-batch tile plan (decoder.cpp small_plan, include/gradtts.h gt_decoder_set_small_batch).
+
+bf16 calls on at most 4 utterances run 1-row (128-wide) / 2-row (64-wide) conv tiles and one-tile conv64
+segments, so that a single utterance fills the GPU. Checked here:
+  * the plan is batch-invariant on its own: an utterance decoded alone, in a pair, or in a batch of 4 gives
+    bit-identical mels (GroupNorm partial slots and attention tiles depend only on the utterance's shape);
+  * the two plans agree within the bf16 sampler gate (1e-2) -- they differ only in how the
+    GroupNorm partial sums are partitioned (fp32 rounding), printed as PARITY lines;
+  * the throughput plan (forced on small batches with gt_decoder_set_small_batch(dec, 0)) still meets the
+    reference-pinned bf16 gates on the golden fixtures (the default run of test_decoder_gpu.py now takes the
+    small plan at those batch sizes);
+  * small-plan latency at B = 1, T = 512 is printed next to the throughput plan's (no timing gate).
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available, load_golden
+from gpu_util import make_decoder, rel_err, report
+from gradtts_amd import _lib
+from gradtts_amd.params import synthetic_inputs
+
+pytestmark = pytest.mark.gpu
+
+BF16_REV_TOL = 1e-2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _inputs(seed, B, T, lengths=None):
+    mu, z, mask, spk = synthetic_inputs(seed, B, T, lengths=lengths)
+    return [torch.from_numpy(a).cuda() for a in (mu, z, mask, spk)]
+
+
+def _set_small(dec, max_b):
+    L = _lib.lib()
+    _lib.check(L.gt_decoder_set_small_batch(dec.estimator._native(), max_b), "gt_decoder_set_small_batch")
+
+
+def test_small_plan_batch_invariant():
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    mu, z, mask, _ = _inputs(21, 4, 256, lengths=[256, 200, 120, 64])
+    y4 = dec(z, mask, mu, 3)
+    y1 = dec(z[1:2].contiguous(), mask[1:2].contiguous(), mu[1:2].contiguous(), 3)
+    y2 = dec(z[2:4].contiguous(), mask[2:4].contiguous(), mu[2:4].contiguous(), 3)
+    assert torch.isfinite(y4).all()
+    assert torch.equal(y4[1:2], y1), float((y4[1:2] - y1).abs().max())
+    assert torch.equal(y4[2:4], y2), float((y4[2:4] - y2).abs().max())
+
+
+@pytest.mark.parametrize("B,T,N", [(1, 512, 10), (3, 256, 10), (4, 128, 10)])
+def test_plans_agree(B, T, N):
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    lengths = [T - 16 * i for i in range(B)]
+    mu, z, mask, _ = _inputs(5 + B, B, T, lengths=lengths)
+    y_small = dec(z, mask, mu, N).cpu().numpy()
+    _set_small(dec, 0)
+    y_tput = dec(z, mask, mu, N).cpu().numpy()
+    assert np.isfinite(y_small).all() and np.isfinite(y_tput).all()
+    report(f"small vs throughput plan bf16 B={B} T={T} N={N}", rel_err(y_small, y_tput), BF16_REV_TOL)
+
+
+@pytest.mark.parametrize("name", ["reverse_s1_N10.npz", "reverse_s247_N10.npz", "reverse_s1_N50.npz"])
+def test_throughput_plan_bf16_matches_reference(name):
+    g = load_golden(name)
+    n_spks = int(g["n_spks"])
+    dec, _ = make_decoder(n_spks, int(g["seed_w"]), torch.bfloat16)
+    _set_small(dec, 0)
+    spk = torch.from_numpy(g["spk"]).cuda() if n_spks != 1 else None
+    c = lambda k: torch.from_numpy(np.ascontiguousarray(g[k])).cuda()
+    y = dec(c("z"), c("mask"), c("mu"), int(g["n_timesteps"]), False, spk).cpu().numpy()
+    report(f"reverse bf16 throughput plan {name}", rel_err(y, g["out"]), BF16_REV_TOL)
+
+
+def test_latency_b1_report():
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    mu, z, mask, _ = _inputs(3, 1, 512)
+    N = 20
+
+    def run():
+        dec(z, mask, mu, N)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        y = dec(z, mask, mu, N)
+        torch.cuda.synchronize()
+        return y, (time.perf_counter() - t0) / N * 1e3
+
+    y_s, ms_s = run()
+    _set_small(dec, 0)
+    y_t, ms_t = run()
+    print(f"LATENCY B=1 T=512 bf16: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
+          f"({512 / (50 * ms_s) * 1e3:.0f} vs {512 / (50 * ms_t) * 1e3:.0f} mel-frames/s for 50-step decodes)")
+    assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()

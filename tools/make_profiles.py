@@ -57,7 +57,7 @@ def norm(name: str) -> str:
         if base == "conv_kernel":            # <A, KIND, IN, OUT, NT, W8, TF>
             A, kind, im, om, nt, w8, tf = args
             return (f"conv_kernel<{ty(A)},{kind},{im},{om},{nt}" + (",w8" if w8 in ("1", "true") else "") +
-                    (",tf5" if tf == "5" else "") + ">")
+                    ("" if tf == "4" else ",tf" + tf) + ">")
         if base == "conv64_kernel":          # <IN>
             return f"conv64_kernel<{args[0]}>"
         if base == "gn_mish_kernel":         # <A, APPLY>: the ResnetBlock output or block2's in-place input
