@@ -77,6 +77,9 @@ struct ConvCfg {
   // the other half of chunk c is in the MFMAs. Every wave issues exactly PA / PB DMA pieces per half and PPT
   // patch loads per chunk, so counted vmcnt waits retire exactly the right ones.
   static constexpr bool SPLIT = !W8 && NA < NTAP && IN != IN_INPUT;
+  // 1x1 convs: two weight slabs, chunk c+1's DMA in flight during chunk c's MFMAs (a 1x1 chunk is one tap, too
+  // short to hide a weight round trip behind; the slab is 4-8 KB)
+  static constexpr bool DBW = !SPLIT && KIND == CONV1;
   static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
   static constexpr int CK = CKB / (int)sizeof(A);
   static constexpr int ICH = 16 / (int)sizeof(A);
@@ -85,7 +88,8 @@ struct ConvCfg {
   static constexpr int PITEMS = PR * PC * SUBS;
   static constexpr int PPT = (PITEMS + 255) / 256;
   static constexpr int A_BYTES = PR * PC * POSB;
-  static constexpr int SMEM0 = A_BYTES + WBYTES + (3 * 256 + 128 + 64 + 16 + 128) * 4;
+  static constexpr int WBUF = DBW ? 2 * WBYTES : WBYTES;   // weight slab(s) in LDS
+  static constexpr int SMEM0 = A_BYTES + WBUF + (3 * 256 + 128 + 64 + 16 + 128) * 4;
   // Workgroups per CU are capped by LDS where more resident tiles measured slower (cache/write
   // contention, not latency hiding, bounds them): CAP = 0 leaves occupancy to registers and LDS.
   // (measured, tools/ab_variants.sh: 64-wide 1x1 and sub-pixel convs 3, stride-2 64-wide 2; the fp8-weight
@@ -97,6 +101,7 @@ struct ConvCfg {
   static_assert(TF * RBT % WM == 0, "row blocks split evenly over the waves");
   static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
   static_assert(WBYTES % 1024 == 0, "whole DMA pieces");
+  static_assert(!DBW || WPIECES_ALL % 4 == 0, "counted waits: every wave issues WPIECES weight pieces");
   static_assert(!SPLIT || (HA % 4096 == 0 && (WBYTES - HA) % 4096 == 0 && PB + PPT <= 63), "wave-even halves");
   static_assert(!W8 || (sizeof(A) == 2 && KIND != CONV1), "fp8 weights: bf16 operands, 3x3 / 2x2 convs");
 };
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   __shared__ __attribute__((aligned(16))) char smem[C::SMEM];   // ONE LDS object (see guide §5 trap a)
   char* sA = smem;
   char* const sW = smem + C::A_BYTES;
-  float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBYTES);
+  float* s_sc = reinterpret_cast<float*>(smem + C::A_BYTES + C::WBUF);
   float* s_sh = s_sc + 256;
   float* s_tb = s_sh + 256;
   float* s_bias = s_tb + 256;    // bias of this tile's NT output channels
@@ -279,16 +284,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int nchunk = p.Cin_pad / C::CK;
   wimg += ((long)(par * gridDim.y + ntile) * nchunk) * C::WBYTES;
 
-  auto dma_weights = [&](int ch) {   // contiguous slab, 1 KiB per wave instruction, compile-time count
+  auto dma_weights_to = [&](int ch, char* dst) {   // contiguous slab, 1 KiB per wave instruction, compile-time count
     const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
 #pragma unroll
     for (int k = 0; k < C::WPIECES; ++k) {
       const int i = wv + 4 * k;
       if (C::WPIECES_ALL % 4 != 0 && i >= C::WPIECES_ALL) break;   // wave-uniform
       __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
-                                       (__attribute__((address_space(3))) void*)(sW + i * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
     }
   };
+  auto dma_weights = [&](int ch) { dma_weights_to(ch, sW); };
+  const char* wcur = sW;   // weight slab the MFMAs read (DBW: alternates between the two buffers)
   // Workgroup barrier for the chunk loop without the memory-model fence of __syncthreads() (which waits
   // for every LDS-DMA in flight); what must be visible is made explicit: own LDS stores (lgkmcnt) and
   // this chunk's weight DMA (vmcnt below).
@@ -335,11 +342,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     const int koff = ks * C::KSTEP_B + h * (C::KSTEP_B / 2);
     const int row = wn * 64 + cb * 32 + r;
     if constexpr (W8)   // 8-byte units swizzled per row (wimage.h conv8_swz; row base is a multiple of 32)
-      return w8_frag(sW + row * C::WROW + ((2 * tap + h) ^ conv8_swz(C::NTAP, r)) * 8);
+      return w8_frag(wcur + row * C::WROW + ((2 * tap + h) ^ conv8_swz(C::NTAP, r)) * 8);
     else if (tap < C::NA)
-      return Mma<A>::load(sW + row * C::WROW + tap * C::CKB + koff);
+      return Mma<A>::load(wcur + row * C::WROW + tap * C::CKB + koff);
     else
-      return Mma<A>::load(sW + C::HA + row * C::WROWB + (tap - C::NA) * C::CKB + koff);
+      return Mma<A>::load(wcur + C::HA + row * C::WROWB + (tap - C::NA) * C::CKB + koff);
   };
   auto mma_taps = [&](int t0, int t1) {
     constexpr int RB = C::RBW, KS = C::KSTEPS;
@@ -418,6 +425,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         dma_half(ch + 1, 1);
         if (ch + 2 < nchunk) issue_patch(ch + 2);
       }
+    }
+  } else if constexpr (C::DBW) {
+    // Per chunk ch: [MFMAs of ch-1 done] patch ch -> LDS (its registers, loaded one chunk ahead, arrive after
+    // weight slab ch, which was issued before them: in-order vmcnt), weight DMA of ch+1 into the other buffer,
+    // counted wait leaving only that DMA in flight | [patch and slab ch visible] patch loads of ch+1, MFMAs.
+    char* const sW1 = sW + C::WBYTES;
+    dma_weights(0);
+    for (int ch = 0; ch < nchunk; ++ch) {
+      cta_sync();
+      store_patch(ch * C::CK);
+      if (ch + 1 < nchunk) {
+        dma_weights_to(ch + 1, (ch & 1) ? sW : sW1);
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::WPIECES) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      cta_sync();
+      if (ch + 1 < nchunk) issue_patch(ch + 1);
+      wcur = (ch & 1) ? sW1 : sW;
+      mma_taps(0, C::NTAP);
     }
   } else {
     for (int ch = 0; ch < nchunk; ++ch) {
@@ -599,6 +626,8 @@ template <class A, int IN, int OUT, int NT>
 static hipError_t launch_c1(const ConvParams& p, hipStream_t s) {
   if constexpr (sizeof(A) == 2)
     if (p.small) return launch_t<A, CONV1, IN, OUT, NT, 0, NT == 128 ? 1 : 2>(p, s);
+  if constexpr (NT == 128 && IN != IN_INPUT)
+    if (conv_tf(CONV1, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV1, IN, OUT, NT, 0, 5>(p, s);
   return launch_t<A, CONV1, IN, OUT, NT>(p, s);
 }
 

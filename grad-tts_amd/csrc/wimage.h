@@ -37,12 +37,18 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_L1_TF5_GN
 #define GT_L1_TF5_GN 1
 #endif
+// 128-wide 1x1 convs on 5-row tiles where that removes a partial round of workgroups (2 per CU): level 2 with 256
+// output channels (640 -> 512 tiles at B = 32) and level 1 (1280 -> 1024)
+#ifndef GT_TF5_1X1
+#define GT_TF5_1X1 1
+#endif
 // mel rows per 3x3 / 1x1 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid
 // rows, small: the small-batch plan). Small batches (decoder.cpp small_plan) take one-row tiles for 128-wide and
 // two-row tiles for 64-wide convs (64 positions per wave pair: 4-5x the workgroups of the throughput tiles, which at
 // B = 1 fill 16-40 of the 256 CUs).
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f, int small = 0) {
   return (small && (kind == 0 /*CONV3*/ || kind == 2 /*CONV1*/)) ? (nt == 128 ? 1 : 2)
+         : (GT_TF5_1X1 && kind == 2 /*CONV1*/ && nt == 128 && (cout >= 256 || f == 40)) ? 5
          : (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
             ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
              (im == 2 && (cout >= 256 || (GT_L1_TF5_GN && cout == 128 && f == 40))))) ? 5 : 4;
