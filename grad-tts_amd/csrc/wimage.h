@@ -24,11 +24,11 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_TF5
 #define GT_TF5 1
 #endif
-// Option (off: measured slower, the level-1 gn_apply pass costs more than the 5-row tiles save): 128-output convs
-// on the 40-row level-1 grid too (1024 tiles at B = 32 instead of 1280); their GroupNorm-input
-// variant then takes the in-place gn_apply pass + plain input (decoder.cpp)
+// 128-output convs without an operand transform on the 40-row level-1 grid on 5-row tiles too (1024 tiles at B = 32
+// instead of 1280). On since round 2 (same-box A/B: 97.5 -> 95.0 us and 65.4 -> 62.3 us for the two level-1 block1
+// convs); in round 1 it was tied to a gn_apply pass for the GroupNorm-input variant, which GT_L1_TF5_GN replaced.
 #ifndef GT_L1_TF5
-#define GT_L1_TF5 0
+#define GT_L1_TF5 1
 #endif
 // The level-1 GroupNorm-input conv (128 -> 128, 40 rows) on 5-row tiles with the in-register GroupNorm transform:
 // 1024 tiles at B = 32 (two whole rounds of 512 slots) instead of 1280. On since round 2: with the interleaved
