@@ -622,6 +622,12 @@ static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
+template <class A, int NT, int W8>
+static hipError_t launch_ct(const ConvParams& p, hipStream_t s) {   // Upsample (f = fine grid rows, as conv_tf takes)
+  if constexpr (NT == 128)
+    if (conv_tf(CONVT4, IN_MASK, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT, W8, 5>(p, s);
+  return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT, W8>(p, s);
+}
 template <class A, int IN, int OUT, int NT>
 static hipError_t launch_c1(const ConvParams& p, hipStream_t s) {
   if constexpr (sizeof(A) == 2)
@@ -658,7 +664,7 @@ static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParam
   if (kind == CONV1 && im == IN_MASK && om == OUT_RBOUT) return launch_c1<A, IN_MASK, OUT_RBOUT, NT>(p, s);
   if (kind == CONV1 && im == IN_PLAIN && om == OUT_RESID) return launch_c1<A, IN_PLAIN, OUT_RESID, NT>(p, s);
   if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONV3_S2, IN_MASK, OUT_PLAIN, NT>(p, s);
-  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<A, CONVT4, IN_MASK, OUT_PLAIN, NT>(p, s);
+  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_ct<A, NT, 0>(p, s);
   return hipErrorNotSupported;
 }
 
@@ -672,7 +678,7 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
     if (im == IN_PLAIN) return launch_c3<bf16, IN_PLAIN, NT, 1>(p, s);
   }
   if (kind == CONV3_S2 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONV3_S2, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
-  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_t<bf16, CONVT4, IN_MASK, OUT_PLAIN, NT, 1>(p, s);
+  if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_ct<bf16, NT, 1>(p, s);
   return hipErrorNotSupported;
 }
 

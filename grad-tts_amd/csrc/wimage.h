@@ -42,6 +42,11 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_TF5_1X1
 #define GT_TF5_1X1 1
 #endif
+// The 128-channel Upsample (level 2 -> 1, 20 coarse rows) on 5-row tiles: 1280 -> 1024 workgroups at B = 32 (two
+// whole rounds of 512 instead of 2.5)
+#ifndef GT_TF5_T
+#define GT_TF5_T 1
+#endif
 // mel rows per 3x3 / 1x1 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid
 // rows, small: the small-batch plan). Small batches (decoder.cpp small_plan) take one-row tiles for 128-wide and
 // two-row tiles for 64-wide convs (64 positions per wave pair: 4-5x the workgroups of the throughput tiles, which at
@@ -49,6 +54,7 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f, int small = 0) {
   return (small && (kind == 0 /*CONV3*/ || kind == 2 /*CONV1*/)) ? (nt == 128 ? 1 : 2)
          : (GT_TF5_1X1 && kind == 2 /*CONV1*/ && nt == 128 && (cout >= 256 || f == 40)) ? 5
+         : (GT_TF5_T && kind == 3 /*CONVT4*/ && nt == 128 && f == 40) ? 5
          : (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
             ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
              (im == 2 && (cout >= 256 || (GT_L1_TF5_GN && cout == 128 && f == 40))))) ? 5 : 4;
