@@ -21,7 +21,10 @@
 
 namespace gt {
 
-template <class A, int CPR>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
+// RB: the input is formed from the ResnetBlock's block2 pre-activation and its residual in the operand load
+// (AttnKVParams::rb_pre); the formed rows also go to rb_out. Same expression and GroupNorm reduction as
+// gn_mish_kernel, so the stored activation is bit-identical to the separate pass it replaces.
+template <class A, int CPR, bool RB>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_kv_kernel(AttnKVParams p) {
   constexpr bool RES = CPR > 0;
   constexpr int CK = 64 / (int)sizeof(A);
@@ -40,6 +43,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const A* x = reinterpret_cast<const A*>(p.x) + (long)b * p.n * p.C;
   const A* wkv = reinterpret_cast<const A*>(p.wkv);
+  const A* pre = RB ? reinterpret_cast<const A*>(p.rb_pre) + (long)b * p.n * p.C : nullptr;
+  A* rb_out = RB ? reinterpret_cast<A*>(p.rb_out) + (long)b * p.n * p.C : nullptr;
+  __shared__ float s_sc[RB ? 256 : 1], s_sh[RB ? 256 : 1], s_mean[8], s_rstd[8];
+  __shared__ double s_red[RB ? 272 : 1];
+  GnLoad gl;
+  if (RB) gl = gn_load(p.rb_part, p.rb_nparts, b);   // slot loads in flight with the weight / first x loads
 
   if (RES) {   // whole [256][C] k/v projection resident in LDS
     for (int it = tid; it < 256 * IPR; it += 256) {
@@ -57,23 +66,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 
   const int tbeg = tile * p.tile_pos;
   const int tend = min(p.n, tbeg + p.tile_pos);
-  uint4 xr[XIT];
+  uint4 xr[XIT], xq[RB ? XIT : 1];   // RB: xr = block2 pre-activation, xq = residual input
+  float mk[RB ? XIT : 1];
   auto load_x = [&](int pos0, int c0) {
 #pragma unroll
     for (int j = 0; j < XIT; ++j) {
       const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
       const int pos = pos0 + row;
-      xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + (long)pos * p.C + c0 + sub * ICH) : make_uint4(0, 0, 0, 0);
+      const long e = (long)pos * p.C + c0 + sub * ICH;
+      if (RB) {
+        xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(pre + e) : make_uint4(0, 0, 0, 0);
+        xq[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + e) : make_uint4(0, 0, 0, 0);
+        mk[j] = pos < tend ? mask_at(p.mask, p.T0, b, pos % p.T, p.lvl) : 0.f;
+      } else {
+        xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + e) : make_uint4(0, 0, 0, 0);
+      }
     }
   };
-  auto store_x = [&]() {
+  auto store_x = [&](int pos0, int c0) {
 #pragma unroll
     for (int j = 0; j < XIT; ++j) {
       const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
-      *reinterpret_cast<uint4*>(sX + row * ROWB + sub * 16) = xr[j];
+      uint4 u = xr[j];
+      if (RB) {   // x_in = Mish(GN(pre))*m + x*m, as gn_mish_kernel<A, false>
+        const int pos = pos0 + row, c = c0 + sub * ICH;
+        if (pos < tend) {
+          float v[ICH], xv[ICH];
+          item_to_f(xr[j], v, A());
+          item_to_f(xq[j], xv, A());
+          const float m = mk[j];
+#pragma unroll
+          for (int k = 0; k < ICH; ++k) v[k] = mish_act<A>(v[k] * s_sc[c + k] + s_sh[c + k]) * m + xv[k] * m;
+          u = f_to_item(v, A());
+          *reinterpret_cast<uint4*>(rb_out + (long)pos * p.C + c) = u;
+        }
+      }
+      *reinterpret_cast<uint4*>(sX + row * ROWB + sub * 16) = u;
     }
   };
   if (RES) load_x(tbeg, 0);
+  if (RB) {
+    gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
+    for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
+  }
   for (int pos0 = tbeg; pos0 < tend; pos0 += 64) {
     f32x16 ak[2], av[2];
 #pragma unroll
@@ -85,10 +120,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int ch = 0; ch < nch; ++ch) {
       __syncthreads();
       if (RES) {
-        store_x();
+        store_x(pos0, 0);
       } else {
         load_x(pos0, ch * CK);
-        store_x();
+        store_x(pos0, ch * CK);
         for (int it = tid; it < 256 * 4; it += 256) {
           const int row = it >> 2, sub = it & 3;
           *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
@@ -303,15 +338,20 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
 
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
+  if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels
+  // resident k/v weights only for C = 64; wider inputs stream 32-channel chunks (3 workgroups/CU,
+  // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
+#define GT_KV(A_, CPR_)                                                                           \
+  do {                                                                                            \
+    if (p.rb_pre) hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, true>), grid, dim3(256), 0, s, p);  \
+    else hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, false>), grid, dim3(256), 0, s, p);          \
+  } while (0)
   if (act_bf16) {
-    // resident k/v weights only for C = 64; wider inputs stream 32-channel chunks (3 workgroups/CU,
-    // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
-    if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<bf16, 64>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_kv_kernel<bf16, 0>), grid, dim3(256), 0, s, p);
+    if (p.Cpad <= 64) GT_KV(bf16, 64); else GT_KV(bf16, 0);
   } else {
-    if (p.Cpad <= 64) hipLaunchKernelGGL((attn_kv_kernel<float, 64>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((attn_kv_kernel<float, 0>), grid, dim3(256), 0, s, p);
+    if (p.Cpad <= 64) GT_KV(float, 64); else GT_KV(float, 0);
   }
+#undef GT_KV
   return hipGetLastError();
 }
 

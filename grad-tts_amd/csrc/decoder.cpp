@@ -585,8 +585,17 @@ struct Run {
   }
 
   // ResnetBlock (diffusion.py:61-79). `in1` != null: channel concat (up path). in0 == null: U-Net input.
+  // Identity-residual ResnetBlock output held back for the attention that consumes it (attn_kv forms it in its
+  // operand load and writes it to `out`): see resnet(..., defer) and attention().
+  struct PendingRb {
+    bool on = false;
+    std::string name;
+    const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
+    const void* x; void* out;
+  } pend;
+
   void resnet(const std::string& k, int lvl, const void* in0, int C0, const void* in1, int C1, int Cout, void* out,
-              int tb_off) {
+              int tb_off, bool defer = false) {
     const bool input = (in0 == nullptr);
     const int cin = input ? (d->n_spks > 1 ? 3 : 2) : C0 + C1;
     void* pre1 = act(lvl, 3);
@@ -648,6 +657,11 @@ struct Run {
       p.pre_beta = Fp(k + "block2.block.1.bias"); p.pre_count = count;
       p.out = out;
       conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
+    } else if (defer && GT_RB_ATTN) {              // Mish(GN(h2))*m + x*m, formed by the next attn_kv
+      pend.on = true; pend.name = k.substr(0, k.size() - 1);
+      pend.pre = pre2; pend.part = st2; pend.nparts = np2; pend.gamma = Fp(k + "block2.block.1.weight");
+      pend.beta = Fp(k + "block2.block.1.bias"); pend.count = count; pend.x = in0; pend.out = out;
+      return;
     } else {                                       // Mish(GN(h2))*m + x*m
       RbOutParams p{};
       p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight"); p.beta = Fp(k + "block2.block.1.bias");
@@ -670,11 +684,21 @@ struct Run {
     a.x = in; a.B = B; a.n = Fl(lvl) * Tl(lvl); a.C = C; a.Cpad = C;
     a.wkv = W(k + "fn.fn.to_qkv.weight");
     a.tile_pos = L.tile_pos[lvl]; a.ntile = L.ntile[lvl]; a.part = part;
+    a.rb_pre = nullptr;
+    const bool rb = pend.on;
+    if (rb) {   // the preceding ResnetBlock's output is formed here and written to `in`
+      if (pend.out != in) { chk(hipErrorInvalidValue); return; }
+      a.x = pend.x; a.rb_pre = pend.pre; a.rb_part = pend.part; a.rb_nparts = pend.nparts; a.rb_gamma = pend.gamma;
+      a.rb_beta = pend.beta; a.rb_count = pend.count; a.rb_out = pend.out; a.mask = mask; a.T = Tl(lvl); a.T0 = T;
+      a.lvl = lvl;
+      pend.on = false;
+    }
     const double npos = (double)B * a.n;
     // reference FLOPs of the attention block: qkv 1x1 (2*C*384) + two einsums (2 * 2*4*32*32) + to_out (2*128*C)
-    timed(std::string("attn_kv_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C) + "x" +
-              std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
-          npos * C * esize(dt), [&] { return launch_attn_kv(dt, a, s); });
+    timed(std::string("attn_kv_kernel<") + (dt ? "bf16" : "float") + (rb ? ",rb>" : ">") + "@" + std::to_string(C) +
+              "x" + std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
+          npos * C * esize(dt) * (rb ? 3.0 : 1.0), [&] { return launch_attn_kv(dt, a, s); });
+    if (rb) tap(pend.name, lvl, in, C);
     timed("attn_merge_kernel", 0.0, 0.0, [&] {
       return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);
     });
@@ -714,30 +738,30 @@ struct Run {
     auto next_tb = [&](int c) { int o = tb_off; tb_off += c; return o; };
     // down 0 (80 x T, 64 ch)
     resnet("downs.0.0.", 0, nullptr, 0, nullptr, 0, 64, act(0, 0), next_tb(64));
-    resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64));
+    resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64), true);
     attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
     downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
     // down 1 (40 x T/2, 128 ch); hidden 1 -> act(1,2)
     resnet("downs.1.0.", 1, act(1, 0), 64, nullptr, 0, 128, act(1, 1), next_tb(128));
-    resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128));
+    resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128), true);
     attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
     downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
     // down 2 (20 x T/4, 256 ch); hidden 2 -> act(2,2); Identity(x*mask) is absorbed by the next block's mask
     resnet("downs.2.0.", 2, act(2, 0), 128, nullptr, 0, 256, act(2, 1), next_tb(256));
-    resnet("downs.2.1.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
+    resnet("downs.2.1.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256), true);
     attention("downs.2.2.", 2, act(2, 0), 256, act(2, 2));
     // mid
-    resnet("mid_block1.", 2, act(2, 2), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
+    resnet("mid_block1.", 2, act(2, 2), 256, nullptr, 0, 256, act(2, 0), next_tb(256), true);
     attention("mid_attn.", 2, act(2, 0), 256, act(2, 1));
     resnet("mid_block2.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256));
     // up 0 at level 2: cat(x, hidden2) -> 128 ch, then ConvTranspose to level 1
     resnet("ups.0.0.", 2, act(2, 0), 256, act(2, 2), 256, 128, act(2, 1), next_tb(128));
-    resnet("ups.0.1.", 2, act(2, 1), 128, nullptr, 0, 128, act(2, 0), next_tb(128));
+    resnet("ups.0.1.", 2, act(2, 1), 128, nullptr, 0, 128, act(2, 0), next_tb(128), true);
     attention("ups.0.2.", 2, act(2, 0), 128, act(2, 1));
     upsample("ups.0.3.", 2, act(2, 1), 128, act(1, 0));
     // up 1 at level 1: cat(x, hidden1) -> 64 ch, then ConvTranspose to level 0
     resnet("ups.1.0.", 1, act(1, 0), 128, act(1, 2), 128, 64, act(1, 1), next_tb(64));
-    resnet("ups.1.1.", 1, act(1, 1), 64, nullptr, 0, 64, act(1, 0), next_tb(64));
+    resnet("ups.1.1.", 1, act(1, 1), 64, nullptr, 0, 64, act(1, 0), next_tb(64), true);
     attention("ups.1.2.", 1, act(1, 0), 64, act(1, 1));
     upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
     // final_block conv (+GN sums), then the fused GN/Mish/final_conv/(Euler) kernel

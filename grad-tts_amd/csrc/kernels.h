@@ -52,6 +52,11 @@ struct AttnKVParams {
   const void* wkv;                    // [256][Cpad]: rows 0..127 = k (head*32+d), 128..255 = v
   int tile_pos, ntile;                // positions per workgroup (multiple of 64), tiles per batch item
   float* part;                        // [B][ntile][4][1088] = {m[32], l[32], ctx[32][32]}
+  // rb_pre != null: the attention input is the preceding ResnetBlock's output with identity residual, formed in the
+  // operand load, x_in = Mish(GN(rb_pre))*m + x*m (diffusion.py:57-58, 77-79), and written to rb_out for the attention
+  // output conv (replaces the separate ResnetBlock-output pass).
+  const void* rb_pre; const float* rb_part; int rb_nparts; const float* rb_gamma; const float* rb_beta; long rb_count;
+  void* rb_out; const float* mask; int T, T0, lvl;
 };
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,

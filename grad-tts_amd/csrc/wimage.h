@@ -42,6 +42,11 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 #ifndef GT_TF5_1X1
 #define GT_TF5_1X1 1
 #endif
+// Identity-residual ResnetBlock outputs that feed an attention block are formed inside attn_kv_kernel (operand load)
+// instead of a separate gn_mish pass (6 of the 7 such blocks per U-Net evaluation; mid_block2 keeps the pass)
+#ifndef GT_RB_ATTN
+#define GT_RB_ATTN 1
+#endif
 // The 128-channel Upsample (level 2 -> 1, 20 coarse rows) on 5-row tiles: 1280 -> 1024 workgroups at B = 32 (two
 // whole rounds of 512 instead of 2.5)
 #ifndef GT_TF5_T

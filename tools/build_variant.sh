@@ -8,11 +8,12 @@ D=$R/ab/$NAME; mkdir -p $D
 # PK="" builds with the compiler's packed-fp32 instructions (the product build disables them, build.py)
 PK=${PK--Xclang -target-feature -Xclang -packed-fp32-ops}
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/include -I $R/grad-tts_amd/csrc -Wno-unused-result $PK"
-for s in conv.hip conv64.hip attn.hip misc.hip mas.hip train.hip bwd.hip decoder.cpp train_bwd.cpp; do
+SRCS="conv.hip conv64.hip attn.hip misc.hip mas.hip train.hip bwd.hip textenc.hip decoder.cpp train_bwd.cpp textenc.cpp vocoder.cpp"
+for s in $SRCS; do
   L=""; case $s in *.cpp) L="-x hip";; esac
   /opt/rocm/bin/hipcc $F "$@" $L -c $R/grad-tts_amd/csrc/$s -o $D/$s.o 2>&1 | grep -v "packed-fp32-ops" || true &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libgradtts.so $D/conv.hip.o $D/conv64.hip.o $D/attn.hip.o $D/misc.hip.o $D/mas.hip.o $D/train.hip.o $D/bwd.hip.o $D/decoder.cpp.o $D/train_bwd.cpp.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/libgradtts.so $(for s in $SRCS; do echo $D/$s.o; done)
 rm -f $D/*.o
 echo built $D/libgradtts.so
