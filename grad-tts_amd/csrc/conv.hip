@@ -60,7 +60,7 @@ struct ConvCfg {
   static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
   static constexpr int PR = (TF - 1) * S + KS;
   static constexpr int PC = (TT - 1) * S + KS;
-  static constexpr int CKB = conv_ckb(sizeof(A) == 2);
+  static constexpr int CKB = conv_ckb(sizeof(A) == 2, KIND == CONV1 ? 1 : 9, IN == IN_INPUT ? 3 : 64);
   static constexpr int SUBS = CKB / 16;
   static constexpr int POSB = CKB + 16;
   // weight slab: bf16/fp32 image (wimage.h: half A = taps [0, NA), half B = the rest) or the fp8 image

@@ -64,8 +64,15 @@ inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int c
             ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
              (im == 2 && (cout >= 256 || (GT_L1_TF5_GN && cout == 128 && f == 40))))) ? 5 : 4;
 }
-// bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32)
-inline __host__ __device__ constexpr int conv_ckb(int act_bf16) { return act_bf16 ? 32 : 64; }
+// bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32). bf16 1x1 convs
+// over activations (cin > 16) take GT_CKB_1X1 bytes (default 32 channels = two k-steps): a 1x1 chunk is one tap, so a
+// 16-channel chunk left one barrier + weight/patch round trip per 10 MFMAs per wave.
+#ifndef GT_CKB_1X1
+#define GT_CKB_1X1 64
+#endif
+inline __host__ __device__ constexpr int conv_ckb(int act_bf16, int ntap = 9, int cin = 0) {
+  return act_bf16 ? ((ntap == 1 && cin > 16) ? GT_CKB_1X1 : 32) : 64;
+}
 inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }
 inline __host__ __device__ constexpr int round4k(int b) { return ((b + 4095) / 4096) * 4096; }
 // taps in half A: split images (bf16, more than one tap) put the first ceil(NTAP/2) taps there
@@ -85,7 +92,7 @@ struct WImg {
 inline __host__ __device__ WImg conv_wimg(int act_bf16, int ntap, int cin, int cout) {
   WImg w;
   w.nt = conv_nt(act_bf16, cout);
-  w.ckb = conv_ckb(act_bf16);
+  w.ckb = conv_ckb(act_bf16, ntap, cin);
   w.ck = w.ckb / (act_bf16 ? 2 : 4);
   w.ntap = ntap;
   w.na = conv_na(act_bf16, ntap);
