@@ -97,3 +97,42 @@ def test_latency_b1_report():
     print(f"LATENCY B=1 T=512 bf16: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
           f"({512 / (50 * ms_s) * 1e3:.0f} vs {512 / (50 * ms_t) * 1e3:.0f} mel-frames/s for 50-step decodes)")
     assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
+
+
+def test_throughput_plan_every_stage_bf16():
+    """Every U-Net stage vs the oracle on the throughput plan (forced at the fixture's batch size): the tiles the
+    bench runs (5-row tiles, 32-channel 1x1 chunks, the ResnetBlock output formed in attn_kv, conv64 column
+    segments), which the default small-batch plan does not run at the fixtures' sizes. bf16 stage gate 2e-2, as
+    test_decoder_gpu's."""
+    from conftest import load_golden
+    from gpu_util import STAGES, probe
+    from oracle import decoder as odec
+    g = load_golden("estimator_s1_T132.npz")
+    dec, sd = make_decoder(1, 0, torch.bfloat16)
+    _set_small(dec, 0)
+    p = odec.to_torch_params(sd)
+    taps = {}
+    with torch.no_grad():
+        odec.estimator(p, torch.from_numpy(g["x"]), torch.from_numpy(g["mask"]), torch.from_numpy(g["mu"]),
+                       torch.from_numpy(g["t"]), None, taps=taps)
+    args = [torch.from_numpy(np.ascontiguousarray(g[k])).cuda() for k in ("x", "mask", "mu", "t")]
+    bad = []
+    for st in STAGES:
+        ref = taps[st].numpy()
+        _, pr = probe(dec.estimator, torch.bfloat16, *args, None, st, ref.shape)
+        e = rel_err(pr.cpu().numpy(), ref)
+        if not report(f"stage {st} bf16 throughput plan", e, 2e-2, gate=False):
+            bad.append(f"{st}: {e:.3e}")
+    assert not bad, "stage mismatches: " + ", ".join(bad)
+
+
+def test_throughput_plan_speaker_input_conv_bf16():
+    """n_spks = 247 (the input conv takes 3 channels: mu, x_t, spk) on ragged lengths: throughput plan vs small plan."""
+    dec, _ = make_decoder(247, 0, torch.bfloat16)
+    B, T = 3, 128
+    mu, z, mask, spk = _inputs(31, B, T, lengths=[128, 100, 60])   # spk: speaker embeddings [B, 64]
+    y_small = dec(z, mask, mu, 4, False, spk).cpu().numpy()
+    _set_small(dec, 0)
+    y_tput = dec(z, mask, mu, 4, False, spk).cpu().numpy()
+    assert np.isfinite(y_tput).all()
+    report(f"small vs throughput plan bf16 n_spks=247 B={B} T={T} N=4", rel_err(y_small, y_tput), BF16_REV_TOL)
