@@ -613,11 +613,11 @@ template <class A, int KIND, int IN, int OUT, int NT, int W8 = 0, int TF_ = 4>
 static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 
 // 3x3 launch with the tile height conv_tf picks (5 rows only exists for 128-wide tiles; the small-batch plan's
-// 1-row (128-wide) / 2-row (64-wide) tiles only for bf16 weights)
+// 1-row (128-wide) / 2-row (64-wide) tiles for bf16 activations, with bf16 or fp8 weights)
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
-  if constexpr (!W8 && sizeof(A) == 2)
-    if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, 0, NT == 128 ? 1 : 2>(p, s);
+  if constexpr (sizeof(A) == 2)
+    if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
   if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
@@ -672,7 +672,7 @@ static hipError_t dispatch(ConvKind kind, InMode im, OutMode om, const ConvParam
 template <int NT>
 static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   if (kind == CONV3 && om == OUT_STATS) {
-    if (im == IN_INPUT) return launch_t<bf16, CONV3, IN_INPUT, OUT_STATS, NT, 1>(p, s);
+    if (im == IN_INPUT) return launch_c3<bf16, IN_INPUT, NT, 1>(p, s);
     if (im == IN_MASK) return launch_c3<bf16, IN_MASK, NT, 1>(p, s);
     if (im == IN_GN) return launch_c3<bf16, IN_GN, NT, 1>(p, s);
     if (im == IN_PLAIN) return launch_c3<bf16, IN_PLAIN, NT, 1>(p, s);
@@ -690,7 +690,7 @@ int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small) {
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   if (p.small && !act_bf16) return hipErrorNotSupported;   // small-batch plan: bf16 weights and activations only
   if (p.wscale) {   // fp8 weight image
-    if (!act_bf16 || p.small) return hipErrorNotSupported;
+    if (!act_bf16) return hipErrorNotSupported;
     return conv_nt(1, p.Cout) == 128 ? dispatch_w8<128>(kind, im, om, p, s) : dispatch_w8<64>(kind, im, om, p, s);
   }
   if (!act_bf16) return dispatch<float, 64>(kind, im, om, p, s);

@@ -786,12 +786,14 @@ struct Run {
   }
 };
 
-// Small-batch tile plan: bf16 (not fp8-weight) calls on at most d->small_b utterances take 1-row (128-wide)
+// Small-batch tile plan: bf16-activation calls (bf16 or fp8 weights) on at most d->small_b utterances take 1-row (128-wide)
 // and 2-row (64-wide) conv tiles and one-tile conv64 segments -- at B = 1 the throughput tiles fill 16-40 of the 256
 // CUs at levels 1-2 and 16 at level 0. Every utterance's arithmetic is the same within a plan (batch-invariant
 // for any B on either side of the threshold); the two plans partition the GroupNorm partial sums differently, so
 // results across plans agree to fp32 rounding of those sums (GPU test: plan agreement within the bf16 gate).
-int small_plan(const gt_decoder* d, int dtype, int64_t nb) { return (dtype == GT_BF16 && nb <= d->small_b) ? 1 : 0; }
+int small_plan(const gt_decoder* d, int dtype, int64_t nb) {
+  return ((dtype == GT_BF16 || dtype == GT_BF16_W8) && nb <= d->small_b) ? 1 : 0;
+}
 
 uint8_t* align_ws(void* ws) { return (uint8_t*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
 

@@ -92,8 +92,8 @@ int gt_reverse_diffusion(gt_decoder* dec, int dtype, const float* z, const float
  * graph). Results are bit-identical with and without graphs. gt_decoder_graph_captures counts captures. */
 int gt_decoder_set_graphs(gt_decoder* dec, int on);
 int64_t gt_decoder_graph_captures(const gt_decoder* dec);
-/* Small-batch tile plan: bf16 calls on at most max_b utterances (env GT_SMALL_B at creation)
- * use 1-/2-row conv tiles and one-tile conv64 segments, so a single utterance fills the GPU (latency). Default 4. Each plan
+/* Small-batch tile plan: GT_BF16 and GT_BF16_W8 calls on at most max_b utterances (env GT_SMALL_B at creation)
+ * use 1-/2-row conv tiles and (GT_BF16) one-tile conv64 segments, so a single utterance fills the GPU (latency). Default 4. Each plan
  * is batch-invariant on its own; across plans results agree to fp32 rounding of the GroupNorm sums. 0 disables. */
 int gt_decoder_set_small_batch(gt_decoder* dec, int64_t max_b);
 

@@ -121,7 +121,7 @@ def test_c5_full_workload_fp8_weights():
     y = dec(z, m, mu, 1000)
     assert torch.isfinite(y).all()
     assert torch.equal(y, dec(z, m, mu, 1000))
-    s = slice(30, 32)
+    s = slice(27, 32)   # 5 utterances: above the small-batch plan's threshold (4), same (throughput) tiles as B = 32
     assert torch.equal(y[s], dec(z[s].contiguous(), m[s].contiguous(), mu[s].contiguous(), 1000))
     dec.compute_dtype = torch.bfloat16
     y16 = dec(z, m, mu, 1000)

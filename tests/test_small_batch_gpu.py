@@ -136,3 +136,39 @@ def test_throughput_plan_speaker_input_conv_bf16():
     y_tput = dec(z, mask, mu, 4, False, spk).cpu().numpy()
     assert np.isfinite(y_tput).all()
     report(f"small vs throughput plan bf16 n_spks=247 B={B} T={T} N=4", rel_err(y_small, y_tput), BF16_REV_TOL)
+
+
+def test_w8_small_plan_batch_invariant_and_agrees():
+    """fp8-weight calls (config 5) on at most 4 utterances take the small-batch tiles too: batch-invariant within
+    the plan, and within the bf16 sampler gate of the throughput plan."""
+    dec, _ = make_decoder(1, 0, "bf16_w8")
+    mu, z, mask, _ = _inputs(23, 4, 256, lengths=[256, 200, 120, 64])
+    y4 = dec(z, mask, mu, 3)
+    y1 = dec(z[1:2].contiguous(), mask[1:2].contiguous(), mu[1:2].contiguous(), 3)
+    assert torch.isfinite(y4).all()
+    assert torch.equal(y4[1:2], y1), float((y4[1:2] - y1).abs().max())
+    _set_small(dec, 0)
+    y4t = dec(z, mask, mu, 3)
+    report("w8 small vs throughput plan B=4 T=256 N=3", rel_err(y4.cpu().numpy(), y4t.cpu().numpy()), BF16_REV_TOL)
+
+
+def test_w8_latency_b1_report():
+    """Config 5 latency (fp8 weights, B = 1, T = 512): small plan vs throughput plan, ms per Euler step."""
+    dec, _ = make_decoder(1, 0, "bf16_w8")
+    mu, z, mask, _ = _inputs(3, 1, 512)
+    N = 20
+
+    def run():
+        dec(z, mask, mu, N)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        y = dec(z, mask, mu, N)
+        torch.cuda.synchronize()
+        return y, (time.perf_counter() - t0) / N * 1e3
+
+    y_s, ms_s = run()
+    _set_small(dec, 0)
+    y_t, ms_t = run()
+    print(f"LATENCY W8 B=1 T=512: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
+          f"({512 / (1000 * ms_s) * 1e3:.0f} vs {512 / (1000 * ms_t) * 1e3:.0f} mel-frames/s for 1000-step decodes)")
+    assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
