@@ -29,6 +29,11 @@
 
 namespace gt {
 
+// 1-D XCD-aware workgroup order (conv_kernel prologue): 2 contiguous spatial range per XCD, 1 interleaved, 0 the
+// (spatial, channel tile, parity) 3-D grid
+#ifndef GT_XCD_MAP
+#define GT_XCD_MAP 2
+#endif
 #ifndef GT_CAP_T
 #define GT_CAP_T 3
 #endif
@@ -122,7 +127,7 @@ GT_DEV bf16x8 w8_frag(const char* src) {
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 // 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 64 && TF_ <= 4) ? 3 : 2))) void conv_kernel(ConvParams p) {
   typedef ConvCfg<A, KIND, IN, OUT, NT, W8, TF_> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
@@ -142,14 +147,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
   const int Fg = CONVT ? p.Fin : p.Fout;
   const int Tg = CONVT ? p.Tin : p.Tout;
   const int n_ft = Fg / C::TF, n_tt = (Tg + C::TT - 1) / C::TT;
-  int bid = blockIdx.x;
+  // 1-D grid, XCD-aware (launch_t): workgroup ids go round robin over the 8 XCDs, so the ny output-channel tiles (x 4
+  // sub-pixel parities for CONVT4) of one spatial tile -- which all read the same input patch -- get ids 8 apart: the
+  // same XCD, dispatched together, the patch fetched into that XCD's L2 once instead of once per tile.
+  const int ny = p.Cout / NT, nyz = ny * (CONVT ? 4 : 1);
+  int bid, ntile, par;
+  if (GT_XCD_MAP) {
+    const int nsp = p.B * n_ft * n_tt, lin = blockIdx.x, j = lin >> 3, yz = j % nyz;
+    // GT_XCD_MAP 2: XCD x walks the contiguous spatial range [x S, x S + S) in order (S = ceil(nsp / 8)), so the
+    // tiles one XCD runs together are vertical neighbours whose halo rows its L2 already holds; 1: interleaved
+    bid = GT_XCD_MAP == 2 ? (lin & 7) * ((nsp + 7) >> 3) + j / nyz : (j / nyz) * 8 + (lin & 7);
+    ntile = yz % ny;
+    par = yz / ny;
+    if (bid >= nsp) return;   // grid padding: the whole workgroup, before any barrier
+  } else {
+    bid = blockIdx.x; ntile = blockIdx.y; par = blockIdx.z;
+  }
   const int tt = bid % n_tt; bid /= n_tt;
   const int ft = bid % n_ft;
   const int b = bid / n_ft;
   const int f0 = ft * C::TF, t0 = tt * C::TT;
-  const int ntile = blockIdx.y;
   const int cout0 = ntile * NT;
-  const int par = blockIdx.z, pf = par >> 1, pt = par & 1;
+  const int pf = par >> 1, pt = par & 1;
 
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) wave index
@@ -282,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
 
   const char* wimg = reinterpret_cast<const char*>(p.w) + (long)b * p.w_bstride;
   const int nchunk = p.Cin_pad / C::CK;
-  wimg += ((long)(par * gridDim.y + ntile) * nchunk) * C::WBYTES;
+  wimg += ((long)(par * ny + ntile) * nchunk) * C::WBYTES;
 
   auto dma_weights_to = [&](int ch, char* dst) {   // contiguous slab, 1 KiB per wave instruction, compile-time count
     const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
@@ -600,8 +619,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
               Q += s_sub[((w * 2 + cb) * 4 + g8) * 2 + 1];
             }
           }
-      const int nparts = n_ft * n_tt * gridDim.y;
-      const int slot = (ft * n_tt + tt) * gridDim.y + ntile;
+      const int nparts = n_ft * n_tt * ny;
+      const int slot = (ft * n_tt + tt) * ny + ntile;
       float* dst = p.out_part + ((long)b * nparts + slot) * 16 + tid * 2;
       dst[0] = S;
       dst[1] = Q;
@@ -620,6 +639,8 @@ static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
   if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
+  if constexpr (GT_C64_TF8 && NT == 64 && IN == IN_MASK && sizeof(A) == 2)   // bf16 activations (bf16 / fp8 weights)
+    if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 8) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 8>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
 template <class A, int NT, int W8>
@@ -646,8 +667,10 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   if (OUT == OUT_STATS && ((p.Cout >> 3) & ((p.Cout >> 3) - 1)) != 0) return hipErrorInvalidValue;  // group size 2^k
   if ((long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * (long)sizeof(A) >= (1L << 31))
     return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
-  dim3 grid((unsigned)(p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT)), (unsigned)(p.Cout / NT),
-            KIND == CONVT4 ? 4u : 1u);
+  const long nsp = (long)p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT);   // spatial tiles
+  const unsigned nyz = (unsigned)(p.Cout / NT) * (KIND == CONVT4 ? 4u : 1u);
+  const dim3 grid = GT_XCD_MAP ? dim3((unsigned)(8 * nyz * ((nsp + 7) / 8)))
+                               : dim3((unsigned)nsp, (unsigned)(p.Cout / NT), KIND == CONVT4 ? 4u : 1u);
   if (W8 && !p.wscale) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8, TF_>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
@@ -684,7 +707,8 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
 
 int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small) {   // CONV3 tiles: TF rows x 64 frames x NT
   const int nt = conv_nt(act_bf16, Cout);
-  return (F / conv_tf(CONV3, im, nt, Cout, F, small)) * ((T + 63) / 64) * (Cout / nt);
+  const int tf = conv_tf(CONV3, im, nt, Cout, F, small);
+  return (F / (act_bf16 || tf != 8 ? tf : 4)) * ((T + 63) / 64) * (Cout / nt);   // 8-row tiles: bf16 only
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
