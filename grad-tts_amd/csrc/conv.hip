@@ -127,7 +127,7 @@ GT_DEV bf16x8 w8_frag(const char* src) {
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 // 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NT == 64 && TF_ <= 4) ? 3 : 2))) void conv_kernel(ConvParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
   typedef ConvCfg<A, KIND, IN, OUT, NT, W8, TF_> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
@@ -639,8 +639,6 @@ static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
   if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
-  if constexpr (GT_C64_TF8 && NT == 64 && IN == IN_MASK && sizeof(A) == 2)   // bf16 activations (bf16 / fp8 weights)
-    if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 8) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 8>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
 template <class A, int NT, int W8>
@@ -707,8 +705,7 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
 
 int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small) {   // CONV3 tiles: TF rows x 64 frames x NT
   const int nt = conv_nt(act_bf16, Cout);
-  const int tf = conv_tf(CONV3, im, nt, Cout, F, small);
-  return (F / (act_bf16 || tf != 8 ? tf : 4)) * ((T + 63) / 64) * (Cout / nt);   // 8-row tiles: bf16 only
+  return (F / conv_tf(CONV3, im, nt, Cout, F, small)) * ((T + 63) / 64) * (Cout / nt);
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {

@@ -56,14 +56,8 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 // rows, small: the small-batch plan). Small batches (decoder.cpp small_plan) take one-row tiles for 128-wide and
 // two-row tiles for 64-wide convs (64 positions per wave pair: 4-5x the workgroups of the throughput tiles, which at
 // B = 1 fill 16-40 of the 256 CUs).
-// The 64-output masked-input 3x3 at level 1 (ups.1.0 block1: 256 concatenated input channels -> 64) on 8-row tiles
-// (GT_C64_TF8): its 4-row tiles restaged 327 KB of weights per 256 positions, more than their input patch.
-#ifndef GT_C64_TF8
-#define GT_C64_TF8 0
-#endif
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f, int small = 0) {
   return (small && (kind == 0 /*CONV3*/ || kind == 2 /*CONV1*/)) ? (nt == 128 ? 1 : 2)
-         : (GT_C64_TF8 && kind == 0 /*CONV3*/ && im == 1 /*IN_MASK*/ && nt == 64 && f == 40) ? 8
          : (GT_TF5_1X1 && kind == 2 /*CONV1*/ && nt == 128 && (cout >= 256 || f == 40)) ? 5
          : (GT_TF5_T && kind == 3 /*CONVT4*/ && nt == 128 && f == 40) ? 5
          : (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
