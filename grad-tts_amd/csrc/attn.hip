@@ -104,7 +104,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       *reinterpret_cast<uint4*>(sX + row * ROWB + sub * 16) = u;
     }
   };
-  if (RES) load_x(tbeg, 0);
+  // chunked path: the next chunk's x (and pre / mask) rows are loaded into registers while the current chunk is in
+  // the MFMAs (a load issued right before its LDS store left one HBM round trip exposed per 32-channel chunk)
+  load_x(tbeg, 0);
   if (RB) {
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
     for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
@@ -118,20 +120,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 
     const int nch = RES ? 1 : p.Cpad / CK;
     for (int ch = 0; ch < nch; ++ch) {
-      __syncthreads();
-      if (RES) {
-        store_x(pos0, 0);
-      } else {
-        load_x(pos0, ch * CK);
-        store_x(pos0, ch * CK);
+      lds_barrier();                                   // every wave is done with the previous chunk's fragments
+      store_x(pos0, ch * CK);
+      if (!RES) {                                      // the k/v weight slice: L2-resident, loaded straight into LDS
         for (int it = tid; it < 256 * 4; it += 256) {
           const int row = it >> 2, sub = it & 3;
           *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
               *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
         }
       }
-      __syncthreads();
-      if (RES && pos0 + 64 < tend) load_x(pos0 + 64, 0);   // next sub-block in flight during the MFMAs
+      lds_barrier();
+      if (RES) {
+        if (pos0 + 64 < tend) load_x(pos0 + 64, 0);   // next sub-block in flight during the MFMAs
+      } else if (ch + 1 < nch) {
+        load_x(pos0, (ch + 1) * CK);
+      } else if (pos0 + 64 < tend) {
+        load_x(pos0 + 64, 0);
+      }
       const int nks = RES ? CPR / 16 : CK / 16;
       for (int ks = 0; ks < nks; ++ks) {
         const int off = ks * KSTEP_B + h * (KSTEP_B / 2);
