@@ -439,11 +439,14 @@ struct Layout {
   int tile_pos[3], ntile[3];
 };
 
-// Attention tile size depends only on the positions per utterance (never on B), so an utterance gets
+// Attention tile size depends only on the positions per utterance and the tile plan (never on B), so an utterance gets
 // the same online-softmax partition -- hence bit-identical arithmetic -- whatever batch or GPU shard it
 // is decoded in (sharded runs must match the single-GPU run).
-void attn_tiles(int64_t n, int& tile_pos, int& ntile) {
-  int64_t tp = (n + 63) / 64;
+// `target` tiles per utterance: the workspace is sized for 64 (the most); the throughput plan takes 16 for utterances
+// of 8192+ positions and 32 below (fewer online-softmax partials to merge, longer streams per workgroup: same-box
+// +1.0-1.3 %), the small-batch plan keeps 64 so that one utterance still spreads over the GPU.
+void attn_tiles(int64_t n, int target, int& tile_pos, int& ntile) {
+  int64_t tp = (n + target - 1) / target;
   tp = (tp + 63) / 64 * 64;
   if (tp < 64) tp = 64;
   tile_pos = (int)tp;
@@ -463,7 +466,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.stats = take((size_t)25 * B * L.pmax * 16 * sizeof(float));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
-    attn_tiles((int64_t)(80 >> l) * (T >> l), L.tile_pos[l], L.ntile[l]);
+    attn_tiles((int64_t)(80 >> l) * (T >> l), 64, L.tile_pos[l], L.ntile[l]);
     maxtile = std::max(maxtile, L.ntile[l]);
   }
   L.part = take((size_t)B * maxtile * 4 * 1088 * 4);
@@ -683,7 +686,12 @@ struct Run {
     AttnKVParams a;
     a.x = in; a.B = B; a.n = Fl(lvl) * Tl(lvl); a.C = C; a.Cpad = C;
     a.wkv = W(k + "fn.fn.to_qkv.weight");
-    a.tile_pos = L.tile_pos[lvl]; a.ntile = L.ntile[lvl]; a.part = part;
+    a.part = part;
+    if (small) {
+      a.tile_pos = L.tile_pos[lvl]; a.ntile = L.ntile[lvl];
+    } else {
+      attn_tiles(a.n, a.n >= 8192 ? 16 : 32, a.tile_pos, a.ntile);   // never more tiles than the workspace holds
+    }
     a.rb_pre = nullptr;
     const bool rb = pend.on;
     if (rb) {   // the preceding ResnetBlock's output is formed here and written to `in`
