@@ -2,7 +2,15 @@
 """Benchmark: mel-frames/s of the N-step reverse-diffusion decoder on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--frames 512] [--n-timesteps 50]
-                    [--dtype bf16|fp32|bf16_w8] [--n-spks 1] [--no-cpu-baseline]
+                    [--dtype bf16|fp32|bf16_w8] [--n-spks 1] [--no-cpu-baseline] [--dry-run]
+
+Launch: ``--gpus N`` with N > 1 and no ``WORLD_SIZE`` in the environment starts N ranks itself
+(``python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py ...``) from a
+parent process that never touches the GPU and exits with the ranks' status; rank 0's JSON line is
+relayed as the last line of stdout. Under an external launcher (the driver's ``torch.distributed.run``)
+``WORLD_SIZE`` must equal ``--gpus``. ``--dry-run`` exercises exactly this launch / rendezvous / gather /
+max-over-ranks plumbing on CPU with gloo and no decoder (the line says ``"dry_run": true``; it is not a
+measurement).
 
 A "step" is one complete ``Diffusion.reverse_diffusion`` call (n_timesteps Euler steps of the U-Net)
 over one batch of synthetic utterances already resident in HBM, followed by the RCCL all_gather of
@@ -24,6 +32,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,7 +65,101 @@ def parse():
     ap.add_argument("--n-spks", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-batch", type=int, default=4)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank launch and gather; no decoder, not a measurement")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """Start args.gpus ranks of this script under torch.distributed.run (one process per GPU) and relay their
+    output. The parent imports torch but makes no HIP call (torch.cuda.device_count() does not initialise the
+    device on this image), so the children own the GPUs. Returns the launcher's exit status."""
+    if not args.dry_run and not SHARED_DEVICE:
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for out in proc.stdout:          # stream the ranks' stdout (progress stays visible); hold back the JSON line
+        if out.startswith("{") and '"metric"' in out:
+            line = out.strip()
+        else:
+            sys.stdout.write(out)
+            sys.stdout.flush()
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        print("bench.py: ranks exited without a result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def dry_run(args, world, rank):
+    """The multi-rank skeleton of main() on CPU: gloo rendezvous, per-rank shard of synthetic inputs, the mel
+    gather, barrier + max-over-ranks timing and the rank-0 line. The decode is replaced by a masked copy."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    B, T = args.batch, args.frames
+    mu, z, mask, _ = synthetic_inputs(1234 + rank, B, T)
+    z, mask = torch.from_numpy(z), torch.from_numpy(mask)
+
+    def step():
+        y = z * mask
+        return gather_shards(y, world * B, world) if world > 1 else y
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = step()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert y.shape == (world * B, 80, T), y.shape
+    if rank == 0:
+        sec = elapsed / max(args.steps, 1)
+        print(json.dumps({
+            "metric": METRIC, "value": world * B * T / sec, "unit": "mel-frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": sec * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "dry_run": True,
+            "data": "dry run: CPU gloo plumbing only, decoder replaced by a masked copy (not a measurement)",
+            "config": config_block(args, world)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# GRADTTS_BENCH_SHARED_DEVICE=1: every rank on cuda:0 with gloo (rehearsal of the N-rank HIP path on a 1-GPU box;
+# RCCL refuses two ranks on one device). Not for measurements.
+SHARED_DEVICE = os.environ.get("GRADTTS_BENCH_SHARED_DEVICE", "0") == "1"
+METRIC = "mel-frames/sec (reverse-diffusion, 80-mel, N=50) at 1/2/4/8 MI355X; RTF"
+
+
+def config_block(args, world):
+    B, T, N = args.batch, args.frames, args.n_timesteps
+    return {"workload": f"LJSpeech single-speaker batch={B}/GPU, T={T} frames, n_timesteps={N}, "
+                        f"{args.dtype} " + ("(BASELINE config 5: fp8 U-Net weights)" if args.dtype == "bf16_w8" else
+                                          "(BASELINE config 2; N GPUs = config 4 weak-scaled)"),
+            "global_batch": world * B, "seq_len": T, "n_timesteps": N, "n_spks": args.n_spks,
+            "parallelism": f"dp{world} utterance shards, RCCL all_gather of mels" if world > 1 else "dp1"}
 
 
 def pmc_traffic(kernel, args, world):
@@ -98,13 +202,23 @@ def cpu_baseline(args, sd):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch with matching values")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if SHARED_DEVICE:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if SHARED_DEVICE else "nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -194,16 +308,12 @@ def main():
         achieved = dom["flop"] / dom["launches"] / avg_s
         total_kernel_ms = sum(p["ms"] for p in prof)
         out = {
-            "metric": "mel-frames/sec (reverse-diffusion, 80-mel, N=50) at 1/2/4/8 MI355X; RTF",
+            "metric": METRIC,
             "value": value, "unit": "mel-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": sec * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic: mu~N(0,1), z=mu+N(0,1), full-length masks; random-init weights (seed 0), no checkpoint",
-            "config": {"workload": f"LJSpeech single-speaker batch={B}/GPU, T={T} frames, n_timesteps={N}, "
-                                   f"{args.dtype} " + ("(BASELINE config 5: fp8 U-Net weights)" if args.dtype == "bf16_w8" else
-                                                     "(BASELINE config 2; N GPUs = config 4 weak-scaled)"),
-                       "global_batch": world * B, "seq_len": T, "n_timesteps": N, "n_spks": args.n_spks,
-                       "parallelism": f"dp{world} utterance shards, RCCL all_gather of mels" if world > 1 else "dp1"},
+            "config": config_block(args, world),
             "rtf": sec * 22050 / (frames * 256),     # inference.py:91 formula
             "frame_steps_per_s": value * N,
             "path_tflops": flop_step * world / sec / 1e12,
@@ -228,6 +338,8 @@ def main():
                        for e in sorted(shapes, key=lambda e: -e["ms"]) if "@" in e["kernel"]},
             "kernel_busy_frac": total_kernel_ms / table_steps / 1e3 / sec,
         }
+        if SHARED_DEVICE:
+            out["shared_device"] = "all ranks on cuda:0 over gloo: launch rehearsal, not a scaling measurement"
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, sd)
         print(json.dumps(out))

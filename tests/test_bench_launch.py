@@ -1,0 +1,51 @@
+"""bench.py's multi-rank launch on CPU (gloo, no decoder): `--gpus N` must start N ranks itself, an external
+torch.distributed.run launch must agree with `--gpus`, and the rank-0 line must report the world it ran on."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--dry-run", "--steps", "2", "--warmup", "1", "--batch", "2", "--frames", "16"]
+
+
+def _run(cmd, **env):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env)
+    return subprocess.run(cmd, cwd=REPO, env=e, capture_output=True, text=True, timeout=180)
+
+
+def _line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    last = r.stdout.strip().splitlines()[-1]
+    return json.loads(last)
+
+
+def test_bench_self_launches_two_ranks():
+    d = _line(_run([sys.executable, "bench.py", "--gpus", "2", *SMALL]))
+    assert d["n_gpus"] == 2 and d["dry_run"] is True
+    assert d["config"]["global_batch"] == 4
+    assert d["config"]["parallelism"].startswith("dp2 ")
+    assert d["value"] > 0 and d["scaling"] == "weak"
+
+
+def test_bench_under_external_launcher():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    d = _line(_run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "2", *SMALL]))
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"].startswith("dp2 ")
+
+
+def test_bench_single_rank_dry_run():
+    d = _line(_run([sys.executable, "bench.py", *SMALL]))
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "dp1"
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    r = _run([sys.executable, "bench.py", "--gpus", "2", *SMALL], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
