@@ -453,6 +453,24 @@ void attn_tiles(int64_t n, int target, int& tile_pos, int& ntile) {
   ntile = (int)((n + tp - 1) / tp);
 }
 
+// Largest number of GroupNorm partial slots one utterance's producer writes, over every level, output width,
+// operand mode and both tile plans (conv_kernel tiles and conv64 segments). Each stats slot holds this many, so no
+// producer spills into the next slot whatever plan a call takes (the small plan's 2-row 64-wide level-0 tiles write
+// 40*ceil(T/64) partials, more than conv64's 20*ceil(T/32) when T % 64 is 1..32). Run::conv3_stats checks it again
+// per launch.
+int max_gn_parts(int dt, int64_t T) {
+  int m = 0;
+  for (int l = 0; l < 3; ++l)
+    for (int small = 0; small < 2; ++small) {
+      if (small && !dt) continue;
+      m = std::max(m, conv64_nparts(80 >> l, (int)(T >> l), small));
+      for (int cout : {64, 128, 256})
+        for (int im : {IN_INPUT, IN_MASK, IN_GN, IN_PLAIN})
+          m = std::max(m, conv_gn_nparts(dt, (InMode)im, 80 >> l, (int)(T >> l), cout, small));
+    }
+  return m;
+}
+
 Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   Layout L{};
   size_t o = 0;
@@ -462,7 +480,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
     const size_t n = (size_t)B * (80 >> l) * (T >> l) * C[l] * esize(dt);
     for (int i = 0; i < 5; ++i) L.act[l][i] = take(n);
   }
-  L.pmax = 20 * (int)((T + 31) / 32);   // GroupNorm partial slots per utterance: largest producer grid (level-0 conv64)
+  L.pmax = max_gn_parts(dt, T);   // GroupNorm partial slots per utterance: the largest producer grid of either tile plan
   L.stats = take((size_t)25 * B * L.pmax * 16 * sizeof(float));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
@@ -538,12 +556,16 @@ struct Run {
         d->dp[wi].count(wkey + ".w64")) {
       p.w = W(wkey + ".w64");
       const double pos = (double)p.B * p.Fout * p.Tout;
+      const int np = conv64_nparts(p.Fout, p.Tout, p.small);
+      if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }   // would spill into the next stats slot
       timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
-      return conv64_nparts(p.Fout, p.Tout, p.small);
+      return np;
     }
+    const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small);
+    if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
     conv(CONV3, im, OUT_STATS, p);
-    return conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small);
+    return np;
   }
 
   // diagnostics: "gnpart.<k>" copies GroupNorm partial slot k (B x pmax x 16 floats) after the launch that
@@ -615,8 +637,9 @@ struct Run {
       setw(p, k + "block1.block.0.weight"); p.bias = Fp(k + "block1.block.0.bias");
       p.out = pre1; p.out_part = st1;
       if (input) {
-        conv(CONV3, IN_INPUT, OUT_STATS, p);
         np1 = conv_gn_nparts(dt, IN_INPUT, Fl(lvl), Tl(lvl), Cout, small);
+        if (np1 > L.pmax) { chk(hipErrorInvalidValue); return; }
+        conv(CONV3, IN_INPUT, OUT_STATS, p);
       } else {
         np1 = conv3_stats(IN_MASK, p, k + "block1.block.0.weight");
       }
@@ -1253,6 +1276,15 @@ int gt_decoder_set_graphs(gt_decoder* d, int on) {
 }
 
 int64_t gt_decoder_graph_captures(const gt_decoder* d) { return d ? d->captures : -1; }
+
+int gt_decoder_set_betas(gt_decoder* d, float beta_min, float beta_max) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  if (d->beta_min != beta_min || d->beta_max != beta_max) {
+    d->beta_min = beta_min; d->beta_max = beta_max;
+    d->drop_graphs();   // captured sampler graphs hold the old beta table
+  }
+  return GT_OK;
+}
 
 int gt_decoder_set_small_batch(gt_decoder* d, int64_t max_b) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");

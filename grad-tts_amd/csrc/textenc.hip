@@ -362,7 +362,7 @@ __global__ void te_durations_kernel(const float* logw, const float* x_mask, int 
   float c = 0.f;
   for (int t = 0; t < Tx; ++t) {
     const long i = (long)b * Tx + t;
-    const float w = __expf(logw[i]) * x_mask[i];
+    const float w = expf(logw[i]) * x_mask[i];   // accurate exp: ceil() flips on a 1-ulp difference
     const float wc = ceilf(w) * ls;
     w_ceil[i] = wc;
     c += wc;

@@ -23,6 +23,7 @@ SIGNATURES = [
     ("gt_decoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_float, _c.c_float, _c.c_float,
                                      _c.POINTER(_c.c_void_p)]),
     ("gt_decoder_destroy", None, [_c.c_void_p]),
+    ("gt_decoder_set_betas", _c.c_int, [_c.c_void_p, _c.c_float, _c.c_float]),
     ("gt_decoder_pack_count", _c.c_int64, [_c.c_void_p]),
     ("gt_decoder_num_params", _c.c_int, [_c.c_void_p]),
     ("gt_decoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),

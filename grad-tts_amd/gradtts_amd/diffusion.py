@@ -174,9 +174,9 @@ class GradLogPEstimator2d(torch.nn.Module):
                                           float(beta_max), float(self.pe_scale), ctypes.byref(h)), "gt_decoder_create")
             self._handle = h
             self._beta = (beta_min, beta_max)
-        elif self._beta != (beta_min, beta_max):
-            self._free_native()
-            return self._native(beta_min, beta_max)
+        elif self._beta != (beta_min, beta_max):   # Diffusion vs SPEECHSDE schedules: a scalar change, weights stay packed
+            check(lib().gt_decoder_set_betas(self._handle, float(beta_min), float(beta_max)), "gt_decoder_set_betas")
+            self._beta = (beta_min, beta_max)
         sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
         if sig != self._synced:
             L = lib()
@@ -228,9 +228,19 @@ class GradLogPEstimator2d(torch.nn.Module):
             raise ValueError(f"spk must be [B,{self.spk_emb_dim}]")
         return spk
 
-    @torch.no_grad()
     def forward(self, x, mask, mu, t, spk=None):
-        """s_theta(x_t, t) -> [B, n_feats, T]  (model/diffusion.py:174-216)."""
+        """s_theta(x_t, t) -> [B, n_feats, T]  (model/diffusion.py:174-216).
+
+        Differentiable in ``x``: with gradients enabled and ``x.requires_grad`` the result carries a backward that
+        runs the U-Net VJP on the device (gt_estimator_vjp, fp32), so the reference's autograd consumers -- the
+        Hutchinson divergence ``get_div_fn(fn)`` (n_best/likelihood/likelihood.py:27-38) -- work unchanged.
+        Parameter gradients come from Diffusion.loss_t (the training step); mu / spk / t are constants here."""
+        if torch.is_grad_enabled() and isinstance(x, torch.Tensor) and x.requires_grad:
+            return _EstimatorX.apply(x, self, mask, mu, t, spk)
+        with torch.no_grad():
+            return self._forward(x, mask, mu, t, spk)
+
+    def _forward(self, x, mask, mu, t, spk=None):
         device = _require_cuda(x, mu, mask)
         self._check_shapes(x, mask, mu)
         B = x.shape[0]
@@ -241,6 +251,39 @@ class GradLogPEstimator2d(torch.nn.Module):
             h = self._native(*getattr(self, "_beta_override", (0.05, 20.0)))
             # torch.ops.gradtts.estimator (csrc/torch_ops.cpp) -> gt_estimator_forward on the current stream
             return ops().estimator(h.value, dcode, x.to(device), mask.to(device), mu.to(device), t, spk32)
+
+
+class _EstimatorX(torch.autograd.Function):
+    """s_theta(x) with d/dx by the device VJP: backward(v) = (ds/dx)^T v from gt_estimator_vjp (fp32 tape + U-Net
+    backward without parameter gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, est, mask, mu, t, spk):
+        ctx.est = est
+        ctx.args = (mask, mu, t, spk)
+        ctx.save_for_backward(x)
+        return est._forward(x.detach(), mask, mu, t, spk)
+
+    @staticmethod
+    def backward(ctx, v):
+        (x,) = ctx.saved_tensors
+        est = ctx.est
+        mask, mu, t, spk = ctx.args
+        device = x.device
+        B, _, T = x.shape
+        x32, m32, mu32, v32 = (_f32c(a, device) for a in (x, mask, mu, v))
+        t32 = _f32c(torch.as_tensor(t, device=device).reshape(-1).expand(B), device)
+        spk32 = est._spk(spk, B, device)
+        score = torch.empty_like(x32)
+        gx = torch.empty_like(x32)
+        with torch.cuda.device(device):
+            h = est._native(*getattr(est, "_beta_override", (0.05, 20.0)))
+            ws = torch.empty(lib().gt_estimator_vjp_workspace_bytes(h, B, T), dtype=torch.uint8, device=device)
+            check(lib().gt_estimator_vjp(h, x32.data_ptr(), m32.data_ptr(), mu32.data_ptr(), t32.data_ptr(),
+                                         spk32.data_ptr() if spk32 is not None else None, v32.data_ptr(), B, T,
+                                         score.data_ptr(), gx.data_ptr(), ws.data_ptr(), ws.numel(),
+                                         _stream_ptr(device)), "gt_estimator_vjp")
+        return gx.to(x.dtype), None, None, None, None, None
 
 
 def get_noise(t, beta_init, beta_term, cumulative=False):

@@ -53,6 +53,10 @@ const char* gt_last_error(void);
 int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float beta_min, float beta_max,
                       float pe_scale, gt_decoder** out);
 void gt_decoder_destroy(gt_decoder* dec);
+/* Change beta_min / beta_max (Diffusion.beta_min/beta_max; SPEECHSDE.beta_0/beta_1, sde_lib.py:258-262) of an
+ * existing decoder: the noise schedule is read at each call, so weights stay packed; captured sampler graphs
+ * are dropped when the values change. */
+int gt_decoder_set_betas(gt_decoder* dec, float beta_min, float beta_max);
 
 /* Parameter inventory = GradLogPEstimator2d.state_dict() keys in registration order (no "estimator." prefix). */
 int gt_decoder_num_params(const gt_decoder* dec);

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -175,6 +176,39 @@ def loss_t(p, x0, mask, mu, t, z, spk=None, n_spks=1, beta_min=0.05, beta_max=20
     noise_estimation = noise_estimation * torch.sqrt(1.0 - torch.exp(-cum_noise))
     loss = torch.sum((noise_estimation + z) ** 2) / (torch.sum(mask) * n_feats)
     return loss, xt
+
+
+def loss_t_grads(sd, x0, mask, mu, t, z, spk=None, n_spks=1, dtype=torch.float64, beta_min=0.05, beta_max=20.0):
+    """``Diffusion.loss_t`` (diffusion.py:274-281) differentiated by torch.autograd in `dtype` (numpy inputs):
+    returns (loss, {param name: grad}, d mu, d spk or None) -- the gradients ``loss.backward()`` gives the
+    reference's training step (train.py:109-113)."""
+    d = lambda a: torch.as_tensor(a).to(dtype)
+    p = {k: torch.as_tensor(v).to(dtype).requires_grad_() for k, v in sd.items()}
+    mu_t = d(mu).requires_grad_()
+    spk_t = d(spk).requires_grad_() if n_spks != 1 and spk is not None else None
+    x0_t, mask_t, t_t, z_t = d(x0), d(mask), d(t), d(z)
+    with torch.enable_grad():
+        xt, zm = forward_diffusion(x0_t, mask_t, mu_t, t_t, z_t, beta_min, beta_max)
+        cum = get_noise(t_t[:, None, None], beta_min, beta_max, cumulative=True)
+        ne = estimator(p, xt, mask_t, mu_t, t_t, spk_t, n_spks) * torch.sqrt(1.0 - torch.exp(-cum))
+        loss = torch.sum((ne + zm) ** 2) / (torch.sum(mask_t) * 80)
+        loss.backward()
+    return float(loss.detach()), {k: (v.grad.numpy() if v.grad is not None else np.zeros(v.shape)) for k, v in p.items()}, \
+        mu_t.grad.numpy(), (spk_t.grad.numpy() if spk_t is not None else None)
+
+
+def grad_probe(name, shape):
+    """Fixed pseudo-random direction of the gradient digests in tests/golden/loss_*.npz (make_golden_train_lik.py)."""
+    seed = int.from_bytes(name.encode()[:8].ljust(8, b"\0"), "little") ^ 0x5EED
+    return np.random.default_rng(seed).standard_normal(shape)
+
+
+def grad_digest(grads, names):
+    """(sum of squares, projection onto grad_probe) per parameter, in `names` order, fp64."""
+    gsq = np.array([float((np.asarray(grads[k], np.float64) ** 2).sum()) for k in names])
+    gproj = np.array([float((np.asarray(grads[k], np.float64) * grad_probe(k, np.shape(grads[k]))).sum())
+                      for k in names])
+    return gsq, gproj
 
 
 def log_prior(mu_x, y, n_feats=80):

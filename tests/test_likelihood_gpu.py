@@ -14,7 +14,7 @@ from conftest import gpu_available
 from gpu_util import make_decoder, rel_err, report
 from gradtts_amd import _lib
 from gradtts_amd.diffusion import _stream_ptr
-from gradtts_amd.likelihood import SPEECHSDE, get_div_fn, get_likelihood_fn
+from gradtts_amd.likelihood import SPEECHSDE, _Evaluator as _Ev, get_div_fn, get_fused_div_fn, get_likelihood_fn
 from gradtts_amd.params import synthetic_inputs
 
 pytestmark = pytest.mark.gpu
@@ -77,9 +77,15 @@ def test_drift_and_divergence_match_oracle(n_spks):
     report(f"likelihood drift n_spks={n_spks}", rel_err(drift.cpu().numpy(), rd.detach().numpy()), 2e-5)
     report(f"likelihood divergence n_spks={n_spks}", float(np.max(np.abs(div.cpu().numpy() - rdiv.numpy()) /
                                                                     np.abs(rdiv.numpy()))), 1e-4)
-    # get_div_fn (the reference's name) returns the same divergence
-    div2 = get_div_fn(dec.estimator, sde)(c(x), c(t), c(eps))
+    # the fused entry point under its own name returns the same divergence
+    div2 = get_fused_div_fn(dec.estimator, sde)(c(x), c(t), c(eps))
     assert torch.equal(div, div2)
+    # the reference's own formulation, get_div_fn(fn) with torch.autograd through the estimator (its backward is
+    # the device VJP) around the reference's drift_fn (likelihood.py:61-68), gives the same divergence
+    rsde = sde.reverse(lambda xx, tt: dec.estimator(xx, c(mask), c(mu), tt, c(spk)), probability_flow=True)
+    div3 = get_div_fn(lambda xx, tt: rsde.sde(xx * c(mask), tt)[0] * c(mask))(c(x), c(t), c(eps))
+    report(f"get_div_fn(fn) autograd vs fused divergence n_spks={n_spks}",
+           float((div3 - div).abs().max() / div.abs().max()), 1e-5)
 
 
 def test_likelihood_euler_matches_oracle():
@@ -189,3 +195,35 @@ def test_get_score_model_and_rescoring_chain(mas_oracle):
     rbpd, _, rdl, _ = olik.likelihood_euler(p, y, ym, r_mu_y, eps, 2)
     report("rescoring bpd (get_score_model + euler 2)", float(np.max(np.abs(bpd.cpu().numpy() - rbpd.numpy()) /
                                                                       np.abs(rbpd.numpy()))), 1e-4)
+
+
+@pytest.mark.parametrize("name", ["lik_s1_E3.npz", "lik_s247_E2.npz"])
+def test_likelihood_matches_reference_fixture(name):
+    """Against the REAL reference (tests/golden/make_golden_train_lik.py: n_best likelihood_fn with euler steps, the
+    reference SPEECHSDE and Rademacher probe; one drift_fn / get_div_fn evaluation), fp32 as the reference runs:
+    drift 2e-5 x max, divergence 1e-4 rel, z 2e-5 x max, delta_logp / prior_logp / bpd 1e-4 rel -- through the fused
+    device path and through the reference's own autograd formulation (get_div_fn(fn) over the estimator)."""
+    from conftest import load_golden
+    from gradtts_amd.tts import ScoreModel
+    g = load_golden(name)
+    n_spks = int(g["n_spks"])
+    dec, _ = make_decoder(n_spks, int(g["seed_w"]), torch.float32)
+    c = lambda k: torch.from_numpy(np.ascontiguousarray(g[k])).cuda()
+    spk = c("spk") if n_spks != 1 else None
+    mu, mask, x, eps = c("mu"), c("mask"), c("x"), c("eps")
+    sde = SPEECHSDE(beta_min=0.05, beta_max=20.0, N=1000, mu=mu, spk=spk, mask=mask)
+    model = ScoreModel(dec.estimator, mask, mu, spk)
+    rel = lambda a, b: float(np.max(np.abs(a - b) / np.abs(b)))
+    B = x.shape[0]
+    tv = torch.full((B,), float(g["t_eval"]), device="cuda")
+    drift, div = _Ev(model, sde).drift_div(x, tv, eps)
+    report(f"likelihood drift vs reference {name}", rel_err(drift.cpu().numpy(), g["drift"]), 2e-5)
+    report(f"likelihood div vs reference {name}", rel(div.cpu().numpy(), g["div"]), 1e-4)
+    rsde = sde.reverse(model, probability_flow=True)
+    div_ag = get_div_fn(lambda xx, tt: rsde.sde(xx * mask, tt)[0] * mask)(x.clone(), tv, eps)
+    report(f"likelihood get_div_fn(fn) autograd vs reference {name}", rel(div_ag.cpu().numpy(), g["div"]), 1e-4)
+    bpd, pl, dl, z = get_likelihood_fn(sde, lambda v: v, euler=int(g["n_euler"]))(model, x, epsilon=eps)
+    report(f"likelihood z vs reference {name}", rel_err(z.cpu().numpy(), g["z"]), 2e-5)
+    report(f"likelihood delta_logp vs reference {name}", rel(dl.cpu().numpy(), g["delta_logp"]), 1e-4)
+    report(f"likelihood prior_logp vs reference {name}", rel(pl.cpu().numpy(), g["prior_logp"]), 1e-4)
+    report(f"likelihood bpd vs reference {name}", rel(bpd.cpu().numpy(), g["bpd"]), 1e-4)

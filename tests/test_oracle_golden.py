@@ -103,3 +103,70 @@ def test_mas_oracle_vs_reference_build_random(mas_oracle):
         paths, vals = mas_oracle(v, t_x, t_y)
         np.testing.assert_array_equal(paths, ref_paths)
         np.testing.assert_array_equal(vals, ref_v)
+
+
+# ---- (f1) training loss and its gradients, (f3) likelihood: fixtures from the real reference
+# (tests/golden/make_golden_train_lik.py: Diffusion.loss_t + loss.backward(); n_best likelihood_fn / drift_fn /
+# get_div_fn with the reference SPEECHSDE)
+
+def _grad_digest_err(gsq, gproj, rsq, rproj):
+    """Relative error of the per-parameter gradient digests: sqrt(sum g^2) within 1e-3 of the reference norm, the
+    projection onto a random direction within 1e-3 of it (plus 1e-3 of the largest norm: biases ahead of a
+    GroupNorm have an exact gradient of 0)."""
+    rn = np.sqrt(rsq)
+    floor = 1e-3 * rn.max()
+    e_norm = np.abs(np.sqrt(gsq) - rn) / (rn + floor)
+    e_proj = np.abs(gproj - rproj) / (rn + floor)
+    return float(max(e_norm.max(), e_proj.max()))
+
+
+@pytest.mark.parametrize("name", ["loss_s1.npz", "loss_s247.npz"])
+def test_oracle_loss_and_gradients_match_reference(name):
+    g = load_golden(name)
+    p = _params(g)
+    sd = {k: v.numpy() for k, v in p.items()}
+    n_spks = int(g["n_spks"])
+    spk = g["spk"] if n_spks != 1 else None
+    args = (g["x0"], g["mask"], g["mu"], g["t"])
+    # fp32 forward value against the reference's fp32 loss_t
+    loss32, xt = odec.loss_t(p, *(torch.from_numpy(a) for a in args), torch.from_numpy(g["z"]),
+                             torch.from_numpy(spk) if spk is not None else None, n_spks)
+    assert abs(float(loss32) - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+    assert _rel(xt.numpy(), g["xt"]) <= 1e-6
+    # fp64 autograd against the reference's fp64 loss.backward()
+    loss, grads, dmu, dspk = odec.loss_t_grads(sd, *args, g["z"], spk, n_spks)
+    assert abs(loss - float(g["loss_f64"])) <= 1e-10 * abs(float(g["loss_f64"]))
+    names = [str(n) for n in g["param_names"]]
+    gsq, gproj = odec.grad_digest(grads, names)
+    assert _grad_digest_err(gsq, gproj, g["gsq_f64"], g["gproj_f64"]) <= 1e-8
+    assert _rel(dmu, g["dmu_f64"]) <= 1e-9
+    if spk is not None:
+        assert _rel(dspk, g["dspk_f64"]) <= 1e-9
+    for k in list(g):
+        if k.startswith("full_f64__"):
+            assert _rel(grads[k[len("full_f64__"):]], g[k]) <= 1e-9, k
+    # the reference's own fp32-vs-fp64 envelope of the digest (what an fp32 implementation can reach)
+    assert _grad_digest_err(g["gsq"], g["gproj"], g["gsq_f64"], g["gproj_f64"]) <= 1e-4
+
+
+@pytest.mark.parametrize("name", ["lik_s1_E3.npz", "lik_s247_E2.npz"])
+def test_oracle_likelihood_matches_reference(name):
+    from oracle import likelihood as olik
+    g = load_golden(name)
+    p = _params(g)
+    n_spks = int(g["n_spks"])
+    c = lambda k: torch.from_numpy(np.ascontiguousarray(g[k]))
+    spk = c("spk") if n_spks != 1 else None
+    B = g["x"].shape[0]
+    tv = torch.full((B,), float(g["t_eval"]))
+    drift = olik.drift_fn(p, c("x"), c("mask"), c("mu"), tv, spk, n_spks)
+    div = olik.div_fn(p, c("x"), c("mask"), c("mu"), tv, c("eps"), spk, n_spks)
+    assert _rel(drift.detach().numpy(), g["drift"]) <= 1e-5
+    assert float(np.max(np.abs(div.numpy() - g["div"]) / np.abs(g["div"]))) <= 1e-4
+    # the whole euler > 0 likelihood (likelihood.py:99-115) in fp32, as the reference evaluates it
+    bpd, pl, dl, z = olik.likelihood_euler(p, c("x"), c("mask"), c("mu"), c("eps"), int(g["n_euler"]), spk, n_spks,
+                                           dtype=torch.float32)
+    assert _rel(z.numpy(), g["z"]) <= 1e-5
+    assert float(np.max(np.abs(dl.numpy() - g["delta_logp"]) / np.abs(g["delta_logp"]))) <= 1e-4
+    assert float(np.max(np.abs(bpd.numpy() - g["bpd"]) / np.abs(g["bpd"]))) <= 1e-5
+    assert float(np.max(np.abs(pl.numpy() - g["prior_logp"]) / np.abs(g["prior_logp"]))) <= 1e-5

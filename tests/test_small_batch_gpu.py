@@ -54,6 +54,23 @@ def test_small_plan_batch_invariant():
     assert torch.equal(y4[2:4], y2), float((y4[2:4] - y2).abs().max())
 
 
+@pytest.mark.parametrize("T", [80, 96, 1040])
+def test_small_plan_batch_invariant_ragged_tiles(T):
+    """T % 64 in 1..32: the small plan's 2-row 64-wide level-0 tiles write 40*ceil(T/64) GroupNorm partials per
+    utterance, more than conv64's 20*ceil(T/32); every utterance of a batch of 4 must still equal its B = 1 decode
+    (the stats slots are sized for the largest producer of either plan)."""
+    for dt in (torch.bfloat16, "bf16_w8"):
+        dec, _ = make_decoder(1, 0, dt)
+        lengths = [T, T - 4, T - 12, max(4, T - 40)]
+        mu, z, mask, _ = _inputs(31, 4, T, lengths=lengths)
+        y4 = dec(z, mask, mu, 2)
+        assert torch.isfinite(y4).all()
+        for b in range(4):
+            sl = slice(b, b + 1)
+            y1 = dec(z[sl].contiguous(), mask[sl].contiguous(), mu[sl].contiguous(), 2)
+            assert torch.equal(y4[sl], y1), (dt, T, b, float((y4[sl] - y1).abs().max()))
+
+
 @pytest.mark.parametrize("B,T,N", [(1, 512, 10), (3, 256, 10), (4, 128, 10)])
 def test_plans_agree(B, T, N):
     dec, _ = make_decoder(1, 0, torch.bfloat16)

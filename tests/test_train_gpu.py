@@ -213,3 +213,37 @@ def test_training_step_speed_vs_torch_eager():
     report(f"training step B={B} T={T}: ours {ms_ours:.2f} ms ({frames / ms_ours * 1e3:.0f} frames/s), torch eager "
            f"{ms_eager:.2f} ms ({frames / ms_eager * 1e3:.0f} frames/s); ratio eager/ours", ms_eager / ms_ours, 0.0,
            gate=False, ms_ours=ms_ours, ms_eager=ms_eager)
+
+
+@pytest.mark.parametrize("name", ["loss_s1.npz", "loss_s247.npz"])
+def test_training_step_matches_reference_fixture(name):
+    """The training step against the REAL reference (tests/golden/make_golden_train_lik.py: Diffusion.loss_t +
+    loss.backward() in fp64 with the same noise): loss rel 1e-5 against the reference's fp32 value; every parameter
+    gradient's digest (norm and random projection, oracle.decoder.grad_digest) within 2e-4 of the reference's fp64
+    gradients relative to that tensor's norm (+ 1e-3 of the largest norm); d mu / d spk 2e-4."""
+    from conftest import load_golden
+    from oracle import decoder as odec
+    g = load_golden(name)
+    n_spks = int(g["n_spks"])
+    dec, _ = make_decoder(n_spks, int(g["seed_w"]), torch.float32)
+    c = lambda k: torch.from_numpy(np.ascontiguousarray(g[k])).cuda()
+    mu_d = c("mu").requires_grad_()
+    s = c("spk").requires_grad_() if n_spks > 1 else None
+    loss, xt = dec.loss_t(c("x0"), c("mask"), mu_d, c("t"), s, z=c("z"))
+    loss.backward()
+    report(f"train loss vs reference {name}", abs(float(loss) - float(g["loss"])) / abs(float(g["loss"])), 1e-5)
+    report(f"train xt vs reference {name}", rel_err(xt.detach().cpu().numpy(), g["xt"]), 1e-6)
+    names = [str(n) for n in g["param_names"]]
+    params = dict(dec.estimator.named_parameters())
+    grads = {k: params[k].grad.detach().cpu().numpy().astype(np.float64) for k in names}
+    gsq, gproj = odec.grad_digest(grads, names)
+    rn = np.sqrt(g["gsq_f64"])
+    floor = 1e-3 * rn.max()
+    err = np.maximum(np.abs(np.sqrt(gsq) - rn), np.abs(gproj - g["gproj_f64"])) / (rn + floor)
+    report(f"train param grad digests vs reference {name} (worst {names[int(err.argmax())]})", float(err.max()), 2e-4)
+    for k in list(g):
+        if k.startswith("full_f64__"):
+            report(f"train grad {k[10:]} vs reference", rel_err(grads[k[10:]], g[k]), 2e-4)
+    report(f"train d mu vs reference {name}", rel_err(mu_d.grad.cpu().numpy(), g["dmu_f64"]), 2e-4)
+    if n_spks > 1:
+        report(f"train d spk vs reference {name}", rel_err(s.grad.cpu().numpy(), g["dspk_f64"]), 2e-4)
