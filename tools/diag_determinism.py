@@ -10,7 +10,7 @@ sys.path[:0] = [os.path.join(REPO, "grad-tts_amd"), os.path.join(REPO, "tests"),
 from gpu_util import STAGES, make_decoder, probe  # noqa: E402
 from gradtts_amd.params import synthetic_inputs  # noqa: E402
 
-cdt = torch.bfloat16 if (len(sys.argv) < 2 or sys.argv[1] == "bf16") else torch.float32
+cdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "w8": "bf16_w8"}[sys.argv[1] if len(sys.argv) > 1 else "bf16"]
 B, T = int(os.environ.get("B", 32)), int(os.environ.get("T", 512))
 dec, _ = make_decoder(1, 0, cdt)
 mu, z, mask, _ = synthetic_inputs(1234, B, T)
