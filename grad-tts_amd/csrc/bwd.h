@@ -97,10 +97,5 @@ hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float
 constexpr long kWPartCap = 8L << 20;
 int mwgrad_splits(const WGradParams& p);
 hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm);
-bool train_valu();
-
-hipError_t launch_wgrad(const WGradParams& p, float* part, int splits, float* dw, long sa, long sb, int accumulate,
-                        hipStream_t s);
-
 
 }  // namespace gt

@@ -1,19 +1,18 @@
 // Backward of the score U-Net for the training step (model/diffusion.py:16-216 through
 // Diffusion.loss_t :274-281), fp32, channels-last activations [B][F_l][T_l][C] as in the forward.
 //
-// Generic building blocks (every conv of the U-Net is one of three gather relations u -> v = u*S - PAD + k):
-//   gconv_kernel    out[u][a] (+)= sum_{k,c} W(a, c, k) in[v(u, k)][c] (* mask)   regular conv; with flipped taps
-//                   and transposed weight strides also the stride-1 dgrad (3x3 and 1x1)
-//   tconv_kernel    out[v][b] (+)= sum_{k,u: v(u,k) = v} W(a, b, k) in[u][a]        transposed relation: the dgrad of
-//                   the stride-2 Downsample conv, and ConvTranspose2d itself
-//   wgrad_kernel    dW(a, b, k) = sum_u P[u][a] Q[v(u, k)][b]                      every weight gradient (split over
-//                   positions, fixed-order reduction by wgrad_reduce_kernel)
+// Generic building blocks on fp32 MFMA (v_mfma_f32_32x32x2_f32; every conv of the U-Net is one of three gather
+// relations u -> v = u*S - PAD + k):
+//   mconv_kernel    out[u][a] (+)= sum_{k,c} W(a, c, k) in[v(u, k)][c] (* mask)   3x3 / 4x4 convs; with flipped taps
+//                   and transposed weight strides also the stride-1 dgrad, and the transposed relation (the dgrad of
+//                   the stride-2 Downsample conv, ConvTranspose2d itself) as a stride-1 conv over the dilated input
+//   mconv1_kernel   the 1x1 convs and their dgrads
+//   mwgrad_kernel   dW(a, b, k) = sum_u P[u][a] Q[v(u, k)][b]                      every weight gradient (split over
+//                   positions, fixed-order reduction by mwgrad_reduce_kernel)
 // plus GroupNorm/Mish (Block) backward, per-channel / per-utterance sums, the LinearAttention algebra, the small
 // MLPs and the loss. Weights are read in the reference layouts (Conv2d [out][in][kh][kw], ConvTranspose2d
 // [in][out][kh][kw]) through element strides. Deterministic: every reduction runs in a fixed order.
-//
-// This is the correctness-first version: LDS-tiled VALU fp32 (the MFMA versions of gconv / wgrad are the
-// next performance step).
+// Measured against torch eager on the same MI355X and the per-kernel breakdown: DESIGN.md §9.
 #include <algorithm>
 #include <cstdlib>
 
@@ -22,93 +21,24 @@
 
 namespace gt {
 
-static const bool kValu = getenv("GT_TRAIN_VALU") != nullptr;   // A/B switch: the VALU gconv / wgrad kernels
-
 // tanh(softplus(x)) = n / (n + 2) with n = e (e + 2), e = exp(x): one exponential per element (softplus threshold
 // 20 as torch: x > 20 -> mish = x, mish' = 1)
 GT_DEV float mish_grad(float x) {   // d/dx x tanh(softplus(x)) = th + x (1 - th^2) sigmoid(x)
   if (x > 20.f) return 1.f;
   const float e = __expf(x), n = e * (e + 2.f);
-  const float th = __fdividef(n, n + 2.f), sg = __fdividef(e, 1.f + e);
+  const float th = n * __builtin_amdgcn_rcpf(n + 2.f), sg = e * __builtin_amdgcn_rcpf(1.f + e);   // v_rcp_f32
   return th + x * (1.f - th * th) * sg;
 }
 GT_DEV float mish_f(float x) {
   if (x > 20.f) return x;
   const float e = __expf(x), n = e * (e + 2.f);
-  return x * __fdividef(n, n + 2.f);
+  return x * (n * __builtin_amdgcn_rcpf(n + 2.f));
 }
 
 GT_DEV void split_range(long n, int S, int s, long* lo, long* hi) {
   const long per = (n + S - 1) / S;
   *lo = (long)s * per;
   *hi = *lo + per < n ? *lo + per : n;
-}
-
-// ---------------------------------------------------------------- gconv: 64 output positions (one row) x 64
-// output channels per workgroup, 8-channel input chunks staged in LDS; thread = 4 positions x 4 channels
-constexpr int GC_CC = 8;
-__global__ __launch_bounds__(256) void gconv_kernel(GConvParams p) {
-  __shared__ float s_in[4][64 * 2 + 4][GC_CC];   // KS <= 4 rows, (64 - 1) S + KS columns
-  __shared__ float s_w[64][GC_CC][16];
-  const int tid = threadIdx.x;
-  const int n_tt = (p.To + 63) / 64;
-  int bid = blockIdx.x;
-  const int tt = bid % n_tt; bid /= n_tt;
-  const int fo = bid % p.Fo;
-  const int b = bid / p.Fo;
-  const int to0 = tt * 64, a0 = blockIdx.y * 64;
-  const int KK = p.KS * p.KS, PC = 63 * p.S + p.KS;
-  const int pl = tid & 15, al = tid >> 4;
-  float acc[4][4] = {};
-  for (int c0 = 0; c0 < p.Cin; c0 += GC_CC) {
-    __syncthreads();
-    for (int i = tid; i < p.KS * PC * GC_CC; i += 256) {
-      const int c = i % GC_CC, col = (i / GC_CC) % PC, row = i / (GC_CC * PC);
-      const int fi = fo * p.S - p.PAD + row, ti = to0 * p.S - p.PAD + col, ci = c0 + c;
-      float v = 0.f;
-      if (fi >= 0 && fi < p.Fi && ti >= 0 && ti < p.Ti && ci < p.Cin) {
-        v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
-        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
-      }
-      s_in[row][col][c] = v;
-    }
-    for (int i = tid; i < 64 * GC_CC * KK; i += 256) {
-      const int k = i % KK, c = (i / KK) % GC_CC, a = i / (KK * GC_CC);
-      const int kk = p.flip ? KK - 1 - k : k;
-      s_w[a][c][k] = (a0 + a < p.Cout && c0 + c < p.Cin) ? p.w[(long)(a0 + a) * p.wsa + (long)(c0 + c) * p.wsc + kk] : 0.f;
-    }
-    __syncthreads();
-    for (int k = 0; k < KK; ++k) {
-      const int kh = k / p.KS, kw = k % p.KS;
-#pragma unroll
-      for (int c = 0; c < GC_CC; ++c) {
-        float x[4], w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = s_in[kh][(pl + 16 * i) * p.S + kw][c];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = s_w[al * 4 + j][c][k];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(w[j], x[i], acc[i][j]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int to = to0 + pl + 16 * i;
-    if (to >= p.To) continue;
-    const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = a0 + al * 4 + j;
-      if (a >= p.Cout) continue;
-      const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
-      float v = acc[i][j] + (p.bias ? p.bias[a] : 0.f);
-      v *= om;
-      p.out[o] = p.accumulate ? p.out[o] + v : v;
-    }
-  }
 }
 
 // ---------------------------------------------------------------- mconv: the gconv relation on fp32 MFMA
@@ -440,8 +370,6 @@ int mwgrad_splits(const WGradParams& p) {
   return (int)std::max<long>(1, s);
 }
 
-bool train_valu() { return kValu; }
-
 hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm) {
   const int cfg = p.KS * 10 + p.S;
   if (!(cfg == 11 || cfg == 31 || cfg == 32 || cfg == 42)) return hipErrorInvalidValue;
@@ -458,136 +386,6 @@ hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, 
   hipLaunchKernelGGL(mwgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, strm, part, splits, p.A,
                      p.Bc, p.KS * p.KS, sa, sb, dw, accumulate);
   return hipGetLastError();
-}
-
-// ---------------------------------------------------------------- tconv: out[v][b] = sum_{u*S-PAD+k = v} W in[u]
-// one workgroup per 64 output positions (one row) x 64 output channels; inputs read through L1 (the transposed
-// gather touches at most ceil(KS/S)^2 taps per output)
-__global__ __launch_bounds__(256) void tconv_kernel(GConvParams p) {
-  const int tid = threadIdx.x;
-  const int n_tt = (p.To + 63) / 64;
-  int bid = blockIdx.x;
-  const int tt = bid % n_tt; bid /= n_tt;
-  const int fo = bid % p.Fo;
-  const int b = bid / p.Fo;
-  const int to0 = tt * 64, a0 = blockIdx.y * 64;
-  const int pl = tid & 15, al = tid >> 4;
-  float acc[4][4] = {};
-  for (int kh = 0; kh < p.KS; ++kh) {
-    const int nf = fo + p.PAD - kh;
-    if (nf < 0 || nf % p.S != 0 || nf / p.S >= p.Fi) continue;
-    const int fi = nf / p.S;
-    for (int kw = 0; kw < p.KS; ++kw) {
-      const int k = kh * p.KS + kw;
-      for (int c = 0; c < p.Cin; ++c) {
-        float w[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int a = a0 + al * 4 + j;
-          w[j] = a < p.Cout ? p.w[(long)c * p.wsc + (long)a * p.wsa + k] : 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int nt = to0 + pl + 16 * i + p.PAD - kw;
-          if (to0 + pl + 16 * i >= p.To || nt < 0 || nt % p.S != 0 || nt / p.S >= p.Ti) continue;
-          const int ti = nt / p.S;
-          float x = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + c];
-          if (p.mask) x *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(w[j], x, acc[i][j]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int to = to0 + pl + 16 * i;
-    if (to >= p.To) continue;
-    const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int a = a0 + al * 4 + j;
-      if (a >= p.Cout) continue;
-      const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
-      float v = acc[i][j] + (p.bias ? p.bias[a] : 0.f);
-      v *= om;
-      p.out[o] = p.accumulate ? p.out[o] + v : v;
-    }
-  }
-}
-
-// ---------------------------------------------------------------- wgrad: dW(a, b, k) = sum_u P[u][a] Q[v(u,k)][b]
-// workgroup = 32 a x 32 b x all taps over its share of the U positions; thread = (a, b) pair x taps.
-// Grid (A/32, B/32, splits); partial[split][a][b][k] -> wgrad_reduce_kernel.
-constexpr int WG_U = 32;
-__global__ __launch_bounds__(256) void wgrad_kernel(WGradParams p) {
-  __shared__ float s_p[WG_U][33];
-  __shared__ float s_q[16][WG_U][33];
-  const int tid = threadIdx.x;
-  const int a0 = blockIdx.x * 32, b0 = blockIdx.y * 32, split = blockIdx.z;
-  const int KK = p.KS * p.KS;
-  const long nU = (long)p.B * p.Fu * p.Tu;
-  const long per = (nU + gridDim.z - 1) / gridDim.z;
-  const long u_lo = split * per, u_hi = u_lo + per < nU ? u_lo + per : nU;
-  const int ai = tid >> 3, bq = (tid & 7) * 4;   // thread: a = a0 + ai, b = b0 + bq .. bq+3
-  float acc[16][4] = {};
-  for (long u0 = u_lo; u0 < u_hi; u0 += WG_U) {
-    __syncthreads();
-    for (int i = tid; i < WG_U * 32; i += 256) {
-      const int uu = i / 32, a = i % 32;
-      const long u = u0 + uu;
-      float v = 0.f;
-      if (u < u_hi && a0 + a < p.A) {
-        const int b = (int)(u / ((long)p.Fu * p.Tu)), t = (int)(u % p.Tu);
-        v = p.P[u * p.A + a0 + a];
-        if (p.pmask) v *= mask_at(p.pmask, p.T0, b, t, p.lvl_p);
-      }
-      s_p[uu][a] = v;
-    }
-    for (int i = tid; i < KK * WG_U * 32; i += 256) {
-      const int bb = i % 32, uu = (i / 32) % WG_U, k = i / (32 * WG_U);
-      const long u = u0 + uu;
-      float v = 0.f;
-      if (u < u_hi && b0 + bb < p.Bc) {
-        const int b = (int)(u / ((long)p.Fu * p.Tu));
-        const int fu = (int)((u / p.Tu) % p.Fu), tu = (int)(u % p.Tu);
-        const int fv = fu * p.S - p.PAD + k / p.KS, tv = tu * p.S - p.PAD + k % p.KS;
-        if (fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv) {
-          v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + bb];
-          if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
-        }
-      }
-      s_q[k][uu][bb] = v;
-    }
-    __syncthreads();
-    for (int uu = 0; uu < WG_U; ++uu) {
-      const float pa = s_p[uu][ai];
-      for (int k = 0; k < KK; ++k) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[k][j] = fmaf(pa, s_q[k][uu][bq + j], acc[k][j]);
-      }
-    }
-  }
-  if (a0 + ai >= p.A) return;
-  for (int k = 0; k < KK; ++k)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int b = b0 + bq + j;
-      if (b < p.Bc) p.part[(((long)split * p.A + a0 + ai) * p.Bc + b) * KK + k] = acc[k][j];
-    }
-}
-
-// sum the splits in order; write dW in the reference layout through strides (a, b, k) -> a*sa + b*sb + k
-__global__ void wgrad_reduce_kernel(const float* part, int splits, int A, int Bc, int KK, long sa, long sb, float* dw,
-                                    int accumulate) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const long n = (long)A * Bc * KK;
-  if (i >= n) return;
-  float s = 0.f;
-  for (int q = 0; q < splits; ++q) s += part[(long)q * n + i];
-  const int k = (int)(i % KK), b = (int)((i / KK) % Bc), a = (int)(i / ((long)KK * Bc));
-  float* d = dw + a * sa + b * sb + k;
-  *d = accumulate ? *d + s : s;
 }
 
 // ---------------------------------------------------------------- per-utterance channel sums
@@ -945,45 +743,26 @@ __global__ void input_pack_kernel(const float* mu, const float* xt, const float*
 
 hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   if (p.KS > 4 || p.S > 2) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)), (unsigned)((p.Cout + 63) / 64));
-  if (kValu) {
-    if (p.transposed) hipLaunchKernelGGL(tconv_kernel, grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(gconv_kernel, grid, dim3(256), 0, s, p);
-  } else {
-    auto mgrid = [&](int rh, int tw) {
-      return dim3((unsigned)((long)p.B * ((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw)), (unsigned)((p.Cout + 63) / 64));
-    };
-    auto slots = [&](int rh, int tw) { return (long)((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw); };
-    const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
-    if (cfg == 11) {
-      hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
-                                             (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);
-    } else if (cfg == 31) {   // the 3x3 stride-1 convs: tile shape with the fewest 256-position tiles
-      const long s4 = slots(4, 64), s8 = slots(8, 32), s5 = slots(5, 48);
-      if (s4 <= s8 && s4 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
-      else if (s8 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 8, 32>), mgrid(8, 32), dim3(256), 0, s, p);
-      else hipLaunchKernelGGL((mconv_kernel<3, 1, 5, 48>), mgrid(5, 48), dim3(256), 0, s, p);
-    }
-    else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
-    else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
-    else if (cfg == 42) hipLaunchKernelGGL((mconv_kernel<4, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
-    else return hipErrorInvalidValue;
+  auto mgrid = [&](int rh, int tw) {
+    return dim3((unsigned)((long)p.B * ((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw)), (unsigned)((p.Cout + 63) / 64));
+  };
+  auto slots = [&](int rh, int tw) { return (long)((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw); };
+  const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
+  if (cfg == 11) {
+    hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
+                                           (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);
+  } else if (cfg == 31) {   // the 3x3 stride-1 convs: tile shape with the fewest 256-position tiles
+    const long s4 = slots(4, 64), s8 = slots(8, 32), s5 = slots(5, 48);
+    if (s4 <= s8 && s4 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+    else if (s8 <= s5) hipLaunchKernelGGL((mconv_kernel<3, 1, 8, 32>), mgrid(8, 32), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((mconv_kernel<3, 1, 5, 48>), mgrid(5, 48), dim3(256), 0, s, p);
   }
+  else if (cfg == 32) hipLaunchKernelGGL((mconv_kernel<3, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+  else if (cfg == 41) hipLaunchKernelGGL((mconv_kernel<4, 1, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+  else if (cfg == 42) hipLaunchKernelGGL((mconv_kernel<4, 2, 4, 64>), mgrid(4, 64), dim3(256), 0, s, p);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
-
-hipError_t launch_wgrad(const WGradParams& p, float* part, int splits, float* dw, long sa, long sb, int accumulate,
-                        hipStream_t s) {
-  if (p.KS > 4) return hipErrorInvalidValue;
-  WGradParams q = p;
-  q.part = part;
-  hipLaunchKernelGGL(wgrad_kernel, dim3((p.A + 31) / 32, (p.Bc + 31) / 32, splits), dim3(256), 0, s, q);
-  const long n = (long)p.A * p.Bc * p.KS * p.KS;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, splits, p.A, p.Bc,
-                     p.KS * p.KS, sa, sb, dw, accumulate);
-  return hipGetLastError();
-}
-
 
 // dX[b][i] = dY[b][i] * mish'(pre[b][i])   (grid B, block >= n)
 __global__ void mish_bwd_kernel(const float* dY, const float* pre, int n, float* dX) {

@@ -546,6 +546,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
           v[8 * pr + q] = __uint_as_float(sw[0]);
           v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
         }
+      permlane_swap_settle();
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int cl = wn * 64 + cb * 32 + pr * 16 + 8 * h;   // tile-local first channel of this lane

@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
 
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: ring-row addressing stays scalar
   const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
   const int F = p.Fout, T = p.Tout;
   const int n_ft = F / TF, n_tt = (T + TT - 1) / TT;
@@ -119,6 +120,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int npos = p.B * F * T;
   const int t0 = tt * TT;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * 128, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, npos * 128, 0x00020000);
   auto load_item = [&](int it, int frow, u32x4_t& v, float& m) {
     const int c = (it >> 3) % PC;
     const int ti = t0 - 1 + c;
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       m = ok ? mv : 0.f;
     }
   };
-  auto put_item = [&](int it, int slot, u32x4_t v4, float m) {
+  auto put_item_at = [&](int lds_off, u32x4_t v4, float m) {
     if (IN == IN_MASK) {
       if (__builtin_expect(m != 0.f && m != 1.f, 0)) {   // x * m, fractional mask value
         float v[8];
@@ -157,7 +159,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const uint4 o = f_to_item(v, bf16());
       v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
     }
-    *reinterpret_cast<u32x4_t*>(sR + slot * ROWB + ((it >> 3) % PC) * POSB + sub * 16) = v4;
+    *reinterpret_cast<u32x4_t*>(sR + lds_off) = v4;
+  };
+  auto put_item = [&](int it, int slot, u32x4_t v4, float m) {
+    put_item_at(slot * ROWB + ((it >> 3) % PC) * POSB + sub * 16, v4, m);
   };
 
   // GroupNorm scale/shift (and time bias) of the input channels of utterance b (IN_GN): once per segment
@@ -189,17 +194,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       if (CPT * NTHR == COLD_ITEMS || it < COLD_ITEMS) put_item(it, it / (PC * 8), cv[j], cm[j]);
     }
   }
-  // the next tile's 4 new rows (mel rows 4 (ft0+1) + 1 .. + 4) in flight
-  u32x4_t preg[PPT];
-  float pm[PPT];
-  auto issue_new = [&](int j, int k) {   // item j of tile k's new rows (k past the segment: harmless reload)
+  // The next tiles' new rows (tile k: mel rows 4 (ft0+k) + 1 .. + 4). A thread's item j of every tile has the same
+  // row-in-tile, frame and 8-channel group, so its frame's mask and column offsets are fixed for the whole segment:
+  // computed once here, so the loop issues only the raw buffer loads (no mask loads, no index division) and the
+  // compiler's vmcnt waits count only loads and stores. A masked (IN_MASK) or out-of-range item reads past the end
+  // of the tensor (zeros from the range check, no traffic).
+  const int oob = npos * 128;
+  int nrow[PPT], ncol[PPT], ngo[PPT];
+  float nm[PPT];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
     const int it = tid + NTHR * j;
-    const int itc = it < NEW_ITEMS ? it : 0;
-    load_item(itc, (ft0 + k) * TF + 1 + itc / (PC * 8), preg[j], pm[j]);
+    const bool have = PPT * NTHR == NEW_ITEMS || it < NEW_ITEMS;
+    const int c = (it >> 3) % PC, ti = t0 - 1 + c;
+    const bool ok = have && ti >= 0 && ti < T;
+    const float mv = mask_at(p.mask, p.T0, b, ti < 0 ? 0 : (ti < T ? ti : T - 1), p.lvl_in);
+    nm[j] = (IN != IN_PLAIN && ok) ? mv : (IN == IN_PLAIN && ok ? 1.f : 0.f);
+    nrow[j] = it / (PC * 8);
+    ncol[j] = c * POSB + sub * 16;
+    ngo[j] = (ok && !(IN == IN_MASK && nm[j] == 0.f)) ? ti * 128 + sub * 16 : -1;
+  }
+  u32x4_t preg[PPT];
+  auto issue_new = [&](int j, int k) {   // item j of tile k's new rows (rows past the mel axis read zeros)
+    const int frow = (ft0 + k) * TF + 1 + nrow[j];
+    const int off = (ngo[j] >= 0 && frow < F) ? (b * F + frow) * T * 128 + ngo[j] : oob;
+    preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
   };
   auto put_new = [&](int j, int k) {     // store item j of tile k's new rows into ring slots 4k + 2 + i
-    const int it = tid + NTHR * j;
-    if (PPT * NTHR == NEW_ITEMS || it < NEW_ITEMS) put_item(it, (4 * k + 2 + it / (PC * 8)) % RING, preg[j], pm[j]);
+    if (PPT * NTHR == NEW_ITEMS || tid + NTHR * j < NEW_ITEMS) {
+      int slot = (4 * k + 2) % RING + nrow[j];
+      slot = slot >= RING ? slot - RING : slot;
+      const bool inrow = (ft0 + k) * TF + 1 + nrow[j] < F;   // the zero padding row below the mel axis (IN_GN: no transform)
+      put_item_at(slot * ROWB + ncol[j], preg[j], inrow ? nm[j] : 0.f);
+    }
   };
 #pragma unroll
   for (int j = 0; j < PPT; ++j) issue_new(j, 1);
@@ -256,9 +283,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           v[8 * pr + q] = __uint_as_float(sw[0]);
           v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
         }
+      permlane_swap_settle();
       const int t = t0 + r;
       const bool valid = t < T;
-      bf16* const outp = reinterpret_cast<bf16*>(p.out) + (((long)b * F + ft * TF + lrow) * T + t) * 64;
+      const int obyte = valid ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
@@ -272,7 +300,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           s += o[e];
           q += o[e] * o[e];
         }
-        if (valid) *reinterpret_cast<uint4*>(outp + c0) = f_to_item(o, bf16());
+        const uint4 ov = f_to_item(o, bf16());
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
         gs[pr] += valid ? s : 0.f;
         gq[pr] += valid ? q : 0.f;
       }

@@ -105,8 +105,7 @@ struct Trainer {
   void wgrad(const float* Pt, int Ad, int l_u, bool pmask, const float* Qt, int Bd, int l_v, bool qmask, int KS, int S,
              int PAD, float* dw, long sa, long sb, int acc, int line = __builtin_LINE()) {
     const long nU = (long)B * L(l_u).F * L(l_u).T;
-    const int splits = (int)std::max<long>(1, std::min<long>(256, nU / 512));
-    float* part = train_valu() ? A.take((size_t)splits * Ad * Bd * KS * KS) : wpart;
+    float* part = wpart;
     if (!run) return;
     need(Pt, nU * Ad, "wgrad P", line);
     need(Qt, (long)B * L(l_v).F * L(l_v).T * Bd, "wgrad Q", line);
@@ -117,8 +116,7 @@ struct Trainer {
     p.B = B; p.Fu = L(l_u).F; p.Tu = L(l_u).T; p.A = Ad; p.Fv = L(l_v).F; p.Tv = L(l_v).T; p.Bc = Bd;
     p.KS = KS; p.S = S; p.PAD = PAD; p.P = Pt; p.pmask = pmask ? mask : nullptr; p.lvl_p = l_u;
     p.Q = Qt; p.qmask = qmask ? mask : nullptr; p.lvl_q = l_v; p.T0 = T;
-    if (train_valu()) chk(launch_wgrad(p, part, splits, dw, sa, sb, acc, s), line);
-    else chk(launch_mwgrad(p, part, dw, sa, sb, acc, s), line);
+    chk(launch_mwgrad(p, part, dw, sa, sb, acc, s), line);
   }
   // out[c] (+)= sum_{b, pos} x   (bias gradients): per-utterance sums, then over the batch in order
   void chansum(const float* x, int l, int C, float* out, int acc, int line = __builtin_LINE()) {

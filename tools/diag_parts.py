@@ -11,17 +11,19 @@ from gpu_util import make_decoder, probe  # noqa: E402
 from gradtts_amd.params import synthetic_inputs  # noqa: E402
 
 B, T = int(os.environ.get("B", 32)), int(os.environ.get("T", 512))
-cdt = torch.bfloat16 if (len(sys.argv) < 2 or sys.argv[1] == "bf16") else torch.float32
+cdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "w8": "bf16_w8"}[sys.argv[1] if len(sys.argv) > 1 else "bf16"]
 dec, _ = make_decoder(1, 0, cdt)
 mu, z, mask, _ = synthetic_inputs(1234, B, T)
 t = np.full(B, 0.5, np.float32)
 args = [torch.from_numpy(a).cuda() for a in (z, mask, mu, t)]
-pmax = 20 * ((T + 31) // 32)   # layout(): largest producer grid (level-0 conv64)
-for k in range(24):
+# the probe copies B x pmax x 16 floats (decoder.cpp layout(): max_gn_parts); the rest of the buffer stays NaN
+_, pr = probe(dec.estimator, cdt, *args, None, "gnpart.0", (B * 8192 * 16,))
+pmax = int((~torch.isnan(pr)).sum().item()) // (B * 16)
+for k in range(int(os.environ.get("SLOTS", 24))):
     outs = []
     for rep in range(4):
-        _, pr = probe(dec.estimator, cdt, *args, None, f"gnpart.{k}", (B, pmax, 8, 2))
-        outs.append(pr.cpu().numpy())
+        _, pr = probe(dec.estimator, cdt, *args, None, f"gnpart.{k}", (B * 8192 * 16,))
+        outs.append(pr[: B * pmax * 16].reshape(B, pmax, 8, 2).cpu().numpy())
     d = [np.argwhere(o != outs[0]) for o in outs[1:]]
     n = [len(x) for x in d]
     msg = f"slot {k:2d}: differing per rep {n}"
