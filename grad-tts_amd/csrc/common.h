@@ -111,20 +111,11 @@ GT_DEV float row_sum16(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false));
   return x;
 }
-// v_permlane16_swap / v_permlane32_swap write BOTH of their VGPR operands. A VALU write to one of those registers
-// issued right behind the swap can be overtaken by the swap's own write-back; the compiler (ROCm 7.2 LLVM) inserts no
-// wait state for it. Two wait states after a swap (group), pinned in place by scheduling barriers.
-GT_DEV void permlane_swap_settle() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 1");
-  __builtin_amdgcn_sched_barrier(0);
-}
 // Sum over the 32 lanes of this half-wave, valid in lanes 0 and 32: row sums, then rows 1/3 brought down to
 // rows 0/2 by v_permlane16_swap
 GT_DEV float half_sum32(float x) {
   const float s = row_sum16(x);
   const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  permlane_swap_settle();   // sw[0] is dead here: its register is the first the compiler reuses
   return s + __uint_as_float(sw[1]);
 }
 

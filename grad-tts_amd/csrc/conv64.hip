@@ -283,7 +283,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           v[8 * pr + q] = __uint_as_float(sw[0]);
           v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
         }
-      permlane_swap_settle();
       const int t = t0 + r;
       const bool valid = t < T;
       const int obyte = valid ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
@@ -299,6 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           o[e] = v[8 * pr + e] + (e < 4 ? b0[e] : b1[e - 4]);
           s += o[e];
           q += o[e] * o[e];
+          asm volatile("" : "+v"(s), "+v"(q));   // scalar chains: see conv.hip (packed-FP32 op_sel hazard)
         }
         const uint4 ov = f_to_item(o, bf16());
         __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
