@@ -210,9 +210,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 pa, pv;
+          typedef float f32x8_t __attribute__((ext_vector_type(8)));
+          f32x8_t fa, fv;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) { pa[i] = (bf16)ak[rb][8 * s + i]; pv[i] = (bf16)av[rb][8 * s + i]; }
+          for (int i = 0; i < 8; ++i) { fa[i] = ak[rb][8 * s + i]; fv[i] = av[rb][8 * s + i]; }
+          const bf16x8 pa = __builtin_convertvector(fa, bf16x8), pv = __builtin_convertvector(fv, bf16x8);   // 4 packed converts each
           ctx = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, pv, ctx, 0, 0, 0);
         }
     } else {

@@ -65,9 +65,12 @@ GT_DEV void item_to_f(const uint4& u, float* f, bf16) {
     f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
   }
 }
+// one v_cvt_pk_bf16_f32 (round to nearest even) for the pair; two scalar (bf16) casts cost four instructions
+// (two half-empty converts, a shift and an or) -- a quarter of the VALU work of some operand transforms
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 GT_DEV uint32_t pack_bf16x2(float lo, float hi) {
-  bf16 a = (bf16)lo, b = (bf16)hi;
-  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 GT_DEV uint4 f_to_item(const float* f, bf16) {
   return make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));

@@ -35,6 +35,10 @@ namespace gt {
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef GT_C64_PF
+#define GT_C64_PF 2   // MFMA steps a fragment read is issued ahead
+#endif
+
 namespace c64 {
 constexpr int TF = 4, TT = 32, PC = TT + 2;               // tile: 4 mel rows x 32 frames; patch rows of 34 positions
 constexpr int POSB = 144;                                 // 128 B of channels + 16 B pad (conflict-free fragments)
@@ -112,7 +116,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   }
   const char* const wlp = sWL + (cb * NCH * 64 + lane) * 16;
-  if (tid < 64) s_bias[tid] = p.bias[tid];
+  f32x16 bias_acc;   // the conv bias in accumulator layout: register q of lane (r, h) is channel cb*32 + acc_row(q, h)
+#pragma unroll
+  for (int q = 0; q < 16; ++q) bias_acc[q] = p.bias[cb * 32 + acc_row(q, h)];
 
   // ---- staging. Item (row i, column c, 8-channel group sub) of patch row i: input frame t0 - 1 + c, mel row
   // given by the caller; out-of-range positions read past the end of the tensor (zeros).
@@ -246,25 +252,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const char* rowp1 = sR + ((sbase + 1) % RING) * ROWB + r * POSB + h * 16;
       const char* rowp2 = sR + ((sbase + 2) % RING) * ROWB + r * POSB + h * 16;
       f32x16 acc;
+      // 36 MFMAs (4 chunks x 9 taps), fragment reads software-pipelined GT_C64_PF steps ahead (issued in the natural
+      // order the compiler waited on each read right before its MFMA); behind each chunk's MFMAs one staging item of
+      // tile k+1's new rows is stored and reloaded for tile k+2 (items spread over the 8 chunk slots of two passes)
+      auto xread = [&](int st) {
+        const int ch = st / 9, tap = st % 9, dr = tap / 3, dc = tap - 3 * dr;
+        const char* rp_ = dr == 0 ? rowp0 : (dr == 1 ? rowp1 : rowp2);
+        return *reinterpret_cast<const bf16x8*>(rp_ + dc * POSB + ch * 32);
+      };
+      auto wread = [&](int st) {
+        const int ch = st / 9, tap = st % 9;
+        return tap < WREG ? wf[ch][tap < WREG ? tap : 0]
+                          : *reinterpret_cast<const bf16x8*>(wlp + (tap - WREG) * WTAP_B + ch * 1024);
+      };
+      constexpr int PF = GT_C64_PF, NB = PF + 1, NST = NCH * 9;
+      bf16x8 xb[NB], wb[NB];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+      for (int st = 0; st < PF; ++st) { xb[st] = xread(st); wb[st] = wread(st); }
 #pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int dr = tap / 3, dc = tap - 3 * dr;
-          const char* rp_ = dr == 0 ? rowp0 : (dr == 1 ? rowp1 : rowp2);
-          const bf16x8 x = *reinterpret_cast<const bf16x8*>(rp_ + dc * POSB + ch * 32);
-          const bf16x8 a = tap < WREG ? wf[ch][tap < WREG ? tap : 0]
-                                      : *reinterpret_cast<const bf16x8*>(wlp + (tap - WREG) * WTAP_B + ch * 1024);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x, acc, 0, 0, 0);
+      for (int st = 0; st < NST; ++st) {
+        if (st + PF < NST) { xb[(st + PF) % NB] = xread(st + PF); wb[(st + PF) % NB] = wread(st + PF); }
+        // the first MFMA of the pass accumulates onto the conv bias (C operand = the bias registers, no epilogue adds)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[st % NB], xb[st % NB], st == 0 ? bias_acc : acc, 0, 0, 0);
+        if (st + PF < NST) {   // pin: the reads of step st + PF ahead of step st's MFMA
+          if ((st + PF) % 9 < WREG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         }
-        // behind this chunk's MFMAs: stage one item of tile k+1's new rows, then load it for tile k+2
-        // (items spread over the 8 chunk slots of the two passes)
-        const int j = ps * NCH + ch;
-        if (j < PPT) {
-          put_new(j, k + 1);
-          issue_new(j, k + 2);
+        if (st % 9 == 8) {
+          const int j = ps * NCH + st / 9;
+          if (j < PPT) {
+            put_new(j, k + 1);
+            issue_new(j, k + 2);
+          }
         }
       }
 
@@ -289,13 +309,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + c0);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + c0 + 4);
         float o[8];
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          o[e] = v[8 * pr + e] + (e < 4 ? b0[e] : b1[e - 4]);
+          o[e] = v[8 * pr + e];
           s += o[e];
           q += o[e] * o[e];
           asm volatile("" : "+v"(s), "+v"(q));   // scalar chains: see conv.hip (packed-FP32 op_sel hazard)
