@@ -37,6 +37,20 @@ template <> GT_DEV float mish_act<bf16>(float x) {
   return x * __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_fmaf(t, t, 1.f)), 1.f);
 }
 
+// Block-conv operand transform of the bf16 / fp8 paths, Mish(GN(h)) + tb (diffusion.py:57-58, 76), in base 2: with the
+// GroupNorm affine's coefficients pre-scaled by log2(e), yl = log2(e) y = fma(h, sc, sh), and
+//   Mish(y) = y (1 - 2 / ((1 + e^y)^2 + 1)) = yl (ln2 - 2 ln2 / ((1 + 2^yl)^2 + 1)),
+// so the whole transform is fma(yl, fma(-2 ln2, rcp((1 + 2^yl)^2 + 1), ln2), tb): five FMA-class ops, one exp2 and
+// one rcp (the mish_act<bf16> form plus the separate affine, time-bias add and log2(e) scaling took eight).
+// 2^yl = inf gives yl ln2 = y (torch's softplus threshold); 2^yl = 0 gives tb.
+constexpr float kLog2e = 1.44269504088896341f, kLn2 = 0.69314718055994531f;
+GT_DEV float gn_mish_tb_l2(float h, float sc_l2, float sh_l2, float tb) {
+  const float yl = __builtin_fmaf(h, sc_l2, sh_l2);
+  const float t = __builtin_amdgcn_exp2f(yl) + 1.f;
+  const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(t, t, 1.f));
+  return __builtin_fmaf(yl, __builtin_fmaf(-2.f * kLn2, r, kLn2), tb);
+}
+
 // ---------------------------------------------------------------- storage
 template <class A> struct Act;
 template <> struct Act<float> {

@@ -65,29 +65,33 @@ struct ConvCfg {
   static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
   static constexpr int PR = (TF - 1) * S + KS;
   static constexpr int PC = (TT - 1) * S + KS;
-  static constexpr int CKB = conv_ckb(sizeof(A) == 2, KIND == CONV1 ? 1 : 9, IN == IN_INPUT ? 3 : 64);
-  static constexpr int SUBS = CKB / 16;
+  // W8 == 2 (A8): fp8 operands on v_mfma_scale_f32_32x32x64_f8f6f4 -- 32-channel chunks of e4m3 activations
+  // (32 B per position in LDS + an E8M0 scale byte in the pad) and the conv_wimga8 weight image
+  static constexpr bool A8 = W8 == 2;
+  static constexpr int CKB = A8 ? 32 : conv_ckb(sizeof(A) == 2, KIND == CONV1 ? 1 : 9, IN == IN_INPUT ? 3 : 64);
+  static constexpr int SUBS = A8 ? 4 : CKB / 16;   // LDS items per position (A8: 8 e4m3 channels = 8 B per item)
   static constexpr int POSB = CKB + 16;
   // weight slab: bf16/fp32 image (wimage.h: half A = taps [0, NA), half B = the rest) or the fp8 image
-  // (conv8_wrow, W8: e4m3 weights, bf16 operands)
+  // (conv8_wrow, W8: e4m3 weights, bf16 operands; conv_wimga8, A8)
   static constexpr int ABF = sizeof(A) == 2 ? 1 : 0;
-  static constexpr int NA = W8 ? NTAP : conv_na(ABF, NTAP);
-  static constexpr int WROW = W8 ? conv8_wrow(NTAP) : conv_wrow(NA, CKB);   // half A rows (all taps if unsplit)
-  static constexpr int WROWB = conv_wrow(NTAP - NA, CKB);
-  static constexpr int HA = W8 ? conv8_wbytes(NT, NTAP) : conv_habytes(ABF, NT, NTAP, CKB);
-  static constexpr int WBYTES = W8 ? HA : HA + conv_hbbytes(ABF, NT, NTAP, CKB);
+  // (A8: NA counts the 32-B tap slots of half A)
+  static constexpr int NA = A8 ? CONVA8_SLOTS_A : W8 ? NTAP : conv_na(ABF, NTAP);
+  static constexpr int WROW = A8 ? CONVA8_WROWA : W8 ? conv8_wrow(NTAP) : conv_wrow(NA, CKB);   // half A rows (all taps if unsplit)
+  static constexpr int WROWB = A8 ? CONVA8_WROWB : conv_wrow(NTAP - NA, CKB);
+  static constexpr int HA = A8 ? round4k(NT * CONVA8_WROWA) : W8 ? conv8_wbytes(NT, NTAP) : conv_habytes(ABF, NT, NTAP, CKB);
+  static constexpr int WBYTES = A8 ? HA + round4k(NT * CONVA8_WROWB) : W8 ? HA : HA + conv_hbbytes(ABF, NT, NTAP, CKB);
   static constexpr int WPIECES_ALL = WBYTES / 1024;        // 1 KiB DMA pieces per chunk
   static constexpr int WPIECES = (WPIECES_ALL + 3) / 4;    // per wave (the last round may be partial)
   // Split pipeline (bf16, multi-tap, operand from an activation): the two halves of chunk c+1 are staged while
   // the other half of chunk c is in the MFMAs. Every wave issues exactly PA / PB DMA pieces per half and PPT
   // patch loads per chunk, so counted vmcnt waits retire exactly the right ones.
-  static constexpr bool SPLIT = !W8 && NA < NTAP && IN != IN_INPUT;
+  static constexpr bool SPLIT = (!W8 && NA < NTAP && IN != IN_INPUT) || A8;
   // 1x1 convs: two weight slabs, chunk c+1's DMA in flight during chunk c's MFMAs (a 1x1 chunk is one tap, too
   // short to hide a weight round trip behind; the slab is 4-8 KB)
   static constexpr bool DBW = !SPLIT && KIND == CONV1;
   static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
-  static constexpr int CK = CKB / (int)sizeof(A);
-  static constexpr int ICH = 16 / (int)sizeof(A);
+  static constexpr int CK = A8 ? 32 : CKB / (int)sizeof(A);   // input channels per chunk
+  static constexpr int ICH = 16 / (int)sizeof(A);            // channels per item (one 16-B global load)
   static constexpr int KSTEP_B = 16 * (int)sizeof(A);
   static constexpr int KSTEPS = CKB / KSTEP_B;
   static constexpr int PITEMS = PR * PC * SUBS;
@@ -109,6 +113,7 @@ struct ConvCfg {
   static_assert(!DBW || WPIECES_ALL % 4 == 0, "counted waits: every wave issues WPIECES weight pieces");
   static_assert(!SPLIT || (HA % 4096 == 0 && (WBYTES - HA) % 4096 == 0 && PB + PPT <= 63), "wave-even halves");
   static_assert(!W8 || (sizeof(A) == 2 && KIND != CONV1), "fp8 weights: bf16 operands, 3x3 / 2x2 convs");
+  static_assert(!A8 || (KIND == CONV3 && IN != IN_INPUT), "fp8 operands: stride-1 3x3 convs over activations");
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -127,7 +132,7 @@ GT_DEV bf16x8 w8_frag(const char* src) {
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 // 64-wide tiles: 3 workgroups per CU (42 KB LDS, <= 168 registers); 128-wide: 2
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 3 : 2))) void conv_kernel(ConvParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 && W8 != 2 ? 3 : 2))) void conv_kernel(ConvParams p) {
   typedef ConvCfg<A, KIND, IN, OUT, NT, W8, TF_> C;
   typedef typename Mma<A>::frag frag;
   constexpr bool CONVT = C::CONVT;
@@ -208,8 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     int q = ok ? ((b * p.Fin + fi) * p.Tin + ti) : npos;
     if (IN == IN_MASK) {
       if (m == 0.f) q = npos;              // x * 0: the range-checked load returns zeros
-      frac |= (m != 0.f && m != 1.f);
     }
+    if (IN == IN_MASK || IN == IN_GN) frac |= (m != 0.f && m != 1.f);
     pidx[j] = q;
     pm[j] = m;
   }
@@ -219,12 +224,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * p.C0 * ES, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.in1 ? p.in1 : p.in0), (short)0, npos * (p.in1 ? p.C1 : p.C0) * ES, 0x00020000);
-  int voff[C::PPT];
-  auto set_offsets = [&](int Cs) {
-#pragma unroll
-    for (int j = 0; j < C::PPT; ++j) voff[j] = pidx[j] * (Cs * ES) + sub * 16;
-  };
-  if (IN != IN_INPUT) set_offsets(p.C0);
+  // byte offset of item j = pidx[j] * pos_bytes + sub * 16, formed per load (one VALU op; no offset registers)
+  int pos_bytes = p.C0 * ES;
+  auto set_offsets = [&](int Cs) { pos_bytes = Cs * ES; };
+  auto voff = [&](int j) { return pidx[j] * pos_bytes + sub * 16; };
 
   u32x4 preg[C::PPT];
   auto load_patch = [&](int c0) {
@@ -241,11 +244,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       }
     } else if (c0 < p.C0) {
 #pragma unroll
-      for (int j = 0; j < C::PPT; ++j) preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs0, voff[j], c0 * ES, 0);
+      for (int j = 0; j < C::PPT; ++j) preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs0, voff(j), c0 * ES, 0);
     } else {
 #pragma unroll
       for (int j = 0; j < C::PPT; ++j)
-        preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, voff[j], (c0 - p.C0) * ES, 0);
+        preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, voff(j), (c0 - p.C0) * ES, 0);
+    }
+  };
+  // A8: one item = 8 channels of a position -> 8 e4m3 bytes, with one E8M0 scale per (position, 32-channel chunk): the
+  // four items of a position sit in lanes 4i..4i+3 (sub = tid & 3), whose |x| maxima meet through two DPP quad swaps.
+  // Scale 2^k with k the least exponent that keeps max|x| / 2^k <= 448 (e4m3's largest finite); an all-zero block
+  // (padding, masked frames) gets 2^0. The conversion divides by the scale (v_cvt_scalef32_pk_fp8_f32, probed).
+  auto store_item_a8 = [&](int it, const float* v, bool zero) {
+    float am = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) am = fmaxf(am, fabsf(v[k]));
+    am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), 0xB1, 0xf, 0xf, false)));   // lane ^ 1
+    am = fmaxf(am, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(am), 0x4E, 0xf, 0xf, false)));   // lane ^ 2
+    const unsigned ab = __float_as_uint(am);
+    int e = (int)(ab >> 23) - 8 + ((ab & 0x7fffffu) > 0x600000u ? 1 : 0);   // max|x| <= 1.75 * 2^(8 + k)
+    e = ab == 0u ? 127 : (e < 1 ? 1 : e);
+    const float sc = __uint_as_float((unsigned)e << 23);
+    typedef short v2s __attribute__((ext_vector_type(2)));
+    unsigned q[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      v2s o = {0, 0};
+      o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[4 * i], v[4 * i + 1], sc, false);
+      o = __builtin_amdgcn_cvt_scalef32_pk_fp8_f32(o, v[4 * i + 2], v[4 * i + 3], sc, true);
+      q[i] = zero ? 0u : __builtin_bit_cast(unsigned, o);
+    }
+    if (it < C::PITEMS) {
+      char* dst = sA + (it / C::SUBS) * C::POSB;
+      *reinterpret_cast<uint2*>(dst + sub * 8) = make_uint2(q[0], q[1]);
+      if (sub == 0) dst[32] = (char)e;
     }
   };
   auto store_patch = [&](int c0) {
@@ -256,6 +288,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
         const int c = c0 + sub * C::ICH + k;
         sc[k] = s_sc[c]; sh[k] = s_sh[c]; tb[k] = s_tb[c];
       }
+    }
+    if constexpr (C::A8) {   // every lane takes part (the scale exchange is a DPP swap)
+#pragma unroll
+      for (int j = 0; j < C::PPT; ++j) {
+        float v[8];
+        item_to_f(make_uint4(preg[j][0], preg[j][1], preg[j][2], preg[j][3]), v, A());
+        if (IN == IN_GN) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = gn_mish_tb_l2(v[k], sc[k], sh[k], tb[k]);
+        }
+        if ((IN == IN_GN || IN == IN_MASK) && frac) {
+          const float m = pm[j];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] *= m;
+        }
+        // IN_GN, masks in {0, 1}: a masked position's bytes are zeroed after the conversion (its scale byte is then
+        // immaterial); IN_MASK's masked positions already loaded as zeros
+        store_item_a8(tid + 256 * j, v, IN == IN_GN && !frac && pm[j] == 0.f);
+      }
+      return;
     }
 #pragma unroll
     for (int j = 0; j < C::PPT; ++j) {
@@ -276,7 +328,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
           for (int k = 0; k < C::ICH; ++k) v[k] = (k < 3 ? f3[k < 3 ? k : 0] : 0.f) * m;
         } else {
           item_to_f(w, v, A());
-          if (IN == IN_GN) {
+          if (IN == IN_GN && sizeof(A) == 2) {   // (Mish(GN(h)) + tb) * m: m in {0, 1} selects the packed item
+#pragma unroll
+            for (int k = 0; k < C::ICH; ++k) v[k] = gn_mish_tb_l2(v[k], sc[k], sh[k], tb[k]);
+            if (frac) {
+#pragma unroll
+              for (int k = 0; k < C::ICH; ++k) v[k] *= m;
+            }
+            const uint4 o = f_to_item(v, A());
+            const bool z = !frac && m == 0.f;
+            *reinterpret_cast<u32x4*>(dst) = u32x4{z ? 0u : o.x, z ? 0u : o.y, z ? 0u : o.z, z ? 0u : o.w};
+            continue;
+          } else if (IN == IN_GN) {
 #pragma unroll
             for (int k = 0; k < C::ICH; ++k)   // (Mish(GN(h)) * m + tb) * m, m in {0,1}
               v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) + tb[k]) * m;
@@ -324,10 +387,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
     if (IN == IN_GN) gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
     else gn_finish(gl, p.pre_part, p.pre_nparts, b, p.pre_count, s_mean, s_rstd, s_red);
     // per-channel GroupNorm scale/shift (and time bias) of the INPUT (IN_GN) / OUTPUT (OUT_RBOUT) channels
-    if (IN == IN_GN && tid < p.Cin) {
+    if (IN == IN_GN && tid < p.Cin) {   // bf16 / fp8 operands: the affine in base 2 (gn_mish_tb_l2)
       const int g = tid / (p.Cin >> 3);
       const float sc = c_g * s_rstd[g];
-      s_sc[tid] = sc; s_sh[tid] = c_b - s_mean[g] * sc; s_tb[tid] = c_t;
+      const float l2 = sizeof(A) == 2 ? kLog2e : 1.f;
+      s_sc[tid] = sc * l2; s_sh[tid] = (c_b - s_mean[g] * sc) * l2; s_tb[tid] = c_t;
     }
     if (OUT == OUT_RBOUT && tid < NT) {
       const int g = (cout0 + tid) / (p.Cout >> 3);
@@ -400,6 +464,92 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       }
     }
   };
+  // A8 MFMAs of the staged chunk: K = 64 per v_mfma_scale_f32_32x32x64_f8f6f4 = two taps x 32 channels. Lane (., h) of
+  // both operands holds channels 16h..16h+15 of tap t in bytes 0..15 and of tap t' in bytes 16..31, so the patch
+  // operand's scale block 0 (bytes 0..15 of both lane halves) is tap t's 32 channels of one position and block 1 tap
+  // t''s: lane (c, 0) supplies the E8M0 scale of column c's tap-t position, lane (c, 1) that of its tap-t' position
+  // (the probed operand semantics, tools/micro/mfma_scale_probe.hip). Taps go in pairs (0,1) (2,3) (4,5) (6,7) (8,9):
+  // slot 9 of the weight image is zero and its patch half re-reads tap 8's position.
+  typedef int v8i_t __attribute__((ext_vector_type(8)));
+  struct FragP { v8i_t v; int s; };
+  int scale_one = 127;                  // weight operand: E8M0 1.0 (its per-channel fp32 scale is applied in the epilogue)
+  if constexpr (C::A8) asm volatile("" : "+v"(scale_one));   // held in a VGPR, as the scale operands are read per lane
+  const int a8_base = ((wm / C::RBT) * C::PC + (wm % C::RBT) * 32 + r) * C::POSB;   // (stride 1, not transposed)
+  // scale byte of lane h = 1: tap t + 1 = the next column, except pair (2, 3) (tap 3 opens the next row) and pair 4
+  const int a8_sc1 = a8_base + 32 + (h ? C::POSB : 0), a8_sc2 = a8_base + 32 + (h ? (C::PC - 2) * C::POSB : 0),
+            a8_sc4 = a8_base + 32;
+  auto a8_off = [&](int tap, int rb) {
+    tap = tap > 8 ? 8 : tap;
+    return ((rb * (C::WM / C::RBT) + tap / 3) * C::PC + tap % 3) * C::POSB;
+  };
+  auto load_pa8 = [&](int pr, int rb) {
+    const char* base = sA + a8_base + h * 16;
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(base + a8_off(2 * pr, rb));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(base + a8_off(2 * pr + 1, rb));
+    FragP f;
+    f.v = v8i_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+    const int sb = pr == 1 ? a8_sc2 : pr == 4 ? a8_sc4 : a8_sc1;
+    f.s = *reinterpret_cast<const unsigned char*>(sA + sb + a8_off(2 * pr, rb));
+    return f;
+  };
+  auto load_wa8 = [&](int pr, int cb) {   // pairs 0-2 in half A, 3-4 in half B
+    const int row = wn * 64 + cb * 32 + r;
+    const char* base = pr < 3 ? wcur + row * C::WROW + h * 16 + pr * 64
+                              : wcur + C::HA + row * C::WROWB + h * 16 + (pr - 3) * 64;
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(base);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(base + 32);
+    return v8i_t{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto mma_a8 = [&](auto P0, auto P1) {   // pairs [P0, P1): compile-time (std::integral_constant), so every index folds
+    constexpr int RB = C::RBW, p0 = decltype(P0)::value, NP = decltype(P1)::value - p0;
+    // weight fragments double-buffered (the next pair's read one step ahead) when the registers allow; 128-wide tiles
+    // (4 row blocks, 128 accumulator VGPRs) read them after the pair's last MFMAs instead
+    constexpr bool WDB = RB < 4;
+    FragP fa[2];
+    v8i_t fb[WDB ? 2 : 1][2];
+    fa[0] = load_pa8(p0, 0);
+    fb[0][0] = load_wa8(p0, 0);
+    fb[0][1] = load_wa8(p0, 1);
+    __builtin_amdgcn_sched_group_barrier(0x100, 7, 0);   // LDS reads of the first step
+#pragma unroll
+    for (int i = 0; i < NP * RB; ++i) {
+      const int u = i / RB, rb = i % RB;
+      const int n = i + 1, un = n / RB, rbn = n % RB;
+      const int wb = WDB ? (u & 1) : 0;
+      if (un < NP) {                                    // step i+1's fragments ahead of step i's MFMAs
+        if (WDB && rbn == 0) {
+          fb[un & 1][0] = load_wa8(p0 + un, 0);
+          fb[un & 1][1] = load_wa8(p0 + un, 1);
+        }
+        fa[n & 1] = load_pa8(p0 + un, rbn);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+        acc[rb][cb] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fb[wb][cb], fa[i & 1].v, acc[rb][cb], 0, 0, 0,
+                                                                      scale_one, 0, fa[i & 1].s);
+      // pin the order (the scheduler otherwise hoists every fragment read of the call ahead of the MFMAs)
+      if constexpr (WDB) {
+        if (un < NP && rbn == 0) __builtin_amdgcn_sched_group_barrier(0x100, 7, 0);
+        if (un < NP && rbn != 0) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      } else {
+        if (un < NP) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        if (un < NP && rbn == 0) {                      // the pair's last MFMAs issued: its weights are free
+          fb[0][0] = load_wa8(p0 + un, 0);
+          fb[0][1] = load_wa8(p0 + un, 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        }
+      }
+    }
+    // Keep this call's MFMAs ahead of the barrier that follows it: MFMAs touch no memory, so the compiler otherwise
+    // sinks the half-A MFMAs below the next barrier and the half-B DMA, next to half B's -- every fragment of the
+    // chunk live at once (256 VGPRs, 200-490 spilled).
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) asm volatile("" : "+v"(acc[rb][cb]));
+  };
   // patch loads of chunk k (channels k*CK..): switch to the second tensor's offsets at the concat boundary
   auto issue_patch = [&](int k) {
     const int ck0 = k * C::CK;
@@ -432,12 +582,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 ? 
       if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PB + C::PPT) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PB) : "memory");
       cta_sync();                                      // A(ch) landed for every wave; patch(ch) stores visible
-      mma_taps(0, C::NA);
+      if constexpr (C::A8) mma_a8(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+      else mma_taps(0, C::NA);
       if (more) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::PPT) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       cta_sync();                                      // B(ch) landed; every wave is done with half A
       if (more) dma_half(ch + 1, 0);
-      mma_taps(C::NA, C::NTAP);
+      if constexpr (C::A8) mma_a8(std::integral_constant<int, 3>{}, std::integral_constant<int, 5>{});
+      else mma_taps(C::NA, C::NTAP);
       if (more) {
         cta_sync();                                    // half B and the patch are free
         store_patch((ch + 1) * C::CK);
@@ -644,7 +796,7 @@ template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
   if constexpr (sizeof(A) == 2)
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
-  if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT)
+  if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT && W8 != 2)   // (A8: 4-row tiles)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
@@ -709,16 +861,28 @@ static hipError_t dispatch_w8(ConvKind kind, InMode im, OutMode om, const ConvPa
   if (kind == CONVT4 && im == IN_MASK && om == OUT_PLAIN) return launch_ct<bf16, NT, 1>(p, s);
   return hipErrorNotSupported;
 }
+// fp8-operand instantiations (GT_FP8, conv_wimga8 images): the stride-1 3x3 convs over activations
+template <int NT>
+static hipError_t dispatch_a8(ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
+  if (kind == CONV3 && om == OUT_STATS) {
+    if (im == IN_MASK) return launch_c3<bf16, IN_MASK, NT, 2>(p, s);
+    if (im == IN_GN) return launch_c3<bf16, IN_GN, NT, 2>(p, s);
+    if (im == IN_PLAIN) return launch_c3<bf16, IN_PLAIN, NT, 2>(p, s);
+  }
+  return hipErrorNotSupported;
+}
 
-int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small) {   // CONV3 tiles: TF rows x 64 frames x NT
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small, int a8) {   // CONV3: TF rows x 64 frames x NT
   const int nt = conv_nt(act_bf16, Cout);
-  return (F / conv_tf(CONV3, im, nt, Cout, F, small)) * ((T + 63) / 64) * (Cout / nt);
+  const int tf = (a8 && !small) ? 4 : conv_tf(CONV3, im, nt, Cout, F, small);   // launch_c3: A8 never takes 5-row tiles
+  return (F / tf) * ((T + 63) / 64) * (Cout / nt);
 }
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s) {
   if (p.small && !act_bf16) return hipErrorNotSupported;   // small-batch plan: bf16 weights and activations only
   if (p.wscale) {   // fp8 weight image
     if (!act_bf16) return hipErrorNotSupported;
+    if (p.a8) return conv_nt(1, p.Cout) == 128 ? dispatch_a8<128>(kind, im, om, p, s) : dispatch_a8<64>(kind, im, om, p, s);
     return conv_nt(1, p.Cout) == 128 ? dispatch_w8<128>(kind, im, om, p, s) : dispatch_w8<64>(kind, im, om, p, s);
   }
   if (!act_bf16) return dispatch<float, 64>(kind, im, om, p, s);

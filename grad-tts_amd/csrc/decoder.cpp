@@ -149,11 +149,12 @@ struct gt_decoder {
   std::map<std::string, int> index;
   std::vector<std::vector<float>> host;
   std::vector<bool> set;
-  // one packed device arena per compute dtype code (GT_F32, GT_BF16, GT_BF16_W8)
-  bool dirty[3] = {true, true, true};
-  void* arena[3] = {nullptr, nullptr, nullptr};
-  std::map<std::string, void*> dp[3];
-  std::map<std::string, int> cinpad[3];
+  // one packed device arena per compute dtype code (GT_F32, GT_BF16, GT_BF16_W8, GT_FP8)
+  static constexpr int kCodes = 4;
+  bool dirty[kCodes] = {true, true, true, true};
+  void* arena[kCodes] = {nullptr, nullptr, nullptr, nullptr};
+  std::map<std::string, void*> dp[kCodes];
+  std::map<std::string, int> cinpad[kCodes];
   float freqs[32];
   int64_t packs = 0;          // weight packings performed (checkpoint tests: exactly one per parameter change)
   // profiling (diagnostics / bench roofline): HIP events around every launch
@@ -290,7 +291,7 @@ namespace {
 
 // fp8 image (wimage.h conv_wimg8) of a 3x3 [Cout][Cin][3][3] or ConvTranspose [Cin][Cout][4][4] weight,
 // quantized per output channel; the scales go to key + ".s"
-void pack_conv8(Blob& blob, gt_decoder* d, const std::string& key, const std::vector<float>& w,
+void pack_conv8(Blob& blob, gt_decoder* d, int code, const std::string& key, const std::vector<float>& w,
                 const std::vector<int64_t>& shp, bool convT) {
   int cin, cout, ntap, npar;
   if (!convT) {
@@ -333,7 +334,27 @@ void pack_conv8(Blob& blob, gt_decoder* d, const std::string& key, const std::ve
   }
   blob.put(key, img.data(), img.size());
   blob.put(key + ".s", sc.data(), sc.size() * 4);
-  d->cinpad[2][key] = W.nchunk * W.ck;
+  d->cinpad[code][key] = W.nchunk * W.ck;
+}
+
+// fp8-operand image (wimage.h conv_wimga8, GT_FP8) of a 3x3 [Cout][Cin][3][3] weight, quantized per output channel as
+// pack_conv8 does; scales to key + ".s", and key + ".a8" marks the image kind for the launch (Run::setw)
+void pack_conva8(Blob& blob, gt_decoder* d, int code, const std::string& key, const std::vector<float>& w,
+                 const std::vector<int64_t>& shp) {
+  const int cout = (int)shp[0], cin = (int)shp[1];
+  std::vector<uint8_t> q(w.size());
+  std::vector<float> sc(cout);
+  gt_quantize_e4m3(w.data(), cout, (int64_t)cin * 9, (int64_t)cin * 9, 1, q.data(), sc.data());
+  const WImg W = conv_wimga8(cin, cout);
+  std::vector<uint8_t> img((size_t)W.total, 0);   // tap slot 9 and the row pads stay zero
+  for (int co = 0; co < cout; ++co)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int t = 0; t < 9; ++t) img[conv_wimga8_off(W, co, t, ci)] = q[((size_t)co * cin + ci) * 9 + t];
+  blob.put(key, img.data(), img.size());
+  blob.put(key + ".s", sc.data(), sc.size() * 4);
+  const int one = 1;
+  blob.put(key + ".a8", &one, sizeof(one));
+  d->cinpad[code][key] = W.nchunk * W.ck;
 }
 
 // pack a 64->64 3x3 [Cout][Cin][3][3] weight in conv64's register-fragment order (conv64.hip), bf16:
@@ -364,7 +385,8 @@ static bool conv64_enabled() {
 int prepare(gt_decoder* d, int code) {
   if (!d->dirty[code]) return GT_OK;
   const int dt = code ? 1 : 0;          // activation dtype: fp32 / bf16
-  const bool w8 = code == GT_BF16_W8;   // fp8 images for the 3x3 / stride-2 / transposed convs
+  const bool w8 = code == GT_BF16_W8 || code == GT_FP8;   // fp8 images for the 3x3 / stride-2 / transposed convs
+  const bool a8 = code == GT_FP8;   // ... fp8 operands too for the 3x3 convs over activations (Cin >= 32)
   for (size_t i = 0; i < d->inv.size(); ++i)
     if (!d->set[i]) return fail(GT_ERR_PARAM, "parameter never set: " + d->inv[i].name);
   Blob blob;
@@ -373,10 +395,12 @@ int prepare(gt_decoder* d, int code) {
     const std::string& k = d->inv[i].name;
     const auto& shp = d->inv[i].dims;
     const auto& w = d->host[i];
-    if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
-      pack_conv8(blob, d, k, w, shp, false);
+    if (a8 && ends_with(k, ".block.0.weight") && shp[1] >= 32) {
+      pack_conva8(blob, d, code, k, w, shp);
+    } else if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
+      pack_conv8(blob, d, code, k, w, shp, false);
     } else if (w8 && starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
-      pack_conv8(blob, d, k, w, shp, true);
+      pack_conv8(blob, d, code, k, w, shp, true);
     } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
@@ -466,7 +490,8 @@ int max_gn_parts(int dt, int64_t T) {
       m = std::max(m, conv64_nparts(80 >> l, (int)(T >> l), small));
       for (int cout : {64, 128, 256})
         for (int im : {IN_INPUT, IN_MASK, IN_GN, IN_PLAIN})
-          m = std::max(m, conv_gn_nparts(dt, (InMode)im, 80 >> l, (int)(T >> l), cout, small));
+          for (int a8 = 0; a8 <= dt; ++a8)   // fp8-operand convs (GT_FP8) tile differently
+            m = std::max(m, conv_gn_nparts(dt, (InMode)im, 80 >> l, (int)(T >> l), cout, small, a8));
     }
   return m;
 }
@@ -502,7 +527,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
 struct Run {
   gt_decoder* d;
   int dt;       // activation dtype: 0 fp32, 1 bf16
-  int wi;       // compute dtype code (GT_F32 / GT_BF16 / GT_BF16_W8) = packed arena index
+  int wi;       // compute dtype code (GT_F32 / GT_BF16 / GT_BF16_W8 / GT_FP8) = packed arena index
   int B, T;
   hipStream_t s;
   uint8_t* ws;
@@ -542,10 +567,10 @@ struct Run {
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
     // "<instantiation as rocprof names it>@<shape>": bench.py aggregates per instantiation
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
-    const int tf = dt ? conv_tf(kind, im, nt, p.Cout, p.Fout, p.small) : 4;
+    const int tf = (dt && !(p.a8 && !p.small)) ? conv_tf(kind, im, nt, p.Cout, p.Fout, p.small) : 4;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
-                             (p.wscale ? ",w8" : "") + (tf != 4 ? ",tf" + std::to_string(tf) : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
+                             (p.a8 ? ",a8" : p.wscale ? ",w8" : "") + (tf != 4 ? ",tf" + std::to_string(tf) : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout);
     timed(name, flop, bytes, [&] { return launch_conv(dt, kind, im, om, p, s); });
   }
 
@@ -562,7 +587,7 @@ struct Run {
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
       return np;
     }
-    const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small);
+    const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
     if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
     conv(CONV3, im, OUT_STATS, p);
     return np;
@@ -587,11 +612,12 @@ struct Run {
 
   void* W(const std::string& k) { return d->dp[wi].at(k); }
   const float* Fp(const std::string& k) { return (const float*)d->dp[wi].at(k); }
-  // weight image of a conv: its fp8 scales too when the image is fp8 (GT_BF16_W8)
+  // weight image of a conv: its fp8 scales too when the image is fp8 (GT_BF16_W8, GT_FP8), and the fp8-operand flag
   void setw(ConvParams& p, const std::string& k) {
     p.w = W(k);
     const auto it = d->dp[wi].find(k + ".s");
     p.wscale = it != d->dp[wi].end() ? (const float*)it->second : nullptr;
+    p.a8 = d->dp[wi].count(k + ".a8") ? 1 : 0;
   }
   void* act(int l, int i) { return ws + L.act[l][i]; }
   float* stats() { return (float*)(ws + L.stats) + (size_t)(stat_slot++) * B * L.pmax * 16; }
@@ -823,7 +849,7 @@ struct Run {
 // for any B on either side of the threshold); the two plans partition the GroupNorm partial sums differently, so
 // results across plans agree to fp32 rounding of those sums (GPU test: plan agreement within the bf16 gate).
 int small_plan(const gt_decoder* d, int dtype, int64_t nb) {
-  return ((dtype == GT_BF16 || dtype == GT_BF16_W8) && nb <= d->small_b) ? 1 : 0;
+  return ((dtype == GT_BF16 || dtype == GT_BF16_W8 || dtype == GT_FP8) && nb <= d->small_b) ? 1 : 0;
 }
 
 uint8_t* align_ws(void* ws) { return (uint8_t*)(((uintptr_t)ws + 255) & ~(uintptr_t)255); }
@@ -842,8 +868,8 @@ int64_t chunk_b(const gt_decoder* d, int dt, int64_t B, int64_t T) {
 
 int check_common(gt_decoder* d, int dtype, int64_t B, int64_t T, void* ws, size_t ws_bytes, int32_t N) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
-  if (dtype != GT_F32 && dtype != GT_BF16 && dtype != GT_BF16_W8)
-    return fail(GT_ERR_ARG, "dtype must be GT_F32, GT_BF16 or GT_BF16_W8");
+  if (dtype != GT_F32 && dtype != GT_BF16 && dtype != GT_BF16_W8 && dtype != GT_FP8)
+    return fail(GT_ERR_ARG, "dtype must be GT_F32, GT_BF16, GT_BF16_W8 or GT_FP8");
   if (B <= 0 || T <= 0) return fail(GT_ERR_ARG, "B and T must be positive");
   if (T % 4 != 0) return fail(GT_ERR_ARG, "T must be a multiple of 4 (fix_len_compatibility)");
   if (B > 65535 || T > (1 << 20)) return fail(GT_ERR_UNSUPPORTED, "B or T too large");
@@ -891,7 +917,7 @@ void gt_decoder_destroy(gt_decoder* d) {
   if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
   if (d->raw) (void)hipFree(d->raw);
   for (auto e : d->pool) (void)hipEventDestroy(e);
-  for (int i = 0; i < 3; ++i)
+  for (int i = 0; i < gt_decoder::kCodes; ++i)
     if (d->arena[i]) (void)hipFree(d->arena[i]);
   delete d;
 }
@@ -952,7 +978,7 @@ int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int
   if (numel != sh.numel()) return fail(GT_ERR_PARAM, std::string("numel mismatch for ") + name);
   d->host[it->second].assign(data, data + numel);
   d->set[it->second] = true;
-  d->dirty[0] = d->dirty[1] = d->dirty[2] = true;
+  for (bool& x : d->dirty) x = true;
   d->raw_dirty = true;
   return GT_OK;
 }

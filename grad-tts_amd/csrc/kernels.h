@@ -36,6 +36,7 @@ struct ConvParams {
   // ---- weights
   const void* w; long w_bstride;                      // packed weight image (wimage.h); per-batch stride in BYTES
   const float* wscale;                                // non-null: fp8 e4m3 image (conv_wimg8), per-Cout scale
+  int a8;                                             // with wscale: fp8 operands too (conv_wimga8 image, CONV3)
   const float* bias;                                  // [Cout]
   // ---- output
   void* out; float* out_part;                         // OUT_STATS: GroupNorm partials of the output (common.h)
@@ -45,7 +46,7 @@ struct ConvParams {
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid
-int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small);
+int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small, int a8 = 0);
 
 struct AttnKVParams {
   const void* x; int B, n, C, Cpad;   // x: [B][n][C] (n = F*T)

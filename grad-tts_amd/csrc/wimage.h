@@ -150,4 +150,35 @@ inline __host__ __device__ long conv_wimg8_off(const WImg& w, int co, int tap, i
   return ((long)tile * w.nchunk + ch) * w.wbytes + (long)n * w.wrowa + unit * 8 + (k & 7);
 }
 
+// ---- fp8 weight image for fp8 ACTIVATIONS too (GT_FP8: v_mfma_scale_f32_32x32x64_f8f6f4) of the stride-1 3x3 convs
+// over activations. Chunks of 32 input channels (one E8M0 scale block of the operand); 10 tap slots of 32 B (channels
+// 0..31 of the chunk; slot 9 is zero: the K = 64 MFMA takes the taps in pairs (0,1) (2,3) (4,5) (6,7) (8,9)), split
+// like the bf16 images into half A = slots 0..5 (pairs 0-2) and half B = slots 6..9 (pairs 3-4), each row padded by
+// 16 B to an odd number of 16-B slots (208 / 144 B: conflict-free ds_read_b128 fragments) and each half to whole
+// 4 KiB (wave-even DMA pieces): conv_kernel stages one half of chunk c+1 while the other half of chunk c is in the
+// MFMAs. NT = 128: 28 + 20 KiB, NT = 64: 16 + 12 KiB.
+constexpr int CONVA8_SLOTS_A = 6, CONVA8_WROWA = CONVA8_SLOTS_A * 32 + 16, CONVA8_WROWB = (10 - CONVA8_SLOTS_A) * 32 + 16;
+inline __host__ __device__ WImg conv_wimga8(int cin, int cout) {
+  WImg w;
+  w.nt = conv_nt(1, cout);
+  w.ckb = 32;
+  w.ck = 32;
+  w.ntap = 9;
+  w.na = CONVA8_SLOTS_A;
+  w.wrowa = CONVA8_WROWA;
+  w.wrowb = CONVA8_WROWB;
+  w.habytes = round4k(w.nt * CONVA8_WROWA);
+  w.wbytes = w.habytes + round4k(w.nt * CONVA8_WROWB);
+  w.nchunk = (cin + w.ck - 1) / w.ck;
+  w.nntile = (cout + w.nt - 1) / w.nt;
+  w.total = (long)w.nntile * w.nchunk * w.wbytes;
+  return w;
+}
+inline __host__ __device__ long conv_wimga8_off(const WImg& w, int co, int tap, int ci) {
+  const int tile = co / w.nt, n = co - tile * w.nt;
+  const long base = ((long)tile * w.nchunk + ci / 32) * w.wbytes + (ci & 31);
+  if (tap < w.na) return base + (long)n * w.wrowa + tap * 32;
+  return base + w.habytes + (long)n * w.wrowb + (tap - w.na) * 32;
+}
+
 }  // namespace gt

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GRADTTS_LIB", os.path.join(_HERE, "libgradtts.so"))
 
 GT_OK, GT_ERR_ARG, GT_ERR_HIP, GT_ERR_PARAM, GT_ERR_UNSUPPORTED, GT_ERR_WORKSPACE = range(6)
-GT_F32, GT_BF16, GT_BF16_W8 = 0, 1, 2
+GT_F32, GT_BF16, GT_BF16_W8, GT_FP8 = 0, 1, 2, 3
 
 # (name, restype, argtypes) for every symbol declared in include/gradtts.h
 _c = ctypes

@@ -12,8 +12,10 @@ Mirrors ``/root/reference/model/diffusion.py``:
 The sub-modules are parameter containers only: the whole U-Net (and the whole N-step sampler) runs
 inside the HIP library; there is no PyTorch compute path. Compute dtype is an extension:
 ``compute_dtype=torch.float32`` (parity path, default), ``torch.bfloat16`` (throughput path; fp32
-accumulation, fp32 sampler state) or ``"bf16_w8"`` (bf16 activations, fp8 e4m3 weights for the 3x3 /
-Downsample / Upsample convs with per-output-channel scales: BASELINE.json config 5).
+accumulation, fp32 sampler state), ``"bf16_w8"`` (bf16 activations, fp8 e4m3 weights for the 3x3 /
+Downsample / Upsample convs with per-output-channel scales: BASELINE.json config 5) or ``"fp8"`` (as
+``"bf16_w8"``, and the 3x3 convs over activations on the block-scaled fp8 MFMA: e4m3 operands with one
+power-of-two scale per position and 32 channels, include/gradtts.h GT_FP8).
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import GT_BF16, GT_BF16_W8, GT_F32, check, lib, ops
+from ._lib import GT_BF16, GT_BF16_W8, GT_F32, GT_FP8, check, lib, ops
 
 
 class _ParamOnly(torch.nn.Module):
@@ -97,9 +99,11 @@ def _dtype_code(dt):
         return GT_F32
     if dt in (torch.bfloat16, "bf16", "bfloat16", GT_BF16):
         return GT_BF16
-    if dt in ("bf16_w8", "fp8", GT_BF16_W8):
+    if dt in ("bf16_w8", GT_BF16_W8):
         return GT_BF16_W8
-    raise ValueError(f"compute_dtype must be float32, bfloat16 or 'bf16_w8', got {dt}")
+    if dt in ("fp8", GT_FP8):
+        return GT_FP8
+    raise ValueError(f"compute_dtype must be float32, bfloat16, 'bf16_w8' or 'fp8', got {dt}")
 
 
 def _stream_ptr(device):

@@ -40,8 +40,11 @@ enum {
  * GT_BF16_W8: bf16 activations with fp8 (OCP e4m3) weights for every 3x3 conv, Downsample and
  * Upsample (ConvTranspose) -- 90 % of the U-Net's parameters -- quantized per output channel by
  * gt_quantize_e4m3 when the weights are packed; 1x1, attention and linear weights stay bf16 / fp32
- * (BASELINE.json config 5). */
-enum { GT_F32 = 0, GT_BF16 = 1, GT_BF16_W8 = 2 };
+ * (BASELINE.json config 5).
+ * GT_FP8: as GT_BF16_W8, and the stride-1 3x3 convs over activations (every Block conv but the U-Net input's) run
+ * on the block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4): their inputs are quantized to e4m3 in the
+ * conv's operand load with one power-of-two (E8M0) scale per position and 32-channel block. */
+enum { GT_F32 = 0, GT_BF16 = 1, GT_BF16_W8 = 2, GT_FP8 = 3 };
 
 typedef struct gt_decoder gt_decoder;
 

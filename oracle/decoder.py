@@ -41,9 +41,17 @@ def linear(p, key, x):
     return F.linear(x, p[key + ".weight"], p[key + ".bias"])
 
 
+# GT_FP8 emulation (not in the reference): when set by fp8_activations(), the input of every 3x3 Block conv with at
+# least 32 input channels is quantized by quantize_act_e4m3 before the conv (what csrc/conv.hip's A8 operand load does)
+_ACT_Q = None
+
+
 def block(p, key, x, mask, taps=None, tap_name=None):
     """``Block`` diffusion.py:49-58: Mish(GN8(conv3x3(x*mask))) * mask."""
-    y = F.conv2d(x * mask, p[key + ".block.0.weight"], p[key + ".block.0.bias"], padding=1)
+    xin = x * mask
+    if _ACT_Q is not None and xin.shape[1] >= 32:
+        xin = _ACT_Q(xin)
+    y = F.conv2d(xin, p[key + ".block.0.weight"], p[key + ".block.0.bias"], padding=1)
     if taps is not None and tap_name:
         taps[tap_name] = y
     y = F.group_norm(y, GROUPS, p[key + ".block.1.weight"], p[key + ".block.1.bias"], eps=1e-5)
@@ -273,3 +281,30 @@ def fp8_params(sd):
             v = dequantize_e4m3(q, s, ax)
         out[k] = v
     return out
+
+
+def quantize_act_e4m3(x, block=32):
+    """GT_FP8 conv-operand quantization (csrc/conv.hip store_item_a8): x [B, C, F, T] -> e4m3 values with one
+    power-of-two scale 2^k per (utterance, position, block of 32 channels); k is the least integer with
+    max|x| / 2^k <= 448 (clamped at -126; an all-zero block stays zero), q = (x / 2^k).to(float8_e4m3fn) * 2^k."""
+    B, C, H, W = x.shape
+    g = x.reshape(B, C // block, block, H, W)
+    amax = g.abs().amax(dim=2, keepdim=True)
+    m, e = torch.frexp(amax)                      # amax = m 2^e, m in [0.5, 1): 2m 2^(e-1), 2m in [1, 2)
+    k = torch.where(2 * m > 1.75, e - 8, e - 9).clamp(min=-126)
+    s = torch.ldexp(torch.ones_like(amax), k)
+    return ((g / s).to(torch.float8_e4m3fn).to(x.dtype) * s).reshape(x.shape)
+
+
+class fp8_activations:
+    """Context: the oracle's Block convs see GT_FP8's quantized operands (use with fp8_params weights)."""
+
+    def __enter__(self):
+        global _ACT_Q
+        self.prev, _ACT_Q = _ACT_Q, quantize_act_e4m3
+        return self
+
+    def __exit__(self, *exc):
+        global _ACT_Q
+        _ACT_Q = self.prev
+        return False

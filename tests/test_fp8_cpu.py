@@ -71,3 +71,26 @@ def test_fp8_params_error_envelope():
         assert bool((err <= bound).all()), k
     q, s = odec.quantize_e4m3(torch.zeros(2, 3, 3, 3), 0)
     assert torch.equal(s, torch.ones(2)) and int(q.sum()) == 0
+
+
+def test_activation_quantizer_of_the_fp8_operand_mode():
+    """oracle.decoder.quantize_act_e4m3 (GT_FP8's conv-operand quantization, csrc/conv.hip store_item_a8): one
+    power-of-two scale 2^k per (utterance, position, 32 channels) with k the least integer keeping max|x| / 2^k <= 448;
+    values already on that grid are unchanged, an all-zero block stays zero, the error is at most half an e4m3 step."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 64, 3, 7, generator=g) * torch.logspace(-6, 6, 7)      # a wide range of magnitudes per column
+    x[0, 32:, 1, 2] = 0
+    q = odec.quantize_act_e4m3(x)
+    blocks = x.reshape(2, 2, 32, 3, 7)
+    amax = blocks.abs().amax(2, keepdim=True)
+    k = torch.ceil(torch.log2(amax / 448.0)).clamp(min=-126)
+    s = torch.exp2(k)
+    assert bool(((amax / s) <= 448).all()) and bool(((amax / s)[amax > 0] > 224).all())   # the least such k
+    err = (q - x).reshape(blocks.shape).abs()
+    assert bool((err <= torch.maximum(blocks.abs() * 2.0 ** -4, s * 2.0 ** -10) * (1 + 1e-6)).all())
+    assert bool((q[0, 32:, 1, 2] == 0).all())
+    on_grid = torch.tensor([448.0, -1.75, 0.5, 2.0 ** -6] + [0.0] * 28).reshape(1, 32, 1, 1) * 2.0 ** 10
+    assert torch.equal(odec.quantize_act_e4m3(on_grid), on_grid)
+    with odec.fp8_activations():   # the context only switches the Block-conv hook on, and restores it
+        assert odec._ACT_Q is odec.quantize_act_e4m3
+    assert odec._ACT_Q is None

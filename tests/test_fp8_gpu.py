@@ -1,0 +1,173 @@
+"""GT_FP8 (compute_dtype "fp8"): fp8 e4m3 weights AND fp8 operands on the block-scaled MFMA
+(v_mfma_scale_f32_32x32x64_f8f6f4) for the stride-1 3x3 convs over activations; BASELINE.json config 5.
+
+The oracle of this mode is the reference algorithm with the dequantized fp8 weights (oracle.decoder.fp8_params) and
+every such conv's input quantized as the library does it (oracle.decoder.fp8_activations: e4m3 with one power-of-two
+scale per position and 32 channels). Two kinds of checks:
+
+* layer parity on identical inputs: a conv whose operand load is a plain mask (block1 of a ResnetBlock, incl. the
+  up path's two-tensor concat) reads a bf16 activation the GPU stored; the oracle quantizes exactly that tensor, so the
+  quantization decisions are identical and the only differences are fp32 summation order and the bf16 rounding of
+  the stored conv output: gate 1.05 x 2^-8 of max|ref| (bf16's half-ulp is 2^-8 of a value in [2^e, 2^(e+1)), so at
+  most 2^-8 of max|ref|; 5 % for the summation order). A wrong operand layout, scale block or tap pairing shows up as
+  an O(1) error here (measured: 2.2-3.3e-3);
+* end to end: one estimator call cannot be pinned tighter than the quantization's own effect -- GPU and oracle see
+  inputs that differ by bf16 rounding, and every e4m3 rounding decision that flips moves an operand by 2^-4 of
+  itself -- so the gates are relative to that effect: the GPU's distance to the fp8 oracle must stay below the fp8
+  oracle's distance to the fp32 reference, and the GPU's distance to fp32 within 1.3x of it.
+Every check prints its achieved error (PARITY lines).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import gpu_available, load_golden
+from gpu_util import make_decoder, probe, rel_err, report
+
+pytestmark = pytest.mark.gpu
+
+FP8 = "fp8"
+LAYER_TOL = 1.05 * 2.0 ** -8
+EST = ["estimator_s1.npz", "estimator_s247.npz", "estimator_sm1.npz", "estimator_s1_T132.npz", "estimator_s1_T20.npz"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _stage(dec, args, name, shape):
+    _, pr = probe(dec.estimator, FP8, *args, None, name, shape)
+    return pr.cpu()
+
+
+# (input stages concatenated on channels, conv output stage, U-Net level, Cin, Cout)
+MASK_LAYERS = [
+    (["downs.0.0"], "downs.0.1.pre1", 0, 64, 64),
+    (["downs.0.3"], "downs.1.0.pre1", 1, 64, 128),
+    (["downs.1.0"], "downs.1.1.pre1", 1, 128, 128),
+    (["downs.1.3"], "downs.2.0.pre1", 2, 128, 256),
+    (["mid_block2", "downs.2.2"], "ups.0.0.pre1", 2, 512, 128),
+    (["ups.0.3", "downs.1.2"], "ups.1.0.pre1", 1, 256, 64),
+]
+
+
+@pytest.mark.parametrize("ins,out,lvl,cin,cout", MASK_LAYERS, ids=[m[1] for m in MASK_LAYERS])
+def test_fp8_mask_conv_matches_oracle_on_identical_inputs(ins, out, lvl, cin, cout):
+    from oracle import decoder as odec
+    g = load_golden("estimator_s1_T132.npz")
+    dec, sd = make_decoder(1, 0, FP8)
+    args = [_cuda(g[k]) for k in ("x", "mask", "mu", "t")]
+    B, _, T = g["x"].shape
+    F_, T_ = 80 >> lvl, T >> lvl
+    xs = []
+    for name in ins:
+        c = {"downs.0.0": 64, "downs.0.3": 64, "downs.1.0": 128, "downs.1.3": 128, "mid_block2": 256,
+             "downs.2.2": 256, "ups.0.3": 128, "downs.1.2": 128}[name]
+        xs.append(_stage(dec, args, name, (B, c, F_, T_)))
+    x = torch.cat(xs, 1)
+    assert x.shape[1] == cin and torch.isfinite(x).all()
+    m = torch.from_numpy(g["mask"]).unsqueeze(1)[:, :, :, ::(1 << lvl)]
+    p8 = odec.fp8_params(sd)
+    key = out[:-len("pre1")] + "block1.block.0."
+    ref = F.conv2d(odec.quantize_act_e4m3(x * m), p8[key + "weight"], p8[key + "bias"], padding=1).numpy()
+    y = _stage(dec, args, out, ref.shape).numpy()
+    report(f"fp8 layer {out} ({cin}->{cout}, identical inputs)", rel_err(y, ref), LAYER_TOL)
+
+
+def test_fp8_gn_conv_close_to_oracle_on_gpu_inputs():
+    """block2 (GroupNorm + Mish + time bias in the operand load) from the GPU's own block1 output. The GroupNorm
+    statistics come from the fp32 conv outputs on the GPU and from their bf16-stored copy here, so a few e4m3
+    rounding decisions may flip: the gate is 2x the layer gate (measured 2.5-3.4e-3; an operand-layout error is O(1))."""
+    from oracle import decoder as odec
+    g = load_golden("estimator_s1_T132.npz")
+    dec, sd = make_decoder(1, 0, FP8)
+    args = [_cuda(g[k]) for k in ("x", "mask", "mu", "t")]
+    B, _, T = g["x"].shape
+    p8 = odec.fp8_params(sd)
+    t = torch.from_numpy(g["t"])
+    t_emb = odec.sinusoidal_pos_emb(t, 64, 1000.0)
+    t_emb = F.linear(odec.mish(odec.linear(p8, "mlp.0", t_emb)), p8["mlp.2.weight"], p8["mlp.2.bias"])
+    for key, lvl, c in (("downs.1.0.", 1, 128), ("downs.2.1.", 2, 256)):
+        pre1 = _stage(dec, args, key + "pre1", (B, c, 80 >> lvl, T >> lvl))
+        m = torch.from_numpy(g["mask"]).unsqueeze(1)[:, :, :, ::(1 << lvl)]
+        h = F.group_norm(pre1, 8, p8[key + "block1.block.1.weight"], p8[key + "block1.block.1.bias"], eps=1e-5)
+        h = odec.mish(h) * m
+        tb = F.linear(odec.mish(t_emb), p8[key + "mlp.1.weight"], p8[key + "mlp.1.bias"])
+        h = h + tb.unsqueeze(-1).unsqueeze(-1)
+        ref = F.conv2d(odec.quantize_act_e4m3(h * m), p8[key + "block2.block.0.weight"],
+                       p8[key + "block2.block.0.bias"], padding=1).numpy()
+        y = _stage(dec, args, key + "pre2", ref.shape).numpy()
+        report(f"fp8 layer {key}pre2 (GroupNorm operand, GPU block1 output)", rel_err(y, ref), 2 * LAYER_TOL)
+
+
+@pytest.mark.parametrize("name", EST)
+def test_fp8_estimator_within_quantization_envelope(name):
+    from oracle import decoder as odec
+    g = load_golden(name)
+    n_spks = int(g["n_spks"])
+    dec, sd = make_decoder(n_spks, int(g["seed_w"]), FP8)
+    spk = g["spk"] if n_spks != 1 else None
+    args = [torch.from_numpy(g[k]) for k in ("x", "mask", "mu", "t")]
+    spk_t = torch.from_numpy(spk) if spk is not None else None
+    with torch.no_grad():
+        with odec.fp8_activations():
+            ref8 = odec.estimator(odec.fp8_params(sd), *args, spk_t, n_spks).numpy()
+    ref32 = g["out"]   # the reference's own fp32 output (golden fixture)
+    y = dec.estimator(*(a.cuda() for a in args), _cuda(spk) if spk is not None else None).cpu().numpy()
+    assert np.isfinite(y).all()
+    q = rel_err(ref8, ref32)   # what the fp8 quantization itself does to this call
+    report(f"fp8 estimator {name} vs fp8 oracle", rel_err(y, ref8), q, quant_effect=q)
+    report(f"fp8 estimator {name} vs fp32 reference", rel_err(y, ref32), 1.3 * q, quant_effect=q)
+
+
+def test_fp8_sampler_N1000_matches_oracle():
+    """Config 5's step count on a small ragged batch (the CPU oracle finishes it in about a minute): over 1000 Euler
+    steps the per-call quantization noise averages out; gate: within the bf16 sampler tolerance (1e-2) of the fp8
+    oracle, and within the fp8 oracle's own distance to the fp32 oracle x 1.3 + 1e-2."""
+    from oracle import decoder as odec
+    from gradtts_amd.params import synthetic_inputs
+    dec, sd = make_decoder(1, 0, FP8)
+    mu, z, mask, _ = synthetic_inputs(11, 2, 16, lengths=[16, 12])
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    args = (torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu))
+    with odec.fp8_activations():
+        ref8 = odec.reverse_diffusion(odec.fp8_params(sd), *args, 1000).numpy()
+    ref32 = odec.reverse_diffusion(odec.to_torch_params(sd), *args, 1000).numpy()
+    y = dec(_cuda(z), _cuda(mask), _cuda(mu), 1000).cpu().numpy()
+    q = rel_err(ref8, ref32)
+    report("fp8 reverse N=1000 vs fp8 oracle", rel_err(y, ref8), 1e-2, quant_effect=q)
+    report("fp8 reverse N=1000 vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
+
+
+def test_fp8_bench_shape_deterministic_and_batch_invariant():
+    from gradtts_amd.params import synthetic_inputs
+    dec, _ = make_decoder(1, 0, FP8)
+    mu, z, mask, _ = synthetic_inputs(1234, 32, 512)
+    zc, mc, muc = _cuda(z), _cuda(mask), _cuda(mu)
+    y1 = dec(zc, mc, muc, 3)
+    y2 = dec(zc, mc, muc, 3)
+    assert torch.isfinite(y1).all()
+    sub = dec(zc[5:10].contiguous(), mc[5:10].contiguous(), muc[5:10].contiguous(), 3)   # throughput plan (B > 4)
+    assert torch.equal(y1, y2) and torch.equal(y1[5:10], sub)
+    dec.compute_dtype = "bf16_w8"
+    yw8 = dec(zc, mc, muc, 3)
+    report("fp8 vs bf16_w8 decode B=32 T=512 N=3", rel_err(y1.cpu().numpy(), yw8.cpu().numpy()), 0.1)
+
+
+def test_fp8_small_plan_agrees_and_is_batch_invariant():
+    from gradtts_amd.params import synthetic_inputs
+    dec, _ = make_decoder(1, 0, FP8)
+    mu, z, mask, _ = synthetic_inputs(77, 5, 256, lengths=[256, 200, 256, 131, 256])
+    zc, mc, muc = _cuda(z), _cuda(mask), _cuda(mu)
+    y4 = dec(zc[:4].contiguous(), mc[:4].contiguous(), muc[:4].contiguous(), 3)    # small-batch plan (B <= 4)
+    y1 = dec(zc[1:2].contiguous(), mc[1:2].contiguous(), muc[1:2].contiguous(), 3)
+    y5 = dec(zc, mc, muc, 3)                                                         # throughput plan
+    assert torch.isfinite(y4).all() and torch.equal(y4[1:2], y1)
+    report("fp8 small vs throughput plan B=4 T=256 N=3", rel_err(y4.cpu().numpy(), y5[:4].cpu().numpy()), 5e-2)
