@@ -74,7 +74,9 @@ GT_DEV float mish_tb(float y, float tb) {
 // One workgroup = one segment: L consecutive 4 x 32 tiles down the mel axis of one utterance's 32-frame column.
 // Two workgroups share a CU (one wave of each per SIMD) and drift out of phase, so one's staging/epilogue VALU
 // work overlaps the other's MFMAs.
-template <int IN>
+// W8: fp8 weights (GT_BF16_W8 / GT_FP8) -- the image holds the e4m3 values (exact in bf16) and p.wscale the
+// per-output-channel scale: the accumulator starts at bias / scale and the epilogue multiplies by the scale.
+template <int IN, bool W8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
@@ -82,8 +84,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   constexpr int WREG = wreg_of(IN);
   char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
   float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB + WLDS_MAX * WTAP_B);   // [scale, shift, tb, unused][64]
-  float* const s_bias = s_coef + 2 * 4 * 64;
-  float* const s_sub = s_bias + 64;                          // [wave][(pr, h) group][sum, sq]
+  float* const s_wsc = s_coef + 2 * 4 * 64;                  // W8: per-output-channel weight scales
+  float* const s_sub = s_wsc + 64;                          // [wave][(pr, h) group][sum, sq]
   float* const s_mean = s_sub + NW * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
@@ -118,7 +120,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const char* const wlp = sWL + (cb * NCH * 64 + lane) * 16;
   f32x16 bias_acc;   // the conv bias in accumulator layout: register q of lane (r, h) is channel cb*32 + acc_row(q, h)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) bias_acc[q] = p.bias[cb * 32 + acc_row(q, h)];
+  for (int q = 0; q < 16; ++q) {
+    const int c = cb * 32 + acc_row(q, h);
+    bias_acc[q] = W8 ? p.bias[c] / p.wscale[c] : p.bias[c];
+  }
+  if (W8 && tid < 64) s_wsc[tid] = p.wscale[tid];   // read by the epilogues, after the first tile's barrier
 
   // ---- staging. Item (row i, column c, 8-channel group sub) of patch row i: input frame t0 - 1 + c, mel row
   // given by the caller; out-of-range positions read past the end of the tensor (zeros).
@@ -309,11 +315,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
-        float o[8];
+        float o[8], ws[8];
+        if (W8) {
+          *reinterpret_cast<f32x4*>(ws) = *reinterpret_cast<const f32x4*>(s_wsc + c0);
+          *reinterpret_cast<f32x4*>(ws + 4) = *reinterpret_cast<const f32x4*>(s_wsc + c0 + 4);
+        }
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          o[e] = v[8 * pr + e];
+          o[e] = W8 ? v[8 * pr + e] * ws[e] : v[8 * pr + e];
           s += o[e];
           q += o[e] * o[e];
           asm volatile("" : "+v"(s), "+v"(q));   // scalar chains: see conv.hip (packed-FP32 op_sel hazard)
@@ -363,7 +373,7 @@ static int cu_count() {
 
 bool conv64_eligible(const ConvParams& p) {
   return p.Cin == 64 && p.Cout == 64 && p.Cin_pad == 64 && p.C0 == 64 && p.in1 == nullptr && p.Fin == p.Fout &&
-         p.Tin == p.Tout && p.Fout % 4 == 0 && p.wscale == nullptr && p.w_bstride == 0 &&
+         p.Tin == p.Tout && p.Fout % 4 == 0 && p.w_bstride == 0 &&
          (long)p.B * p.Fout * p.Tout * 128 < (1L << 31);
 }
 
@@ -385,10 +395,17 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
   const int L = conv64_seg(p.Fout, p.small);
   const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
-  if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK>), dim3(grid), dim3(256), 0, s, p, L);
-  else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN>), dim3(grid), dim3(256), 0, s, p, L);
-  else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN>), dim3(grid), dim3(256), 0, s, p, L);
-  else return hipErrorNotSupported;
+  if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)
+    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(256), 0, s, p, L);
+    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, true>), dim3(grid), dim3(256), 0, s, p, L);
+    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, true>), dim3(grid), dim3(256), 0, s, p, L);
+    else return hipErrorNotSupported;
+  } else {
+    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(256), 0, s, p, L);
+    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), dim3(256), 0, s, p, L);
+    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), dim3(256), 0, s, p, L);
+    else return hipErrorNotSupported;
+  }
   return hipGetLastError();
 }
 

@@ -373,6 +373,22 @@ void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w
   blob.put(key, img.data(), img.size() * 2);
 }
 
+// e4m3 values (codes decoded, without the scale) of a [rows][...] weight quantized per row as gt_quantize_e4m3 does:
+// exact in bf16, for the conv64 image of an fp8-weight conv (the scale is applied in conv64's epilogue)
+std::vector<float> e4m3_values(const std::vector<float>& w, int rows) {
+  const int64_t cols = (int64_t)w.size() / rows;
+  std::vector<uint8_t> q(w.size());
+  std::vector<float> sc(rows);
+  gt_quantize_e4m3(w.data(), rows, cols, cols, 1, q.data(), sc.data());
+  std::vector<float> v(w.size());
+  for (size_t i = 0; i < q.size(); ++i) {
+    const int s = q[i] >> 7, e = (q[i] >> 3) & 15, m = q[i] & 7;
+    const float a = e ? std::ldexp(1.f + m / 8.f, e - 7) : std::ldexp(m / 8.f, -6);
+    v[i] = s ? -a : a;
+  }
+  return v;
+}
+
 // conv64 (persistent weight-resident 64-channel 3x3 conv, conv64.hip) for bf16; GT_CONV64=0 disables it (A/B)
 static bool conv64_enabled() {
   static const bool v = [] {
@@ -395,7 +411,11 @@ int prepare(gt_decoder* d, int code) {
     const std::string& k = d->inv[i].name;
     const auto& shp = d->inv[i].dims;
     const auto& w = d->host[i];
-    if (a8 && ends_with(k, ".block.0.weight") && shp[1] >= 32) {
+    const bool c64 = dt && ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 64 && shp[2] == 3 && shp[3] == 3;
+    if (w8 && c64) {   // 64 -> 64 (level 0): conv64 with the e4m3 values (fp8 modes alike: bf16 operands there)
+      pack_conv8(blob, d, code, k, w, shp, false);
+      pack_conv64(blob, k + ".w64", e4m3_values(w, 64));
+    } else if (a8 && ends_with(k, ".block.0.weight") && shp[1] >= 32) {
       pack_conva8(blob, d, code, k, w, shp);
     } else if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
       pack_conv8(blob, d, code, k, w, shp, false);
@@ -404,8 +424,7 @@ int prepare(gt_decoder* d, int code) {
     } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
-      if (dt && ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 64 && shp[2] == 3 && shp[3] == 3)
-        pack_conv64(blob, k + ".w64", w);
+      if (c64) pack_conv64(blob, k + ".w64", w);
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
     } else if (ends_with(k, "to_qkv.weight")) {
@@ -575,15 +594,18 @@ struct Run {
   }
 
   // 3x3 stride-1 conv with GroupNorm partial sums of the output; returns the number of partial slots per
-  // utterance it wrote. bf16 64 -> 64 convs take conv64 (weight-resident), everything else conv_kernel.
+  // utterance it wrote. bf16-operand 64 -> 64 convs (bf16 or fp8 weights; GT_FP8 too) take conv64 (weight-resident),
+  // everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
     if (dt && conv64_enabled() && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
         d->dp[wi].count(wkey + ".w64")) {
-      p.w = W(wkey + ".w64");
+      p.w = W(wkey + ".w64");   // (fp8 weights: their e4m3 values; p.wscale stays the per-channel scale)
+      p.a8 = 0;
       const double pos = (double)p.B * p.Fout * p.Tout;
       const int np = conv64_nparts(p.Fout, p.Tout, p.small);
       if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }   // would spill into the next stats slot
-      timed(std::string("conv64_kernel<") + std::to_string((int)im) + ">@64x64x" + std::to_string(p.Fout),
+      timed(std::string("conv64_kernel<") + std::to_string((int)im) + (p.wscale ? ",w8" : "") + ">@64x64x" +
+                std::to_string(p.Fout),
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
       return np;
     }

@@ -41,15 +41,22 @@ def linear(p, key, x):
     return F.linear(x, p[key + ".weight"], p[key + ".bias"])
 
 
-# GT_FP8 emulation (not in the reference): when set by fp8_activations(), the input of every 3x3 Block conv with at
-# least 32 input channels is quantized by quantize_act_e4m3 before the conv (what csrc/conv.hip's A8 operand load does)
+# GT_FP8 emulation (not in the reference): when set by fp8_activations(), the input of every 3x3 Block conv that runs
+# on fp8 operands (fp8_operand_conv) is quantized by quantize_act_e4m3 before the conv (what csrc/conv.hip's A8 operand
+# load does)
 _ACT_Q = None
+
+
+def fp8_operand_conv(cin, cout):
+    """GT_FP8's fp8-operand Block convs: at least 32 input channels, except 64 -> 64 (level 0), which keeps bf16
+    operands on conv64 (with the fp8 weights)."""
+    return cin >= 32 and not (cin == 64 and cout == 64)
 
 
 def block(p, key, x, mask, taps=None, tap_name=None):
     """``Block`` diffusion.py:49-58: Mish(GN8(conv3x3(x*mask))) * mask."""
     xin = x * mask
-    if _ACT_Q is not None and xin.shape[1] >= 32:
+    if _ACT_Q is not None and fp8_operand_conv(xin.shape[1], p[key + ".block.0.weight"].shape[0]):
         xin = _ACT_Q(xin)
     y = F.conv2d(xin, p[key + ".block.0.weight"], p[key + ".block.0.bias"], padding=1)
     if taps is not None and tap_name:
