@@ -1286,6 +1286,8 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
       R.tb_bstride = 0; R.stepp = stepp;
       R.tb = tbuf; R.betas = betas;
       if (!use_graph) {
+        // a kernel, not hipMemsetD32Async: captured into a caller's graph (torch.cuda.graph), a memset node misbehaves
+        // from its second replay on (tools/memset_capture_probe.py)
         R.chk(launch_set_step(stepp, 0, R.s));
         for (int i = 0; i < n_timesteps && R.err == hipSuccess; ++i) {
           R.tb = tbuf + (size_t)i * kTbRow;

@@ -96,6 +96,8 @@ hipError_t launch_temb(const TembParams& p, hipStream_t s);
 hipError_t launch_spk_mlp(const float* spk, int B, const float* w0, const float* b0, const float* w2,
                           const float* b2, float* s_out, hipStream_t s);
 hipError_t launch_set_step(int* stepp, int v, hipStream_t s);
+hipError_t launch_fill_f32(float* p, long n, float v, hipStream_t s);            // (kernel nodes in captures, misc.hip)
+hipError_t launch_copy_f32(float* dst, const float* src, long n, hipStream_t s);
 hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s);
 // debug probe: channels-last activation [B][F][T][C] (act dtype) -> fp32 NCHW [B][C][F][T]
 hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, int C, float* dst, hipStream_t s);

@@ -263,6 +263,27 @@ hipError_t launch_set_step(int* stepp, int v, hipStream_t s) {
   return hipGetLastError();
 }
 
+// fill / copy of fp32 buffers as kernel launches: a kernel node in any capture. Memset and memcpy nodes are avoided:
+// a HIP graph's memset node wrote garbage from its second launch on when the graph was launched on a stream other
+// than its capture stream -- which torch.cuda.graph's replay does (tools/memset_capture_probe.py).
+__global__ void fill_f32_kernel(float* p, long n, float v) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = v;
+}
+__global__ void copy_f32_kernel(float* dst, const float* src, long n) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+static unsigned grid_for(long n) { return (unsigned)std::max<long>(1, std::min<long>((n + 255) / 256, 8192)); }
+hipError_t launch_fill_f32(float* p, long n, float v, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, p, n, v);
+  return hipGetLastError();
+}
+hipError_t launch_copy_f32(float* dst, const float* src, long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(copy_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_mask_copy(const float* z, const float* mask, int B, int F, int T, float* out, hipStream_t s) {
   const long n = (long)B * F * T;
   hipLaunchKernelGGL(mask_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, z, mask, F, T, n, out);

@@ -572,7 +572,7 @@ struct Trainer {
   const float* spkin = nullptr;
   void zero(float* p, long n, int line = __builtin_LINE()) {
     if (run) need(p, n, "zero", line);
-    if (live()) chk(hipMemsetAsync(p, 0, (size_t)n * 4, s), line);
+    if (live()) chk(launch_fill_f32(p, n, 0.f, s), line);
   }
 };
 
@@ -630,7 +630,7 @@ static int train_pass(gt_decoder* d, const float* x0, const float* mask, const f
   float* zm = tr.A.take((size_t)n0);
   float* lpart = tr.A.take((size_t)n0 * 2);   // loss partials (generous)
   float* lossv = tr.A.take(2);
-  if (!dry) tr.chk(hipMemsetAsync(grads, 0, (size_t)gt_internal_numel(d) * 4, tr.s));
+  if (!dry) tr.chk(launch_fill_f32(grads, gt_internal_numel(d), 0.f, tr.s));
   // forward diffusion (diffusion.py:275), then the taped U-Net forward on x_t
   FwdDiffParams fp;
   fp.x0 = x0; fp.mu = mu; fp.z = z; fp.mask = mask; fp.t = t; fp.B = (int)B; fp.F = 80; fp.T = (int)T;
@@ -654,7 +654,7 @@ static int train_pass(gt_decoder* d, const float* x0, const float* mask, const f
                                                    " B past the workspace " + std::to_string(workspace_bytes) + " B");
     return GT_OK;
   }
-  tr.chk(hipMemcpyAsync(loss, lossv, 4, hipMemcpyDeviceToDevice, tr.s));
+  tr.chk(launch_copy_f32(loss, lossv, 1, tr.s));
   if (tr.err != hipSuccess)
     return gt_internal_fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(tr.err) +
                                             " (train_bwd.cpp:" + std::to_string(tr.err_line) + ", block " + tr.err_cur + ")");
@@ -736,7 +736,7 @@ static int vjp_pass(gt_decoder* d, const float* x, const float* mask, const floa
       return gt_internal_fail(GT_ERR_WORKSPACE, "estimator VJP extent check: arena past the workspace");
     return GT_OK;
   }
-  if (score) tr.chk(hipMemcpyAsync(score, tr.score, (size_t)n0 * 4, hipMemcpyDeviceToDevice, tr.s));
+  if (score) tr.chk(launch_copy_f32(score, tr.score, n0, tr.s));
   if (tr.err != hipSuccess)
     return gt_internal_fail(GT_ERR_HIP, std::string("HIP launch failed: ") + hipGetErrorString(tr.err) +
                                             " (train_bwd.cpp:" + std::to_string(tr.err_line) + ", " + tr.err_cur + ")");

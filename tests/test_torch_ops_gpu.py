@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 def _need_gpu():
     if not gpu_available():
         pytest.skip("no HIP device")
+    _lib.ops()   # registers torch.ops.gradtts (libgradtts_ops.so) for tests that name the ops directly
 
 
 def _c(a):
