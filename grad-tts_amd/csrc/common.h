@@ -28,7 +28,7 @@ GT_DEV float mishf(float x) {
   return x * (n * __builtin_amdgcn_rcpf(n + 2.f));   // v_rcp_f32 (1 ulp): __fdividef lowered to the IEEE divide
 }
 // Mish for a bf16 activation path: tanh(softplus(x)) = 1 - 2 / ((e^x + 1)^2 + 1) -> one exp2, one rcp, four
-// FMA-class ops (conv64.hip's mish_tb form). e^x = inf gives x (torch's threshold); absolute error <= |x| 2^-23
+// FMA-class ops (the gn_mish_tb_l2 form below, without its folded affine). e^x = inf gives x (torch's threshold); absolute error <= |x| 2^-23
 // (cancellation for x << 0), far below the bf16 rounding of the result. fp32 paths keep mishf.
 template <class A> GT_DEV float mish_act(float x) { return mishf(x); }
 template <> GT_DEV float mish_act<bf16>(float x) {

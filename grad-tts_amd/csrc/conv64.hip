@@ -58,17 +58,6 @@ constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
 
-// Mish(y) + tb for the bf16 operand path: tanh(softplus(y)) = 1 - 2 / ((e^y + 1)^2 + 1), so
-// Mish(y) + tb = y * (1 - 2 r) + tb with r = 1 / ((e^y + 1)^2 + 1): one v_exp_f32, one v_rcp_f32, five FMA-class
-// ops. e^y = inf for large y gives r = 0, i.e. y + tb (torch's softplus threshold). Absolute error
-// <= |y| * 2^-23 (cancellation in 1 - 2r for y << 0), far below the bf16 rounding of the result.
-GT_DEV float mish_tb(float y, float tb) {
-  const float e = __builtin_amdgcn_exp2f(y * 1.44269504088896341f);
-  const float t = e + 1.f;
-  const float r = __builtin_amdgcn_rcpf(__builtin_fmaf(t, t, 1.f));
-  return __builtin_fmaf(y, __builtin_fmaf(-2.f, r, 1.f), tb);
-}
-
 // IN: IN_MASK / IN_GN / IN_PLAIN. Masks from sequence_mask are 0/1: x * m is then a select, decided per item on
 // the device (a fractional mask value takes a multiply in a branch that 0/1 masks never enter).
 // One workgroup = one segment: L consecutive 4 x 32 tiles down the mel axis of one utterance's 32-frame column.
@@ -166,7 +155,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
         const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_tb(v[4 * hq + k] * sc[k] + sh[k], tb[k]);
+        for (int k = 0; k < 4; ++k) v[4 * hq + k] = gn_mish_tb_l2(v[4 * hq + k], sc[k], sh[k], tb[k]);
       }
       const uint4 o = f_to_item(v, bf16());
       v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
@@ -185,8 +174,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const float tbv = tid < 64 ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid] : 0.f;
     gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
     if (tid < 64) {
-      const float sc = c_g * s_rstd[tid >> 3];
-      s_coef[tid] = sc; s_coef[64 + tid] = c_b - s_mean[tid >> 3] * sc; s_coef[128 + tid] = tbv;
+      const float sc = c_g * s_rstd[tid >> 3];   // the affine in base 2 (common.h gn_mish_tb_l2)
+      s_coef[tid] = sc * kLog2e; s_coef[64 + tid] = (c_b - s_mean[tid >> 3] * sc) * kLog2e; s_coef[128 + tid] = tbv;
     }
     lds_barrier();
   }

