@@ -24,7 +24,7 @@ GT_DEV float wave_sum(float x) {   // butterfly over the 64 lanes (every lane ge
   return x;
 }
 
-constexpr int C1_KMAX = 11, C1_SPAN = 50;   // taps, (K - 1) |dilation|
+constexpr int C1_KMAX = 11, C1_SPAN = 80;   // taps, (K - 1) |dilation| (HiFi-GAN V3: (7 - 1) x 12 = 72)
 C1dParams c1d_defaults() {
   C1dParams p{};
   p.tap_step = 1;

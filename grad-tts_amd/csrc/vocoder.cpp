@@ -1,12 +1,14 @@
-// HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1 :13-48) on the MI355X: the vocoder that turns the
+// HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1 :13-48, ResBlock2 :53-74) on the MI355X: the vocoder that turns the
 // decoder's mel into audio (inference.py:97). fp32; activations channels-last [B][T][C]; every conv is the fp32-MFMA
 // c1d kernel (textenc.hip) with the leaky ReLU folded into its operand staging and the residual / resblock
 // average / tanh into its epilogue:
 //   conv_pre                 k7 on the channel-major mel
 //   ups[i] (ConvTranspose1d)  u phases, each a 2-tap conv over the input (taps r and r + u of the kernel, input
 //                             frames q and q - 1) writing output frames q u + r - P: no zero-stuffed input
-//   resblocks                 per stage 3 x ResBlock1; the last conv of each adds the residual and accumulates into
-//                             the stage sum (the third divides by 3: x = xs / num_kernels)
+//   resblocks                 per stage num_kernels resblocks (ResBlock1: per dilation leaky -> dilated conv -> leaky ->
+//                             conv -> + x; ResBlock2: per dilation leaky -> dilated conv -> + x); the last conv of each
+//                             adds the residual and accumulates into the stage sum (the last resblock divides by
+//                             num_kernels: x = xs / num_kernels)
 //   conv_post                 leaky ReLU (0.01) staged, k7, tanh in the epilogue
 // Weight norm (weight_g, weight_v) is baked on upload as remove_weight_norm() does (inference.py:76).
 #include <hip/hip_runtime.h>
@@ -25,6 +27,7 @@ using namespace gt;
 
 struct gt_vocoder {
   int n_mels, c0, n_up, nk;
+  int rb_type = 1;                       // h.resblock: 1 (ResBlock1) or 2 (ResBlock2)
   std::vector<int> rates, kernels, rb_k;
   std::vector<std::vector<int>> rb_d;
   std::vector<std::pair<std::string, std::vector<int64_t>>> inv;
@@ -125,38 +128,45 @@ int64_t max_buf(const gt_vocoder* v, int64_t T) {   // largest [T_stage][C_stage
 
 extern "C" {
 
-int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
-                      const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes,
-                      const int* resblock_dilations, gt_vocoder** out) {
+int gt_vocoder_create2(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
+                       const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes, int resblock,
+                       int n_dil, const int* resblock_dilations, gt_vocoder** out) {
   if (!out || !upsample_rates || !upsample_kernel_sizes || !resblock_kernel_sizes || !resblock_dilations)
     return gt_internal_fail(GT_ERR_ARG, "null argument");
   *out = nullptr;
-  if (n_up <= 0 || n_kernels <= 0 || upsample_initial_channel >> n_up <= 0)
+  if (n_up <= 0 || n_kernels <= 0 || n_dil <= 0 || upsample_initial_channel >> n_up <= 0)
     return gt_internal_fail(GT_ERR_ARG, "bad configuration");
+  if (resblock != 1 && resblock != 2) return gt_internal_fail(GT_ERR_ARG, "resblock must be 1 or 2 (h.resblock)");
   for (int i = 0; i < n_up; ++i)
     if (upsample_kernel_sizes[i] != 2 * upsample_rates[i])
-      return gt_internal_fail(GT_ERR_UNSUPPORTED, "upsampling implemented for kernel = 2 x rate (HiFi-GAN V1/V2)");
+      return gt_internal_fail(GT_ERR_UNSUPPORTED, "upsampling implemented for kernel = 2 x rate (HiFi-GAN V1/V2/V3)");
   for (int j = 0; j < n_kernels; ++j)
-    for (int m = 0; m < 3; ++m)
-      if ((resblock_kernel_sizes[j] - 1) * resblock_dilations[j * 3 + m] > 50 || resblock_kernel_sizes[j] > 11)
-        return gt_internal_fail(GT_ERR_UNSUPPORTED, "resblock kernel <= 11 and (k - 1) dilation <= 50");
+    for (int m = 0; m < n_dil; ++m)
+      if ((resblock_kernel_sizes[j] - 1) * resblock_dilations[j * n_dil + m] > 80 || resblock_kernel_sizes[j] > 11 ||
+          resblock_dilations[j * n_dil + m] < 1)
+        return gt_internal_fail(GT_ERR_UNSUPPORTED, "resblock kernel <= 11 and 1 <= dilation, (k - 1) dilation <= 80");
   gt_vocoder* v = new gt_vocoder();
-  v->n_mels = n_mels; v->c0 = upsample_initial_channel; v->n_up = n_up; v->nk = n_kernels;
+  v->n_mels = n_mels; v->c0 = upsample_initial_channel; v->n_up = n_up; v->nk = n_kernels; v->rb_type = resblock;
   v->rates.assign(upsample_rates, upsample_rates + n_up);
   v->kernels.assign(upsample_kernel_sizes, upsample_kernel_sizes + n_up);
   v->rb_k.assign(resblock_kernel_sizes, resblock_kernel_sizes + n_kernels);
-  for (int j = 0; j < n_kernels; ++j) v->rb_d.push_back({resblock_dilations[3 * j], resblock_dilations[3 * j + 1],
-                                                         resblock_dilations[3 * j + 2]});
+  for (int j = 0; j < n_kernels; ++j)
+    v->rb_d.push_back(std::vector<int>(resblock_dilations + j * n_dil, resblock_dilations + (j + 1) * n_dil));
   add_wn(v, "conv_pre", {v->c0, n_mels, 7}, v->c0);
   for (int i = 0; i < n_up; ++i)
     add_wn(v, "ups." + std::to_string(i), {v->c0 >> i, v->c0 >> (i + 1), v->kernels[i]}, v->c0 >> (i + 1));
   int n = 0;
-  for (int i = 0; i < n_up; ++i) {
+  for (int i = 0; i < n_up; ++i) {   // registration order of the reference modules (weight_norm: bias, g, v)
     const int64_t ch = v->c0 >> (i + 1);
-    for (int j = 0; j < n_kernels; ++j, ++n)
-      for (const char* part : {"convs1", "convs2"})
-        for (int m = 0; m < 3; ++m)
-          add_wn(v, "resblocks." + std::to_string(n) + "." + part + "." + std::to_string(m), {ch, ch, v->rb_k[j]}, ch);
+    for (int j = 0; j < n_kernels; ++j, ++n) {
+      const std::string rk = "resblocks." + std::to_string(n) + ".";
+      if (resblock == 1) {
+        for (const char* part : {"convs1", "convs2"})
+          for (int m = 0; m < n_dil; ++m) add_wn(v, rk + part + "." + std::to_string(m), {ch, ch, v->rb_k[j]}, ch);
+      } else {
+        for (int m = 0; m < n_dil; ++m) add_wn(v, rk + "convs." + std::to_string(m), {ch, ch, v->rb_k[j]}, ch);
+      }
+    }
   }
   add_wn(v, "conv_post", {1, v->c0 >> n_up, 7}, 1);
   for (size_t i = 0; i < v->inv.size(); ++i) v->index[v->inv[i].first] = (int)i;
@@ -164,6 +174,13 @@ int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const 
   v->set.assign(v->inv.size(), false);
   *out = v;
   return GT_OK;
+}
+
+int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
+                      const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes,
+                      const int* resblock_dilations, gt_vocoder** out) {
+  return gt_vocoder_create2(n_mels, upsample_initial_channel, n_up, upsample_rates, upsample_kernel_sizes, n_kernels,
+                            resblock_kernel_sizes, 1, 3, resblock_dilations, out);
 }
 
 void gt_vocoder_destroy(gt_vocoder* v) {
@@ -261,9 +278,29 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
     float* t1 = buf[3];
     float* xs = buf[0];   // the stage input x is dead after the upsampling
     for (int j = 0; j < v->nk; ++j, ++n) {
-      const int kk = v->rb_k[j];
+      const int kk = v->rb_k[j], nd = (int)v->rb_d[j].size();
       const float* y = xu;
-      for (int m = 0; m < 3; ++m) {
+      if (v->rb_type == 2) {   // ResBlock2 (models.py:68-72): y = conv_m(leaky_relu(y, 0.1)) + y per dilation
+        for (int m = 0; m < nd; ++m) {
+          const int d = v->rb_d[j][m];
+          const std::string c = "resblocks." + std::to_string(n) + ".convs." + std::to_string(m);
+          C1dParams q = c1d_defaults();
+          q.in = y; q.in_cs = cout; q.in_act = 1; q.in_slope = 0.1f;
+          q.w = W(c); q.bias = Bs(c); q.wso = (long)cout * kk; q.wsc = kk;
+          q.B = Bi; q.T = Tout; q.Q = Tout; q.Tout = Tout; q.Cin = cout; q.Cout = cout; q.K = kk; q.dil = d;
+          q.pad = (kk * d - d) / 2; q.res = y; q.res_cs = cout; q.out_cs = cout;
+          if (m < nd - 1) {
+            q.out = (y == cur) ? t1 : cur;   // ping-pong: a dilated conv never writes the tensor it reads
+          } else {
+            q.out = xs; q.accumulate = j > 0;
+            if (j == v->nk - 1) q.div = (float)v->nk;
+          }
+          launch(q, c, 0);
+          y = q.out;
+        }
+        continue;
+      }
+      for (int m = 0; m < nd; ++m) {
         const int d = v->rb_d[j][m];
         const std::string c1 = "resblocks." + std::to_string(n) + ".convs1." + std::to_string(m);
         const std::string c2 = "resblocks." + std::to_string(n) + ".convs2." + std::to_string(m);
@@ -278,7 +315,7 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
         q.w = W(c2); q.bias = Bs(c2); q.wso = (long)cout * kk; q.wsc = kk;
         q.B = Bi; q.T = Tout; q.Q = Tout; q.Tout = Tout; q.Cin = cout; q.Cout = cout; q.K = kk; q.pad = (kk - 1) / 2;
         q.res = y; q.res_cs = cout; q.out_cs = cout;
-        if (m < 2) {
+        if (m < nd - 1) {
           q.out = cur;
         } else {   // last conv of the resblock: xs (+)= y; the stage's last divides by num_kernels
           q.out = xs; q.accumulate = j > 0;

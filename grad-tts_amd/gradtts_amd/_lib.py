@@ -81,6 +81,8 @@ SIGNATURES = [
                                   _c.c_void_p, _c.c_void_p]),
     ("gt_vocoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                      _c.c_void_p, _c.c_void_p]),
+    ("gt_vocoder_create2", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
+                                      _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p]),
     ("gt_vocoder_destroy", None, [_c.c_void_p]),
     ("gt_vocoder_num_params", _c.c_int, [_c.c_void_p]),
     ("gt_vocoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),

@@ -263,6 +263,11 @@ def synthetic_text_encoder_state_dict(seed: int = 0, **kw) -> "OrderedDict[str, 
 HIFIGAN_V1 = {"resblock": "1", "upsample_rates": [8, 8, 2, 2], "upsample_kernel_sizes": [16, 16, 4, 4],
               "upsample_initial_channel": 512, "resblock_kernel_sizes": [3, 7, 11],
               "resblock_dilation_sizes": [[1, 3, 5], [1, 3, 5], [1, 3, 5]], "num_mels": 80}
+# HiFi-GAN V3 (the published config_v3.json of the HiFi-GAN repository; not shipped in the reference, whose models.py
+# builds it with ResBlock2, models.py:53-74 / :84)
+HIFIGAN_V3 = {"resblock": "2", "upsample_rates": [8, 8, 4], "upsample_kernel_sizes": [16, 16, 8],
+              "upsample_initial_channel": 256, "resblock_kernel_sizes": [3, 5, 7],
+              "resblock_dilation_sizes": [[1, 2], [2, 6], [3, 12]], "num_mels": 80}
 
 
 def _wn(out, key, w_shape, g_dim0):
@@ -284,7 +289,8 @@ def vocoder_param_shapes(h=None):
     for i in range(len(h["upsample_rates"])):
         ch = c0 // 2 ** (i + 1)
         for k, d in zip(h["resblock_kernel_sizes"], h["resblock_dilation_sizes"]):
-            for part in ("convs1", "convs2"):
+            parts = ("convs1", "convs2") if str(h["resblock"]) == "1" else ("convs",)
+            for part in parts:
                 for m in range(len(d)):
                     _wn(out, f"resblocks.{n}.{part}.{m}", (ch, ch, k), ch)
             n += 1

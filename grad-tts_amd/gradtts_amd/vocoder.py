@@ -1,4 +1,4 @@
-"""Drop-in HiFi-GAN ``Generator`` (hifi-gan/models.py:77-128, ResBlock1 :13-48): the reference's module tree and
+"""Drop-in HiFi-GAN ``Generator`` (hifi-gan/models.py:77-128, ResBlock1 :13-48, ResBlock2 :53-74): the reference's module tree and
 parameter names (``bias`` / ``weight_g`` / ``weight_v`` from torch's weight_norm), so the ``generator`` entry of a
 HiFi-GAN checkpoint loads unchanged (inference.py:73-76); compute in libgradtts.so (``gt_vocoder_forward``, fp32 MFMA
 convs on the MI355X). ``remove_weight_norm()`` is accepted and does nothing: the library bakes g * v / ||v|| itself."""
@@ -33,8 +33,15 @@ class ResBlock1(torch.nn.Module):
                                            for _ in dilation])
 
 
+class ResBlock2(torch.nn.Module):
+    def __init__(self, h, channels, kernel_size=3, dilation=(1, 3)):
+        super().__init__()
+        self.convs = torch.nn.ModuleList([_wn(torch.nn.Conv1d(channels, channels, kernel_size, 1, dilation=d,
+                                                              padding=get_padding(kernel_size, d))) for d in dilation])
+
+
 class Generator(torch.nn.Module):
-    """``Generator(h, compute_dtype=torch.float32)`` with h the HiFi-GAN config (AttrDict or dict: resblock '1',
+    """``Generator(h, compute_dtype=torch.float32)`` with h the HiFi-GAN config (AttrDict or dict: resblock '1' / '2',
     upsample_rates, upsample_kernel_sizes, upsample_initial_channel, resblock_kernel_sizes,
     resblock_dilation_sizes). compute_dtype=torch.bfloat16 rounds the conv operands to bf16 (fp32 accumulation,
     fp32 activations in memory): the throughput mode; fp32 is the parity path."""
@@ -45,8 +52,9 @@ class Generator(torch.nn.Module):
             raise ValueError("compute_dtype must be torch.float32 (parity path) or torch.bfloat16 (throughput)")
         self.compute_dtype = compute_dtype
         g = (lambda k: h[k]) if isinstance(h, dict) else (lambda k: getattr(h, k))
-        if str(g("resblock")) != "1":
-            raise ValueError("the HIP vocoder implements ResBlock1 (HiFi-GAN V1 / V2)")
+        self.resblock = str(g("resblock"))
+        if self.resblock not in ("1", "2"):
+            raise ValueError("resblock must be '1' (ResBlock1) or '2' (ResBlock2), as models.py:84 reads it")
         self.rates = list(g("upsample_rates"))
         self.kernels = list(g("upsample_kernel_sizes"))
         self.c0 = int(g("upsample_initial_channel"))
@@ -64,7 +72,7 @@ class Generator(torch.nn.Module):
         for i in range(len(self.ups)):
             ch = self.c0 // (2 ** (i + 1))
             for k, d in zip(self.rb_k, self.rb_d):
-                self.resblocks.append(ResBlock1(h, ch, k, d))
+                self.resblocks.append((ResBlock1 if self.resblock == "1" else ResBlock2)(h, ch, k, d))
         self.conv_post = _wn(torch.nn.Conv1d(ch, 1, 7, 1, padding=3))
         self._handle = None
         self._synced = None
@@ -77,9 +85,13 @@ class Generator(torch.nn.Module):
         if self._handle is None:
             h = ctypes.c_void_p()
             ia = lambda xs: (ctypes.c_int * len(xs))(*xs)
+            nd = len(self.rb_d[0])
+            if any(len(d) != nd for d in self.rb_d):
+                raise ValueError("every resblock needs the same number of dilations")
             dil = [d for ds in self.rb_d for d in ds]
-            check(L.gt_vocoder_create(self.n_mels, self.c0, self.num_upsamples, ia(self.rates), ia(self.kernels),
-                                      self.num_kernels, ia(self.rb_k), ia(dil), ctypes.byref(h)), "gt_vocoder_create")
+            check(L.gt_vocoder_create2(self.n_mels, self.c0, self.num_upsamples, ia(self.rates), ia(self.kernels),
+                                       self.num_kernels, ia(self.rb_k), int(self.resblock), nd, ia(dil),
+                                       ctypes.byref(h)), "gt_vocoder_create2")
             self._handle = h
         check(L.gt_vocoder_set_compute_dtype(self._handle, 1 if self.compute_dtype == torch.bfloat16 else 0),
               "gt_vocoder_set_compute_dtype")

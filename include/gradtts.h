@@ -213,14 +213,21 @@ int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const in
 int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
                    float* mu_y, void* stream);
 
-/* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1; the vocoder of inference.py:73-97). fp32. Parameters by
- * the reference Generator's state_dict names (bias, weight_g, weight_v per conv); weight norm baked on upload as
- * remove_weight_norm() does. gt_vocoder_forward: mel [B,n_mels,T] -> audio [B,1,T*hop], hop = prod(upsample_rates).
- * Implemented: ResBlock1 with 3 dilations per resblock, upsampling kernel = 2 x rate (V1 / V2). */
+/* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1 :13-48 / ResBlock2 :53-74; the vocoder of
+ * inference.py:73-97). fp32. Parameters by the reference Generator's state_dict names (bias, weight_g, weight_v per
+ * conv); weight norm baked on upload as remove_weight_norm() does. gt_vocoder_forward: mel [B,n_mels,T] -> audio
+ * [B,1,T*hop], hop = prod(upsample_rates). Implemented: upsampling kernel = 2 x rate (V1 / V2 / V3), resblock kernels
+ * <= 11 with (k - 1) dilation <= 80.
+ * gt_vocoder_create: ResBlock1 with 3 dilations per resblock (h.resblock == '1'); resblock_dilations [n_kernels][3].
+ * gt_vocoder_create2: resblock = 1 or 2 (h.resblock), n_dil dilations per resblock, resblock_dilations
+ * [n_kernels][n_dil] (HiFi-GAN V3: resblock 2, 2 dilations). */
 typedef struct gt_vocoder gt_vocoder;
 int gt_vocoder_create(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
                       const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes,
                       const int* resblock_dilations, gt_vocoder** out);
+int gt_vocoder_create2(int n_mels, int upsample_initial_channel, int n_up, const int* upsample_rates,
+                       const int* upsample_kernel_sizes, int n_kernels, const int* resblock_kernel_sizes, int resblock,
+                       int n_dil, const int* resblock_dilations, gt_vocoder** out);
 void gt_vocoder_destroy(gt_vocoder* voc);
 int gt_vocoder_num_params(gt_vocoder* voc);
 const char* gt_vocoder_param_name(gt_vocoder* voc, int i);

@@ -5,6 +5,7 @@ tests/golden/voc_*.npz (tests/golden/make_golden_vocoder.py ran the reference it
 * weight      torch.nn.utils.weight_norm's weight = g * v / ||v|| (norm over all dims but 0), as
               remove_weight_norm() bakes it (inference.py:76)
 * resblock1   models.py:13-48: 3 x [leaky_relu(0.1) -> dilated conv -> leaky_relu(0.1) -> conv -> + x]
+* resblock2   models.py:53-74: per dilation [leaky_relu(0.1) -> dilated conv -> + x] (h["resblock"] == "2", V3)
 * generator   models.py:77-110: conv_pre, per stage leaky_relu(0.1) -> ConvTranspose1d -> mean of the resblocks,
               leaky_relu (slope 0.01, the default) -> conv_post -> tanh
 """
@@ -33,6 +34,11 @@ def generator(p, mel, h=None):
             y = x
             for m, d in enumerate(dd):
                 xt = F.leaky_relu(y, 0.1)
+                if str(h["resblock"]) == "2":
+                    xt = F.conv1d(xt, weight(p, f"resblocks.{n}.convs.{m}"), p[f"resblocks.{n}.convs.{m}.bias"],
+                                  dilation=d, padding=(kk * d - d) // 2)
+                    y = xt + y
+                    continue
                 xt = F.conv1d(xt, weight(p, f"resblocks.{n}.convs1.{m}"), p[f"resblocks.{n}.convs1.{m}.bias"],
                               dilation=d, padding=(kk * d - d) // 2)
                 xt = F.leaky_relu(xt, 0.1)

@@ -3,7 +3,9 @@
 running the REAL reference in the build container: /root/reference/hifi-gan/models.py ``Generator`` (:77-128) with
 the configuration of checkpts/hifigan-config.json (V1), synthetic weights (``synthetic_vocoder_state_dict``; seed
 and SHA-256 stored) loaded as weight_g / weight_v / bias, ``remove_weight_norm()`` as inference.py:76 does, eval,
-float32 and float64. Also records the state_dict layout (keys + shapes) of the reference Generator.
+float32 and float64. Also records the state_dict layout (keys + shapes) of the reference Generator. A second set
+(voc3_*) runs the same reference Generator with the HiFi-GAN V3 configuration (resblock '2': ResBlock2,
+models.py:53-74), which the reference code supports although its checkpts ship only the V1 config.
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_vocoder.py
 """
@@ -19,7 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = os.environ.get("GRADTTS_REFERENCE", "/root/reference")
 sys.path.insert(0, os.path.join(REPO, "grad-tts_amd"))
-from gradtts_amd.params import HIFIGAN_V1, state_dict_sha256, synthetic_vocoder_state_dict  # noqa: E402
+from gradtts_amd.params import HIFIGAN_V1, HIFIGAN_V3, state_dict_sha256, synthetic_vocoder_state_dict  # noqa: E402
 
 sys.dont_write_bytecode = True
 SEED = 7
@@ -46,13 +48,18 @@ def main():
     assert all(list(sd[k].shape) == s for k, s in layout)
     with open(os.path.join(HERE, "hifigan_layout.json"), "w") as f:
         json.dump(layout, f)
-    for name, B, T, seed in (("voc_B2_T6", 2, 6, 11), ("voc_B1_T13", 1, 13, 12)):
+    from env import AttrDict  # noqa: E402  (hifi-gan/env.py)
+    h3 = AttrDict(dict(HIFIGAN_V3))
+    sd3 = synthetic_vocoder_state_dict(SEED, HIFIGAN_V3)
+    assert list(mod.Generator(h3).state_dict()) == list(sd3), "synthetic V3 layout != reference Generator layout"
+    for name, B, T, seed, hh, sdd in (("voc_B2_T6", 2, 6, 11, h, sd), ("voc_B1_T13", 1, 13, 12, h, sd),
+                                      ("voc3_B2_T7", 2, 7, 13, h3, sd3)):
         rng = np.random.default_rng(seed)
         mel = (rng.standard_normal((B, 80, T)) * 2.0 - 5.0).astype(np.float32)   # log-mel-like range
-        out = {"mel": mel, "weights_seed": np.array(SEED), "weights_sha256": np.array(state_dict_sha256(sd))}
+        out = {"mel": mel, "weights_seed": np.array(SEED), "weights_sha256": np.array(state_dict_sha256(sdd))}
         for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
-            g = mod.Generator(h)
-            g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+            g = mod.Generator(hh)
+            g.load_state_dict({k: torch.from_numpy(v) for k, v in sdd.items()}, strict=True)
             g = g.to(dt).eval()
             g.remove_weight_norm()
             with torch.no_grad():

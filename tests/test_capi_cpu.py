@@ -169,3 +169,17 @@ def test_text_encoder_and_vocoder_registries_match_reference_layouts():
         L.gt_vocoder_destroy(v)
     # an unsupported configuration (upsampling kernel != 2 x rate) is refused at creation
     assert L.gt_vocoder_create(80, 512, 1, ia([8]), ia([15]), 3, ia([3, 7, 11]), ia(dil), ctypes.byref(v)) == 4
+    # HiFi-GAN V3 (ResBlock2, 2 dilations per resblock): the reference Generator's layout
+    from gradtts_amd.params import HIFIGAN_V3, vocoder_param_shapes
+    dil3 = [d for ds in HIFIGAN_V3["resblock_dilation_sizes"] for d in ds]
+    assert L.gt_vocoder_create2(80, 256, 3, ia([8, 8, 4]), ia([16, 16, 8]), 3, ia([3, 5, 7]), 2, 2, ia(dil3),
+                                ctypes.byref(v)) == 0
+    try:
+        got = [(L.gt_vocoder_param_name(v, i).decode(), L.gt_vocoder_param_numel(v, i))
+               for i in range(L.gt_vocoder_num_params(v))]
+        assert got == [(k, int(np.prod(s))) for k, s in vocoder_param_shapes(HIFIGAN_V3).items()]
+        assert L.gt_vocoder_hop(v) == 256
+    finally:
+        L.gt_vocoder_destroy(v)
+    assert L.gt_vocoder_create2(80, 256, 3, ia([8, 8, 4]), ia([16, 16, 8]), 3, ia([3, 5, 7]), 3, 2, ia(dil3),
+                                ctypes.byref(v)) == 1   # resblock must be 1 or 2

@@ -12,7 +12,7 @@ import torch
 
 from conftest import gpu_available
 from gpu_util import rel_err, report
-from gradtts_amd.params import HIFIGAN_V1, synthetic_vocoder_state_dict
+from gradtts_amd.params import HIFIGAN_V1, HIFIGAN_V3, synthetic_vocoder_state_dict
 from gradtts_amd.vocoder import Generator
 
 pytestmark = pytest.mark.gpu
@@ -25,18 +25,19 @@ def _need_gpu():
         pytest.skip("no HIP device")
 
 
-def make_vocoder(seed, compute_dtype=torch.float32):
-    g = Generator(HIFIGAN_V1, compute_dtype=compute_dtype)
-    sd = synthetic_vocoder_state_dict(seed)
+def make_vocoder(seed, compute_dtype=torch.float32, h=HIFIGAN_V1):
+    g = Generator(h, compute_dtype=compute_dtype)
+    sd = synthetic_vocoder_state_dict(seed, h)
     g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
     g.remove_weight_norm()
     return g.cuda().eval(), sd
 
 
-@pytest.mark.parametrize("name", ["voc_B2_T6", "voc_B1_T13"])
-def test_vocoder_matches_reference_golden(name):
+@pytest.mark.parametrize("name,h", [("voc_B2_T6", HIFIGAN_V1), ("voc_B1_T13", HIFIGAN_V1),
+                                    ("voc3_B2_T7", HIFIGAN_V3)])   # voc3: HiFi-GAN V3, ResBlock2
+def test_vocoder_matches_reference_golden(name, h):
     g = np.load(os.path.join(GOLD, name + ".npz"))
-    voc, _ = make_vocoder(int(g["weights_seed"]))
+    voc, _ = make_vocoder(int(g["weights_seed"]), h=h)
     audio = voc(torch.from_numpy(g["mel"]).cuda())
     torch.cuda.synchronize()
     assert audio.shape == g["audio_f64"].shape
@@ -44,10 +45,11 @@ def test_vocoder_matches_reference_golden(name):
     report(f"vocoder audio {name} vs fp32 reference", rel_err(audio.cpu().numpy(), g["audio_f32"]), 1e-5)
 
 
-@pytest.mark.parametrize("name", ["voc_B2_T6", "voc_B1_T13"])
-def test_vocoder_bf16_mode_within_envelope(name):
+@pytest.mark.parametrize("name,h", [("voc_B2_T6", HIFIGAN_V1), ("voc_B1_T13", HIFIGAN_V1),
+                                    ("voc3_B2_T7", HIFIGAN_V3)])
+def test_vocoder_bf16_mode_within_envelope(name, h):
     g = np.load(os.path.join(GOLD, name + ".npz"))
-    voc, _ = make_vocoder(int(g["weights_seed"]), torch.bfloat16)
+    voc, _ = make_vocoder(int(g["weights_seed"]), torch.bfloat16, h)
     audio = voc(torch.from_numpy(g["mel"]).cuda())
     report(f"vocoder bf16 mode audio {name} vs fp64 reference", rel_err(audio.cpu().numpy(), g["audio_f64"]), 2e-2)
 

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from gradtts_amd.params import state_dict_sha256, synthetic_vocoder_state_dict, vocoder_param_shapes
+from gradtts_amd.params import HIFIGAN_V1, HIFIGAN_V3, state_dict_sha256, synthetic_vocoder_state_dict, vocoder_param_shapes
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -17,13 +17,14 @@ def test_layout_matches_reference_generator():
     assert [(k, tuple(s)) for k, s in layout] == list(vocoder_param_shapes().items())
 
 
-@pytest.mark.parametrize("name", ["voc_B2_T6", "voc_B1_T13"])
-def test_oracle_matches_reference_golden(name):
+@pytest.mark.parametrize("name,h", [("voc_B2_T6", HIFIGAN_V1), ("voc_B1_T13", HIFIGAN_V1),
+                                    ("voc3_B2_T7", HIFIGAN_V3)])   # voc3: V3, ResBlock2 (models.py:53-74)
+def test_oracle_matches_reference_golden(name, h):
     from oracle import vocoder as ov
     g = np.load(os.path.join(GOLD, name + ".npz"))
-    sd = synthetic_vocoder_state_dict(int(g["weights_seed"]))
+    sd = synthetic_vocoder_state_dict(int(g["weights_seed"]), h)
     assert state_dict_sha256(sd) == str(g["weights_sha256"])
     for tag, dt, tol in (("f64", torch.float64, 1e-10), ("f32", torch.float32, 1e-5)):
-        a = ov.generator(ov.to_torch_params(sd, dt), torch.from_numpy(g["mel"]).to(dt)).numpy()
+        a = ov.generator(ov.to_torch_params(sd, dt), torch.from_numpy(g["mel"]).to(dt), h).numpy()
         ref = g[f"audio_{tag}"]
         assert np.max(np.abs(a - ref)) / np.max(np.abs(ref)) <= tol, tag
