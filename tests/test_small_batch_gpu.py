@@ -169,9 +169,11 @@ def test_w8_small_plan_batch_invariant_and_agrees():
     report("w8 small vs throughput plan B=4 T=256 N=3", rel_err(y4.cpu().numpy(), y4t.cpu().numpy()), BF16_REV_TOL)
 
 
-def test_w8_latency_b1_report():
-    """Config 5 latency (fp8 weights, B = 1, T = 512): small plan vs throughput plan, ms per Euler step."""
-    dec, _ = make_decoder(1, 0, "bf16_w8")
+@pytest.mark.parametrize("mode", ["bf16_w8", "fp8", torch.bfloat16])
+def test_latency_b1_report(mode):
+    """Config 5 latency (fp8 weights / fp8 operands; bf16 for comparison), B = 1, T = 512: small plan vs throughput
+    plan, ms per Euler step."""
+    dec, _ = make_decoder(1, 0, mode)
     mu, z, mask, _ = _inputs(3, 1, 512)
     N = 20
 
@@ -186,6 +188,6 @@ def test_w8_latency_b1_report():
     y_s, ms_s = run()
     _set_small(dec, 0)
     y_t, ms_t = run()
-    print(f"LATENCY W8 B=1 T=512: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
+    print(f"LATENCY {mode} B=1 T=512: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
           f"({512 / (1000 * ms_s) * 1e3:.0f} vs {512 / (1000 * ms_t) * 1e3:.0f} mel-frames/s for 1000-step decodes)")
     assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
