@@ -29,6 +29,8 @@ struct C1dParams {
   const float* out_mask;
   const uint16_t* wbf;                 // bf16 mode: weights [Cout][K][Cin] bf16 (Cin % 8 == 0); operands rounded to
   int bf16;                            // bf16 at staging, fp32 accumulation (v_mfma_f32_32x32x16_bf16)
+  const float* wpk;                    // fp32 weights packed [Cout][K][Cin] (Cin % 4 == 0): with a channels-last input
+                                       // (in_cs % 4 == 0) the packed kernel runs (float4 staging, register prefetch)
 };
 // Conv1d defaults (wso = Cin K, wsc = K, tap_step = 1, dil = 1, Q = Tout = T, out_stride = 1)
 C1dParams c1d_defaults();

@@ -100,6 +100,132 @@ __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
   }
 }
 
+// Packed fp32 variant for channels-last inputs (the HiFi-GAN generator's convs, hifi-gan/models.py:13-128): weights
+// pre-packed [Cout][K][Cin] so a chunk of KC input channels is one float4 run per (o, k) row, staged without index
+// divisions; the next chunk is fetched into registers while the MFMAs run on the current one (one LDS buffer, two
+// barriers per chunk); the leaky ReLU / mask are applied when the registers are written to LDS. Tile: CT output
+// channels x FT frames, each wave 32 channels x NB 32-frame blocks; operands read as float4 (channels 8g + 4h ..
+// + 3 for lane half h) and fed to four v_mfma_f32_32x32x2_f32 (element e = K index h of channel 8g + 4h + e on
+// both operands), one B read shared by the NB frame blocks.
+template <int KM, int KC, int SP, int CT, int NB>
+__global__ __launch_bounds__(256, 2) void c1d_pk_kernel(C1dParams p) {
+  constexpr int WC = CT / 32, WF = 4 / WC, FT = WF * 32 * NB, LD = KC + 4, G4 = KC / 4;
+  constexpr int G4S = G4 == 4 ? 2 : 3;   // log2(G4)
+  constexpr int NIN = ((FT + SP) * G4 + 255) / 256, NW = (KM * CT * G4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_in[(FT + SP) * LD];
+  __shared__ __attribute__((aligned(16))) float s_w[KM * CT * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_qt = (p.Q + FT - 1) / FT;
+  const int qt = blockIdx.x % n_qt, b = blockIdx.x / n_qt;
+  const int q0 = qt * FT, a0 = blockIdx.y * CT;
+  const int pb = (wv % WF) * 32 * NB, cb = (wv / WF) * 32;
+  const int K = p.K, span = (K - 1) * p.dil;
+  const int lo = span < 0 ? span : 0, NP = FT + (span < 0 ? -span : span);
+  const int start = q0 - p.pad + lo;
+  const int nw = K * CT * G4, wrows = K * (p.Cout - a0);   // packed (o, k) rows valid: o < Cout - a0
+  float4 rin[NIN], rw[NW];
+  float rm[NIN];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int n = 0; n < NIN; ++n) {
+      const int i = tid + 256 * n, pp = i >> G4S, g = i & (G4 - 1), t = start + pp;
+      rin[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+      rm[n] = 1.f;
+      if (pp < NP && t >= 0 && t < p.T && c0 + 4 * g < p.Cin) {
+        rin[n] = *reinterpret_cast<const float4*>(p.in + ((long)b * p.T + t) * p.in_cs + c0 + 4 * g);
+        if (p.in_mask) rm[n] = p.in_mask[(long)b * p.T + t];
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NW; ++n) {
+      const int i = tid + 256 * n, ok = i >> G4S, g = i & (G4 - 1);
+      rw[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < nw && ok < wrows && c0 + 4 * g < p.Cin)
+        rw[n] = *reinterpret_cast<const float4*>(p.wpk + ((long)a0 * K + ok) * p.Cin + c0 + 4 * g);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int n = 0; n < NIN; ++n) {
+      const int i = tid + 256 * n, pp = i >> G4S, g = i & (G4 - 1);
+      if (pp < NP) {
+        float4 v = rin[n];
+        if (p.in_act) {
+          v.x = v.x < 0.f ? v.x * p.in_slope : v.x;
+          v.y = v.y < 0.f ? v.y * p.in_slope : v.y;
+          v.z = v.z < 0.f ? v.z * p.in_slope : v.z;
+          v.w = v.w < 0.f ? v.w * p.in_slope : v.w;
+        }
+        v.x *= rm[n]; v.y *= rm[n]; v.z *= rm[n]; v.w *= rm[n];
+        *reinterpret_cast<float4*>(s_in + pp * LD + 4 * g) = v;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NW; ++n) {
+      const int i = tid + 256 * n;
+      if (i < nw) *reinterpret_cast<float4*>(s_w + (i >> G4S) * LD + 4 * (i & (G4 - 1))) = rw[n];
+    }
+  };
+  f32x16 acc[NB];
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[m][j] = 0.f;
+  fetch(0);
+  store();
+  __syncthreads();
+  for (int c0 = 0; c0 < p.Cin; c0 += KC) {
+    const bool more = c0 + KC < p.Cin;
+    if (more) fetch(c0 + KC);
+    const float* pw = s_w + (cb + r) * K * LD + 4 * hh;
+    const float* pa = s_in + (pb + r - lo) * LD + 4 * hh;
+    for (int k = 0; k < K; ++k) {
+      const float* pak = pa + k * p.dil * LD;
+      const float* pwk = pw + k * LD;
+#pragma unroll
+      for (int g = 0; g < KC / 8; ++g) {
+        const float4 w = *reinterpret_cast<const float4*>(pwk + 8 * g);
+        float4 a[NB];
+#pragma unroll
+        for (int m = 0; m < NB; ++m) a[m] = *reinterpret_cast<const float4*>(pak + m * 32 * LD + 8 * g);
+#pragma unroll
+        for (int m = 0; m < NB; ++m) {
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].x, w.x, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].y, w.y, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].z, w.z, acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m].w, w.w, acc[m], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  const int o = a0 + cb + r;
+  if (o >= p.Cout) return;
+  const float bias = p.bias ? p.bias[o] : 0.f;
+#pragma unroll
+  for (int m = 0; m < NB; ++m)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int q = q0 + pb + 32 * m + acc_row(j, hh);
+      if (q >= p.Q) continue;
+      const int t = q * p.out_stride + p.out_off;
+      if (t < 0 || t >= p.Tout) continue;
+      float v = acc[m][j] + bias;
+      if (p.relu) v = fmaxf(v, 0.f);
+      if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
+      const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
+      if (p.accumulate) v = p.out[oi] + v;
+      if (p.div != 0.f) v = v / p.div;
+      if (p.out_tanh) v = tanhf(v);
+      if (p.out_mask) v *= p.out_mask[(long)b * p.Tout + t];
+      p.out[oi] = v;
+    }
+}
+
 // bf16 variant (HiFi-GAN throughput mode): operands rounded to bf16 when staged, fp32 accumulation on
 // v_mfma_f32_32x32x16_bf16; 32-channel chunks = two 16-deep MFMA steps per tap; same tile, epilogue and semantics
 template <int KM, int SP>
@@ -185,6 +311,35 @@ hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
     if (p.K <= 3 && span <= 10) hipLaunchKernelGGL((c1d_bf16_kernel<3, 10>), grid, dim3(256), 0, s, p);
     else if (p.K <= 7 && span <= 30) hipLaunchKernelGGL((c1d_bf16_kernel<7, 30>), grid, dim3(256), 0, s, p);
     else hipLaunchKernelGGL((c1d_bf16_kernel<C1_KMAX, C1_SPAN>), grid, dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
+  if (p.wpk && !p.in_chan_major && p.Cin % 4 == 0 && p.in_cs % 4 == 0 && ((uintptr_t)p.in & 15) == 0 &&
+      ((uintptr_t)p.wpk & 15) == 0) {
+    // output-channel tile 32 for narrow convs (HiFi-GAN's last stage, conv_post); 64 frames per wave, or 32 when the
+    // 64-frame grid leaves most of the last round of workgroups (2 per CU) empty
+    const bool narrow = p.Cout <= 32;
+    const int ft2 = narrow ? 256 : 128, ct = narrow ? 32 : 64;
+    const long n2 = (long)p.B * ((p.Q + ft2 - 1) / ft2) * ((p.Cout + ct - 1) / ct);
+    const long n1 = (long)p.B * ((p.Q + ft2 / 2 - 1) / (ft2 / 2)) * ((p.Cout + ct - 1) / ct);
+    auto fill = [](long n) { const long slots = 512; return (double)n / (double)(((n + slots - 1) / slots) * slots); };
+    const int nb = fill(n1) > fill(n2) + 0.2 ? 1 : 2;
+    const dim3 g((unsigned)(p.B * ((p.Q + (nb == 2 ? ft2 : ft2 / 2) - 1) / (nb == 2 ? ft2 : ft2 / 2))),
+                 (unsigned)((p.Cout + ct - 1) / ct));
+#define GT_C1D_PK(KM, KC, SP)                                                                               \
+  do {                                                                                                      \
+    if (narrow) {                                                                                           \
+      if (nb == 2) hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 32, 2>), g, dim3(256), 0, s, p);           \
+      else hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 32, 1>), g, dim3(256), 0, s, p);                   \
+    } else {                                                                                                \
+      if (nb == 2) hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 64, 2>), g, dim3(256), 0, s, p);           \
+      else hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 64, 1>), g, dim3(256), 0, s, p);                   \
+    }                                                                                                       \
+  } while (0)
+    if (p.K <= 3 && span <= 10) GT_C1D_PK(3, 32, 10);
+    else if (p.K <= 7 && span <= 30) GT_C1D_PK(7, 16, 30);
+    else if (span <= 50) GT_C1D_PK(11, 16, 50);
+    else GT_C1D_PK(11, 16, C1_SPAN);
+#undef GT_C1D_PK
     return hipGetLastError();
   }
   if (p.K <= 3 && span <= 10) hipLaunchKernelGGL((c1d_kernel<3, 32, 10>), grid, dim3(256), 0, s, p);

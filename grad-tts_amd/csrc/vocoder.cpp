@@ -42,6 +42,8 @@ struct gt_vocoder {
   std::map<std::string, int64_t> bfoff;  // bf16 weights [o][k][c] (ups: [phase][o][2][c]) in devbf
   uint16_t* devbf = nullptr;
   int64_t devbf_numel = 0;
+  float* devpk = nullptr;                // fp32 weights in the same [o][k][c] layout (c1d_pk_kernel), offsets = bfoff
+  int64_t devpk_numel = 0;
 };
 
 namespace {
@@ -82,28 +84,36 @@ int upload(gt_vocoder* v) {
     v->woff[key + ".bias"] = (int64_t)h.size();
     h.insert(h.end(), b.begin(), b.end());
   }
-  // bf16 copies of the effective weights in the operand layout of c1d_bf16_kernel
+  // bf16 and fp32 copies of the effective weights in the operand layout of c1d_bf16_kernel / c1d_pk_kernel
   std::vector<uint16_t> hb;
+  std::vector<float> hp;
   v->bfoff.clear();
   for (size_t i = 0; i < v->inv.size(); i += 3) {
     const std::string key = v->inv[i].first.substr(0, v->inv[i].first.size() - 5);
     const std::vector<int64_t>& d = v->inv[i + 2].second;
     const float* w = h.data() + v->woff[key + ".weight"];
-    v->bfoff[key] = (int64_t)hb.size();
+    v->bfoff[key] = (int64_t)hp.size();
     if (key.rfind("ups.", 0) == 0) {   // ConvTranspose1d [Cin][Cout][k], k = 2u: per phase r, [o][j][c] = w[c][o][r + u j]
       const int64_t ci = d[0], co = d[1], kk = d[2], u = kk / 2;
       for (int64_t r = 0; r < u; ++r)
         for (int64_t o = 0; o < co; ++o)
           for (int64_t j = 0; j < 2; ++j)
-            for (int64_t c = 0; c < ci; ++c) hb.push_back(to_bf16(w[(c * co + o) * kk + r + u * j]));
+            for (int64_t c = 0; c < ci; ++c) hp.push_back(w[(c * co + o) * kk + r + u * j]);
     } else {                             // Conv1d [Cout][Cin][k] -> [o][k][c]
       const int64_t co = d[0], ci = d[1], kk = d[2];
       for (int64_t o = 0; o < co; ++o)
         for (int64_t k = 0; k < kk; ++k)
-          for (int64_t c = 0; c < ci; ++c) hb.push_back(to_bf16(w[(o * ci + c) * kk + k]));
+          for (int64_t c = 0; c < ci; ++c) hp.push_back(w[(o * ci + c) * kk + k]);
     }
-    while (hb.size() % 8) hb.push_back(0);   // 16-byte aligned starts
+    while (hp.size() % 8) hp.push_back(0.f);   // 16-byte aligned bf16 starts (32-byte fp32)
   }
+  hb.reserve(hp.size());
+  for (float x : hp) hb.push_back(to_bf16(x));
+  if (v->devpk && (int64_t)hp.size() != v->devpk_numel) { (void)hipFree(v->devpk); v->devpk = nullptr; }
+  if (!v->devpk && hipMalloc(&v->devpk, hp.size() * 4) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
+  v->devpk_numel = (int64_t)hp.size();
+  if (hipMemcpy(v->devpk, hp.data(), hp.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
   if (v->devbf && (int64_t)hb.size() != v->devbf_numel) { (void)hipFree(v->devbf); v->devbf = nullptr; }
   if (!v->devbf && hipMalloc(&v->devbf, hb.size() * 2) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
   v->devbf_numel = (int64_t)hb.size();
@@ -187,6 +197,7 @@ void gt_vocoder_destroy(gt_vocoder* v) {
   if (!v) return;
   if (v->dev) (void)hipFree(v->dev);
   if (v->devbf) (void)hipFree(v->devbf);
+  if (v->devpk) (void)hipFree(v->devpk);
   delete v;
 }
 
@@ -242,11 +253,13 @@ int gt_vocoder_forward(gt_vocoder* v, const float* mel, int64_t B, int64_t T, fl
   hipError_t err = hipSuccess;
   auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
   const int Bi = (int)B;
-  auto BF = [&](const std::string& k) { return v->devbf + v->bfoff.at(k); };
   auto launch = [&](C1dParams& p, const std::string& key, int phase) {   // fp32 or bf16 operands per the handle
+    const int64_t off = v->bfoff.at(key) + (int64_t)phase * p.Cout * p.K * p.Cin;
     if (v->bf16) {
       p.bf16 = 1;
-      p.wbf = BF(key) + (int64_t)phase * p.Cout * p.K * p.Cin;
+      p.wbf = v->devbf + off;
+    } else {
+      p.wpk = v->devpk + off;
     }
     chk(launch_c1d(p, s));
   };
