@@ -17,7 +17,11 @@ struct GConvParams {
   const float* out_mask; int lvl_out; // non-null: multiply the output by the level mask
   float* out; int out_cs, out_c0;     // output channel stride / first channel (writes into a wider tensor)
   int accumulate;
+  float* wpk;                         // scratch of Cout * KS^2 * Cin floats (gconv_wpk_floats): the 3x3 / 4x4
+                                      // stride-1 relations repack the weights there and run the float4-staged kernel
 };
+// scratch the packed-weight path of launch_gconv needs (0: the relation runs without it)
+long gconv_wpk_floats(const GConvParams& p);
 // dW(a, b, k) = sum_u P[u][a] Q[v(u,k)][b]; U grid (Fu, Tu), V grid (Fv, Tv)
 struct WGradParams {
   int B, Fu, Tu, A, Fv, Tv, Bc, KS, S, PAD;

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   const bool flip = dil ? !p.flip : p.flip != 0;
   const bool a_fast = p.wsa < p.wsc;   // stage weights along their contiguous axis
   const int ic = tid % MC_KC, iq = tid / MC_KC;   // input staging: channel, column lane (NCL columns per pass)
-  float rin[PR][NCOL], rw[NWJ];
+  float rin[PR][NCOL], rw[NWJ], rm[NCOL];
   auto load = [&](int c0) {   // next chunk into registers (in flight during the MFMAs of the current one)
     const int ci = c0 + ic;
 #pragma unroll
@@ -86,11 +86,12 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
         bool ok = col < PC && fd >= 0 && td >= 0 && ci < p.Cin;
         int fi = fd, ti = td;
         if (dil) { ok = ok && fd % p.S == 0 && td % p.S == 0; fi = fd / p.S; ti = td / p.S; }
-        if (ok && fi < p.Fi && ti < p.Ti) {
-          v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
-          if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
-        }
+        if (ok && fi < p.Fi && ti < p.Ti) v = p.in[(((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + ci];
         rin[row][q] = v;
+        if (row == 0) {   // the mask depends on the column only; multiplied in when staged
+          const int tc = dil ? td / p.S : td;
+          rm[q] = (p.mask && tc >= 0 && tc < p.Ti) ? mask_at(p.mask, p.T0, b, tc, p.lvl_in) : 1.f;
+        }
       }
     }
 #pragma unroll
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
     for (int row = 0; row < PR; ++row)
 #pragma unroll
       for (int q = 0; q < NCOL; ++q)
-        if (iq + NCL * q < PC) s_in[row][iq + NCL * q][ic] = rin[row][q];
+        if (iq + NCL * q < PC) s_in[row][iq + NCL * q][ic] = rin[row][q] * rm[q];
 #pragma unroll
     for (int j = 0; j < NWJ; ++j) {
       const int i = tid + 256 * j;
@@ -178,6 +179,162 @@ __global__ __launch_bounds__(256) void mconv_kernel(GConvParams p) {
   }
 }
 
+// wpk[a][k][c] = W(a, c, flip ? KK - 1 - k : k): the weights of one gconv launch with the input channel contiguous,
+// so mconv_pk_kernel stages a chunk of KC channels of every (a, k) row as float4 runs
+__global__ void gconv_wpack_kernel(const float* w, long wsa, long wsc, int KK, int flip, int Cout, int Cin, float* wpk) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)Cout * KK * Cin) return;
+  const int c = (int)(i % Cin);
+  const long rk = i / Cin;
+  const int k = (int)(rk % KK), a = (int)(rk / KK);
+  wpk[i] = w[(long)a * wsa + (long)c * wsc + (flip ? KK - 1 - k : k)];
+}
+
+// The stride-1 relations (3x3 convs and their dgrads; with the S = 2 dilated input, the Downsample dgrad and
+// ConvTranspose2d) with packed weights: same tile and wave ownership as mconv_kernel (RH x TW positions x 64 output
+// channels, each wave 64 positions x 64 channels as 2 x 2 blocks of 32 x 32), but KC-channel chunks staged as float4
+// (input [row][col][c] and weights [a][k][c], LDS rows of KC + 4 floats), the next chunk fetched into registers
+// during the MFMAs (mask applied when the registers are written to LDS), and operands read as float4: channels
+// 8g + 4h .. + 3 for lane half h feed four v_mfma_f32_32x32x2_f32 (element e = K index h of channel 8g + 4h + e on
+// both operands), so one read of each of the four operands feeds 16 MFMAs.
+// NY = 32-channel blocks per wave (tile of 32 NY output channels): NY = 1 doubles the workgroups of the small
+// levels (level 2 has 64 position tiles per batch of 16) and fits three workgroups per CU.
+template <int KS, int RH, int TW, int KC, int NY>
+__global__ __launch_bounds__(256, NY == 1 ? 3 : 2) void mconv_pk_kernel(GConvParams p) {
+  constexpr int KK = KS * KS, PC = TW - 1 + KS, PR = RH - 1 + KS, LD = KC + 4, G4 = KC / 4;
+  constexpr int G4S = G4 == 8 ? 3 : G4 == 4 ? 2 : 1;   // log2(G4)
+  // output-channel row stride of the weights: an odd number of 16-byte groups, so the 16 lanes of a float4 read
+  // (16 output channels) hit distinct bank groups (KS = 4, KC = 8: 16 x 12 floats would put all of them on one)
+  constexpr int WAS = ((KK * LD / 4) & 1) ? KK * LD : KK * LD + 4;
+  constexpr int CT = 32 * NY, NPOS = PR * PC, NIN = (NPOS * G4 + 255) / 256, NWT = (CT * KK * G4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_in[NPOS * LD];
+  __shared__ __attribute__((aligned(16))) float s_w[CT * WAS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int n_tt = (p.To + TW - 1) / TW, n_fr = (p.Fo + RH - 1) / RH;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int fo0 = (bid % n_fr) * RH;
+  const int b = bid / n_fr;
+  const int to0 = tt * TW, a0 = blockIdx.y * CT;
+  const bool dil = p.transposed != 0;   // the S = 2 dilated input: odd coordinates are zeros
+  const int pad = dil ? KS - 1 - p.PAD : p.PAD;
+  const int nw = CT * KK * G4, wrows = KK * (p.Cout - a0);
+  float4 rin[NIN], rw[NWT];
+  float rm[NIN];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int n = 0; n < NIN; ++n) {
+      const int i = tid + 256 * n, rc = i >> G4S, g = i & (G4 - 1);
+      const int row = rc / PC, col = rc - row * PC;
+      int fi = fo0 - pad + row, ti = to0 - pad + col;
+      bool ok = rc < NPOS && fi >= 0 && ti >= 0 && c0 + 4 * g < p.Cin;
+      if (dil) { ok = ok && !(fi & 1) && !(ti & 1); fi >>= 1; ti >>= 1; }
+      rin[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+      rm[n] = 1.f;
+      if (ok && fi < p.Fi && ti < p.Ti) {
+        rin[n] = *reinterpret_cast<const float4*>(p.in + (((long)b * p.Fi + fi) * p.Ti + ti) * p.Cin + c0 + 4 * g);
+        if (p.mask) rm[n] = mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NWT; ++n) {
+      const int i = tid + 256 * n, ok = i >> G4S, g = i & (G4 - 1);
+      rw[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < nw && ok < wrows && c0 + 4 * g < p.Cin)
+        rw[n] = *reinterpret_cast<const float4*>(p.wpk + ((long)a0 * KK + ok) * p.Cin + c0 + 4 * g);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int n = 0; n < NIN; ++n) {
+      const int i = tid + 256 * n, rc = i >> G4S, g = i & (G4 - 1);
+      if (rc < NPOS) {
+        float4 v = rin[n];
+        v.x *= rm[n]; v.y *= rm[n]; v.z *= rm[n]; v.w *= rm[n];
+        *reinterpret_cast<float4*>(s_in + rc * LD + 4 * g) = v;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NWT; ++n) {
+      const int i = tid + 256 * n;
+      if (i < nw) {
+        const int ak = i >> G4S, a = ak / KK;
+        *reinterpret_cast<float4*>(s_w + a * WAS + (ak - a * KK) * LD + 4 * (i & (G4 - 1))) = rw[n];
+      }
+    }
+  };
+  f32x16 acc[2][NY];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < NY; ++y)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[x][y][j] = 0.f;
+  const float* pa[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const int q = 64 * wv + 32 * x + r;
+    const int prow = q / TW < RH ? q / TW : 0;   // positions past RH rows read row 0; their outputs are dropped
+    pa[x] = s_in + (prow * PC + q % TW) * LD + 4 * hh;
+  }
+  const float* pw = s_w + r * WAS + 4 * hh;   // output channel r; + 32 WAS for the second block
+  fetch(0);
+  store();
+  __syncthreads();
+  for (int c0 = 0; c0 < p.Cin; c0 += KC) {
+    const bool more = c0 + KC < p.Cin;
+    if (more) fetch(c0 + KC);
+    // (tap, 8-channel group) steps, software-pipelined: the operands of step s + 1 are read before the 16 MFMAs of
+    // step s are issued
+    constexpr int NST = KK * (KC / 8);
+    auto rd = [&](int st, float4* o) {
+      const int k = st / (KC / 8), g = st % (KC / 8);
+      const int off = ((k / KS) * PC + k % KS) * LD + 8 * g;
+      o[0] = *reinterpret_cast<const float4*>(pa[0] + off);
+      o[1] = *reinterpret_cast<const float4*>(pa[1] + off);
+      o[2] = *reinterpret_cast<const float4*>(pw + k * LD + 8 * g);
+      if (NY == 2) o[3] = *reinterpret_cast<const float4*>(pw + 32 * WAS + k * LD + 8 * g);
+    };
+    float4 opd[2][4];
+    rd(0, opd[0]);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      if (st + 1 < NST) rd(st + 1, opd[(st + 1) & 1]);
+      const float4 x0 = opd[st & 1][0], x1 = opd[st & 1][1], w0 = opd[st & 1][2], w1 = opd[st & 1][3];
+#define GT_MC4(E)                                                                                    \
+  acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.E, w0.E, acc[0][0], 0, 0, 0);                  \
+  if (NY == 2) acc[0][NY - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.E, w1.E, acc[0][NY - 1], 0, 0, 0); \
+  acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.E, w0.E, acc[1][0], 0, 0, 0);                  \
+  if (NY == 2) acc[1][NY - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.E, w1.E, acc[1][NY - 1], 0, 0, 0);
+      GT_MC4(x) GT_MC4(y) GT_MC4(z) GT_MC4(w)
+#undef GT_MC4
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int y = 0; y < NY; ++y) {
+    const int a = a0 + 32 * y + r;
+    if (a >= p.Cout) continue;
+    const float bias = p.bias ? p.bias[a] : 0.f;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int q = 64 * wv + 32 * x + acc_row(j, hh);
+        const int fo = fo0 + q / TW, to = to0 + q % TW;
+        if (q / TW >= RH || fo >= p.Fo || to >= p.To) continue;
+        const float om = p.out_mask ? mask_at(p.out_mask, p.T0, b, to, p.lvl_out) : 1.f;
+        const long o = (((long)b * p.Fo + fo) * p.To + to) * p.out_cs + p.out_c0 + a;
+        const float v = (acc[x][y][j] + bias) * om;
+        p.out[o] = p.accumulate ? p.out[o] + v : v;
+      }
+  }
+}
+
 // 1x1 convs (qkv / to_out / res_conv / final_conv and their dgrads): one row of 64 positions x 64 channels per
 // workgroup, 32-channel chunks (128-byte input rows), waves 2 x 2 over (positions, channels)
 __global__ __launch_bounds__(256) void mconv1_kernel(GConvParams p) {
@@ -193,18 +350,19 @@ __global__ __launch_bounds__(256) void mconv1_kernel(GConvParams p) {
   const int to0 = tt * 64, a0 = blockIdx.y * 64;
   const int pb = (wv & 1) * 32, cb = (wv >> 1) * 32;
   const bool a_fast = p.wsa < p.wsc;
-  float rin[8], rw[8];
+  float rin[8], rw[8], rm[8];
   auto load = [&](int c0) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {   // input: 32 channels x 64 positions
+    for (int j = 0; j < 8; ++j) {   // input: 32 channels x 64 positions (mask multiplied in when staged)
       const int i = tid + 256 * j, c = i & 31, pp = i >> 5;
       const int ti = to0 + pp, ci = c0 + c;
-      float v = 0.f;
+      float v = 0.f, m = 1.f;
       if (ti < p.Ti && ci < p.Cin) {
         v = p.in[(((long)b * p.Fi + fo) * p.Ti + ti) * p.Cin + ci];
-        if (p.mask) v *= mask_at(p.mask, p.T0, b, ti, p.lvl_in);
+        if (p.mask) m = mask_at(p.mask, p.T0, b, ti, p.lvl_in);
       }
       rin[j] = v;
+      rm[j] = m;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {   // weights: 64 a x 32 c
@@ -222,7 +380,7 @@ __global__ __launch_bounds__(256) void mconv1_kernel(GConvParams p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int i = tid + 256 * j;
-      s_in[i >> 5][i & 31] = rin[j];
+      s_in[i >> 5][i & 31] = rin[j] * rm[j];
       const int a = a_fast ? (i & 63) : (i >> 5), c = a_fast ? (i >> 6) : (i & 31);
       s_w[c][a] = rw[j];
     }
@@ -274,7 +432,8 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
   for (int g = 0; g < KG; ++g)
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[g][j] = 0.f;
-  float rp[NPJ], rq[NR][NQ];
+  float rp[NPJ], rq[NR][NQ], pm[NPJ], qm[NQ];   // masks kept apart: multiplied in when staged, so the loads stay
+                                                //   in flight during the MFMAs
   auto load = [&](long sg) {
     const int tt = (int)(sg % n_tt);
     const int fu = (int)((sg / n_tt) % p.Fu);
@@ -283,12 +442,18 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
 #pragma unroll
     for (int j = 0; j < NPJ; ++j) {
       const int u = sl + 4 * j;
-      float v = 0.f;
+      float v = 0.f, m = 1.f;
       if (t0 + u < p.Tu && a0 + sc < p.A) {
         v = p.P[(((long)b * p.Fu + fu) * p.Tu + t0 + u) * p.A + a0 + sc];
-        if (p.pmask) v *= mask_at(p.pmask, p.T0, b, t0 + u, p.lvl_p);
+        if (p.pmask) m = mask_at(p.pmask, p.T0, b, t0 + u, p.lvl_p);
       }
       rp[j] = v;
+      pm[j] = m;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int col = sl + 4 * q, tv = t0 * S - p.PAD + col;
+      qm[q] = (p.qmask && col < NCOL && tv >= 0 && tv < p.Tv) ? mask_at(p.qmask, p.T0, b, tv, p.lvl_q) : 1.f;
     }
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) {
@@ -297,10 +462,8 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
       for (int q = 0; q < NQ; ++q) {
         const int col = sl + 4 * q, tv = t0 * S - p.PAD + col;
         float v = 0.f;
-        if (col < NCOL && fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + sc < p.Bc) {
+        if (col < NCOL && fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + sc < p.Bc)
           v = p.Q[(((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + sc];
-          if (p.qmask) v *= mask_at(p.qmask, p.T0, b, tv, p.lvl_q);
-        }
         rq[rr][q] = v;
       }
     }
@@ -309,12 +472,12 @@ __global__ __launch_bounds__(256) void mwgrad_kernel(WGradParams p, int splits, 
   for (long sg = s_lo; sg < s_hi; ++sg) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < NPJ; ++j) s_p[(sl + 4 * j) * PS + sc] = rp[j];
+    for (int j = 0; j < NPJ; ++j) s_p[(sl + 4 * j) * PS + sc] = rp[j] * pm[j];
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr)
 #pragma unroll
       for (int q = 0; q < NQ; ++q)
-        if (sl + 4 * q < NCOL) s_q[(rr * NCOL + sl + 4 * q) * QS + sc] = rq[rr][q];
+        if (sl + 4 * q < NCOL) s_q[(rr * NCOL + sl + 4 * q) * QS + sc] = rq[rr][q] * qm[q];
     __syncthreads();
     if (sg + 1 < s_hi) load(sg + 1);
 #pragma unroll 2
@@ -741,6 +904,13 @@ __global__ void input_pack_kernel(const float* mu, const float* xt, const float*
   if (cin == 3) out[i * cin + 2] = s[(long)b * 80 + f];
 }
 
+long gconv_wpk_floats(const GConvParams& p) {
+  // the stride-1 relations (S = 2 only through the dilated input of the transposed relation), whole float4 runs
+  const bool ok = (p.KS == 1 || p.KS == 3 || p.KS == 4) && (p.transposed ? p.S == 2 : p.S == 1) && p.Cin % 4 == 0 &&
+                  (p.KS == 4 ? p.transposed : true) && (p.KS == 1 ? !p.transposed : true);
+  return ok ? (long)p.Cout * p.KS * p.KS * p.Cin : 0;
+}
+
 hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   if (p.KS > 4 || p.S > 2) return hipErrorInvalidValue;
   auto mgrid = [&](int rh, int tw) {
@@ -748,6 +918,37 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   };
   auto slots = [&](int rh, int tw) { return (long)((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw); };
   const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
+  if (gconv_wpk_floats(p) > 0 && p.wpk && ((uintptr_t)p.in & 15) == 0 && ((uintptr_t)p.wpk & 15) == 0) {
+    const int KK = p.KS * p.KS;
+    const bool flip = p.transposed ? !p.flip : p.flip != 0;
+    const long n = (long)p.Cout * KK * p.Cin;
+    hipLaunchKernelGGL(gconv_wpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.w, p.wsa, p.wsc, KK,
+                       (int)flip, p.Cout, p.Cin, p.wpk);
+    // 32-channel tiles when 64-channel tiles would leave the CUs less than two workgroups each
+    auto ny1 = [&](int rh, int tw) { return (long)p.B * slots(rh, tw) * ((p.Cout + 63) / 64) < 384; };
+    auto g2 = [&](int rh, int tw, int ct) {
+      return dim3((unsigned)((long)p.B * slots(rh, tw)), (unsigned)((p.Cout + ct - 1) / ct));
+    };
+#define GT_MPK(KS_, RH_, TW_, KC_)                                                                            \
+  do {                                                                                                        \
+    if (ny1(RH_, TW_)) hipLaunchKernelGGL((mconv_pk_kernel<KS_, RH_, TW_, KC_, 1>), g2(RH_, TW_, 32), dim3(256), 0, s, p); \
+    else hipLaunchKernelGGL((mconv_pk_kernel<KS_, RH_, TW_, KC_, 2>), g2(RH_, TW_, 64), dim3(256), 0, s, p);           \
+  } while (0)
+    const long s4 = slots(4, 64), s8 = slots(8, 32), s5 = slots(5, 48);
+    const int shape = (s4 <= s8 && s4 <= s5) ? 4 : (s8 <= s5) ? 8 : 5;
+    if (p.KS == 4) GT_MPK(4, 4, 64, 8);
+    else if (p.KS == 1) {   // 1x1: 32-channel chunks
+      if (shape == 4) GT_MPK(1, 4, 64, 32);
+      else if (shape == 8) GT_MPK(1, 8, 32, 32);
+      else GT_MPK(1, 5, 48, 32);
+    } else {
+      if (shape == 4) GT_MPK(3, 4, 64, 16);
+      else if (shape == 8) GT_MPK(3, 8, 32, 16);
+      else GT_MPK(3, 5, 48, 16);
+    }
+#undef GT_MPK
+    return hipGetLastError();
+  }
   if (cfg == 11) {
     hipLaunchKernelGGL(mconv1_kernel, dim3((unsigned)((long)p.B * p.Fo * ((p.To + 63) / 64)),
                                            (unsigned)((p.Cout + 63) / 64)), dim3(256), 0, s, p);

@@ -83,6 +83,10 @@ struct Trainer {
   void gconv(const float* in, int Ci, int l_in, bool in_mask, const float* w, long wsa, long wsc, int KS, int S, int PAD,
              int flip, const float* bias, float* out, int Co, int l_out, bool out_mask, int out_cs, int out_c0, int acc,
              bool transposed = false, int line = __builtin_LINE()) {
+    GConvParams p{};
+    p.Cin = Ci; p.Cout = Co; p.KS = KS; p.S = S; p.transposed = transposed;
+    const long nwpk = gconv_wpk_floats(p);   // repacked weights of this launch (taken in the measuring pass too)
+    float* wpk = nwpk > 0 ? A.take((size_t)nwpk) : nullptr;
     if (!run) return;
     {
       const Lvl I = L(l_in), O = L(l_out);
@@ -91,8 +95,9 @@ struct Trainer {
       need(w, (long)(Co - 1) * wsa + (long)(Ci - 1) * wsc + KS * KS, "gconv weight", line);
       if (bias) need(bias, Co, "gconv bias", line);
     }
+    if (wpk) need(wpk, nwpk, "gconv packed weights", line);
     if (dry) return;
-    GConvParams p{};
+    p.wpk = wpk;
     p.B = B; p.Fi = L(l_in).F; p.Ti = L(l_in).T; p.Cin = Ci; p.Fo = L(l_out).F; p.To = L(l_out).T; p.Cout = Co;
     p.KS = KS; p.S = S; p.PAD = PAD; p.transposed = transposed; p.flip = flip;
     p.in = in; p.w = w; p.wsa = wsa; p.wsc = wsc; p.bias = bias;
