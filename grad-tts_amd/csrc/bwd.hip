@@ -517,6 +517,105 @@ __global__ void mwgrad_reduce_kernel(const float* part, int splits, int A, int B
   *d = accumulate ? *d + s : s;
 }
 
+// 3x3 stride-1 weight gradient with the positions contiguous in LDS: P^T [a][u] and the 3-row Q^T patch [b][kh][col]
+// staged from float4 loads along the channels (transposed on the LDS write; masks multiplied in there, so the next
+// segment's loads stay in flight during the MFMAs). Per 8 positions u0: one float4 of P^T (positions u0 + 4h .. + 3)
+// feeds the nine taps; tap (kh, kw) reads Q^T at column u0 + 4h + kw (16-, 4- or 8-byte aligned for kw = 0, 1, 2),
+// four v_mfma_f32_32x32x2_f32 each (element e = K index h of position u0 + 4h + e on both operands). Same tile, split
+// and partial layout as mwgrad_kernel; LDS row strides of an odd number of 16-byte groups.
+template <int SEG>
+__global__ __launch_bounds__(256, 2) void mwgrad_pk_kernel(WGradParams p, int splits, float* part) {
+  constexpr int NCOL = SEG + 2, PST = SEG + 4, QW = SEG + 4, QBS = 3 * QW;
+  static_assert(((PST / 4) & 1) && ((QBS / 4) & 1) && SEG % 16 == 0, "LDS strides");
+  constexpr int NPF = SEG * 16 / 256, NQF = (3 * NCOL * 16 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_p[64 * PST];
+  __shared__ __attribute__((aligned(16))) float s_q[64 * QBS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 64, split = blockIdx.z;
+  const int n_tt = (p.Tu + SEG - 1) / SEG, nseg = p.B * p.Fu * n_tt;
+  const int per = (nseg + splits - 1) / splits;
+  const int s_lo = split * per, s_hi = s_lo + per < nseg ? s_lo + per : nseg;
+  const int ab = (wv & 1) * 32, bb = (wv >> 1) * 32;
+  f32x16 acc[9];
+#pragma unroll
+  for (int g = 0; g < 9; ++g)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[g][j] = 0.f;
+  float4 rp[NPF], rq[NQF];
+  float pm[NPF], qm[NQF];
+  auto fetch = [&](int sg) {
+    const int tt = sg % n_tt, fu = (sg / n_tt) % p.Fu, b = sg / (n_tt * p.Fu), t0 = tt * SEG;
+#pragma unroll
+    for (int n = 0; n < NPF; ++n) {
+      const int i = tid + 256 * n, u = i >> 4, a4 = i & 15, t = t0 + u;
+      const bool ok = t < p.Tu && a0 + 4 * a4 < p.A;
+      rp[n] = ok ? *reinterpret_cast<const float4*>(p.P + (((long)b * p.Fu + fu) * p.Tu + t) * p.A + a0 + 4 * a4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      pm[n] = (ok && p.pmask) ? mask_at(p.pmask, p.T0, b, t, p.lvl_p) : 1.f;
+    }
+#pragma unroll
+    for (int n = 0; n < NQF; ++n) {
+      const int i = tid + 256 * n, rc = i >> 4, b4 = i & 15, row = rc / NCOL, col = rc - row * NCOL;
+      const int fv = fu - p.PAD + row, tv = t0 - p.PAD + col;
+      const bool ok = rc < 3 * NCOL && fv >= 0 && fv < p.Fv && tv >= 0 && tv < p.Tv && b0 + 4 * b4 < p.Bc;
+      rq[n] = ok ? *reinterpret_cast<const float4*>(p.Q + (((long)b * p.Fv + fv) * p.Tv + tv) * p.Bc + b0 + 4 * b4)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      qm[n] = (ok && p.qmask) ? mask_at(p.qmask, p.T0, b, tv, p.lvl_q) : 1.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int n = 0; n < NPF; ++n) {
+      const int i = tid + 256 * n, u = i >> 4, a4 = i & 15;
+      float* d = s_p + 4 * a4 * PST + u;
+      d[0] = rp[n].x * pm[n]; d[PST] = rp[n].y * pm[n]; d[2 * PST] = rp[n].z * pm[n]; d[3 * PST] = rp[n].w * pm[n];
+    }
+#pragma unroll
+    for (int n = 0; n < NQF; ++n) {
+      const int i = tid + 256 * n, rc = i >> 4, b4 = i & 15, row = rc / NCOL, col = rc - row * NCOL;
+      if (rc < 3 * NCOL) {
+        float* d = s_q + 4 * b4 * QBS + row * QW + col;
+        d[0] = rq[n].x * qm[n]; d[QBS] = rq[n].y * qm[n]; d[2 * QBS] = rq[n].z * qm[n]; d[3 * QBS] = rq[n].w * qm[n];
+      }
+    }
+  };
+  const float* pp = s_p + (ab + r) * PST + 4 * hh;
+  const float* pq = s_q + (bb + r) * QBS + 4 * hh;
+  if (s_lo < s_hi) fetch(s_lo);
+  for (int sg = s_lo; sg < s_hi; ++sg) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (sg + 1 < s_hi) fetch(sg + 1);
+#pragma unroll
+    for (int u0 = 0; u0 < SEG; u0 += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(pp + u0);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const float* q = pq + kh * QW + u0;
+        const float4 q0 = *reinterpret_cast<const float4*>(q);
+        const float4 q1 = make_float4(q[1], q[2], q[3], q[4]);
+        const float2 q2a = *reinterpret_cast<const float2*>(q + 2), q2b = *reinterpret_cast<const float2*>(q + 4);
+        const float4 q2 = make_float4(q2a.x, q2a.y, q2b.x, q2b.y);
+#define GT_WG3(E)                                                                          \
+  acc[3 * kh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q0.E, acc[3 * kh], 0, 0, 0);         \
+  acc[3 * kh + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q1.E, acc[3 * kh + 1], 0, 0, 0); \
+  acc[3 * kh + 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q2.E, acc[3 * kh + 2], 0, 0, 0);
+        GT_WG3(x) GT_WG3(y) GT_WG3(z) GT_WG3(w)   // three independent accumulator chains interleaved
+#undef GT_WG3
+      }
+    }
+  }
+  const int bc = b0 + bb + r;
+#pragma unroll
+  for (int g = 0; g < 9; ++g)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int a = a0 + ab + acc_row(j, hh);
+      if (a < p.A && bc < p.Bc) part[(((long)split * 9 + g) * p.A + a) * p.Bc + bc] = acc[g][j];
+    }
+}
+
 // 48-position segments where they cut the padded frames (a level-2 row of 43 frames: 48 instead of 64)
 static int mwgrad_seg(const WGradParams& p) {
   return (p.KS == 3 && p.S == 1 && (p.Tu + 47) / 48 * 48 < (p.Tu + 31) / 32 * 32) ? 48 : 32;
@@ -539,7 +638,10 @@ hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, 
   const int splits = mwgrad_splits(p);
   const int groups = p.KS == 4 ? 2 : 1;
   const dim3 grid((p.A + 63) / 64, (p.Bc + 63) / 64, splits * groups);
-  if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
+  const bool pk = cfg == 31 && p.A % 4 == 0 && p.Bc % 4 == 0 && ((uintptr_t)p.P & 15) == 0 && ((uintptr_t)p.Q & 15) == 0;
+  // (48-position segments for the 43-frame rows would need more registers than two waves per SIMD leave)
+  if (pk) hipLaunchKernelGGL((mwgrad_pk_kernel<32>), grid, dim3(256), 0, strm, p, splits, part);
+  else if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
   else if (cfg == 31 && mwgrad_seg(p) == 48)
     hipLaunchKernelGGL((mwgrad_kernel<3, 1, 48>), grid, dim3(256), 0, strm, p, splits, part);
   else if (cfg == 31) hipLaunchKernelGGL((mwgrad_kernel<3, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
@@ -863,14 +965,25 @@ __global__ void linear_wgrad_kernel(const float* dY, const float* X, int B, int 
   }
 }
 // dX[b][i] (+)= (sum_o W[o][i] dY[b][o]) * (pre ? mish'(pre[b][i]) : 1)
-__global__ void linear_dgrad_kernel(const float* dY, const float* W, int I, int O, const float* pre, float* dX,
-                                    int accumulate) {
-  const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < I; i += blockDim.x) {
+__global__ __launch_bounds__(256) void linear_dgrad_kernel(const float* dY, const float* W, int I, int O,
+                                                           const float* pre, float* dX, int accumulate) {
+  // four partial sums over o (o = q mod 4) per input i, added in a fixed order
+  __shared__ float red[4][64];
+  const int b = blockIdx.x, il = threadIdx.x & 63, q = threadIdx.x >> 6;
+  for (int i0 = 0; i0 < I; i0 += 64) {
+    const int i = i0 + il;
     float s = 0.f;
-    for (int o = 0; o < O; ++o) s += W[(long)o * I + i] * dY[(long)b * O + o];
-    if (pre) s *= mish_grad(pre[(long)b * I + i]);
-    dX[(long)b * I + i] = accumulate ? dX[(long)b * I + i] + s : s;
+    if (i < I)
+#pragma unroll 4
+      for (int o = q; o < O; o += 4) s += W[(long)o * I + i] * dY[(long)b * O + o];
+    red[q][il] = s;
+    __syncthreads();
+    if (q == 0 && i < I) {
+      float t = ((red[0][il] + red[1][il]) + red[2][il]) + red[3][il];
+      if (pre) t *= mish_grad(pre[(long)b * I + i]);
+      dX[(long)b * I + i] = accumulate ? dX[(long)b * I + i] + t : t;
+    }
+    __syncthreads();
   }
 }
 // SinusoidalPosEmb (diffusion.py:113-125) of t[b] -> [B][64]
@@ -1009,15 +1122,29 @@ __global__ void mask_sum_kernel(const float* mask, long n, float* out) {
 int pos_splits(long npos) { return (int)std::max<long>(1, std::min<long>(128, npos / 128)); }
 
 
-// out[g][j] (+)= sum_q part[g][q][j], q ascending
-__global__ void sum_splits_kernel(const float* part, int G, int S, long n, float* out, int accumulate) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long)G * n) return;
-  const long g = i / n, j = i % n;
+// out[g][j] (+)= sum_q part[g][q][j]: 16 outputs x 16 split lanes per workgroup; lane l sums q = l, l + 16, ...
+// ascending, then the 16 lane sums are added in lane order (fixed order: deterministic)
+__global__ __launch_bounds__(256) void sum_splits_kernel(const float* part, int G, int S, long n, float* out,
+                                                         int accumulate) {
+  __shared__ float red[16][17];
+  const int jl = threadIdx.x & 15, ql = threadIdx.x >> 4;
+  const long nj = (n + 15) / 16;
+  const long g = blockIdx.x / nj, j = (blockIdx.x % nj) * 16 + jl;
   float s = 0.f;
-#pragma unroll 8
-  for (int q = 0; q < S; ++q) s += part[(g * S + q) * n + j];
-  out[i] = accumulate ? out[i] + s : s;
+  if (j < n) {
+    const float* pg = part + g * S * n + j;
+#pragma unroll 4
+    for (int q = ql; q < S; q += 16) s += pg[(long)q * n];
+  }
+  red[ql][jl] = s;
+  __syncthreads();
+  if (ql == 0 && j < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) t += red[l][jl];
+    const long i = g * n + j;
+    out[i] = accumulate ? out[i] + t : t;
+  }
 }
 
 // part[b][s][c] = sum over split s of utterance b's positions of x[b][pos][c] (* y): grid (C/64, S, B), 64 channels
@@ -1226,7 +1353,7 @@ hipError_t launch_attn_headmm_mfma(const float* M, int trans, const float* X, in
 }
 
 static hipError_t sum_splits(const float* part, int G, int S, long n, float* out, int accumulate, hipStream_t strm) {
-  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)(((long)G * n + 255) / 256)), dim3(256), 0, strm, part, G, S, n,
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((long)G * ((n + 15) / 16))), dim3(256), 0, strm, part, G, S, n,
                      out, accumulate);
   return hipGetLastError();
 }
@@ -1336,7 +1463,8 @@ hipError_t launch_linear_wgrad(dim3 grid, dim3 block, hipStream_t strm, const fl
   return hipGetLastError();
 }
 hipError_t launch_linear_dgrad(dim3 grid, dim3 block, hipStream_t strm, const float* dY, const float* W, int I, int O, const float* pre, float* dX, int accumulate) {
-  hipLaunchKernelGGL(linear_dgrad_kernel, grid, block, 0, strm, dY, W, I, O, pre, dX, accumulate);
+  (void)block;   // 256 threads: 64 inputs x 4 partial sums
+  hipLaunchKernelGGL(linear_dgrad_kernel, grid, dim3(256), 0, strm, dY, W, I, O, pre, dX, accumulate);
   return hipGetLastError();
 }
 hipError_t launch_posemb(dim3 grid, dim3 block, hipStream_t strm, const float* t, float scale, const float* freqs, float* out) {
