@@ -98,7 +98,7 @@ hipError_t launch_attn_rowdot_split(const float* a, int csa, int ao, const float
                                     float* part, float* S_out, hipStream_t strm);
 
 // fp32-MFMA weight gradient: part holds mwgrad_splits(p) * KS^2 * A * Bc floats (<= kWPartCap, one shared buffer)
-constexpr long kWPartCap = 8L << 20;
+constexpr long kWPartCap = 40L << 20;   // 160 MB: 32 splits of the 256 x 256 x 9 level-2 gradients
 int mwgrad_splits(const WGradParams& p);
 hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, long sb, int accumulate, hipStream_t strm);
 
