@@ -25,6 +25,10 @@ struct gt_text_encoder {
   int64_t numel = 0;
   float* dev = nullptr;
   bool dirty = true;
+  // conv weights repacked [Cout][K][Cin] (16-byte aligned) for c1d_pk_kernel
+  std::map<std::string, int64_t> pkoff;
+  float* devpk = nullptr;
+  int64_t pk_numel = 0;
 };
 
 namespace {
@@ -78,6 +82,24 @@ int upload(gt_text_encoder* e) {
   if (!e->dev && hipMalloc(&e->dev, h.size() * 4) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
   if (hipMemcpy(e->dev, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
     return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
+  std::vector<float> hp;
+  e->pkoff.clear();
+  for (size_t i = 0; i < e->inv.size(); ++i) {
+    const auto& d = e->inv[i].second;
+    if (d.size() != 3 || e->inv[i].first.find(".weight") == std::string::npos) continue;
+    e->pkoff[e->inv[i].first] = (int64_t)hp.size();
+    const float* w = e->host[i].data();
+    for (int64_t o = 0; o < d[0]; ++o)
+      for (int64_t k = 0; k < d[2]; ++k)
+        for (int64_t c = 0; c < d[1]; ++c) hp.push_back(w[(o * d[1] + c) * d[2] + k]);
+    while (hp.size() % 4) hp.push_back(0.f);   // 16-byte aligned starts
+  }
+  if (e->devpk && (int64_t)hp.size() != e->pk_numel) { (void)hipFree(e->devpk); e->devpk = nullptr; }
+  if (!e->devpk && !hp.empty() && hipMalloc(&e->devpk, hp.size() * 4) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
+  e->pk_numel = (int64_t)hp.size();
+  if (!hp.empty() && hipMemcpy(e->devpk, hp.data(), hp.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
   e->dirty = false;
   return GT_OK;
 }
@@ -120,6 +142,7 @@ int gt_text_encoder_create(int n_vocab, int n_feats, int n_channels, int filter_
 void gt_text_encoder_destroy(gt_text_encoder* e) {
   if (!e) return;
   if (e->dev) (void)hipFree(e->dev);
+  if (e->devpk) (void)hipFree(e->devpk);
   delete e;
 }
 
@@ -162,6 +185,11 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
   float* x0 = buf(w.x0); float* xa = buf(w.xa); float* xb = buf(w.xb); float* x1 = buf(w.x1);
   float* hid = buf(w.hid); float* qkv = buf(w.qkv); float* att = buf(w.att); float* d1 = buf(w.d1); float* d2 = buf(w.d2);
   auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
+  // weights in the [Cout][K][Cin] layout of c1d_pk_kernel (channels-last inputs)
+  auto PK = [&](const std::string& k) {
+    const auto it = e->pkoff.find(k);
+    return it != e->pkoff.end() ? e->devpk + it->second : P(k);
+  };
   hipError_t err = hipSuccess;
   auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
   const int C = e->C, Bi = (int)B, Ti = (int)T;
@@ -170,6 +198,7 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
                   float* out, int out_cs, int out_c0, int relu, const float* res, const float* out_mask, int chan_major) {
     C1dParams p = c1d_defaults();
     p.in = in; p.in_cs = in_cs; p.in_mask = in_mask; p.w = P(key + ".weight"); p.bias = P(key + ".bias");
+    p.wpk = PK(key + ".weight");
     p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = cin; p.Cout = cout; p.K = k; p.pad = k / 2;
     p.wso = (long)cin * k; p.wsc = k;
     p.out = out; p.out_cs = out_cs; p.out_c0 = out_c0; p.chan_major = chan_major; p.relu = relu;
@@ -204,6 +233,7 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
     conv(xb, C, C, x_mask, f + "conv_1", e->Fc, e->K, hid, e->Fc, 0, 1, nullptr, nullptr, 0);
     C1dParams p = c1d_defaults();
     p.in = hid; p.in_cs = e->Fc; p.in_mask = x_mask; p.w = P(f + "conv_2.weight"); p.bias = P(f + "conv_2.bias");
+    p.wpk = PK(f + "conv_2.weight");
     p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fc; p.Cout = C; p.K = e->K; p.pad = e->K / 2;
     p.wso = (long)e->Fc * e->K; p.wsc = e->K;
     p.out = xa; p.out_cs = C; p.out_mask = x_mask;
@@ -218,6 +248,7 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
   {
     C1dParams p = c1d_defaults();
     p.in = d2; p.in_cs = e->Fdp; p.in_mask = x_mask; p.w = P("proj_w.conv_2.weight"); p.bias = P("proj_w.conv_2.bias");
+    p.wpk = PK("proj_w.conv_2.weight");
     p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fdp; p.Cout = e->Fdp; p.K = e->K; p.pad = e->K / 2;
     p.wso = (long)e->Fdp * e->K; p.wsc = e->K;
     p.out = d1; p.out_cs = e->Fdp; p.relu = 1;
@@ -227,6 +258,7 @@ int gt_text_encoder_forward(gt_text_encoder* e, const int64_t* tokens, const int
   {
     C1dParams p = c1d_defaults();
     p.in = d2; p.in_cs = e->Fdp; p.in_mask = x_mask; p.w = P("proj_w.proj.weight"); p.bias = P("proj_w.proj.bias");
+    p.wpk = PK("proj_w.proj.weight");
     p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fdp; p.Cout = 1; p.K = 1; p.pad = 0;
     p.wso = e->Fdp; p.wsc = 1;
     p.out = logw; p.chan_major = 1; p.out_mask = x_mask;
