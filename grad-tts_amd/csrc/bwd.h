@@ -19,9 +19,17 @@ struct GConvParams {
   int accumulate;
   float* wpk;                         // scratch of Cout * KS^2 * Cin floats (gconv_wpk_floats): the 3x3 / 4x4
                                       // stride-1 relations repack the weights there and run the float4-staged kernel
+  int wpk_ready;                      // 1: wpk already holds the repacked weights (launch_gconv_wpack_batch)
 };
 // scratch the packed-weight path of launch_gconv needs (0: the relation runs without it)
 long gconv_wpk_floats(const GConvParams& p);
+// one weight repack of a launch_gconv (wpk[a][k][c] = W(a, c, flip' ? KK - 1 - k : k)), batched
+struct GconvPack {
+  const float* w; float* dst; long wsa, wsc; int KK, flip, Cout, Cin;
+};
+// the repacks a launch_gconv of p would do itself (p.wpk set, packed path eligible); false: none
+bool gconv_pack_desc(const GConvParams& p, GconvPack* out);
+hipError_t launch_gconv_wpack_batch(const GconvPack* packs, int n, hipStream_t s);
 // dW(a, b, k) = sum_u P[u][a] Q[v(u,k)][b]; U grid (Fu, Tu), V grid (Fv, Tv)
 struct WGradParams {
   int B, Fu, Tu, A, Fv, Tv, Bc, KS, S, PAD;

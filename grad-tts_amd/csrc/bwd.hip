@@ -190,6 +190,41 @@ __global__ void gconv_wpack_kernel(const float* w, long wsa, long wsc, int KK, i
   wpk[i] = w[(long)a * wsa + (long)c * wsc + (flip ? KK - 1 - k : k)];
 }
 
+// Many repacks in one launch (the training step's ~95 conv launches): descriptors in the kernel arguments, a
+// workgroup finds its descriptor by the running element counts
+constexpr int kPackBatch = 32;
+struct PackBatch {
+  GconvPack d[kPackBatch];
+  long start[kPackBatch + 1];
+  int n;
+};
+__global__ void gconv_wpack_batch_kernel(PackBatch pb) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= pb.start[pb.n]) return;
+  int j = 0;
+  while (j + 1 < pb.n && pb.start[j + 1] <= i) ++j;
+  const GconvPack& d = pb.d[j];
+  const long e = i - pb.start[j];
+  const int c = (int)(e % d.Cin);
+  const long rk = e / d.Cin;
+  const int k = (int)(rk % d.KK), a = (int)(rk / d.KK);
+  d.dst[e] = d.w[(long)a * d.wsa + (long)c * d.wsc + (d.flip ? d.KK - 1 - k : k)];
+}
+
+hipError_t launch_gconv_wpack_batch(const GconvPack* packs, int n, hipStream_t s) {
+  for (int b0 = 0; b0 < n; b0 += kPackBatch) {
+    PackBatch pb{};
+    pb.n = std::min(kPackBatch, n - b0);
+    pb.start[0] = 0;
+    for (int j = 0; j < pb.n; ++j) {
+      pb.d[j] = packs[b0 + j];
+      pb.start[j + 1] = pb.start[j] + (long)pb.d[j].Cout * pb.d[j].KK * pb.d[j].Cin;
+    }
+    hipLaunchKernelGGL(gconv_wpack_batch_kernel, dim3((unsigned)((pb.start[pb.n] + 255) / 256)), dim3(256), 0, s, pb);
+  }
+  return hipGetLastError();
+}
+
 // The stride-1 relations (3x3 convs and their dgrads; with the S = 2 dilated input, the Downsample dgrad and
 // ConvTranspose2d) with packed weights: same tile and wave ownership as mconv_kernel (RH x TW positions x 64 output
 // channels, each wave 64 positions x 64 channels as 2 x 2 blocks of 32 x 32), but KC-channel chunks staged as float4
@@ -1017,6 +1052,14 @@ __global__ void input_pack_kernel(const float* mu, const float* xt, const float*
   if (cin == 3) out[i * cin + 2] = s[(long)b * 80 + f];
 }
 
+bool gconv_pack_desc(const GConvParams& p, GconvPack* out) {
+  if (gconv_wpk_floats(p) <= 0 || !p.wpk) return false;
+  out->w = p.w; out->dst = p.wpk; out->wsa = p.wsa; out->wsc = p.wsc; out->KK = p.KS * p.KS;
+  out->flip = (p.transposed ? !p.flip : p.flip != 0) ? 1 : 0;
+  out->Cout = p.Cout; out->Cin = p.Cin;
+  return true;
+}
+
 long gconv_wpk_floats(const GConvParams& p) {
   // the stride-1 relations (S = 2 only through the dilated input of the transposed relation), whole float4 runs
   const bool ok = (p.KS == 1 || p.KS == 3 || p.KS == 4) && (p.transposed ? p.S == 2 : p.S == 1) && p.Cin % 4 == 0 &&
@@ -1032,11 +1075,12 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
   auto slots = [&](int rh, int tw) { return (long)((p.Fo + rh - 1) / rh) * ((p.To + tw - 1) / tw); };
   const int se = p.transposed ? 1 : p.S, cfg = p.KS * 10 + se;
   if (gconv_wpk_floats(p) > 0 && p.wpk && ((uintptr_t)p.in & 15) == 0 && ((uintptr_t)p.wpk & 15) == 0) {
-    const int KK = p.KS * p.KS;
-    const bool flip = p.transposed ? !p.flip : p.flip != 0;
-    const long n = (long)p.Cout * KK * p.Cin;
-    hipLaunchKernelGGL(gconv_wpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.w, p.wsa, p.wsc, KK,
-                       (int)flip, p.Cout, p.Cin, p.wpk);
+    GconvPack pk;
+    if (!p.wpk_ready && gconv_pack_desc(p, &pk)) {
+      const long n = (long)pk.Cout * pk.KK * pk.Cin;
+      hipLaunchKernelGGL(gconv_wpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, pk.w, pk.wsa, pk.wsc,
+                         pk.KK, pk.flip, pk.Cout, pk.Cin, pk.dst);
+    }
     // 32-channel tiles when 64-channel tiles would leave the CUs less than two workgroups each
     auto ny1 = [&](int rh, int tw) { return (long)p.B * slots(rh, tw) * ((p.Cout + 63) / 64) < 384; };
     auto g2 = [&](int rh, int tw, int ct) {

@@ -62,6 +62,8 @@ struct Trainer {
   std::string bad;
   bool live() const { return run && !dry; }
   bool pgrads = true;       // false (estimator VJP): no parameter-gradient work, only the input cotangents
+  std::vector<GconvPack>* packs = nullptr;   // dry pass: every conv's weight repack (same arena, same addresses)
+  bool packed_ahead = false;                 // live pass: the repacks ran before the forward
   void need(const void* p, long elems, const char* what, int line) {
     if (!dry || !bad.empty() || elems <= 0) return;
     const uintptr_t a = (uintptr_t)p, e = a + (uintptr_t)elems * 4;
@@ -96,7 +98,6 @@ struct Trainer {
       if (bias) need(bias, Co, "gconv bias", line);
     }
     if (wpk) need(wpk, nwpk, "gconv packed weights", line);
-    if (dry) return;
     p.wpk = wpk;
     p.B = B; p.Fi = L(l_in).F; p.Ti = L(l_in).T; p.Cin = Ci; p.Fo = L(l_out).F; p.To = L(l_out).T; p.Cout = Co;
     p.KS = KS; p.S = S; p.PAD = PAD; p.transposed = transposed; p.flip = flip;
@@ -104,6 +105,12 @@ struct Trainer {
     p.mask = in_mask ? mask : nullptr; p.T0 = T; p.lvl_in = l_in;
     p.out_mask = out_mask ? mask : nullptr; p.lvl_out = l_out;
     p.out = out; p.out_cs = out_cs; p.out_c0 = out_c0; p.accumulate = acc;
+    if (dry) {   // the dry pass collects the weight repacks; the live pass does them up front in a few launches
+      GconvPack pk;
+      if (packs && gconv_pack_desc(p, &pk)) packs->push_back(pk);
+      return;
+    }
+    p.wpk_ready = packed_ahead ? 1 : 0;
     chk(launch_gconv(p, s), line);
   }
   // dW(a, b, k) (+)= sum_u P[u][a] Q[v(u,k)][b]; written at dw + a*sa + b*sb + k
@@ -608,7 +615,7 @@ size_t gt_train_workspace_bytes(gt_decoder* d, int64_t B, int64_t T) {
 static int train_pass(gt_decoder* d, const float* x0, const float* mask, const float* mu, const float* t,
                       const float* z, const float* spk, int64_t B, int64_t T, float* loss, float* xt, float* grads,
                       float* dmu, float* dspk, void* workspace, size_t workspace_bytes, hipStream_t stream, bool dry,
-                      bool debug) {
+                      bool debug, std::vector<GconvPack>* packs) {
   Trainer tr;
   tr.d = d; tr.B = (int)B; tr.T = (int)T; tr.run = true; tr.s = stream;
   float bmax;
@@ -631,6 +638,12 @@ static int train_pass(gt_decoder* d, const float* x0, const float* mask, const f
     tr.A.rec = &tr.regions;
   }
   tr.A.base = (uint8_t*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  if (dry) {
+    tr.packs = packs;
+  } else if (packs && !packs->empty()) {
+    tr.chk(launch_gconv_wpack_batch(packs->data(), (int)packs->size(), tr.s));
+    tr.packed_ahead = true;
+  }
   const long n0 = (long)B * 80 * T;
   float* zm = tr.A.take((size_t)n0);
   float* lpart = tr.A.take((size_t)n0 * 2);   // loss partials (generous)
@@ -684,11 +697,12 @@ int gt_diffusion_loss_grad(gt_decoder* d, const float* x0, const float* mask, co
   int n_spks; float bmin, bmax, pe;
   gt_internal_consts(d, &n_spks, &bmin, &bmax, &pe);
   if (n_spks > 1 && !spk) return gt_internal_fail(GT_ERR_ARG, "n_spks > 1 needs spk");
+  std::vector<GconvPack> packs;
   rc = train_pass(d, x0, mask, mu, t, z, spk, B, T, loss, xt, grads, dmu, dspk, workspace, workspace_bytes,
-                  (hipStream_t)stream, true, false);
+                  (hipStream_t)stream, true, false, &packs);
   if (rc || dry_only) return rc;
   return train_pass(d, x0, mask, mu, t, z, spk, B, T, loss, xt, grads, dmu, dspk, workspace, workspace_bytes,
-                    (hipStream_t)stream, false, dbg && dbg[0] == '1');
+                    (hipStream_t)stream, false, dbg && dbg[0] == '1', &packs);
 }
 
 int64_t gt_decoder_grad_numel(gt_decoder* d) {
