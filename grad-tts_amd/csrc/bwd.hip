@@ -651,6 +651,79 @@ __global__ __launch_bounds__(256, 2) void mwgrad_pk_kernel(WGradParams p, int sp
     }
 }
 
+// 1x1 weight gradient dW(a, b) = sum_u P[u][a] Q[u][b] with the positions flattened over (utterance, row, frame)
+// (a 1x1 conv has no spatial neighbourhood): 64-position segments, P^T [a][u] and Q^T [b][u] in LDS (transposed at
+// the LDS write from float4 loads along the channels, masks applied there, next segment in flight during the MFMAs);
+// waves 2 x 2 over (a, b), one float4 of each operand feeds four v_mfma_f32_32x32x2_f32. Partials as mwgrad_kernel.
+constexpr int kW1Seg = 64;
+__global__ __launch_bounds__(256) void mwgrad1_pk_kernel(WGradParams p, int splits, float* part) {
+  constexpr int SEG = kW1Seg, ST = SEG + 4, NF = SEG * 16 / 256;
+  static_assert((ST / 4) & 1, "LDS stride");
+  __shared__ __attribute__((aligned(16))) float s_p[64 * ST];
+  __shared__ __attribute__((aligned(16))) float s_q[64 * ST];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int a0 = blockIdx.x * 64, b0 = blockIdx.y * 64, split = blockIdx.z;
+  const int FT = p.Fu * p.Tu;
+  const long npos = (long)p.B * FT;
+  const long nseg = (npos + SEG - 1) / SEG;
+  const long per = (nseg + splits - 1) / splits;
+  const long s_lo = split * per, s_hi = s_lo + per < nseg ? s_lo + per : nseg;
+  const int ab = (wv & 1) * 32, bb = (wv >> 1) * 32;
+  f32x16 acc;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+  float4 rp[NF], rq[NF];
+  float pm[NF], qm[NF];
+  auto fetch = [&](long sg) {
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int i = tid + 256 * n, c4 = i & 15;
+      const long u = sg * SEG + (i >> 4);
+      const bool in = u < npos;
+      const int b = in ? (int)(u / FT) : 0, t = in ? (int)(u % p.Tu) : 0;
+      const bool okp = in && a0 + 4 * c4 < p.A, okq = in && b0 + 4 * c4 < p.Bc;
+      rp[n] = okp ? *reinterpret_cast<const float4*>(p.P + u * p.A + a0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      rq[n] = okq ? *reinterpret_cast<const float4*>(p.Q + u * p.Bc + b0 + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pm[n] = (in && p.pmask) ? mask_at(p.pmask, p.T0, b, t, p.lvl_p) : 1.f;
+      qm[n] = (in && p.qmask) ? mask_at(p.qmask, p.T0, b, t, p.lvl_q) : 1.f;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int i = tid + 256 * n, u = i >> 4, c4 = i & 15;
+      float* dp = s_p + 4 * c4 * ST + u;
+      float* dq = s_q + 4 * c4 * ST + u;
+      dp[0] = rp[n].x * pm[n]; dp[ST] = rp[n].y * pm[n]; dp[2 * ST] = rp[n].z * pm[n]; dp[3 * ST] = rp[n].w * pm[n];
+      dq[0] = rq[n].x * qm[n]; dq[ST] = rq[n].y * qm[n]; dq[2 * ST] = rq[n].z * qm[n]; dq[3 * ST] = rq[n].w * qm[n];
+    }
+  };
+  const float* pp = s_p + (ab + r) * ST + 4 * hh;
+  const float* pq = s_q + (bb + r) * ST + 4 * hh;
+  if (s_lo < s_hi) fetch(s_lo);
+  for (long sg = s_lo; sg < s_hi; ++sg) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (sg + 1 < s_hi) fetch(sg + 1);
+#pragma unroll
+    for (int u0 = 0; u0 < SEG; u0 += 8) {
+      const float4 a = *reinterpret_cast<const float4*>(pp + u0);
+      const float4 q = *reinterpret_cast<const float4*>(pq + u0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, q.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, q.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, q.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, q.w, acc, 0, 0, 0);
+    }
+  }
+  const int bc = b0 + bb + r;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int a = a0 + ab + acc_row(j, hh);
+    if (a < p.A && bc < p.Bc) part[((long)split * p.A + a) * p.Bc + bc] = acc[j];
+  }
+}
+
 // 48-position segments where they cut the padded frames (a level-2 row of 43 frames: 48 instead of 64)
 static int mwgrad_seg(const WGradParams& p) {
   return (p.KS == 3 && p.S == 1 && (p.Tu + 47) / 48 * 48 < (p.Tu + 31) / 32 * 32) ? 48 : 32;
@@ -673,7 +746,21 @@ hipError_t launch_mwgrad(const WGradParams& p, float* part, float* dw, long sa, 
   const int splits = mwgrad_splits(p);
   const int groups = p.KS == 4 ? 2 : 1;
   const dim3 grid((p.A + 63) / 64, (p.Bc + 63) / 64, splits * groups);
-  const bool pk = cfg == 31 && p.A % 4 == 0 && p.Bc % 4 == 0 && ((uintptr_t)p.P & 15) == 0 && ((uintptr_t)p.Q & 15) == 0;
+  const bool aligned = p.A % 4 == 0 && p.Bc % 4 == 0 && ((uintptr_t)p.P & 15) == 0 && ((uintptr_t)p.Q & 15) == 0;
+  const bool pk = cfg == 31 && aligned;
+  if (cfg == 11 && aligned && p.PAD == 0 && p.Fu == p.Fv && p.Tu == p.Tv) {   // 1x1: flattened positions
+    const long tiles = (long)((p.A + 63) / 64) * ((p.Bc + 63) / 64);
+    const long nseg = ((long)p.B * p.Fu * p.Tu + kW1Seg - 1) / kW1Seg;
+    long sp = std::max<long>(1, 1024 / tiles);
+    sp = std::min<long>(sp, nseg);
+    sp = std::min<long>(sp, kWPartCap / ((long)p.A * p.Bc));
+    const int s1 = (int)std::max<long>(1, sp);
+    hipLaunchKernelGGL(mwgrad1_pk_kernel, dim3((p.A + 63) / 64, (p.Bc + 63) / 64, s1), dim3(256), 0, strm, p, s1, part);
+    const long n = (long)p.A * p.Bc;
+    hipLaunchKernelGGL(mwgrad_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, strm, part, s1, p.A,
+                       p.Bc, 1, sa, sb, dw, accumulate);
+    return hipGetLastError();
+  }
   // (48-position segments for the 43-frame rows would need more registers than two waves per SIMD leave)
   if (pk) hipLaunchKernelGGL((mwgrad_pk_kernel<32>), grid, dim3(256), 0, strm, p, splits, part);
   else if (cfg == 11) hipLaunchKernelGGL((mwgrad_kernel<1, 1, 32>), grid, dim3(256), 0, strm, p, splits, part);
