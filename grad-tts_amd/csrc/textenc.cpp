@@ -12,6 +12,7 @@
 #include "decoder_internal.h"
 #include "gradtts.h"
 #include "textenc.h"
+#include "textenc_train.h"
 
 using namespace gt;
 
@@ -29,6 +30,11 @@ struct gt_text_encoder {
   std::map<std::string, int64_t> pkoff;
   float* devpk = nullptr;
   int64_t pk_numel = 0;
+  // the last gt_text_encoder_forward_train call (its tape is the backward's input)
+  const void* tr_ws = nullptr;
+  int64_t tr_B = 0, tr_T = 0;
+  uint64_t tr_seed = 0;
+  float tr_p = 0.f, tr_ppre = 0.f;
 };
 
 namespace {
@@ -289,6 +295,301 @@ int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, 
                    void* stream) {
   if (!attn || !mu_x || !mu_y || B <= 0 || Tx <= 0 || Ty <= 0) return gt_internal_fail(GT_ERR_ARG, "bad argument");
   const hipError_t e = launch_te_path_gather(attn, mu_x, (int)B, (int)Tx, (int)Ty, n_feats, mu_y, (hipStream_t)stream);
+  return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
+}
+
+}  // extern "C"
+
+// ================================================================ training pass (GradTTS.compute_loss's encoder)
+namespace {
+
+// tape + backward scratch (floats unless noted), 256-byte aligned pieces
+struct TrWs {
+  size_t tokens, mask, x0, pre_c[3], pre_h[3], x1, d1c, d1d, d2c, d2d;
+  std::vector<size_t> qkv, P, Pd, att, y1, xmid, hd, y2, xout;
+  size_t g1, g2, datt, dy, dh, dqkv, ds, drel, wpart, cpart, lpart, dmu;
+  long wpart_floats, cpart_floats;
+  size_t total;
+};
+
+TrWs tr_layout(const gt_text_encoder* e, int64_t B, int64_t T) {
+  TrWs w{};
+  size_t off = 0;
+  auto put = [&](size_t floats) { const size_t o = off; off += (floats * 4 + 255) & ~size_t(255); return o; };
+  const size_t n = (size_t)B * T, C = e->C, Fc = e->Fc, Fd = e->Fdp, att = (size_t)B * e->H * T * T;
+  w.tokens = put(2 * n);
+  w.mask = put(n);
+  w.x0 = put(n * C);
+  for (int i = 0; i < 3; ++i) { w.pre_c[i] = put(n * C); w.pre_h[i] = put(n * C); }
+  w.x1 = put(n * C);
+  for (int l = 0; l < e->L; ++l) {
+    w.qkv.push_back(put(n * 3 * C)); w.P.push_back(put(att)); w.Pd.push_back(put(att));
+    w.att.push_back(put(n * C)); w.y1.push_back(put(n * C)); w.xmid.push_back(put(n * C));
+    w.hd.push_back(put(n * Fc)); w.y2.push_back(put(n * C)); w.xout.push_back(put(n * C));
+  }
+  w.d1c = put(n * Fd); w.d1d = put(n * Fd); w.d2c = put(n * Fd); w.d2d = put(n * Fd);
+  const size_t wide = std::max({C, Fc, Fd, (size_t)e->n_feats});
+  w.g1 = put(n * C); w.g2 = put(n * C); w.datt = put(n * C);
+  w.dy = put(n * wide); w.dh = put(n * wide); w.dqkv = put(n * 3 * C); w.ds = put(att);
+  w.drel = put((size_t)B * 2 * (2 * e->W + 1) * 96);
+  w.wpart_floats = 8L << 20;
+  w.wpart = put((size_t)w.wpart_floats);
+  w.cpart_floats = 64L * (long)wide;
+  w.cpart = put((size_t)w.cpart_floats);
+  w.lpart = put((size_t)tt_ln_bwd_blocks((long)n) * 2 * 256);
+  w.dmu = put(n * wide);
+  w.total = off + 256;
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gt_text_encoder_train_workspace_bytes(gt_text_encoder* e, int64_t B, int64_t T) {
+  if (!e || B <= 0 || T <= 0 || T > TT_TMAX) return 0;
+  return tr_layout(e, B, T).total;
+}
+
+int64_t gt_text_encoder_grad_numel(gt_text_encoder* e) { return e ? e->numel : -1; }
+
+int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, const int64_t* x_lengths, int64_t B,
+                                  int64_t T, float p_dropout, float p_dropout_prenet, uint64_t seed, float* mu_x,
+                                  float* logw, float* x_mask, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!e || !tokens || !x_lengths || !mu_x || !logw || !x_mask || !workspace) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (B <= 0 || T <= 0) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
+  if (T > TT_TMAX) return gt_internal_fail(GT_ERR_UNSUPPORTED, "training attention supports Tx <= 4096");
+  if (!(p_dropout >= 0.f && p_dropout < 1.f && p_dropout_prenet >= 0.f && p_dropout_prenet < 1.f))
+    return gt_internal_fail(GT_ERR_ARG, "dropout probabilities must lie in [0, 1)");
+  const TrWs w = tr_layout(e, B, T);
+  if (workspace_bytes < w.total) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
+  int rc = upload(e);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  auto F = [&](size_t o) { return (float*)(base + o * 4); };
+  auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
+  auto PK = [&](const std::string& k) {
+    const auto it = e->pkoff.find(k);
+    return it != e->pkoff.end() ? e->devpk + it->second : P(k);
+  };
+  hipError_t err = hipSuccess;
+  auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
+  const int C = e->C, Bi = (int)B, Ti = (int)T;
+  const long npos = (long)B * T;
+  float* mask = F(w.mask);
+  auto conv = [&](const float* in, int cin, const float* in_mask, const std::string& key, int cout, int k, float* out,
+                  int out_cs, int out_c0, int relu, const float* res, const float* out_mask, int chan_major, Drop drop) {
+    C1dParams p = c1d_defaults();
+    p.in = in; p.in_cs = cin; p.in_mask = in_mask; p.w = P(key + ".weight"); p.bias = P(key + ".bias");
+    p.wpk = PK(key + ".weight");
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = cin; p.Cout = cout; p.K = k; p.pad = k / 2;
+    p.wso = (long)cin * k; p.wsc = k;
+    p.out = out; p.out_cs = out_cs; p.out_c0 = out_c0; p.chan_major = chan_major; p.relu = relu;
+    p.res = res; p.res_cs = C; p.out_mask = out_mask; p.drop = drop;
+    chk(launch_c1d(p, s));
+  };
+  auto ln = [&](const float* x, const float* res, const std::string& key, int c, int relu, const float* m, float* out,
+                Drop drop) {
+    chk(launch_te_ln(x, c, res, c, P(key + ".gamma"), P(key + ".beta"), npos, c, 1e-4f, relu, m, out, c, s, drop));
+  };
+  const Drop none = make_drop(0, 0, 0.f);
+  // tokens into the tape (the embedding gradient needs them), embedding * sqrt(C), x_mask (text_encoder.py:322-324)
+  chk(launch_tt_copy_words((uint32_t*)F(w.tokens), (const uint32_t*)tokens, 2 * npos, s));
+  chk(launch_te_embed(tokens, x_lengths, P("emb.weight"), e->n_vocab, Bi, Ti, C, (float)std::sqrt((double)C), F(w.x0),
+                      mask, s));
+  // prenet: ConvReluNorm (:57-64), relu_drop = ReLU + Dropout(p_dropout_prenet)
+  const float* h = F(w.x0);
+  for (int i = 0; i < 3; ++i) {
+    const std::string k = std::to_string(i);
+    conv(h, C, mask, "prenet.conv_layers." + k, C, 5, F(w.pre_c[i]), C, 0, 0, nullptr, nullptr, 0, none);
+    ln(F(w.pre_c[i]), nullptr, "prenet.norm_layers." + k, C, 1, nullptr, F(w.pre_h[i]),
+       make_drop(seed, 1 + i, p_dropout_prenet));
+    h = F(w.pre_h[i]);
+  }
+  conv(h, C, nullptr, "prenet.proj", C, 1, F(w.x1), C, 0, 0, F(w.x0), mask, 0, none);
+  const float* x = F(w.x1);
+  for (int l = 0; l < e->L; ++l) {
+    const std::string a = "encoder.attn_layers." + std::to_string(l) + ".";
+    const std::string f = "encoder.ffn_layers." + std::to_string(l) + ".";
+    const uint32_t site = 16 + 8 * l;
+    float* qkv = F(w.qkv[l]);
+    conv(x, C, nullptr, a + "conv_q", C, 1, qkv, 3 * C, 0, 0, nullptr, nullptr, 0, none);
+    conv(x, C, nullptr, a + "conv_k", C, 1, qkv, 3 * C, C, 0, nullptr, nullptr, 0, none);
+    conv(x, C, nullptr, a + "conv_v", C, 1, qkv, 3 * C, 2 * C, 0, nullptr, nullptr, 0, none);
+    chk(launch_tt_attn_fwd(qkv, mask, P(a + "emb_rel_k"), P(a + "emb_rel_v"), Bi, Ti, C, e->H, e->W,
+                           make_drop(seed, site, p_dropout), F(w.P[l]), F(w.Pd[l]), F(w.att[l]), s));
+    conv(F(w.att[l]), C, nullptr, a + "conv_o", C, 1, F(w.y1[l]), C, 0, 0, nullptr, nullptr, 0,
+         make_drop(seed, site + 1, p_dropout));                                                      // y = drop(attn)
+    ln(x, F(w.y1[l]), "encoder.norm_layers_1." + std::to_string(l), C, 0, nullptr, F(w.xmid[l]), none);
+    conv(F(w.xmid[l]), C, mask, f + "conv_1", e->Fc, e->K, F(w.hd[l]), e->Fc, 0, 1, nullptr, nullptr, 0,
+         make_drop(seed, site + 2, p_dropout));                                                      // drop(relu(conv_1))
+    {
+      C1dParams p = c1d_defaults();
+      p.in = F(w.hd[l]); p.in_cs = e->Fc; p.in_mask = mask; p.w = P(f + "conv_2.weight"); p.bias = P(f + "conv_2.bias");
+      p.wpk = PK(f + "conv_2.weight");
+      p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = e->Fc; p.Cout = C; p.K = e->K; p.pad = e->K / 2;
+      p.wso = (long)e->Fc * e->K; p.wsc = e->K;
+      p.out = F(w.y2[l]); p.out_cs = C; p.out_mask = mask; p.drop = make_drop(seed, site + 3, p_dropout);
+      chk(launch_c1d(p, s));
+    }
+    ln(F(w.xmid[l]), F(w.y2[l]), "encoder.norm_layers_2." + std::to_string(l), C, 0, mask, F(w.xout[l]), none);
+    x = F(w.xout[l]);
+  }
+  conv(x, C, nullptr, "proj_m", e->n_feats, 1, mu_x, 0, 0, 0, nullptr, mask, 1, none);
+  // duration predictor on the detached x (:332, :83-93)
+  conv(x, C, mask, "proj_w.conv_1", e->Fdp, e->K, F(w.d1c), e->Fdp, 0, 1, nullptr, nullptr, 0, none);
+  ln(F(w.d1c), nullptr, "proj_w.norm_1", e->Fdp, 0, nullptr, F(w.d1d), make_drop(seed, 8, p_dropout));
+  conv(F(w.d1d), e->Fdp, mask, "proj_w.conv_2", e->Fdp, e->K, F(w.d2c), e->Fdp, 0, 1, nullptr, nullptr, 0, none);
+  ln(F(w.d2c), nullptr, "proj_w.norm_2", e->Fdp, 0, nullptr, F(w.d2d), make_drop(seed, 9, p_dropout));
+  conv(F(w.d2d), e->Fdp, mask, "proj_w.proj", 1, 1, logw, 0, 0, 0, nullptr, mask, 1, none);
+  {
+    EwParams c{};
+    c.dst = x_mask; c.dst_cs = 1; c.src = mask; c.src_cs = 1; c.npos = npos; c.T = Ti; c.C = 1; c.drop = none;
+    chk(launch_tt_ew(c, s));
+  }
+  if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder training forward: ") + hipGetErrorString(err));
+  e->tr_ws = workspace; e->tr_B = B; e->tr_T = T; e->tr_seed = seed; e->tr_p = p_dropout; e->tr_ppre = p_dropout_prenet;
+  return GT_OK;
+}
+
+int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float* dlogw, int64_t B, int64_t T,
+                             float* grads, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!e || !grads || !workspace) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (workspace != e->tr_ws || B != e->tr_B || T != e->tr_T)
+    return gt_internal_fail(GT_ERR_ARG, "gt_text_encoder_backward must follow gt_text_encoder_forward_train with the "
+                                        "same B, Tx and workspace");
+  const TrWs w = tr_layout(e, B, T);
+  if (workspace_bytes < w.total) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
+  if (e->dirty) return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
+  hipStream_t s = (hipStream_t)stream;
+  char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  auto F = [&](size_t o) { return (float*)(base + o * 4); };
+  auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
+  auto G = [&](const std::string& k) { return grads + e->off[e->index.at(k)]; };
+  hipError_t err = hipSuccess;
+  auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
+  const int C = e->C, Bi = (int)B, Ti = (int)T, K = e->K, Fc = e->Fc, Fd = e->Fdp, NF = e->n_feats;
+  const long npos = (long)B * T;
+  const uint64_t seed = e->tr_seed;
+  const float pd = e->tr_p, ppre = e->tr_ppre;
+  const float* mask = F(w.mask);
+  const Drop none = make_drop(0, 0, 0.f);
+  float *G1 = F(w.g1), *G2 = F(w.g2), *DATT = F(w.datt), *DY = F(w.dy), *DH = F(w.dh), *DQKV = F(w.dqkv);
+  // dW / db of conv `key` (Cout x Cin x k) from dout [npos][d_cs] and its input x [npos][x_cs] (* xm)
+  auto wgrad = [&](const float* dout, int d_cs, const float* xin, int x_cs, const float* xm, const std::string& key,
+                   int cout, int cin, int k) {
+    WgradParams p{};
+    p.dout = dout; p.d_cs = d_cs; p.x = xin; p.x_cs = x_cs; p.x_mask = xm;
+    p.B = Bi; p.T = Ti; p.Cin = cin; p.Cout = cout; p.K = k; p.pad = k / 2;
+    chk(launch_tt_wgrad(p, G(key + ".weight"), F(w.wpart), w.wpart_floats, s));
+    chk(launch_tt_colsum(dout, d_cs, npos, cout, F(w.cpart), w.cpart_floats, G(key + ".bias"), s));
+  };
+  // dx [npos][out_cs] (=|+=) conv^T(dout) (* m): the input gradient of conv `key` as a conv over dout with the taps
+  // flipped and the weight strides swapped (W'(c, o, j) = W(o, c, k - 1 - j), padding k - 1 - k / 2)
+  auto dgrad = [&](const float* dout, int d_cs, const std::string& key, int cout, int cin, int k, float* dx,
+                   int out_cs, int accumulate, const float* m) {
+    C1dParams p = c1d_defaults();
+    p.in = dout; p.in_cs = d_cs; p.w = P(key + ".weight"); p.bias = nullptr; p.wpk = nullptr;
+    p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = cout; p.Cout = cin; p.K = k; p.pad = k - 1 - k / 2;
+    p.wso = k; p.wsc = (long)cin * k; p.tap0 = k - 1; p.tap_step = -1;
+    p.out = dx; p.out_cs = out_cs; p.accumulate = accumulate; p.out_mask = m;
+    chk(launch_c1d(p, s));
+  };
+  auto lnb = [&](const float* x, const float* res, const std::string& key, int c, const float* dy, Drop drop,
+                 const float* relu_ref, int post_relu, float* dx, int accumulate, const float* dx_mask) {
+    LnBwdParams p{};
+    p.x = x; p.x_cs = c; p.res = res; p.res_cs = c; p.gamma = P(key + ".gamma"); p.C = c; p.eps = 1e-4f; p.npos = npos;
+    p.dy = dy; p.dy_cs = c; p.drop = drop; p.relu_ref = relu_ref; p.post_relu = post_relu; p.dx_mask = dx_mask;
+    p.dx = dx; p.dx_cs = c; p.dx_accumulate = accumulate; p.part = F(w.lpart);
+    chk(launch_tt_ln_bwd(p, G(key + ".gamma"), s));   // gamma | beta are adjacent in the inventory
+  };
+  auto ew = [&](float* dst, int dst_cs, const float* src, int src_cs, int chan_major, int c, const float* m, Drop drop,
+                const float* relu_ref, int relu_cs) {
+    EwParams p{};
+    p.dst = dst; p.dst_cs = dst_cs; p.src = src; p.src_cs = src_cs; p.src_chan_major = chan_major; p.npos = npos;
+    p.T = Ti; p.C = c; p.mask = m; p.drop = drop; p.relu_ref = relu_ref; p.relu_cs = relu_cs;
+    chk(launch_tt_ew(p, s));
+  };
+  const float* xf = F(w.xout[e->L - 1]);
+  // ---- duration predictor (its input is detached: the gradient stops at proj_w.conv_1's parameters)
+  float* DLW = F(w.dmu);
+  ew(DLW, 1, dlogw, 1, 0, 1, mask, none, nullptr, 0);   // NULL upstream gradient: zeros
+  wgrad(DLW, 1, F(w.d2d), Fd, mask, "proj_w.proj", 1, Fd, 1);
+  dgrad(DLW, 1, "proj_w.proj", 1, Fd, 1, DH, Fd, 0, mask);
+  lnb(F(w.d2c), nullptr, "proj_w.norm_2", Fd, DH, make_drop(seed, 9, pd), nullptr, 1, DY, 0, nullptr);
+  wgrad(DY, Fd, F(w.d1d), Fd, mask, "proj_w.conv_2", Fd, Fd, K);
+  dgrad(DY, Fd, "proj_w.conv_2", Fd, Fd, K, DH, Fd, 0, mask);
+  lnb(F(w.d1c), nullptr, "proj_w.norm_1", Fd, DH, make_drop(seed, 8, pd), nullptr, 1, DY, 0, nullptr);
+  wgrad(DY, Fd, xf, C, mask, "proj_w.conv_1", Fd, C, K);
+  // ---- mu_x = proj_m(x) * x_mask, x = x * x_mask (:281, :330)
+  float* DMU = F(w.dmu);
+  ew(DMU, NF, dmu_x, NF, 1, NF, mask, none, nullptr, 0);
+  wgrad(DMU, NF, xf, C, nullptr, "proj_m", NF, C, 1);
+  dgrad(DMU, NF, "proj_m", NF, C, 1, G1, C, 0, mask);
+  // ---- encoder layers, last to first; G1 = dL/d(layer output), masked
+  for (int l = e->L - 1; l >= 0; --l) {
+    const std::string a = "encoder.attn_layers." + std::to_string(l) + ".";
+    const std::string f = "encoder.ffn_layers." + std::to_string(l) + ".";
+    const uint32_t site = 16 + 8 * l;
+    const float* xin = l ? F(w.xout[l - 1]) : F(w.x1);
+    // x_out = LN2(x_mid + drop(FFN(x_mid)))
+    lnb(F(w.xmid[l]), F(w.y2[l]), "encoder.norm_layers_2." + std::to_string(l), C, G1, none, nullptr, 0, G2, 0,
+        nullptr);
+    ew(DY, C, G2, C, 0, C, mask, make_drop(seed, site + 3, pd), nullptr, 0);
+    wgrad(DY, C, F(w.hd[l]), Fc, mask, f + "conv_2", C, Fc, K);
+    dgrad(DY, C, f + "conv_2", C, Fc, K, DH, Fc, 0, nullptr);
+    ew(DH, Fc, DH, Fc, 0, Fc, mask, make_drop(seed, site + 2, pd), F(w.hd[l]), Fc);
+    wgrad(DH, Fc, F(w.xmid[l]), C, mask, f + "conv_1", Fc, C, K);
+    dgrad(DH, Fc, f + "conv_1", Fc, C, K, G2, C, 1, mask);
+    // x_mid = LN1(x_in + drop(attn(x_in)))
+    lnb(xin, F(w.y1[l]), "encoder.norm_layers_1." + std::to_string(l), C, G2, none, nullptr, 0, G1, 0, nullptr);
+    ew(DY, C, G1, C, 0, C, nullptr, make_drop(seed, site + 1, pd), nullptr, 0);
+    wgrad(DY, C, F(w.att[l]), C, nullptr, a + "conv_o", C, C, 1);
+    dgrad(DY, C, a + "conv_o", C, C, 1, DATT, C, 0, nullptr);
+    chk(launch_tt_attn_bwd(F(w.qkv[l]), F(w.P[l]), F(w.Pd[l]), DATT, mask, P(a + "emb_rel_k"), P(a + "emb_rel_v"), Bi,
+                           Ti, C, e->H, e->W, make_drop(seed, site, pd), F(w.ds), DQKV, F(w.drel), G(a + "emb_rel_k"),
+                           s));
+    const char* qkvn[3] = {"conv_q", "conv_k", "conv_v"};
+    for (int j = 0; j < 3; ++j) {
+      wgrad(DQKV + j * C, 3 * C, xin, C, nullptr, a + qkvn[j], C, C, 1);
+      dgrad(DQKV + j * C, 3 * C, a + qkvn[j], C, C, 1, G1, C, 1, mask);   // x_in = x * x_mask (:274)
+    }
+  }
+  // ---- prenet: x1 = (x0 + proj(h2)) * x_mask; G1 = dL/dx1 (masked) is also dL/dx0's residual part
+  wgrad(G1, C, F(w.pre_h[2]), C, nullptr, "prenet.proj", C, C, 1);
+  dgrad(G1, C, "prenet.proj", C, C, 1, DH, C, 0, nullptr);
+  for (int i = 2; i >= 0; --i) {
+    const std::string k = std::to_string(i);
+    lnb(F(w.pre_c[i]), nullptr, "prenet.norm_layers." + k, C, DH, make_drop(seed, 1 + i, ppre), F(w.pre_h[i]), 0, DY,
+        0, nullptr);
+    const float* xin = i ? F(w.pre_h[i - 1]) : F(w.x0);
+    wgrad(DY, C, xin, C, mask, "prenet.conv_layers." + k, C, C, 5);
+    if (i) dgrad(DY, C, "prenet.conv_layers." + k, C, C, 5, DH, C, 0, mask);
+    else dgrad(DY, C, "prenet.conv_layers." + k, C, C, 5, G1, C, 1, mask);
+  }
+  chk(launch_tt_emb_bwd((const int64_t*)F(w.tokens), npos, G1, e->n_vocab, C, (float)std::sqrt((double)C),
+                        G("emb.weight"), s));
+  if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder backward: ") + hipGetErrorString(err));
+  return GT_OK;
+}
+
+int gt_path_scatter(const float* attn, const float* dmu_y, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
+                    float* dmu_x, void* stream) {
+  if (!attn || !dmu_y || !dmu_x || B <= 0 || Tx <= 0 || Ty <= 0 || n_feats <= 0 || n_feats > 128)
+    return gt_internal_fail(GT_ERR_ARG, "bad argument");
+  const hipError_t e = launch_tt_path_scatter(attn, dmu_y, (int)B, (int)Tx, (int)Ty, n_feats, dmu_x, (hipStream_t)stream);
+  return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
+}
+
+int gt_tts_aux_losses(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths, int64_t B,
+                      int64_t Tx, int64_t Ty_attn, const float* y, const float* mu_y, const float* y_mask, int64_t Ty,
+                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* stream) {
+  if (!logw || !attn || !x_mask || !x_lengths || !y || !mu_y || !y_mask || !losses || !dlogw_unit || !dmu_y_unit ||
+      B <= 0 || Tx <= 0 || Ty_attn <= 0 || Ty <= 0 || n_feats <= 0)
+    return gt_internal_fail(GT_ERR_ARG, "bad argument");
+  const hipError_t e = launch_tt_aux_loss(logw, attn, x_mask, x_lengths, y, mu_y, y_mask, (int)B, (int)Tx, (int)Ty_attn,
+                                          (int)Ty, n_feats, losses, dlogw_unit, dmu_y_unit, (hipStream_t)stream);
   return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
 }
 

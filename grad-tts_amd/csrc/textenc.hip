@@ -90,6 +90,7 @@ __global__ __launch_bounds__(256) void c1d_kernel(C1dParams p) {
     if (t < 0 || t >= p.Tout) continue;
     float v = acc[j] + bias;
     if (p.relu) v = fmaxf(v, 0.f);
+    v *= drop_scale(p.drop, ((uint64_t)b * p.Tout + t) * p.Cout + o);
     if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
     const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
     if (p.accumulate) v = p.out[oi] + v;
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(256, 2) void c1d_pk_kernel(C1dParams p) {
       if (t < 0 || t >= p.Tout) continue;
       float v = acc[m][j] + bias;
       if (p.relu) v = fmaxf(v, 0.f);
+      v *= drop_scale(p.drop, ((uint64_t)b * p.Tout + t) * p.Cout + o);
       if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
       const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
       if (p.accumulate) v = p.out[oi] + v;
@@ -292,6 +294,7 @@ __global__ __launch_bounds__(256) void c1d_bf16_kernel(C1dParams p) {
     if (t < 0 || t >= p.Tout) continue;
     float v = acc[j] + bias;
     if (p.relu) v = fmaxf(v, 0.f);
+    v *= drop_scale(p.drop, ((uint64_t)b * p.Tout + t) * p.Cout + o);
     if (p.res) v = p.res[((long)b * p.Tout + t) * p.res_cs + o] + v;
     const long oi = p.chan_major ? ((long)b * p.Cout + o) * p.Tout + t : ((long)b * p.Tout + t) * p.out_cs + p.out_c0 + o;
     if (p.accumulate) v = p.out[oi] + v;
@@ -351,7 +354,8 @@ hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
 // ---------------------------------------------------------------- LayerNorm
 __global__ __launch_bounds__(256) void te_ln_kernel(const float* x, int x_cs, const float* res, int res_cs,
                                                     const float* gamma, const float* beta, long npos, int C, float eps,
-                                                    int relu_after, const float* mask, float* out, int out_cs) {
+                                                    int relu_after, const float* mask, float* out, int out_cs,
+                                                    Drop drop) {
   const long pos = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (pos >= npos) return;
@@ -382,16 +386,17 @@ __global__ __launch_bounds__(256) void te_ln_kernel(const float* x, int x_cs, co
     if (c >= C) continue;
     float y = (v[k] - mean) * rs * gamma[c] + beta[c];
     if (relu_after) y = fmaxf(y, 0.f);
+    y *= drop_scale(drop, (uint64_t)pos * C + c);
     out[pos * out_cs + c] = y * m;
   }
 }
 
 hipError_t launch_te_ln(const float* x, int x_cs, const float* res, int res_cs, const float* gamma, const float* beta,
                         long npos, int C, float eps, int relu_after, const float* mask, float* out, int out_cs,
-                        hipStream_t s) {
+                        hipStream_t s, Drop drop) {
   if (C > 256) return hipErrorInvalidValue;
   hipLaunchKernelGGL(te_ln_kernel, dim3((unsigned)((npos + 3) / 4)), dim3(256), 0, s, x, x_cs, res, res_cs, gamma, beta,
-                     npos, C, eps, relu_after, mask, out, out_cs);
+                     npos, C, eps, relu_after, mask, out, out_cs, drop);
   return hipGetLastError();
 }
 

@@ -1,0 +1,588 @@
+// Training pass of GradTTS's text encoder and the encoder-side losses of GradTTS.compute_loss (gfx950, fp32):
+//
+//   tt_attn_p_kernel      relative-position attention probabilities (text_encoder.py:145-165) with the training
+//                         dropout of p_attn (:166); writes P (softmax) and Pd (dropped) for the backward
+//   tt_attn_pv_kernel     output = Pd v + relative-value term (:167-172)
+//   tt_attn_ds_kernel     backward of the attention core: dPd -> dP (dropout) -> dS (softmax, masked_fill)
+//   tt_attn_dqkv_kernel   dq (keys + relative keys), dk, dv from dS / Pd
+//   tt_attn_drel_kernel   gradients of emb_rel_k / emb_rel_v (shared by the heads), per-utterance partials
+//   tt_ln_bwd_kernel      LayerNorm backward (:11-29) with the ReLU / dropout / mask factors around it and
+//                         per-workgroup partial dgamma / dbeta
+//   tt_wgrad_kernel       Conv1d weight gradient dW[o][c][k] = sum_t dout[t][o] x[t + k - pad][c] as a GEMM over
+//                         positions on v_mfma_f32_32x32x2_f32 (64 x 64 tiles, all taps per staged chunk), position
+//                         splits reduced in a fixed order
+//   tt_colsum_kernel      bias gradients (channel sums over positions), split + fixed-order reduction
+//   tt_emb_bwd_kernel     embedding gradient (:322), per vocabulary row in position order (no atomics)
+//   tt_ew_kernel          elementwise gradient factors (mask, dropout, ReLU) and the channel-major -> channels-last
+//                         transpose of dmu_x / dlogw
+//   tt_path_scatter_kernel  backward of mu_y = attn^T mu_x (tts.py:184-185)
+//   tt_aux_loss_kernel    dur_loss (tts.py:155-156, utils.py:42-44) and prior_loss (tts.py:191-192) with their unit
+//                         gradients, one workgroup, fixed summation order
+// Every reduction has a fixed order: two calls give bit-identical gradients.
+#include <math.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "textenc.h"
+#include "textenc_train.h"
+
+namespace gt {
+
+constexpr int TT_D = 96, TT_WMAX = 17;
+
+GT_DEV float tt_wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+GT_DEV float tt_wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+// 256-thread block reductions (every thread gets the result; waves combined in order)
+GT_DEV float tt_block_sum(float x, float* red) {
+  x = tt_wave_sum(x);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = x;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+GT_DEV float tt_block_max(float x, float* red) {
+  x = tt_wave_max(x);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = x;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+GT_DEV float dot96(const float* s, const float* g) {   // s in LDS, g 16-byte aligned global row
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float d = 0.f;
+#pragma unroll 4
+  for (int k = 0; k < TT_D / 4; ++k) {
+    const float4 v = g4[k];
+    d = fmaf(s[4 * k], v.x, d);
+    d = fmaf(s[4 * k + 1], v.y, d);
+    d = fmaf(s[4 * k + 2], v.z, d);
+    d = fmaf(s[4 * k + 3], v.w, d);
+  }
+  return d;
+}
+
+// ---------------------------------------------------------------- attention, forward (training)
+// one workgroup per (query i, head h, utterance b); the score row lives in LDS (T <= TT_TMAX)
+__global__ __launch_bounds__(256) void tt_attn_p_kernel(const float* qkv, const float* x_mask, const float* erk, int T,
+                                                        int C, int W, Drop drop, float* P, float* Pd) {
+  __shared__ float s_q[TT_D], s_ek[TT_WMAX * TT_D], s_row[TT_TMAX], s_red[4];
+  const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z, H = gridDim.y, tid = threadIdx.x, nw = 2 * W + 1;
+  const long C3 = 3L * C;
+  const float* base = qkv + (long)b * T * C3;
+  for (int e = tid; e < TT_D; e += 256) s_q[e] = base[(long)i * C3 + h * TT_D + e];
+  for (int e = tid; e < nw * TT_D; e += 256) s_ek[e] = erk[e];
+  __syncthreads();
+  const float sq = sqrtf((float)TT_D);
+  const bool qi = x_mask[(long)b * T + i] != 0.f;
+  float mx = -INFINITY;
+  for (int j = tid; j < T; j += 256) {
+    float sc = dot96(s_q, base + (long)j * C3 + C + h * TT_D) / sq;
+    const int rel = j - i;
+    if (rel >= -W && rel <= W) {
+      float dr = 0.f;
+      for (int d = 0; d < TT_D; ++d) dr = fmaf(s_q[d], s_ek[(rel + W) * TT_D + d], dr);
+      sc = sc + dr / sq;
+    }
+    if (!(qi && x_mask[(long)b * T + j] != 0.f)) sc = -1e4f;   // masked_fill(mask == 0, -1e4)
+    s_row[j] = sc;
+    mx = fmaxf(mx, sc);
+  }
+  mx = tt_block_max(mx, s_red);
+  float l = 0.f;
+  for (int j = tid; j < T; j += 256) {
+    const float e = expf(s_row[j] - mx);
+    s_row[j] = e;
+    l += e;
+  }
+  l = tt_block_sum(l, s_red);
+  const long row = (((long)b * H + h) * T + i) * T;
+  for (int j = tid; j < T; j += 256) {
+    const float p = s_row[j] / l;
+    P[row + j] = p;
+    Pd[row + j] = p * drop_scale(drop, (uint64_t)(row + j));
+  }
+}
+
+// out[b][i][h 96 + d] = sum_j Pd[i][j] v[j][h 96 + d] + sum_{|r| <= W} Pd[i][i + r] erv[r + W][d]
+__global__ __launch_bounds__(256) void tt_attn_pv_kernel(const float* qkv, const float* Pd, const float* erv, int T,
+                                                         int C, int H, int W, float* out) {
+  const int i = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  if (tid >= C) return;
+  const int h = tid / TT_D, d = tid % TT_D;
+  const long C3 = 3L * C;
+  const float* prow = Pd + (((long)b * H + h) * T + i) * T;
+  const float* vb = qkv + (long)b * T * C3 + 2 * C + tid;
+  float o = 0.f;
+  for (int j = 0; j < T; ++j) o = fmaf(prow[j], vb[(long)j * C3], o);
+  for (int r = -W; r <= W; ++r) {
+    const int j = i + r;
+    if (j >= 0 && j < T) o = fmaf(prow[j], erv[(r + W) * TT_D + d], o);
+  }
+  out[((long)b * T + i) * C + tid] = o;
+}
+
+// ---------------------------------------------------------------- attention, backward
+// dPd[j] = g_i . v_j + [|j - i| <= W] g_i . erv[j - i + W]; dP = dPd * drop; dS = P (dP - sum_j P dP), 0 where masked
+__global__ __launch_bounds__(256) void tt_attn_ds_kernel(const float* qkv, const float* P, const float* datt,
+                                                         const float* x_mask, const float* erv, int T, int C, int W,
+                                                         Drop drop, float* dS) {
+  __shared__ float s_g[TT_D], s_ev[TT_WMAX * TT_D], s_dp[TT_TMAX], s_red[4];
+  const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z, H = gridDim.y, tid = threadIdx.x, nw = 2 * W + 1;
+  const long C3 = 3L * C;
+  const float* base = qkv + (long)b * T * C3;
+  for (int e = tid; e < TT_D; e += 256) s_g[e] = datt[((long)b * T + i) * C + h * TT_D + e];
+  for (int e = tid; e < nw * TT_D; e += 256) s_ev[e] = erv[e];
+  __syncthreads();
+  const long row = (((long)b * H + h) * T + i) * T;
+  float acc = 0.f;
+  for (int j = tid; j < T; j += 256) {
+    float dpd = dot96(s_g, base + (long)j * C3 + 2 * C + h * TT_D);
+    const int rel = j - i;
+    if (rel >= -W && rel <= W) {
+      float dr = 0.f;
+      for (int d = 0; d < TT_D; ++d) dr = fmaf(s_g[d], s_ev[(rel + W) * TT_D + d], dr);
+      dpd += dr;
+    }
+    const float dp = dpd * drop_scale(drop, (uint64_t)(row + j));
+    s_dp[j] = dp;
+    acc = fmaf(P[row + j], dp, acc);
+  }
+  acc = tt_block_sum(acc, s_red);
+  const bool qi = x_mask[(long)b * T + i] != 0.f;
+  for (int j = tid; j < T; j += 256) {
+    float ds = P[row + j] * (s_dp[j] - acc);
+    if (!(qi && x_mask[(long)b * T + j] != 0.f)) ds = 0.f;
+    dS[row + j] = ds;
+  }
+}
+
+// position i of utterance b, thread = (h, d): dq_i = (sum_j dS[i][j] k_j + sum_r dS[i][i + r] erk[r]) / sqrt(96),
+// dk_i = sum_j dS[j][i] q_j / sqrt(96), dv_i = sum_j Pd[j][i] g_j   -> dqkv [B][T][3C] (q | k | v)
+__global__ __launch_bounds__(256) void tt_attn_dqkv_kernel(const float* qkv, const float* Pd, const float* dS,
+                                                           const float* datt, const float* erk, int T, int C, int H,
+                                                           int W, float* dqkv) {
+  const int i = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  if (tid >= C) return;
+  const int h = tid / TT_D, d = tid % TT_D;
+  const long C3 = 3L * C, hb = ((long)b * H + h) * T * T;
+  const float* q = qkv + (long)b * T * C3 + tid;
+  const float* g = datt + (long)b * T * C + tid;
+  float dq = 0.f, dk = 0.f, dv = 0.f;
+  for (int j = 0; j < T; ++j) {
+    dq = fmaf(dS[hb + (long)i * T + j], q[(long)j * C3 + C], dq);
+    dk = fmaf(dS[hb + (long)j * T + i], q[(long)j * C3], dk);
+    dv = fmaf(Pd[hb + (long)j * T + i], g[(long)j * C], dv);
+  }
+  for (int r = -W; r <= W; ++r) {
+    const int j = i + r;
+    if (j >= 0 && j < T) dq = fmaf(dS[hb + (long)i * T + j], erk[(r + W) * TT_D + d], dq);
+  }
+  const float sq = sqrtf((float)TT_D);
+  float* o = dqkv + ((long)b * T + i) * C3 + tid;
+  o[0] = dq / sq;
+  o[C] = dk / sq;
+  o[2 * C] = dv;
+}
+
+// per utterance b (grid z), offset r (grid x) and tensor (grid y: 0 = emb_rel_k, 1 = emb_rel_v):
+// part[b][y][r][d] = sum_{h, i} dS[h][i][i + r] q[i][h 96 + d] / sqrt(96)   |   Pd[h][i][i + r] g[i][h 96 + d]
+__global__ __launch_bounds__(128) void tt_attn_drel_kernel(const float* qkv, const float* Pd, const float* dS,
+                                                           const float* datt, int T, int C, int H, int W, float* part) {
+  const int r = (int)blockIdx.x - W, which = blockIdx.y, b = blockIdx.z, d = threadIdx.x, nw = 2 * W + 1;
+  if (d >= TT_D) return;
+  const long C3 = 3L * C;
+  const float* M = which ? Pd : dS;
+  float acc = 0.f;
+  for (int h = 0; h < H; ++h) {
+    const long hb = ((long)b * H + h) * T * T;
+    const float* v = which ? datt + (long)b * T * C + h * TT_D + d : qkv + (long)b * T * C3 + h * TT_D + d;
+    const long vs = which ? C : C3;
+    for (int i = 0; i < T; ++i) {
+      const int j = i + r;
+      if (j < 0 || j >= T) continue;
+      acc = fmaf(M[hb + (long)i * T + j], v[(long)i * vs], acc);
+    }
+  }
+  if (!which) acc = acc / sqrtf((float)TT_D);
+  part[(((long)b * 2 + which) * nw + (r + W)) * TT_D + d] = acc;
+}
+
+// ---------------------------------------------------------------- LayerNorm backward
+constexpr int TT_LN_NPB = 32;   // positions per workgroup (8 per wave)
+__global__ __launch_bounds__(256) void tt_ln_bwd_kernel(LnBwdParams p) {
+  __shared__ float s_part[4][2][256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, C = p.C;
+  const long p0 = (long)blockIdx.x * TT_LN_NPB, p1 = min(p.npos, p0 + TT_LN_NPB);
+  float ga[4] = {0.f, 0.f, 0.f, 0.f}, ba[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long pos = p0 + wv; pos < p1; pos += 4) {
+    float v[4], g[4], xh[4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = lane + 64 * k;
+      v[k] = 0.f;
+      if (c < C) {
+        v[k] = p.x[pos * p.x_cs + c];
+        if (p.res) v[k] = v[k] + p.res[pos * p.res_cs + c];
+        s += v[k];
+      }
+    }
+    s = tt_wave_sum(s);
+    const float mean = s / (float)C;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lane + 64 * k < C) q += (v[k] - mean) * (v[k] - mean);
+    q = tt_wave_sum(q);
+    const float rs = rsqrtf(q / (float)C + p.eps);
+    const float dm = p.dy_mask ? p.dy_mask[pos] : 1.f;
+    float m1 = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = lane + 64 * k;
+      g[k] = 0.f;
+      xh[k] = 0.f;
+      if (c >= C) continue;
+      xh[k] = (v[k] - mean) * rs;
+      float gy = p.dy[pos * p.dy_cs + c] * dm * drop_scale(p.drop, (uint64_t)pos * C + c);
+      if (p.relu_ref && !(p.relu_ref[pos * C + c] > 0.f)) gy = 0.f;
+      ga[k] = fmaf(gy, xh[k], ga[k]);
+      ba[k] += gy;
+      g[k] = gy * p.gamma[c];
+      m1 += g[k];
+      m2 = fmaf(g[k], xh[k], m2);
+    }
+    m1 = tt_wave_sum(m1) / (float)C;
+    m2 = tt_wave_sum(m2) / (float)C;
+    const float xm = p.dx_mask ? p.dx_mask[pos] : 1.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = lane + 64 * k;
+      if (c >= C) continue;
+      float dx = rs * (g[k] - m1 - xh[k] * m2);
+      if (p.post_relu && !(v[k] > 0.f)) dx = 0.f;
+      dx *= xm;
+      float* o = p.dx + pos * p.dx_cs + c;
+      *o = p.dx_accumulate ? *o + dx : dx;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s_part[wv][0][lane + 64 * k] = ga[k];
+    s_part[wv][1][lane + 64 * k] = ba[k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * C; e += 256) {
+    const int w2 = e / C, c = e % C;
+    p.part[(long)blockIdx.x * 2 * C + e] =
+        ((s_part[0][w2][c] + s_part[1][w2][c]) + s_part[2][w2][c]) + s_part[3][w2][c];
+  }
+}
+
+// ---------------------------------------------------------------- conv1d weight gradient
+template <int KM>
+__global__ __launch_bounds__(256) void tt_wgrad_kernel(WgradParams p) {
+  __shared__ float s_d[32][65];
+  __shared__ float s_x[32 + KM - 1][65];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+  const int o0 = blockIdx.x * 64, c0 = blockIdx.y * 64, split = blockIdx.z;
+  const int wo = (wv & 1) * 32, wc = (wv >> 1) * 32, K = p.K;
+  const int nct = (p.T + 31) / 32, nch = p.B * nct;
+  const int ch0 = (int)((long)split * nch / p.nsplit), ch1 = (int)((long)(split + 1) * nch / p.nsplit);
+  f32x16 acc[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[k][j] = 0.f;
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int b = ch / nct, t0 = (ch % nct) * 32;
+    __syncthreads();
+    for (int e = tid; e < 32 * 64; e += 256) {
+      const int pp = e >> 6, oo = e & 63, t = t0 + pp;
+      s_d[pp][oo] = (t < p.T && o0 + oo < p.Cout) ? p.dout[((long)b * p.T + t) * p.d_cs + o0 + oo] : 0.f;
+    }
+    for (int e = tid; e < (32 + K - 1) * 64; e += 256) {
+      const int pp = e >> 6, cc = e & 63, t = t0 + pp - p.pad;
+      float v = 0.f;
+      if (t >= 0 && t < p.T && c0 + cc < p.Cin) {
+        v = p.x[((long)b * p.T + t) * p.x_cs + c0 + cc];
+        if (p.x_mask) v *= p.x_mask[(long)b * p.T + t];
+      }
+      s_x[pp][cc] = v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      const int kp = 2 * s + hh;
+      const float a = s_d[kp][wo + r];
+#pragma unroll
+      for (int k = 0; k < KM; ++k)
+        if (k < K) acc[k] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, s_x[kp + k][wc + r], acc[k], 0, 0, 0);
+    }
+  }
+  const int c = c0 + wc + r;
+  if (c >= p.Cin) return;
+  float* out = p.out + (long)split * p.Cout * p.Cin * K;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k >= K) break;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int o = o0 + wo + acc_row(j, hh);
+      if (o < p.Cout) out[((long)o * p.Cin + c) * K + k] = acc[k][j];
+    }
+  }
+}
+
+// part[s][c] = sum over split s's positions of x[pos][c] (4 position lanes per channel, combined in order)
+__global__ __launch_bounds__(256) void tt_colsum_kernel(const float* x, int x_cs, long npos, int C, int nsplit,
+                                                        float* part) {
+  __shared__ float s_p[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, s = blockIdx.y;
+  const long a = (long)s * npos / nsplit, e = (long)(s + 1) * npos / nsplit;
+  float acc = 0.f;
+  if (c < C)
+    for (long pos = a + g; pos < e; pos += 4) acc += x[pos * x_cs + c];
+  s_p[g][cl] = acc;
+  __syncthreads();
+  if (g == 0 && c < C) part[(long)s * C + c] = ((s_p[0][cl] + s_p[1][cl]) + s_p[2][cl]) + s_p[3][cl];
+}
+
+// out[i] = sum_s part[s n + i] in split order
+__global__ void tt_sum_splits_kernel(const float* part, int nsplit, long n, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a = 0.f;
+  for (int s = 0; s < nsplit; ++s) a += part[(long)s * n + i];
+  out[i] = a;
+}
+
+// ---------------------------------------------------------------- embedding, elementwise
+__global__ __launch_bounds__(256) void tt_emb_bwd_kernel(const int64_t* tokens, long npos, const float* dx0, int C,
+                                                         float scale, float* demb) {
+  const int v = blockIdx.x, c = threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.f;
+  for (long pos = 0; pos < npos; ++pos)
+    if (tokens[pos] == v) acc += dx0[pos * C + c];
+  demb[(long)v * C + c] = acc * scale;
+}
+
+__global__ void tt_ew_kernel(EwParams p) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= p.npos * p.C) return;
+  const long pos = e / p.C;
+  const int c = (int)(e % p.C);
+  float v;
+  if (!p.src) {
+    v = 0.f;
+  } else if (p.src_chan_major) {
+    const long b = pos / p.T, t = pos % p.T;
+    v = p.src[(b * p.C + c) * p.T + t];
+  } else {
+    v = p.src[pos * p.src_cs + c];
+  }
+  if (p.mask) v *= p.mask[pos];
+  v *= drop_scale(p.drop, (uint64_t)pos * p.C + c);
+  if (p.relu_ref && !(p.relu_ref[pos * p.relu_cs + c] > 0.f)) v = 0.f;
+  p.dst[pos * p.dst_cs + c] = v;
+}
+
+__global__ void tt_copy_words_kernel(uint32_t* dst, const uint32_t* src, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- GradTTS.compute_loss glue
+// dmu_x[b][f][i] = sum_j attn[b][i][j] dmu_y[b][f][j]   (backward of tts.py:184-185's matmul)
+__global__ __launch_bounds__(128) void tt_path_scatter_kernel(const float* attn, const float* dmu_y, int Tx, int Ty,
+                                                              int F, float* dmu_x) {
+  const int i = blockIdx.x, b = blockIdx.y, f = threadIdx.x;
+  if (f >= F) return;
+  const float* a = attn + ((long)b * Tx + i) * Ty;
+  const float* g = dmu_y + ((long)b * F + f) * Ty;
+  float acc = 0.f;
+  for (int j = 0; j < Ty; ++j) {
+    const float w = a[j];
+    if (w != 0.f) acc = fmaf(w, g[j], acc);
+  }
+  dmu_x[((long)b * F + f) * Tx + i] = acc;
+}
+
+// out[0] = dur_loss = sum_{b,i} (logw - log(1e-8 + sum_j attn) x_mask)^2 / sum x_lengths
+// out[1] = prior_loss = sum_{b,f,t} 0.5 ((y - mu_y)^2 + log 2 pi) y_mask / (sum y_mask * F)
+// dlogw_unit = d dur_loss / d logw, dmu_unit = d prior_loss / d mu_y  (second phase, after the sums)
+__global__ __launch_bounds__(1024) void tt_aux_loss_kernel(const float* logw, const float* attn, const float* x_mask,
+                                                           const int64_t* x_lengths, const float* y,
+                                                           const float* mu_y, const float* y_mask, int B, int Tx,
+                                                           int Ta, int Ty, int F, float* out, float* dlogw_unit,
+                                                           float* dmu_unit) {
+  __shared__ double s_red[16];
+  const int tid = threadIdx.x;
+  auto bsum = [&](double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    __syncthreads();
+    if ((tid & 63) == 0) s_red[tid >> 6] = x;
+    __syncthreads();
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += s_red[w];
+    return t;
+  };
+  // duration loss
+  double dsum = 0.0;
+  for (long e = tid; e < (long)B * Tx; e += 1024) {
+    const float* a = attn + e * Ta;
+    float dur = 0.f;
+    for (int j = 0; j < Ta; ++j) dur += a[j];
+    const float lw_ = logf(1e-8f + dur) * x_mask[e];
+    const float df = logw[e] - lw_;
+    dsum += (double)df * df;
+    dlogw_unit[e] = df;   // scaled below
+  }
+  dsum = bsum(dsum);
+  double lsum = 0.0;
+  for (int b = 0; b < B; ++b) lsum += (double)x_lengths[b];
+  // prior loss
+  const float l2pi = 1.8378770664093453f;   // log(2 pi)
+  double psum = 0.0, msum = 0.0;
+  for (long e = tid; e < (long)B * F * Ty; e += 1024) {
+    const long b = e / ((long)F * Ty), t = e % Ty;
+    const float m = y_mask[b * Ty + t];
+    const float d = y[e] - mu_y[e];
+    psum += (double)(0.5f * (d * d + l2pi) * m);
+  }
+  for (long e = tid; e < (long)B * Ty; e += 1024) msum += (double)y_mask[e];
+  psum = bsum(psum);
+  msum = bsum(msum);
+  const double pden = msum * F;
+  if (tid == 0) {
+    out[0] = (float)(dsum / lsum);
+    out[1] = (float)(psum / pden);
+  }
+  const float dscale = (float)(2.0 / lsum), pscale = (float)(1.0 / pden);
+  for (long e = tid; e < (long)B * Tx; e += 1024) dlogw_unit[e] = dlogw_unit[e] * dscale;
+  for (long e = tid; e < (long)B * F * Ty; e += 1024) {
+    const long b = e / ((long)F * Ty), t = e % Ty;
+    dmu_unit[e] = -(y[e] - mu_y[e]) * y_mask[b * Ty + t] * pscale;
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_tt_attn_fwd(const float* qkv, const float* x_mask, const float* erk, const float* erv, int B, int T,
+                              int C, int H, int W, Drop drop, float* P, float* Pd, float* out, hipStream_t s) {
+  if (C != H * TT_D || 2 * W + 1 > TT_WMAX || T > TT_TMAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tt_attn_p_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, x_mask, erk, T, C, W, drop, P, Pd);
+  hipLaunchKernelGGL(tt_attn_pv_kernel, dim3(T, B), dim3(256), 0, s, qkv, Pd, erv, T, C, H, W, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_attn_bwd(const float* qkv, const float* P, const float* Pd, const float* datt,
+                              const float* x_mask, const float* erk, const float* erv, int B, int T, int C, int H,
+                              int W, Drop drop, float* dS, float* dqkv, float* drel_part, float* derk_derv,
+                              hipStream_t s) {
+  if (C != H * TT_D || 2 * W + 1 > TT_WMAX || T > TT_TMAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tt_attn_ds_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, P, datt, x_mask, erv, T, C, W, drop, dS);
+  hipLaunchKernelGGL(tt_attn_dqkv_kernel, dim3(T, B), dim3(256), 0, s, qkv, Pd, dS, datt, erk, T, C, H, W, dqkv);
+  const int nw = 2 * W + 1;
+  hipLaunchKernelGGL(tt_attn_drel_kernel, dim3(nw, 2, B), dim3(128), 0, s, qkv, Pd, dS, datt, T, C, H, W, drel_part);
+  // derk_derv = [emb_rel_k grad (nw x 96) | emb_rel_v grad (nw x 96)] summed over utterances in order
+  const long n = 2L * nw * TT_D;
+  hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, drel_part, B, n,
+                     derk_derv);
+  return hipGetLastError();
+}
+
+long tt_ln_bwd_blocks(long npos) { return (npos + TT_LN_NPB - 1) / TT_LN_NPB; }
+
+hipError_t launch_tt_ln_bwd(const LnBwdParams& p, float* dgamma_dbeta, hipStream_t s) {
+  if (p.C > 256 || p.npos <= 0) return hipErrorInvalidValue;
+  const long nb = tt_ln_bwd_blocks(p.npos);
+  hipLaunchKernelGGL(tt_ln_bwd_kernel, dim3((unsigned)nb), dim3(256), 0, s, p);
+  const long n = 2L * p.C;
+  hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p.part, (int)nb, n,
+                     dgamma_dbeta);
+  return hipGetLastError();
+}
+
+int tt_wgrad_splits(const WgradParams& p) {
+  const long tiles = (long)((p.Cout + 63) / 64) * ((p.Cin + 63) / 64);
+  const long nch = (long)p.B * ((p.T + 31) / 32);
+  long ns = (512 + tiles - 1) / tiles;
+  ns = std::min(ns, std::max(1L, nch / 2));
+  return (int)std::max(1L, ns);
+}
+
+hipError_t launch_tt_wgrad(WgradParams p, float* dW, float* partial, long partial_floats, hipStream_t s) {
+  if (p.K < 1 || p.K > 5) return hipErrorInvalidValue;
+  p.nsplit = tt_wgrad_splits(p);
+  const long n = (long)p.Cout * p.Cin * p.K;
+  if (p.nsplit > 1 && (long)p.nsplit * n > partial_floats) p.nsplit = (int)std::max(1L, partial_floats / n);
+  p.out = p.nsplit > 1 ? partial : dW;
+  const dim3 grid((unsigned)((p.Cout + 63) / 64), (unsigned)((p.Cin + 63) / 64), (unsigned)p.nsplit);
+  if (p.K == 1) hipLaunchKernelGGL((tt_wgrad_kernel<1>), grid, dim3(256), 0, s, p);
+  else if (p.K <= 3) hipLaunchKernelGGL((tt_wgrad_kernel<3>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((tt_wgrad_kernel<5>), grid, dim3(256), 0, s, p);
+  if (p.nsplit > 1)
+    hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, partial, p.nsplit, n,
+                       dW);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_colsum(const float* x, int x_cs, long npos, int C, float* part, long part_floats, float* out,
+                            hipStream_t s) {
+  int ns = (int)std::min<long>(64, std::max(1L, npos / 64));
+  ns = (int)std::max<long>(1, std::min<long>(ns, part_floats / C));
+  hipLaunchKernelGGL(tt_colsum_kernel, dim3((unsigned)((C + 63) / 64), ns), dim3(256), 0, s, x, x_cs, npos, C, ns, part);
+  hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, ns, (long)C, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_emb_bwd(const int64_t* tokens, long npos, const float* dx0, int n_vocab, int C, float scale,
+                             float* demb, hipStream_t s) {
+  if (C > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tt_emb_bwd_kernel, dim3(n_vocab), dim3(256), 0, s, tokens, npos, dx0, C, scale, demb);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_ew(const EwParams& p, hipStream_t s) {
+  const long n = p.npos * p.C;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tt_ew_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_copy_words(uint32_t* dst, const uint32_t* src, long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tt_copy_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_path_scatter(const float* attn, const float* dmu_y, int B, int Tx, int Ty, int F, float* dmu_x,
+                                  hipStream_t s) {
+  if (F > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tt_path_scatter_kernel, dim3(Tx, B), dim3(128), 0, s, attn, dmu_y, Tx, Ty, F, dmu_x);
+  return hipGetLastError();
+}
+
+hipError_t launch_tt_aux_loss(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths,
+                              const float* y, const float* mu_y, const float* y_mask, int B, int Tx, int Ta, int Ty,
+                              int F, float* out, float* dlogw_unit, float* dmu_unit, hipStream_t s) {
+  hipLaunchKernelGGL(tt_aux_loss_kernel, dim3(1), dim3(1024), 0, s, logw, attn, x_mask, x_lengths, y, mu_y, y_mask, B,
+                     Tx, Ta, Ty, F, out, dlogw_unit, dmu_unit);
+  return hipGetLastError();
+}
+
+}  // namespace gt

@@ -104,7 +104,13 @@ class Encoder(torch.nn.Module):
 class TextEncoder(torch.nn.Module):
     """``TextEncoder(n_vocab, n_feats, n_channels, filter_channels, filter_channels_dp, n_heads, n_layers,
     kernel_size, p_dropout, window_size=None, spk_emb_dim=64, n_spks=1)``; ``forward(x, x_lengths, spk=None)`` ->
-    (mu [B, n_feats, Tx], logw [B, 1, Tx], x_mask [B, 1, Tx]) in eval semantics (no dropout)."""
+    (mu [B, n_feats, Tx], logw [B, 1, Tx], x_mask [B, 1, Tx]).
+
+    With gradients enabled and parameters that require them, ``forward`` is the training pass
+    (``gt_text_encoder_forward_train`` + ``gt_text_encoder_backward`` behind an autograd Function): in train mode the
+    reference's dropouts apply (``p_dropout`` at the attention probabilities, attention / FFN outputs, FFN hidden
+    and duration predictor; 0.5 in the prenet), drawn from the library's counter-based generator with a seed taken
+    from torch's CPU generator; in eval mode none do. Otherwise it is the inference pass (eval semantics)."""
 
     def __init__(self, n_vocab, n_feats, n_channels, filter_channels, filter_channels_dp, n_heads, n_layers,
                  kernel_size, p_dropout, window_size=None, spk_emb_dim=64, n_spks=1):
@@ -115,6 +121,7 @@ class TextEncoder(torch.nn.Module):
         self.n_vocab, self.n_feats, self.n_channels = n_vocab, n_feats, n_channels
         self.filter_channels, self.filter_channels_dp = filter_channels, filter_channels_dp
         self.n_heads, self.n_layers, self.kernel_size, self.window_size = n_heads, n_layers, kernel_size, window_size
+        self.p_dropout = p_dropout
         self.emb = torch.nn.Embedding(n_vocab, n_channels)
         torch.nn.init.normal_(self.emb.weight, 0.0, n_channels ** -0.5)
         self.prenet = ConvReluNorm(n_channels, n_channels, n_channels, kernel_size=5, n_layers=3, p_dropout=0.5)
@@ -160,6 +167,15 @@ class TextEncoder(torch.nn.Module):
         tokens = x.to(device=device, dtype=torch.int64).contiguous()
         lengths = x_lengths.to(device=device, dtype=torch.int64).contiguous()
         B, Tx = tokens.shape
+        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
+            p, ppre = (float(self.p_dropout), 0.5) if self.training else (0.0, 0.0)
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (p > 0 or ppre > 0) else 0
+            with torch.cuda.device(device):
+                h = self._native()
+                named = dict(self.named_parameters())
+                plist = [named[lib().gt_text_encoder_param_name(h, i).decode()]
+                         for i in range(lib().gt_text_encoder_num_params(h))]   # the library's inventory order
+                return _TextEncoderTrain.apply(self, h, tokens, lengths, p, ppre, seed, *plist)
         with torch.cuda.device(device):
             h = self._native()
             mu = torch.empty(B, self.n_feats, Tx, dtype=torch.float32, device=device)
@@ -170,6 +186,52 @@ class TextEncoder(torch.nn.Module):
                                                 logw.data_ptr(), x_mask.data_ptr(), ws.data_ptr(), ws.numel(),
                                                 _stream_ptr(device)), "gt_text_encoder_forward")
         return mu, logw, x_mask
+
+
+class _TextEncoderTrain(torch.autograd.Function):
+    """TextEncoder.forward with gradients: the library's training forward keeps a tape in a workspace this Function
+    holds until backward, which writes every parameter's gradient into one flat buffer (views of it go to the
+    parameters, passed in the library's inventory order)."""
+
+    @staticmethod
+    def forward(ctx, enc, h, tokens, lengths, p, ppre, seed, *params):
+        from .diffusion import _stream_ptr
+        device = tokens.device
+        B, Tx = tokens.shape
+        L = lib()
+        mu = torch.empty(B, enc.n_feats, Tx, dtype=torch.float32, device=device)
+        logw = torch.empty(B, 1, Tx, dtype=torch.float32, device=device)
+        x_mask = torch.empty(B, 1, Tx, dtype=torch.float32, device=device)
+        ws = torch.empty(L.gt_text_encoder_train_workspace_bytes(h, B, Tx), dtype=torch.uint8, device=device)
+        check(L.gt_text_encoder_forward_train(h, tokens.data_ptr(), lengths.data_ptr(), B, Tx, p, ppre, seed,
+                                              mu.data_ptr(), logw.data_ptr(), x_mask.data_ptr(), ws.data_ptr(),
+                                              ws.numel(), _stream_ptr(device)), "gt_text_encoder_forward_train")
+        ctx.h, ctx.ws, ctx.shape = h, ws, (B, Tx)
+        ctx.pshapes = [q.shape for q in params]
+        ctx.mark_non_differentiable(x_mask)
+        return mu, logw, x_mask
+
+    @staticmethod
+    def backward(ctx, dmu, dlogw, _dmask):
+        from .diffusion import _stream_ptr
+        B, Tx = ctx.shape
+        device = ctx.ws.device
+        L = lib()
+        grads = torch.empty(L.gt_text_encoder_grad_numel(ctx.h), dtype=torch.float32, device=device)
+        dmu = dmu.to(torch.float32).contiguous() if dmu is not None else None
+        dlogw = dlogw.to(torch.float32).contiguous() if dlogw is not None else None
+        with torch.cuda.device(device):
+            check(L.gt_text_encoder_backward(ctx.h, dmu.data_ptr() if dmu is not None else None,
+                                             dlogw.data_ptr() if dlogw is not None else None, B, Tx, grads.data_ptr(),
+                                             ctx.ws.data_ptr(), ctx.ws.numel(), _stream_ptr(device)),
+                  "gt_text_encoder_backward")
+        out, off = [], 0
+        for shp in ctx.pshapes:
+            n = int(np.prod(shp)) if len(shp) else 1
+            out.append(grads[off:off + n].view(shp))
+            off += n
+        ctx.ws = None
+        return (None, None, None, None, None, None, None, *out)
 
 
 def fix_len_compatibility(length, num_downsamplings_in_unet=2):

@@ -213,6 +213,33 @@ int gt_expand(const float* mu_x, const float* cum, const float* x_mask, const in
 int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
                    float* mu_y, void* stream);
 
+/* Text-encoder training pass of GradTTS.compute_loss (model/tts.py:136: TextEncoder.forward in train mode,
+ * text_encoder.py:321-335) and its backward. gt_text_encoder_forward_train = gt_text_encoder_forward plus the
+ * training dropouts (p_dropout: attention probabilities, attention / FFN outputs, FFN hidden, duration predictor;
+ * p_dropout_prenet: ConvReluNorm's 0.5; 0 = eval semantics) drawn from `seed` by the library's counter-based
+ * generator, and a tape of the activations in `workspace` (gt_text_encoder_train_workspace_bytes). Tx <= 4096.
+ * gt_text_encoder_backward: given dmu_x [B,n_feats,Tx] and dlogw [B,1,Tx] (either may be NULL = zero), writes the
+ * gradient of every encoder parameter into grads (gt_text_encoder_grad_numel floats, state_dict inventory order,
+ * reference layouts); the duration predictor sees a detached input (text_encoder.py:332), so dlogw reaches only its
+ * parameters. Same encoder, B, Tx and workspace as the forward_train call it follows, parameters unchanged between. */
+size_t gt_text_encoder_train_workspace_bytes(gt_text_encoder* enc, int64_t B, int64_t Tx);
+int64_t gt_text_encoder_grad_numel(gt_text_encoder* enc);
+int gt_text_encoder_forward_train(gt_text_encoder* enc, const int64_t* tokens, const int64_t* x_lengths, int64_t B,
+                                  int64_t Tx, float p_dropout, float p_dropout_prenet, uint64_t seed, float* mu_x,
+                                  float* logw, float* x_mask, void* workspace, size_t workspace_bytes, void* stream);
+int gt_text_encoder_backward(gt_text_encoder* enc, const float* dmu_x, const float* dlogw, int64_t B, int64_t Tx,
+                             float* grads, void* workspace, size_t workspace_bytes, void* stream);
+/* dmu_x [B,n_feats,Tx] = attn dmu_y: the backward of mu_y = attn^T mu_x (tts.py:184-185), attn [B,Tx,Ty] 0/1 */
+int gt_path_scatter(const float* attn, const float* dmu_y, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
+                    float* dmu_x, void* stream);
+/* dur_loss (tts.py:155-156 with utils.py:42-44 duration_loss over logw [B,1,Tx] and the MAS attn [B,Tx,Ty]) and
+ * prior_loss (tts.py:191-192 over y, mu_y [B,n_feats,Ty'] and y_mask [B,1,Ty']) in one call: losses[0] = dur_loss,
+ * losses[1] = prior_loss (device); dlogw_unit = d dur_loss / d logw, dmu_y_unit = d prior_loss / d mu_y. Fixed
+ * summation order (fp64 accumulators). */
+int gt_tts_aux_losses(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths, int64_t B,
+                      int64_t Tx, int64_t Ty_attn, const float* y, const float* mu_y, const float* y_mask, int64_t Ty,
+                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* stream);
+
 /* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1 :13-48 / ResBlock2 :53-74; the vocoder of
  * inference.py:73-97). fp32. Parameters by the reference Generator's state_dict names (bias, weight_g, weight_v per
  * conv); weight norm baked on upload as remove_weight_norm() does. gt_vocoder_forward: mel [B,n_mels,T] -> audio

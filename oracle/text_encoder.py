@@ -9,11 +9,57 @@ tests/golden/make_golden_tts.py produced by running the reference itself.
 * ffn, encoder          :220-282
 * text_encoder          :321-335
 * front_end             model/tts.py:86-101 with utils.py:6-39 (durations, y_lengths, generate_path, mu_y)
+* dropout_keep          the library's training-dropout generator (csrc/textenc.h Drop): NOT a reference algorithm
+                        (torch's dropout draws cannot be reproduced), restated so the training pass with dropout
+                        can be checked mask for mask; ``text_encoder(..., drop=...)`` applies the reference's
+                        dropouts (text_encoder.py:48, 166, 234-239, 258-280, 74-91) with these masks
 """
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
+
+
+M64 = (1 << 64) - 1
+
+
+def dropout_keep(seed, site, idx, p):
+    """Scale factor (1 / (1 - p) kept, 0 dropped) of the library's dropout for element indices `idx` (uint64 array):
+    u = top 24 bits of splitmix64's finaliser over seed + site 0x9E37..15 + idx 0xD1B5..03 (mod 2^64), kept iff
+    u >= round(p 2^24). p = 0: all ones."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    if p <= 0:
+        return np.ones(idx.shape)
+    thr = max(1, int(p * 16777216.0 + 0.5))
+    with np.errstate(over="ignore"):
+        x = (np.uint64((seed + site * 0x9E3779B97F4A7C15) & M64) + idx * np.uint64(0xD1B54A32D192ED03))
+        x = x ^ (x >> np.uint64(30))
+        x = x * np.uint64(0xBF58476D1CE4E5B9)
+        x = x ^ (x >> np.uint64(27))
+        x = x * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    u = (x >> np.uint64(40)).astype(np.int64)
+    return np.where(u >= thr, 1.0 / (1.0 - p), 0.0)
+
+
+class Dropouts:
+    """The masks of one training pass: seed, p (encoder / duration predictor) and p_prenet, as the library uses
+    them (sites: prenet 1-3, duration predictor 8-9, layer l: 16 + 8 l + {0 p_attn, 1 attention output, 2 FFN
+    hidden, 3 FFN output}); element index = (b T + t) C + c for [B, C, T] activations, ((b H + h) T + i) T + j
+    for p_attn."""
+
+    def __init__(self, seed, p, p_prenet):
+        self.seed, self.p, self.pp = seed, p, p_prenet
+
+    def chan(self, site, x, p):   # x [B, C, T]
+        B, C, T = x.shape
+        idx = (np.arange(B)[:, None, None] * T + np.arange(T)[None, None, :]) * C + np.arange(C)[None, :, None]
+        return x * torch.as_tensor(dropout_keep(self.seed, site, idx, p), dtype=x.dtype)
+
+    def attn(self, site, pa):     # pa [B, H, T, T]
+        idx = np.arange(pa.numel()).reshape(pa.shape)
+        return pa * torch.as_tensor(dropout_keep(self.seed, site, idx, self.p), dtype=pa.dtype)
 
 
 def layer_norm(x, g, b, eps=1e-4):
@@ -32,7 +78,7 @@ def ln(p, key, x):
     return layer_norm(x, p[key + ".gamma"], p[key + ".beta"])
 
 
-def attention(p, key, x, attn_mask, n_heads=2, window=4):
+def attention(p, key, x, attn_mask, n_heads=2, window=4, drop=None, site=0):
     q, k, v = conv(p, key + "conv_q", x), conv(p, key + "conv_k", x), conv(p, key + "conv_v", x)
     b, d, t = k.shape
     kc = d // n_heads
@@ -51,6 +97,8 @@ def attention(p, key, x, attn_mask, n_heads=2, window=4):
     scores = scores + rl / math.sqrt(kc)
     scores = scores.masked_fill(attn_mask == 0, -1e4)
     pa = torch.softmax(scores, dim=-1)
+    if drop is not None:
+        pa = drop.attn(site, pa)                        # MultiHeadAttention.drop(p_attn) (:166)
     out = torch.matmul(pa, v)
     Ev_full = Ev[(rel.clamp(-window, window) + window)] * inside[..., None]
     out = out + torch.einsum("bhij,ijc->bhic", pa, Ev_full)
@@ -58,7 +106,11 @@ def attention(p, key, x, attn_mask, n_heads=2, window=4):
     return conv(p, key + "conv_o", out)
 
 
-def text_encoder(p, tokens, x_lengths, n_layers=6, n_heads=2, window=4):
+def text_encoder(p, tokens, x_lengths, n_layers=6, n_heads=2, window=4, drop=None):
+    """drop: None (eval semantics) or a Dropouts (train mode with the library's masks). The duration predictor
+    reads x.detach() (:332)."""
+    D = (lambda site, v, q: drop.chan(site, v, q)) if drop is not None else (lambda site, v, q: v)
+    pe, pp = (drop.p, drop.pp) if drop is not None else (0.0, 0.0)
     C = p["emb.weight"].shape[1]
     x = p["emb.weight"][tokens] * math.sqrt(C)
     x = x.transpose(1, -1)
@@ -67,22 +119,25 @@ def text_encoder(p, tokens, x_lengths, n_layers=6, n_heads=2, window=4):
     x_org = x
     for i in range(3):                                  # ConvReluNorm (prenet)
         x = conv(p, f"prenet.conv_layers.{i}", x * x_mask)
-        x = torch.relu(ln(p, f"prenet.norm_layers.{i}", x))
+        x = D(1 + i, torch.relu(ln(p, f"prenet.norm_layers.{i}", x)), pp)
     x = (x_org + conv(p, "prenet.proj", x)) * x_mask
     attn_mask = x_mask.unsqueeze(2) * x_mask.unsqueeze(-1)
     for l in range(n_layers):                           # Encoder
+        site = 16 + 8 * l
         x = x * x_mask
-        y = attention(p, f"encoder.attn_layers.{l}.", x, attn_mask, n_heads, window)
-        x = ln(p, f"encoder.norm_layers_1.{l}", x + y)
+        y = attention(p, f"encoder.attn_layers.{l}.", x, attn_mask, n_heads, window, drop, site)
+        x = ln(p, f"encoder.norm_layers_1.{l}", x + D(site + 1, y, pe))
         f = f"encoder.ffn_layers.{l}."
-        y = conv(p, f + "conv_2", torch.relu(conv(p, f + "conv_1", x * x_mask)) * x_mask) * x_mask
-        x = ln(p, f"encoder.norm_layers_2.{l}", x + y)
+        hdn = D(site + 2, torch.relu(conv(p, f + "conv_1", x * x_mask)), pe)
+        y = conv(p, f + "conv_2", hdn * x_mask) * x_mask
+        x = ln(p, f"encoder.norm_layers_2.{l}", x + D(site + 3, y, pe))
     x = x * x_mask
     mu = conv(p, "proj_m", x) * x_mask
+    x = x.detach()
     d = torch.relu(conv(p, "proj_w.conv_1", x * x_mask))
-    d = ln(p, "proj_w.norm_1", d)
+    d = D(8, ln(p, "proj_w.norm_1", d), pe)
     d = torch.relu(conv(p, "proj_w.conv_2", d * x_mask))
-    d = ln(p, "proj_w.norm_2", d)
+    d = D(9, ln(p, "proj_w.norm_2", d), pe)
     logw = conv(p, "proj_w.proj", d * x_mask) * x_mask
     return mu, logw, x_mask
 

@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Golden fixtures for ``GradTTS.compute_loss`` (model/tts.py:110-194 -- text encoder, log-prior +
+MAS, duration loss, the ``out_size`` crop, ``mu_y``, the decoder's diffusion loss and the prior loss), produced by
+running the REAL reference in this container (the fixtures are data; the reference does not travel).
+
+* The reference ``model.tts.GradTTS`` with GradTTS's configuration (params.py: 149 symbols, 192 / 768 / 256 channels,
+  2 heads, 6 layers, kernel 3, window 4, 80 mels, decoder dim 64, single speaker), eval mode (dropout off: the
+  reference's dropout draws cannot be reproduced outside torch's generator), synthetic weights
+  (``gradtts_amd.params.synthetic_text_encoder_state_dict`` / ``synthetic_state_dict``; seeds and SHA-256 stored), in
+  float64 and float32.
+* The draws: ``random.seed(py_seed)`` before the call fixes the crop offsets (``random.choice``, tts.py:161-165; the
+  offsets are stored), ``torch.rand`` (t, diffusion.py:284) and ``torch.randn`` (z, diffusion.py:249) return stored
+  values.
+* Stored: the three losses, the MAS path, ``(dur + prior + diff).backward()``'s gradient of every parameter as a
+  digest (sum of squares, projection on ``oracle.decoder.grad_probe``) and a few full gradients.
+
+Usage:  make -C oracle ref && PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_tts_loss.py
+"""
+from __future__ import annotations
+
+import os
+import random
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "grad-tts_amd"))
+sys.dont_write_bytecode = True
+from make_golden import import_reference, save  # noqa: E402
+from make_golden_train_lik import fixed_randn  # noqa: E402
+from gradtts_amd.params import (state_dict_sha256, synthetic_state_dict,  # noqa: E402
+                                synthetic_text_encoder_state_dict)
+sys.path.insert(0, REPO)
+from oracle.decoder import grad_probe  # noqa: E402
+
+FULL = ("encoder.emb.weight", "encoder.encoder.attn_layers.0.emb_rel_k", "encoder.encoder.attn_layers.5.emb_rel_v",
+        "encoder.proj_m.bias", "encoder.proj_w.proj.weight", "encoder.encoder.norm_layers_1.2.gamma",
+        "encoder.prenet.norm_layers.0.beta", "encoder.prenet.proj.bias", "decoder.estimator.final_conv.bias")
+
+
+class fixed_rand:
+    """torch.rand(n, dtype=...) inside the block returns the stored t (Diffusion.compute_loss's only torch.rand)."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __enter__(self):
+        self.orig = torch.rand
+
+        def rand(*shape, dtype=None, device=None, requires_grad=False, **kw):
+            shape = tuple(shape[0]) if len(shape) == 1 and not isinstance(shape[0], int) else shape
+            assert tuple(shape) == tuple(self.t.shape), shape
+            return self.t.to(dtype=dtype or torch.float32, device=device).clone()
+
+        torch.rand = rand
+
+    def __exit__(self, *exc):
+        torch.rand = self.orig
+        return False
+
+
+def gradtts_state_dict(seed_enc, seed_dec):
+    sd = {f"encoder.{k}": v for k, v in synthetic_text_encoder_state_dict(seed_enc).items()}
+    sd.update({f"decoder.estimator.{k}": v for k, v in synthetic_state_dict(seed=seed_dec).items()})
+    return sd
+
+
+def case(tts, name, x_lengths, y_lengths, Tx, Ty, out_size, py_seed, tvals, seed_in, seed_z, seed_enc=5, seed_dec=0):
+    rng = np.random.default_rng(seed_in)
+    B = len(x_lengths)
+    tokens = rng.integers(0, 149, size=(B, Tx)).astype(np.int64)
+    y = (rng.standard_normal((B, 80, Ty)) * 1.5).astype(np.float32)
+    for b, yl in enumerate(y_lengths):
+        y[b, :, yl:] = 0.0                      # padded frames of a batch are zero (data.py's collate)
+    t = np.asarray(tvals, np.float32)
+    Tz = out_size if out_size is not None else Ty
+    z32 = torch.from_numpy(np.random.default_rng(seed_z).standard_normal((B, 80, Tz)).astype(np.float32))
+    sd = gradtts_state_dict(seed_enc, seed_dec)
+    random.seed(py_seed)
+    mo = (np.array(y_lengths) - out_size).clip(0) if out_size is not None else np.zeros(B, np.int64)
+    offsets = np.array([random.choice(range(0, int(e))) if e > 0 else 0 for e in mo], np.int64)
+    out = dict(tokens=tokens, x_lengths=np.array(x_lengths, np.int64), y=y, y_lengths=np.array(y_lengths, np.int64),
+               out_size=np.int64(out_size if out_size is not None else -1), py_seed=np.int64(py_seed),
+               offsets=offsets, t=t, z=z32.numpy(), seed_enc=np.int64(seed_enc), seed_dec=np.int64(seed_dec),
+               weights_sha256=np.array(state_dict_sha256(sd)))
+    for dt, tag in ((torch.float64, "f64"), (torch.float32, "f32")):
+        torch.manual_seed(0)
+        model = tts.GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+        assert list(model.state_dict().keys()) == list(sd.keys()), "inventory differs from the reference"
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        model = model.to(dt).eval()
+        random.seed(py_seed)
+        with fixed_rand(torch.from_numpy(t)), fixed_randn(z32) as drawn:
+            dur, prior, diff = model.compute_loss(torch.from_numpy(tokens), torch.from_numpy(out["x_lengths"]),
+                                                  torch.from_numpy(y).to(dt), torch.from_numpy(out["y_lengths"]),
+                                                  out_size=out_size)
+        assert drawn == [(B, 80, Tz)], drawn
+        (dur + prior + diff).backward()
+        named = dict(model.named_parameters())
+        keys = list(sd.keys())
+        g = [named[k].grad for k in keys]
+        out[f"losses_{tag}"] = np.array([float(dur), float(prior), float(diff)])
+        out[f"gsq_{tag}"] = np.array([float((gi.double() ** 2).sum()) if gi is not None else 0.0 for gi in g])
+        out[f"gproj_{tag}"] = np.array([float((gi.double() * torch.from_numpy(grad_probe(k, tuple(gi.shape)))).sum())
+                                        if gi is not None else 0.0 for k, gi in zip(keys, g)])
+        if tag == "f64":
+            for k in FULL:
+                out["full__" + k] = named[k].grad.numpy()
+    # the MAS path of the fp32 run (recomputed with the reference's own modules, tts.py:136-152)
+    out["param_names"] = np.array(list(sd.keys()))
+    save(name, **out)
+
+
+def main():
+    import_reference()
+    import model.tts as tts   # noqa: E402  (model.text_encoder, model.utils, model.monotonic_align as installed above)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    case(tts, "tts_loss_B2.npz", [13, 9], [56, 41], 13, 56, 32, py_seed=3, tvals=[0.63, 0.18], seed_in=61, seed_z=62)
+    case(tts, "tts_loss_B3_nocut.npz", [7, 11, 5], [30, 44, 21], 11, 44, None, py_seed=4, tvals=[0.35, 0.77, 0.52],
+         seed_in=63, seed_z=64)
+
+
+if __name__ == "__main__":
+    main()

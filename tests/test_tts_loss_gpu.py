@@ -1,0 +1,157 @@
+"""GradTTS.compute_loss (model/tts.py:110-194) on the MI355X: the text encoder's training pass
+(gt_text_encoder_forward_train / gt_text_encoder_backward), the alignment, the crop, mu_y, the auxiliary losses and
+the decoder's training step, all through the library.
+
+Tolerances (written here):
+* against the REAL reference (tests/golden/tts_loss_*.npz, eval mode, fp64 reference gradients): each loss rel 1e-5
+  of the reference's fp32 value; every parameter gradient's digest (norm and random projection,
+  oracle.decoder.grad_digest) within 1e-3 of the reference's fp64 gradient relative to that tensor's norm (+ 1e-3 of
+  the largest norm) -- fp32 through six transformer layers and the U-Net;
+* train mode (dropout on, the library's masks restated by oracle.text_encoder.dropout_keep): mu_x / logw 1e-5 x
+  max|ref|, encoder parameter gradients under random upstream gradients as above, against torch.autograd through
+  oracle/text_encoder.py in fp64;
+* two calls bit-identical (fixed-order reductions).
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available, load_golden
+from gpu_util import rel_err, report
+from gradtts_amd.params import synthetic_state_dict, synthetic_text_encoder_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def make_gradtts(seed_enc=5, seed_dec=0):
+    from gradtts_amd.tts import GradTTS
+    m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+    sd = {f"encoder.{k}": torch.from_numpy(v) for k, v in synthetic_text_encoder_state_dict(seed_enc).items()}
+    sd.update({f"decoder.estimator.{k}": torch.from_numpy(v) for k, v in synthetic_state_dict(seed=seed_dec).items()})
+    m.load_state_dict(sd, strict=True)
+    return m.cuda()
+
+
+class fixed_draws:
+    """torch.rand -> t, torch.randn -> z (the decoder's two draws, diffusion.py:284 / :249) inside the block."""
+
+    def __init__(self, t, z):
+        self.t, self.z = t, z
+
+    def __enter__(self):
+        self.orig = (torch.rand, torch.randn)
+
+        def rand(*shape, dtype=None, device=None, requires_grad=False, **kw):
+            return self.t.to(dtype=dtype or torch.float32, device=device).clone()
+
+        def randn(*shape, dtype=None, device=None, requires_grad=False, **kw):
+            shape = tuple(shape[0]) if len(shape) == 1 and not isinstance(shape[0], int) else shape
+            assert tuple(shape) == tuple(self.z.shape), shape
+            return self.z.to(dtype=dtype or torch.float32, device=device).clone()
+
+        torch.rand, torch.randn = rand, randn
+
+    def __exit__(self, *exc):
+        torch.rand, torch.randn = self.orig
+        return False
+
+
+def run_fixture(m, g):
+    out_size = int(g["out_size"])
+    random.seed(int(g["py_seed"]))
+    with fixed_draws(torch.from_numpy(g["t"]), torch.from_numpy(g["z"])):
+        dur, prior, diff = m.compute_loss(torch.from_numpy(g["tokens"]).cuda(), torch.from_numpy(g["x_lengths"]).cuda(),
+                                          torch.from_numpy(g["y"]).cuda(), torch.from_numpy(g["y_lengths"]).cuda(),
+                                          out_size=out_size if out_size > 0 else None)
+    return dur, prior, diff
+
+
+@pytest.mark.parametrize("name", ["tts_loss_B2.npz", "tts_loss_B3_nocut.npz"])
+def test_compute_loss_matches_reference_fixture(name):
+    from oracle import decoder as odec
+    g = load_golden(name)
+    m = make_gradtts(int(g["seed_enc"]), int(g["seed_dec"])).eval()
+    dur, prior, diff = run_fixture(m, g)
+    (dur + prior + diff).backward()
+    ref = g["losses_f32"]
+    for i, (nm, v) in enumerate((("dur_loss", dur), ("prior_loss", prior), ("diff_loss", diff))):
+        report(f"compute_loss {nm} vs reference {name}", abs(float(v) - ref[i]) / abs(ref[i]), 1e-5)
+    names = [str(n) for n in g["param_names"]]
+    params = dict(m.named_parameters())
+    grads = {k: params[k].grad.detach().cpu().numpy().astype(np.float64) for k in names}
+    gsq, gproj = odec.grad_digest(grads, names)
+    rn = np.sqrt(g["gsq_f64"])
+    floor = 1e-3 * rn.max()
+    err = np.maximum(np.abs(np.sqrt(gsq) - rn), np.abs(gproj - g["gproj_f64"])) / (rn + floor)
+    enc = np.array([n.startswith("encoder.") for n in names])
+    report(f"compute_loss encoder grad digests vs reference {name} (worst "
+           f"{names[int(np.where(enc, err, -1).argmax())]})", float(err[enc].max()), 1e-3)
+    report(f"compute_loss decoder grad digests vs reference {name} (worst "
+           f"{names[int(np.where(~enc, err, -1).argmax())]})", float(err[~enc].max()), 1e-3)
+    for k in list(g):
+        if k.startswith("full__"):
+            report(f"compute_loss grad {k[6:]} vs reference", rel_err(grads[k[6:]], g[k]), 1e-3)
+
+
+def test_compute_loss_deterministic():
+    g = load_golden("tts_loss_B2.npz")
+    m = make_gradtts(int(g["seed_enc"]), int(g["seed_dec"])).train()
+    res = []
+    for _ in range(2):
+        m.zero_grad()
+        torch.manual_seed(11)
+        dur, prior, diff = run_fixture(m, g)
+        (dur + prior + diff).backward()
+        res.append([float(dur), float(prior), float(diff)] +
+                   [p.grad.detach().clone() for p in m.parameters() if p.grad is not None])
+    assert res[0][:3] == res[1][:3]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][3:], res[1][3:]))
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_text_encoder_training_pass_matches_oracle(p_drop):
+    """Train mode with dropout p (prenet 0.5): forward values and the gradients of every encoder parameter under
+    random upstream gradients of mu_x and logw, against autograd through the oracle with the same masks (fp64)."""
+    from oracle import text_encoder as ote
+    from oracle.decoder import grad_digest
+    m = make_gradtts()
+    enc = m.encoder.train() if p_drop > 0 else m.encoder.eval()
+    enc.p_dropout = p_drop
+    rng = np.random.default_rng(7)
+    lengths = [29, 17, 23]
+    B, Tx = len(lengths), 29
+    tokens = rng.integers(0, 149, size=(B, Tx)).astype(np.int64)
+    gmu = rng.standard_normal((B, 80, Tx))
+    glw = rng.standard_normal((B, 1, Tx))
+    torch.manual_seed(3)
+    seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p_drop > 0 else 0
+    torch.manual_seed(3)
+    mu, logw, xm = enc(torch.from_numpy(tokens).cuda(), torch.tensor(lengths).cuda())
+    (torch.sum(mu * torch.from_numpy(gmu).float().cuda()) + torch.sum(logw * torch.from_numpy(glw).float().cuda())).backward()
+    sd = synthetic_text_encoder_state_dict(5)
+    p = {k: torch.as_tensor(v).double().requires_grad_() for k, v in sd.items()}
+    drop = ote.Dropouts(seed, p_drop, 0.5) if p_drop > 0 else None
+    rmu, rlw, _ = ote.text_encoder(p, torch.from_numpy(tokens), torch.tensor(lengths), drop=drop)
+    (torch.sum(rmu * torch.from_numpy(gmu)) + torch.sum(rlw * torch.from_numpy(glw))).backward()
+    report(f"encoder train pass mu_x p={p_drop}", rel_err(mu.detach().cpu().numpy(), rmu.detach().numpy()), 1e-5)
+    report(f"encoder train pass logw p={p_drop}", rel_err(logw.detach().cpu().numpy(), rlw.detach().numpy()), 1e-5)
+    names = list(sd.keys())
+    params = dict(enc.named_parameters())
+    ours = {k: params[k].grad.detach().cpu().numpy().astype(np.float64) for k in names}
+    refg = {k: p[k].grad.numpy() for k in names}
+    gsq, gproj = grad_digest(ours, names)
+    rsq, rproj = grad_digest(refg, names)
+    rn = np.sqrt(rsq)
+    err = np.maximum(np.abs(np.sqrt(gsq) - rn), np.abs(gproj - rproj)) / (rn + 1e-3 * rn.max())
+    report(f"encoder train pass grad digests p={p_drop} (worst {names[int(err.argmax())]})", float(err.max()), 1e-3)
+    worst = max(rel_err(ours[k], refg[k]) for k in names if np.abs(refg[k]).max() > 1e-3 * max(
+        np.abs(v).max() for v in refg.values()))
+    report(f"encoder train pass elementwise grads p={p_drop}", worst, 1e-3)
