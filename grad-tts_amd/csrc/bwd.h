@@ -50,6 +50,7 @@ struct EwParams {
   const float* x2; float alpha2;      // optional second term (same channel count, dense)
   const float* mask; int T0, lvl;
   float* y; int ycs, yc0; int accumulate;
+  const float* alphap; const float* alpha2p;   // device scalars: alpha / alpha2 read from memory when non-null
 };
 
 hipError_t launch_gconv(const GConvParams& p, hipStream_t s);

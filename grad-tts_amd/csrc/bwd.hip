@@ -957,9 +957,10 @@ __global__ void ew_kernel(EwParams p) {
   const long pos = i / p.C;
   const int t = (int)(pos % p.T);
   const int b = (int)(pos / ((long)p.F * p.T));
-  float v = p.alpha * p.x[pos * p.xcs + p.xc0 + c];
+  const float alpha = p.alphap ? *p.alphap : p.alpha, alpha2 = p.alpha2p ? *p.alpha2p : p.alpha2;
+  float v = alpha * p.x[pos * p.xcs + p.xc0 + c];
   if (p.mask) v *= mask_at(p.mask, p.T0, b, t, p.lvl);
-  if (p.x2) v += p.alpha2 * p.x2[pos * p.C + c];
+  if (p.x2) v += alpha2 * p.x2[pos * p.C + c];
   float* o = p.y + pos * p.ycs + p.yc0 + c;
   *o = p.accumulate ? *o + v : v;
 }

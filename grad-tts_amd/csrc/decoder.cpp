@@ -180,6 +180,10 @@ struct gt_decoder {
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
+  // gt_decoder_set_params_device wrote the fp32 block on the device: the host copies (and every weight image
+  // packed from them) are stale until refresh_host() reads the block back
+  bool host_stale = false;
+  hipStream_t dev_stream = nullptr;
   float* raw = nullptr;
   std::vector<int64_t> raw_off;
   int64_t raw_numel = 0;
@@ -398,8 +402,11 @@ static bool conv64_enabled() {
   return v;
 }
 
+
+
 int prepare(gt_decoder* d, int code) {
   if (!d->dirty[code]) return GT_OK;
+  if (int rc = gt_internal_refresh_host(d)) return rc;
   const int dt = code ? 1 : 0;          // activation dtype: fp32 / bf16
   const bool w8 = code == GT_BF16_W8 || code == GT_FP8;   // fp8 images for the 3x3 / stride-2 / transposed convs
   const bool a8 = code == GT_FP8;   // ... fp8 operands too for the 3x3 convs over activations (Cin >= 32)
@@ -994,6 +1001,7 @@ int64_t gt_decoder_param_numel(const gt_decoder* d, int i) {
 
 int gt_decoder_set_param(gt_decoder* d, const char* name, const float* data, int64_t numel) {
   if (!d || !name || !data) return fail(GT_ERR_ARG, "null argument");
+  if (int rc = gt_internal_refresh_host(d)) return rc;   // the other parameters' current values first
   auto it = d->index.find(name);
   if (it == d->index.end()) return fail(GT_ERR_PARAM, std::string("unknown parameter: ") + name);
   const Shape& sh = d->inv[it->second];
@@ -1098,7 +1106,36 @@ int64_t gt_internal_param_offset(gt_decoder* d, const std::string& name) {
   return it == d->index.end() ? -1 : d->raw_off[it->second];
 }
 bool gt_internal_has_param(gt_decoder* d, const std::string& name) { return d->index.count(name) != 0; }
-float gt_internal_host_scalar(gt_decoder* d, const std::string& name) { return d->host[d->index.at(name)][0]; }
+float gt_internal_host_scalar(gt_decoder* d, const std::string& name) {
+  (void)gt_internal_refresh_host(d);
+  return d->host[d->index.at(name)][0];
+}
+
+// host copies <- the device fp32 block after gt_decoder_set_params_device (synchronous; only when an inference
+// image, a host scalar or a host-side parameter change needs them)
+int gt_internal_refresh_host(gt_decoder* d) {
+  if (!d->host_stale) return GT_OK;
+  if (hipStreamSynchronize(d->dev_stream) != hipSuccess) return fail(GT_ERR_HIP, "hipStreamSynchronize failed");
+  std::vector<float> h((size_t)d->raw_numel);
+  if (hipMemcpy(h.data(), d->raw, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipMemcpy(raw params -> host) failed");
+  for (size_t i = 0; i < d->inv.size(); ++i)
+    memcpy(d->host[i].data(), h.data() + d->raw_off[i], d->host[i].size() * 4);
+  d->host_stale = false;
+  return GT_OK;
+}
+
+int gt_decoder_set_params_device(gt_decoder* d, const float* params, int64_t numel, void* stream) {
+  if (!d || !params) return fail(GT_ERR_ARG, "null argument");
+  if (int rc = gt_internal_prepare_raw(d)) return rc;   // the block exists (parameters were set once from the host)
+  if (numel != d->raw_numel) return fail(GT_ERR_ARG, "numel != gt_decoder_grad_numel");
+  const hipError_t e = launch_copy_f32(d->raw, params, (long)numel, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(GT_ERR_HIP, std::string("parameter copy: ") + hipGetErrorString(e));
+  for (bool& x : d->dirty) x = true;
+  d->host_stale = true;
+  d->dev_stream = (hipStream_t)stream;
+  return GT_OK;
+}
 const float* gt_internal_freqs(gt_decoder* d) { return d->raw + d->raw_numel; }
 int64_t gt_internal_numel(gt_decoder* d) { return d->raw_numel; }
 void gt_internal_consts(gt_decoder* d, int* n_spks, float* bmin, float* bmax, float* pe_scale) {

@@ -13,6 +13,8 @@ const float* gt_internal_param(gt_decoder* d, const std::string& name);
 int64_t gt_internal_param_offset(gt_decoder* d, const std::string& name);
 bool gt_internal_has_param(gt_decoder* d, const std::string& name);
 float gt_internal_host_scalar(gt_decoder* d, const std::string& name);
+// host copies <- the device fp32 block after gt_decoder_set_params_device (no-op when they are current)
+int gt_internal_refresh_host(gt_decoder* d);
 const float* gt_internal_freqs(gt_decoder* d);
 int64_t gt_internal_numel(gt_decoder* d);
 void gt_internal_consts(gt_decoder* d, int* n_spks, float* bmin, float* bmax, float* pe_scale);

@@ -11,6 +11,7 @@
 
 #include "decoder_internal.h"
 #include "gradtts.h"
+#include "kernels.h"
 #include "textenc.h"
 #include "textenc_train.h"
 
@@ -30,6 +31,14 @@ struct gt_text_encoder {
   std::map<std::string, int64_t> pkoff;
   float* devpk = nullptr;
   int64_t pk_numel = 0;
+  // the same weights flipped and transposed, [Cin][K][Cout] with W^T(c, j, o) = W(o, c, K - 1 - j): the input
+  // gradient of a conv as a packed conv over its output gradient (training backward)
+  std::map<std::string, int64_t> pktoff;
+  // device-side parameter updates: the repack table (device) and the host copies' staleness
+  RepackEntry* devtab = nullptr;
+  int ntab = 0;
+  bool host_stale = false;
+  hipStream_t dev_stream = nullptr;
   // the last gt_text_encoder_forward_train call (its tape is the backward's input)
   const void* tr_ws = nullptr;
   int64_t tr_B = 0, tr_T = 0;
@@ -90,6 +99,7 @@ int upload(gt_text_encoder* e) {
     return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
   std::vector<float> hp;
   e->pkoff.clear();
+  e->pktoff.clear();
   for (size_t i = 0; i < e->inv.size(); ++i) {
     const auto& d = e->inv[i].second;
     if (d.size() != 3 || e->inv[i].first.find(".weight") == std::string::npos) continue;
@@ -99,6 +109,25 @@ int upload(gt_text_encoder* e) {
       for (int64_t k = 0; k < d[2]; ++k)
         for (int64_t c = 0; c < d[1]; ++c) hp.push_back(w[(o * d[1] + c) * d[2] + k]);
     while (hp.size() % 4) hp.push_back(0.f);   // 16-byte aligned starts
+    e->pktoff[e->inv[i].first] = (int64_t)hp.size();
+    for (int64_t c = 0; c < d[1]; ++c)
+      for (int64_t j = 0; j < d[2]; ++j)
+        for (int64_t o = 0; o < d[0]; ++o) hp.push_back(w[(o * d[1] + c) * d[2] + (d[2] - 1 - j)]);
+    while (hp.size() % 4) hp.push_back(0.f);
+  }
+  std::vector<RepackEntry> tab;
+  for (size_t i = 0; i < e->inv.size(); ++i) {
+    const auto it = e->pkoff.find(e->inv[i].first);
+    if (it == e->pkoff.end()) continue;
+    const auto& d = e->inv[i].second;
+    tab.push_back(RepackEntry{(long)e->off[i], (long)it->second, (long)e->pktoff.at(e->inv[i].first), (int)d[0],
+                              (int)d[1], (int)d[2]});
+  }
+  if (!e->devtab) {
+    if (hipMalloc(&e->devtab, tab.size() * sizeof(RepackEntry)) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipMalloc failed");
+    if (hipMemcpy(e->devtab, tab.data(), tab.size() * sizeof(RepackEntry), hipMemcpyHostToDevice) != hipSuccess)
+      return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
+    e->ntab = (int)tab.size();
   }
   if (e->devpk && (int64_t)hp.size() != e->pk_numel) { (void)hipFree(e->devpk); e->devpk = nullptr; }
   if (!e->devpk && !hp.empty() && hipMalloc(&e->devpk, hp.size() * 4) != hipSuccess)
@@ -147,6 +176,7 @@ int gt_text_encoder_create(int n_vocab, int n_feats, int n_channels, int filter_
 
 void gt_text_encoder_destroy(gt_text_encoder* e) {
   if (!e) return;
+  if (e->devtab) (void)hipFree(e->devtab);
   if (e->dev) (void)hipFree(e->dev);
   if (e->devpk) (void)hipFree(e->devpk);
   delete e;
@@ -160,14 +190,40 @@ int64_t gt_text_encoder_param_numel(gt_text_encoder* e, int i) {
   return (e && i >= 0 && i < (int)e->inv.size()) ? prod(e->inv[i].second) : -1;
 }
 
+// host copies <- the device block after gt_text_encoder_set_params_device (only when a host-side change needs them)
+static int refresh_host(gt_text_encoder* e) {
+  if (!e->host_stale) return GT_OK;
+  if (hipStreamSynchronize(e->dev_stream) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipStreamSynchronize failed");
+  std::vector<float> h((size_t)e->numel);
+  if (hipMemcpy(h.data(), e->dev, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
+  for (size_t i = 0; i < e->inv.size(); ++i) memcpy(e->host[i].data(), h.data() + e->off[i], e->host[i].size() * 4);
+  e->host_stale = false;
+  return GT_OK;
+}
+
 int gt_text_encoder_set_param(gt_text_encoder* e, const char* name, const float* data, int64_t numel) {
   if (!e || !name || !data) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (int rc = refresh_host(e)) return rc;
   auto it = e->index.find(name);
   if (it == e->index.end()) return gt_internal_fail(GT_ERR_PARAM, std::string("unknown parameter: ") + name);
   if (numel != prod(e->inv[it->second].second)) return gt_internal_fail(GT_ERR_PARAM, std::string("numel mismatch for ") + name);
   e->host[it->second].assign(data, data + numel);
   e->set[it->second] = true;
   e->dirty = true;
+  return GT_OK;
+}
+
+int gt_text_encoder_set_params_device(gt_text_encoder* e, const float* params, int64_t numel, void* stream) {
+  if (!e || !params) return gt_internal_fail(GT_ERR_ARG, "null argument");
+  if (int rc = upload(e)) return rc;   // device blocks exist (every parameter was set once from the host)
+  if (numel != e->numel) return gt_internal_fail(GT_ERR_ARG, "numel != gt_text_encoder_grad_numel");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t err = launch_copy_f32(e->dev, params, (long)numel, s);
+  if (err == hipSuccess) err = launch_tt_repack(e->dev, e->devtab, e->ntab, e->devpk, s);
+  if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("parameter update: ") + hipGetErrorString(err));
+  e->host_stale = true;
+  e->dev_stream = s;
   return GT_OK;
 }
 
@@ -367,7 +423,7 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  auto F = [&](size_t o) { return (float*)(base + o * 4); };
+  auto F = [&](size_t o) { return (float*)(base + o); };   // o: byte offset (tr_layout)
   auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
   auto PK = [&](const std::string& k) {
     const auto it = e->pkoff.find(k);
@@ -464,7 +520,7 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   if (e->dirty) return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  auto F = [&](size_t o) { return (float*)(base + o * 4); };
+  auto F = [&](size_t o) { return (float*)(base + o); };   // o: byte offset (tr_layout)
   auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
   auto G = [&](const std::string& k) { return grads + e->off[e->index.at(k)]; };
   hipError_t err = hipSuccess;
@@ -490,7 +546,8 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   auto dgrad = [&](const float* dout, int d_cs, const std::string& key, int cout, int cin, int k, float* dx,
                    int out_cs, int accumulate, const float* m) {
     C1dParams p = c1d_defaults();
-    p.in = dout; p.in_cs = d_cs; p.w = P(key + ".weight"); p.bias = nullptr; p.wpk = nullptr;
+    p.in = dout; p.in_cs = d_cs; p.w = P(key + ".weight"); p.bias = nullptr;
+    p.wpk = e->devpk + e->pktoff.at(key + ".weight");   // packed path when the channel counts allow it
     p.B = Bi; p.T = Ti; p.Q = Ti; p.Tout = Ti; p.Cin = cout; p.Cout = cin; p.K = k; p.pad = k - 1 - k / 2;
     p.wso = k; p.wsc = (long)cin * k; p.tap0 = k - 1; p.tap_step = -1;
     p.out = dx; p.out_cs = out_cs; p.accumulate = accumulate; p.out_mask = m;
@@ -582,14 +639,21 @@ int gt_path_scatter(const float* attn, const float* dmu_y, int64_t B, int64_t Tx
   return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
 }
 
+size_t gt_tts_aux_losses_workspace_bytes(int64_t B, int64_t Tx) {
+  return B > 0 && Tx > 0 ? (size_t)tt_aux_loss_scratch_doubles(B, Tx) * 8 + 8 : 0;
+}
+
 int gt_tts_aux_losses(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths, int64_t B,
                       int64_t Tx, int64_t Ty_attn, const float* y, const float* mu_y, const float* y_mask, int64_t Ty,
-                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* stream) {
+                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* workspace,
+                      size_t workspace_bytes, void* stream) {
   if (!logw || !attn || !x_mask || !x_lengths || !y || !mu_y || !y_mask || !losses || !dlogw_unit || !dmu_y_unit ||
-      B <= 0 || Tx <= 0 || Ty_attn <= 0 || Ty <= 0 || n_feats <= 0)
+      !workspace || B <= 0 || Tx <= 0 || Ty_attn <= 0 || Ty <= 0 || n_feats <= 0)
     return gt_internal_fail(GT_ERR_ARG, "bad argument");
+  if (workspace_bytes < gt_tts_aux_losses_workspace_bytes(B, Tx)) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
+  double* scratch = (double*)(((uintptr_t)workspace + 7) & ~(uintptr_t)7);
   const hipError_t e = launch_tt_aux_loss(logw, attn, x_mask, x_lengths, y, mu_y, y_mask, (int)B, (int)Tx, (int)Ty_attn,
-                                          (int)Ty, n_feats, losses, dlogw_unit, dmu_y_unit, (hipStream_t)stream);
+                                          (int)Ty, n_feats, losses, dlogw_unit, dmu_y_unit, scratch, (hipStream_t)stream);
   return e == hipSuccess ? GT_OK : gt_internal_fail(GT_ERR_HIP, hipGetErrorString(e));
 }
 

@@ -71,11 +71,21 @@ struct EwParams {
 hipError_t launch_tt_ew(const EwParams& p, hipStream_t s);
 hipError_t launch_tt_copy_words(uint32_t* dst, const uint32_t* src, long n, hipStream_t s);
 
+// device-side repack of the conv weights (after gt_text_encoder_set_params_device)
+struct RepackEntry {
+  long raw_off, pk_off, pkt_off;
+  int O, Ci, K;
+};
+hipError_t launch_tt_repack(const float* raw, const RepackEntry* tab, int n_entries, float* pk, hipStream_t s);
+
 // GradTTS.compute_loss glue
 hipError_t launch_tt_path_scatter(const float* attn, const float* dmu_y, int B, int Tx, int Ty, int F, float* dmu_x,
                                   hipStream_t s);
+// losses: out[0] dur_loss, out[1] prior_loss, out[2..3] gradient scales (out holds 4 floats)
 hipError_t launch_tt_aux_loss(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths,
                               const float* y, const float* mu_y, const float* y_mask, int B, int Tx, int Ta, int Ty,
-                              int F, float* out, float* dlogw_unit, float* dmu_unit, hipStream_t s);
+                              int F, float* out, float* dlogw_unit, float* dmu_unit, double* scratch, hipStream_t s);
+// fp64 scratch of launch_tt_aux_loss (block partials)
+long tt_aux_loss_scratch_doubles(long B, long Tx);
 
 }  // namespace gt

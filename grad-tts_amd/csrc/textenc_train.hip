@@ -421,62 +421,94 @@ __global__ __launch_bounds__(128) void tt_path_scatter_kernel(const float* attn,
   dmu_x[((long)b * F + f) * Tx + i] = acc;
 }
 
-// out[0] = dur_loss = sum_{b,i} (logw - log(1e-8 + sum_j attn) x_mask)^2 / sum x_lengths
-// out[1] = prior_loss = sum_{b,f,t} 0.5 ((y - mu_y)^2 + log 2 pi) y_mask / (sum y_mask * F)
-// dlogw_unit = d dur_loss / d logw, dmu_unit = d prior_loss / d mu_y  (second phase, after the sums)
-__global__ __launch_bounds__(1024) void tt_aux_loss_kernel(const float* logw, const float* attn, const float* x_mask,
-                                                           const int64_t* x_lengths, const float* y,
-                                                           const float* mu_y, const float* y_mask, int B, int Tx,
-                                                           int Ta, int Ty, int F, float* out, float* dlogw_unit,
-                                                           float* dmu_unit) {
-  __shared__ double s_red[16];
-  const int tid = threadIdx.x;
-  auto bsum = [&](double x) {
+// dur_loss (tts.py:155-156, utils.py:42-44) and prior_loss (tts.py:191-192) in four fixed-order passes:
+//   tt_dur_kernel        per (b, i): d = logw - log(1e-8 + sum_j attn) x_mask -> dlogw_unit (unscaled), block
+//                        partial of d^2 (fp64)
+//   tt_prior_kernel      block partials of 0.5 ((y - mu_y)^2 + log 2 pi) y_mask and of y_mask (fp64)
+//   tt_aux_final_kernel  out[0] = dur_loss, out[1] = prior_loss, out[2] = 2 / sum x_lengths,
+//                        out[3] = 1 / (sum y_mask F)
+//   tt_aux_grad_kernel   dlogw_unit *= out[2]; dmu_unit = -(y - mu_y) y_mask out[3]
+constexpr int TT_PRIOR_BLOCKS = 256;
+GT_DEV double tt_block_sum_d(double x, double* red) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    __syncthreads();
-    if ((tid & 63) == 0) s_red[tid >> 6] = x;
-    __syncthreads();
-    double t = 0.0;
-    for (int w = 0; w < 16; ++w) t += s_red[w];
-    return t;
-  };
-  // duration loss
-  double dsum = 0.0;
-  for (long e = tid; e < (long)B * Tx; e += 1024) {
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  return ((red[0] + red[1]) + red[2]) + red[3];
+}
+__global__ __launch_bounds__(256) void tt_dur_kernel(const float* logw, const float* attn, const float* x_mask,
+                                                     long n, int Ta, float* dlogw_unit, double* part) {
+  __shared__ double s_red[4];
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  double sq = 0.0;
+  if (e < n) {
     const float* a = attn + e * Ta;
     float dur = 0.f;
     for (int j = 0; j < Ta; ++j) dur += a[j];
-    const float lw_ = logf(1e-8f + dur) * x_mask[e];
-    const float df = logw[e] - lw_;
-    dsum += (double)df * df;
-    dlogw_unit[e] = df;   // scaled below
+    const float df = logw[e] - logf(1e-8f + dur) * x_mask[e];
+    dlogw_unit[e] = df;
+    sq = (double)df * df;
   }
-  dsum = bsum(dsum);
-  double lsum = 0.0;
-  for (int b = 0; b < B; ++b) lsum += (double)x_lengths[b];
-  // prior loss
+  sq = tt_block_sum_d(sq, s_red);
+  if (threadIdx.x == 0) part[blockIdx.x] = sq;
+}
+__global__ __launch_bounds__(256) void tt_prior_kernel(const float* y, const float* mu_y, const float* y_mask, int B,
+                                                       int F, int Ty, double* part) {
+  __shared__ double s_red[4];
+  const long n = (long)B * F * Ty, a = (long)blockIdx.x * n / gridDim.x, z = (long)(blockIdx.x + 1) * n / gridDim.x;
+  const long nm = (long)B * Ty, am = (long)blockIdx.x * nm / gridDim.x, zm = (long)(blockIdx.x + 1) * nm / gridDim.x;
   const float l2pi = 1.8378770664093453f;   // log(2 pi)
-  double psum = 0.0, msum = 0.0;
-  for (long e = tid; e < (long)B * F * Ty; e += 1024) {
+  double ps = 0.0, ms = 0.0;
+  for (long e = a + threadIdx.x; e < z; e += 256) {
     const long b = e / ((long)F * Ty), t = e % Ty;
-    const float m = y_mask[b * Ty + t];
     const float d = y[e] - mu_y[e];
-    psum += (double)(0.5f * (d * d + l2pi) * m);
+    ps += (double)(0.5f * (d * d + l2pi) * y_mask[b * Ty + t]);
   }
-  for (long e = tid; e < (long)B * Ty; e += 1024) msum += (double)y_mask[e];
-  psum = bsum(psum);
-  msum = bsum(msum);
-  const double pden = msum * F;
-  if (tid == 0) {
-    out[0] = (float)(dsum / lsum);
-    out[1] = (float)(psum / pden);
+  for (long e = am + threadIdx.x; e < zm; e += 256) ms += (double)y_mask[e];
+  ps = tt_block_sum_d(ps, s_red);
+  ms = tt_block_sum_d(ms, s_red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ps;
+    part[2 * blockIdx.x + 1] = ms;
   }
-  const float dscale = (float)(2.0 / lsum), pscale = (float)(1.0 / pden);
-  for (long e = tid; e < (long)B * Tx; e += 1024) dlogw_unit[e] = dlogw_unit[e] * dscale;
-  for (long e = tid; e < (long)B * F * Ty; e += 1024) {
+}
+__global__ void tt_aux_final_kernel(const double* dpart, int nd, const double* ppart, int np, const int64_t* x_lengths,
+                                    int B, int F, float* out) {
+  if (threadIdx.x != 0) return;
+  double ds = 0.0, ps = 0.0, ms = 0.0, ls = 0.0;
+  for (int i = 0; i < nd; ++i) ds += dpart[i];
+  for (int i = 0; i < np; ++i) { ps += ppart[2 * i]; ms += ppart[2 * i + 1]; }
+  for (int b = 0; b < B; ++b) ls += (double)x_lengths[b];
+  const double pden = ms * F;
+  out[0] = (float)(ds / ls);
+  out[1] = (float)(ps / pden);
+  out[2] = (float)(2.0 / ls);
+  out[3] = (float)(1.0 / pden);
+}
+__global__ void tt_aux_grad_kernel(const float* y, const float* mu_y, const float* y_mask, int B, int F, int Ty, long nx,
+                                   const float* out, float* dlogw_unit, float* dmu_unit) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e < nx) dlogw_unit[e] = dlogw_unit[e] * out[2];
+  if (e < (long)B * F * Ty) {
     const long b = e / ((long)F * Ty), t = e % Ty;
-    dmu_unit[e] = -(y[e] - mu_y[e]) * y_mask[b * Ty + t] * pscale;
+    dmu_unit[e] = -(y[e] - mu_y[e]) * y_mask[b * Ty + t] * out[3];
+  }
+}
+
+// ---------------------------------------------------------------- device-side weight repack
+// pk[(o K + k) Ci + c] = W[o][c][k] and pkt[(c K + K - 1 - k) O + o] = W[o][c][k] for every conv weight of the table
+// (the layouts textenc.cpp's upload() builds on the host), after a device-side parameter update
+__global__ void tt_repack_kernel(const float* raw, const RepackEntry* tab, float* pk) {
+  const RepackEntry t = tab[blockIdx.y];
+  const long n = (long)t.O * t.Ci * t.K;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int k = (int)(i % t.K);
+    const long oc = i / t.K;
+    const int c = (int)(oc % t.Ci), o = (int)(oc / t.Ci);
+    const float v = raw[t.raw_off + i];
+    pk[t.pk_off + ((long)o * t.K + k) * t.Ci + c] = v;
+    pk[t.pkt_off + ((long)c * t.K + (t.K - 1 - k)) * t.O + o] = v;
   }
 }
 
@@ -570,6 +602,12 @@ hipError_t launch_tt_copy_words(uint32_t* dst, const uint32_t* src, long n, hipS
   return hipGetLastError();
 }
 
+hipError_t launch_tt_repack(const float* raw, const RepackEntry* tab, int n_entries, float* pk, hipStream_t s) {
+  if (n_entries <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tt_repack_kernel, dim3(64, n_entries), dim3(256), 0, s, raw, tab, pk);
+  return hipGetLastError();
+}
+
 hipError_t launch_tt_path_scatter(const float* attn, const float* dmu_y, int B, int Tx, int Ty, int F, float* dmu_x,
                                   hipStream_t s) {
   if (F > 128) return hipErrorInvalidValue;
@@ -579,10 +617,21 @@ hipError_t launch_tt_path_scatter(const float* attn, const float* dmu_y, int B, 
 
 hipError_t launch_tt_aux_loss(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths,
                               const float* y, const float* mu_y, const float* y_mask, int B, int Tx, int Ta, int Ty,
-                              int F, float* out, float* dlogw_unit, float* dmu_unit, hipStream_t s) {
-  hipLaunchKernelGGL(tt_aux_loss_kernel, dim3(1), dim3(1024), 0, s, logw, attn, x_mask, x_lengths, y, mu_y, y_mask, B,
-                     Tx, Ta, Ty, F, out, dlogw_unit, dmu_unit);
+                              int F, float* out, float* dlogw_unit, float* dmu_unit, double* scratch, hipStream_t s) {
+  const long nx = (long)B * Tx, ny = (long)B * F * Ty;
+  const int nd = (int)((nx + 255) / 256);
+  double* dpart = scratch;
+  double* ppart = scratch + nd;
+  hipLaunchKernelGGL(tt_dur_kernel, dim3(nd), dim3(256), 0, s, logw, attn, x_mask, nx, Ta, dlogw_unit, dpart);
+  hipLaunchKernelGGL(tt_prior_kernel, dim3(TT_PRIOR_BLOCKS), dim3(256), 0, s, y, mu_y, y_mask, B, F, Ty, ppart);
+  hipLaunchKernelGGL(tt_aux_final_kernel, dim3(1), dim3(64), 0, s, dpart, nd, ppart, TT_PRIOR_BLOCKS, x_lengths, B, F,
+                     out);
+  const long ng = std::max(nx, ny);
+  hipLaunchKernelGGL(tt_aux_grad_kernel, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, y, mu_y, y_mask, B, F, Ty,
+                     nx, out, dlogw_unit, dmu_unit);
   return hipGetLastError();
 }
+
+long tt_aux_loss_scratch_doubles(long B, long Tx) { return (B * Tx + 255) / 256 + 2 * TT_PRIOR_BLOCKS; }
 
 }  // namespace gt

@@ -141,6 +141,9 @@ struct Trainer {
     if (dry) return;
     chk(launch_chan_sums(x, nullptr, B, npos, C, part, out, 0, acc, s), line);
   }
+  // alphap / alpha2p: device scalars (a parameter in the fp32 block) in place of alpha / alpha2
+  const float* ew_alphap = nullptr;
+  const float* ew_alpha2p = nullptr;
   void ew(const float* x, int xcs, int xc0, float alpha, const float* x2, float alpha2, int l, int C, bool m, float* y,
           int ycs, int yc0, int acc, int line = __builtin_LINE()) {
     if (!run) return;
@@ -155,6 +158,7 @@ struct Trainer {
     p.B = B; p.F = L(l).F; p.T = L(l).T; p.C = C; p.x = x; p.xcs = xcs; p.xc0 = xc0; p.alpha = alpha;
     p.x2 = x2; p.alpha2 = alpha2; p.mask = m ? mask : nullptr; p.T0 = T; p.lvl = l; p.y = y; p.ycs = ycs; p.yc0 = yc0;
     p.accumulate = acc;
+    p.alphap = ew_alphap; p.alpha2p = ew_alpha2p;
     chk(launch_ew(g1((long)B * L(l).F * L(l).T * C), dim3(256), s, p), line);
   }
   BlockBwdParams bp(int l, int C, const float* h, const float* st, const std::string& gn) {
@@ -290,8 +294,9 @@ struct Trainer {
     }
     gconv(a.o, 128, l, false, P(k + "fn.fn.to_out.weight"), 128, 1, 1, 1, 0, 0, P(k + "fn.fn.to_out.bias"), a.z, C, l,
           false, C, 0, 0);
-    const float g = gt_internal_host_scalar(d, k + "fn.g");
-    ew(x, C, 0, 1.f, a.z, g, l, C, false, a.y, C, 0, 0);
+    ew_alpha2p = P(k + "fn.g");   // Rezero g read on the device (the block may have been updated there)
+    ew(x, C, 0, 1.f, a.z, 0.f, l, C, false, a.y, C, 0, 0);
+    ew_alpha2p = nullptr;
     ats.push_back(a);
     return a.y;
   }
@@ -422,12 +427,13 @@ struct Trainer {
     cur = k + " bwd";
     const int l = a.l, C = a.C;
     const long np = (long)L(l).F * L(l).T, n = (long)B * np;
-    const float g = gt_internal_host_scalar(d, k + "fn.g");
     ew(dy, C, 0, 1.f, nullptr, 0.f, l, C, false, dx, C, 0, 1);                 // residual
     double* dpart = reinterpret_cast<double*>(A.take(2 * kDotBlocks));
     if (live() && pgrads) chk(launch_dot_sum(dy, a.z, n * C, dpart, G(k + "fn.g"), 1, s));   // d g = sum dy . z
     float* dz = A.take((size_t)n * C);
-    ew(dy, C, 0, g, nullptr, 0.f, l, C, false, dz, C, 0, 0);
+    ew_alphap = P(k + "fn.g");
+    ew(dy, C, 0, 0.f, nullptr, 0.f, l, C, false, dz, C, 0, 0);
+    ew_alphap = nullptr;
     wgrad(dz, C, l, false, a.o, 128, l, false, 1, 1, 0, G(k + "fn.fn.to_out.weight"), 128, 1, 1);
     chansum(dz, l, C, G(k + "fn.fn.to_out.bias"), 1);
     float* dO = A.take((size_t)n * 128);

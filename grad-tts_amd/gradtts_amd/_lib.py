@@ -25,6 +25,7 @@ SIGNATURES = [
     ("gt_decoder_destroy", None, [_c.c_void_p]),
     ("gt_decoder_set_betas", _c.c_int, [_c.c_void_p, _c.c_float, _c.c_float]),
     ("gt_decoder_pack_count", _c.c_int64, [_c.c_void_p]),
+    ("gt_decoder_set_params_device", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_void_p]),
     ("gt_decoder_num_params", _c.c_int, [_c.c_void_p]),
     ("gt_decoder_param_name", _c.c_char_p, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_param_numel", _c.c_int64, [_c.c_void_p, _c.c_int]),
@@ -79,6 +80,7 @@ SIGNATURES = [
     ("gt_expand", _c.c_int, [_c.c_void_p] * 4 + [_c.c_int64] * 3 + [_c.c_int32] + [_c.c_void_p] * 4),
     ("gt_path_gather", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int32,
                                   _c.c_void_p, _c.c_void_p]),
+    ("gt_text_encoder_set_params_device", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_void_p]),
     ("gt_text_encoder_train_workspace_bytes", _c.c_size_t, [_c.c_void_p, _c.c_int64, _c.c_int64]),
     ("gt_text_encoder_grad_numel", _c.c_int64, [_c.c_void_p]),
     ("gt_text_encoder_forward_train", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 2 + [_c.c_int64, _c.c_int64] +
@@ -87,8 +89,9 @@ SIGNATURES = [
      [_c.c_void_p] + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_path_scatter", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int32,
                                    _c.c_void_p, _c.c_void_p]),
+    ("gt_tts_aux_losses_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64]),
     ("gt_tts_aux_losses", _c.c_int, [_c.c_void_p] * 4 + [_c.c_int64] * 3 + [_c.c_void_p] * 3 +
-     [_c.c_int64, _c.c_int32] + [_c.c_void_p] * 4),
+     [_c.c_int64, _c.c_int32] + [_c.c_void_p] * 3 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_vocoder_create", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,
                                      _c.c_void_p, _c.c_void_p]),
     ("gt_vocoder_create2", _c.c_int, [_c.c_int, _c.c_int, _c.c_int, _c.c_void_p, _c.c_void_p, _c.c_int, _c.c_void_p,

@@ -185,11 +185,18 @@ class GradLogPEstimator2d(torch.nn.Module):
         if sig != self._synced:
             L = lib()
             params = dict(self.named_parameters())
-            for i in range(L.gt_decoder_num_params(self._handle)):
-                name = L.gt_decoder_param_name(self._handle, i).decode()
-                arr = np.ascontiguousarray(params[name].detach().to("cpu", torch.float32).numpy())
-                check(L.gt_decoder_set_param(self._handle, name.encode(), arr.ctypes.data, arr.size),
-                      f"gt_decoder_set_param({name})")
+            names = [L.gt_decoder_param_name(self._handle, i).decode() for i in range(L.gt_decoder_num_params(self._handle))]
+            if self._synced is not None and all(params[n].is_cuda for n in names):
+                # after an optimizer step: one device-side copy into the library's fp32 block, no host round trip
+                # (the inference images re-pack lazily from it)
+                flat = torch.cat([params[n].detach().reshape(-1).to(torch.float32) for n in names])
+                check(L.gt_decoder_set_params_device(self._handle, flat.data_ptr(), flat.numel(),
+                                                     _stream_ptr(flat.device)), "gt_decoder_set_params_device")
+            else:
+                for name in names:
+                    arr = np.ascontiguousarray(params[name].detach().to("cpu", torch.float32).numpy())
+                    check(L.gt_decoder_set_param(self._handle, name.encode(), arr.ctypes.data, arr.size),
+                          f"gt_decoder_set_param({name})")
             self._synced = sig
         return self._handle
 

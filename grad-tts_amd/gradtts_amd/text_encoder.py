@@ -142,12 +142,20 @@ class TextEncoder(torch.nn.Module):
             self._handle = h
         sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
         if sig != self._synced:
+            from .diffusion import _stream_ptr
             params = dict(self.named_parameters())
-            for i in range(L.gt_text_encoder_num_params(self._handle)):
-                name = L.gt_text_encoder_param_name(self._handle, i).decode()
-                arr = np.ascontiguousarray(params[name].detach().to("cpu", torch.float32).numpy())
-                check(L.gt_text_encoder_set_param(self._handle, name.encode(), arr.ctypes.data, arr.size),
-                      f"gt_text_encoder_set_param({name})")
+            names = [L.gt_text_encoder_param_name(self._handle, i).decode()
+                     for i in range(L.gt_text_encoder_num_params(self._handle))]
+            if self._synced is not None and all(params[n].is_cuda for n in names):
+                # after an optimizer step: device-side copy + repack, no host round trip
+                flat = torch.cat([params[n].detach().reshape(-1).to(torch.float32) for n in names])
+                check(L.gt_text_encoder_set_params_device(self._handle, flat.data_ptr(), flat.numel(),
+                                                          _stream_ptr(flat.device)), "gt_text_encoder_set_params_device")
+            else:
+                for name in names:
+                    arr = np.ascontiguousarray(params[name].detach().to("cpu", torch.float32).numpy())
+                    check(L.gt_text_encoder_set_param(self._handle, name.encode(), arr.ctypes.data, arr.size),
+                          f"gt_text_encoder_set_param({name})")
             self._synced = sig
         return self._handle
 

@@ -179,13 +179,14 @@ class _AuxLosses(torch.autograd.Function):
         xl = x_lengths.to(device=dev, dtype=torch.int64).contiguous()
         B, Tx = lw.shape[0], lw.shape[-1]
         F, Ty = mu.shape[1], mu.shape[2]
-        losses = torch.empty(2, dtype=torch.float32, device=dev)
+        losses = torch.empty(4, dtype=torch.float32, device=dev)
         dlw, dmu = torch.empty_like(lw), torch.empty_like(mu)
         with torch.cuda.device(dev):
+            ws = torch.empty(lib().gt_tts_aux_losses_workspace_bytes(B, Tx), dtype=torch.uint8, device=dev)
             check(lib().gt_tts_aux_losses(lw.data_ptr(), at.data_ptr(), xm.data_ptr(), xl.data_ptr(), B, Tx,
                                           at.shape[-1], yy.data_ptr(), mu.data_ptr(), ym.data_ptr(), Ty, F,
-                                          losses.data_ptr(), dlw.data_ptr(), dmu.data_ptr(), _stream_ptr(dev)),
-                  "gt_tts_aux_losses")
+                                          losses.data_ptr(), dlw.data_ptr(), dmu.data_ptr(), ws.data_ptr(), ws.numel(),
+                                          _stream_ptr(dev)), "gt_tts_aux_losses")
         ctx.save_for_backward(dlw, dmu)
         ctx.dtypes = (logw.dtype, mu_y.dtype)
         return losses[0].clone().to(logw.dtype), losses[1].clone().to(mu_y.dtype)

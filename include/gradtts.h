@@ -68,6 +68,12 @@ int64_t gt_decoder_param_numel(const gt_decoder* dec, int i);
 /* Copy one parameter (host fp32, contiguous, reference shape) into the decoder. Packing to device
  * layouts happens lazily at the next compute call (synchronously, outside any stream capture). */
 int gt_decoder_set_param(gt_decoder* dec, const char* name, const float* host_data, int64_t numel);
+/* Device-side parameter update (a training loop's optimizer step, no host round trip): params = every parameter in
+ * inventory order, fp32 contiguous on the device (gt_decoder_grad_numel floats, the gradient buffer's layout),
+ * copied on `stream` into the fp32 block the training / VJP / likelihood calls read. Inference weight images are
+ * re-packed from it lazily (one device -> host read) at the next inference call. Every parameter must have been set
+ * once with gt_decoder_set_param. */
+int gt_decoder_set_params_device(gt_decoder* dec, const float* params, int64_t numel, void* stream);
 
 /* Number of times the weights were packed into device layouts so far (one per compute dtype in use after
  * each parameter change; the reference re-reads weights on every call, this library packs them once). */
@@ -223,6 +229,11 @@ int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, 
  * reference layouts); the duration predictor sees a detached input (text_encoder.py:332), so dlogw reaches only its
  * parameters. Same encoder, B, Tx and workspace as the forward_train call it follows, parameters unchanged between. */
 size_t gt_text_encoder_train_workspace_bytes(gt_text_encoder* enc, int64_t B, int64_t Tx);
+/* Device-side parameter update (a training loop's optimizer step, no host round trip): params = every parameter in
+ * inventory order, fp32 contiguous on the device (the gradient buffer's layout), copied and repacked on `stream`.
+ * Every parameter must have been set once with gt_text_encoder_set_param; a later host-side set_param first reads
+ * the device values back. */
+int gt_text_encoder_set_params_device(gt_text_encoder* enc, const float* params, int64_t numel, void* stream);
 int64_t gt_text_encoder_grad_numel(gt_text_encoder* enc);
 int gt_text_encoder_forward_train(gt_text_encoder* enc, const int64_t* tokens, const int64_t* x_lengths, int64_t B,
                                   int64_t Tx, float p_dropout, float p_dropout_prenet, uint64_t seed, float* mu_x,
@@ -233,12 +244,14 @@ int gt_text_encoder_backward(gt_text_encoder* enc, const float* dmu_x, const flo
 int gt_path_scatter(const float* attn, const float* dmu_y, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
                     float* dmu_x, void* stream);
 /* dur_loss (tts.py:155-156 with utils.py:42-44 duration_loss over logw [B,1,Tx] and the MAS attn [B,Tx,Ty]) and
- * prior_loss (tts.py:191-192 over y, mu_y [B,n_feats,Ty'] and y_mask [B,1,Ty']) in one call: losses[0] = dur_loss,
- * losses[1] = prior_loss (device); dlogw_unit = d dur_loss / d logw, dmu_y_unit = d prior_loss / d mu_y. Fixed
- * summation order (fp64 accumulators). */
+ * prior_loss (tts.py:191-192 over y, mu_y [B,n_feats,Ty'] and y_mask [B,1,Ty']) in one call: losses (4 floats,
+ * device): [0] = dur_loss, [1] = prior_loss, [2..3] internal scales; dlogw_unit = d dur_loss / d logw, dmu_y_unit =
+ * d prior_loss / d mu_y. Fixed summation order (fp64 block partials). */
+size_t gt_tts_aux_losses_workspace_bytes(int64_t B, int64_t Tx);
 int gt_tts_aux_losses(const float* logw, const float* attn, const float* x_mask, const int64_t* x_lengths, int64_t B,
                       int64_t Tx, int64_t Ty_attn, const float* y, const float* mu_y, const float* y_mask, int64_t Ty,
-                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* stream);
+                      int32_t n_feats, float* losses, float* dlogw_unit, float* dmu_y_unit, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* HiFi-GAN generator (hifi-gan/models.py:77-128, ResBlock1 :13-48 / ResBlock2 :53-74; the vocoder of
  * inference.py:73-97). fp32. Parameters by the reference Generator's state_dict names (bias, weight_g, weight_v per

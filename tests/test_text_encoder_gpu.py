@@ -37,7 +37,14 @@ def make_encoder(seed):
 def test_text_encoder_matches_reference_golden(name):
     g = np.load(os.path.join(GOLD, name + ".npz"))
     enc, _ = make_encoder(int(g["weights_seed"]))
-    mu, logw, xm = enc(torch.from_numpy(g["tokens"]).cuda(), torch.from_numpy(g["x_lengths"]).cuda())
+    with torch.no_grad():   # the inference pass (gt_text_encoder_forward)
+        mu, logw, xm = enc(torch.from_numpy(g["tokens"]).cuda(), torch.from_numpy(g["x_lengths"]).cuda())
+    # with gradients the training pass runs (gt_text_encoder_forward_train; eval mode: no dropout): same values
+    mu_t, logw_t, _ = enc.eval()(torch.from_numpy(g["tokens"]).cuda(), torch.from_numpy(g["x_lengths"]).cuda())
+    report(f"text encoder training-pass mu_x {name} vs fp64 reference", rel_err(mu_t.detach().cpu().numpy(),
+                                                                                g["mu_x_f64"]), 2e-5)
+    report(f"text encoder training-pass logw {name} vs fp64 reference", rel_err(logw_t.detach().cpu().numpy(),
+                                                                                g["logw_f64"]), 2e-5)
     torch.cuda.synchronize()
     report(f"text encoder mu_x {name} vs fp64 reference", rel_err(mu.cpu().numpy(), g["mu_x_f64"]), 2e-5)
     report(f"text encoder logw {name} vs fp64 reference", rel_err(logw.cpu().numpy(), g["logw_f64"]), 2e-5)
@@ -141,6 +148,7 @@ def test_text_encoder_speed_vs_torch_eager():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / n * 1e3
 
-    ms_ours, ms_eager = timed(ours), timed(eager)
+    with torch.no_grad():   # inference (GradTTS.forward is no_grad)
+        ms_ours, ms_eager = timed(ours), timed(eager)
     report(f"text encoder + front-end B={B} Tx={Tx}: ours {ms_ours:.2f} ms, torch eager {ms_eager:.2f} ms; "
            f"ratio eager/ours", ms_eager / ms_ours, 0.0, gate=False, ms_ours=ms_ours, ms_eager=ms_eager)
