@@ -211,6 +211,13 @@ size_t esize(int dt) { return dt ? 2 : 4; }
 // on 5-row tiles the in-register transform (recomputed by both 128-channel tiles and the halo rows) costs
 // 103 us per launch against 87 + 35 us for the plain conv plus the pass (same box, tools/ab_env.sh); the
 // knob (GT_GN_APPLY_MIN_C=256 restores the round-1 split) stays for A/B runs.
+// the first ResnetBlock's output + res_conv over the input channels as an elementwise pass (GT_RB_INPUT=0: the
+// 1x1 conv_kernel with IN_INPUT / OUT_RBOUT, as before round 3)
+static bool rb_input_on() {
+  static const bool v = [] { const char* e = getenv("GT_RB_INPUT"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 static int gn_apply_min_c() {
   static const int v = [] {
     const char* e = getenv("GT_GN_APPLY_MIN_C");
@@ -432,6 +439,7 @@ int prepare(gt_decoder* d, int code) {
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
       if (c64) pack_conv64(blob, k + ".w64", w);
+      if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
     } else if (ends_with(k, "to_qkv.weight")) {
@@ -728,7 +736,19 @@ struct Run {
       tap(k + "pre2", lvl, pre2, Cout);
       tap_part(stat_slot - 1);
     }
-    if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
+    if (d->index.count(k + "res_conv.weight") && input && rb_input_on()) {
+      // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m) as an elementwise pass
+      RbOutParams p{};
+      p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight");
+      p.beta = Fp(k + "block2.block.1.bias"); p.count = count; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl);
+      p.T = Tl(lvl); p.C = Cout; p.T0 = T; p.lvl = lvl;
+      p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin = cin; p.rw = Fp(k + "res_conv.weight.f32");
+      p.rb = Fp(k + "res_conv.bias");
+      const double by = (2.0 * Cout * esize(dt) + 8.0) * B * Fl(lvl) * Tl(lvl);
+      timed(std::string("rbout_input_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
+                std::to_string(Fl(lvl)), 2.0 * cin * Cout * B * Fl(lvl) * Tl(lvl), by,
+            [&] { return launch_rbout_input(dt, p, s); });
+    } else if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);
       p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "res_conv.weight");
       p.in0 = in0; p.C0 = C0; p.in1 = in1; p.C1 = C1;

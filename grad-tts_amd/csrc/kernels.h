@@ -79,8 +79,14 @@ struct RbOutParams {
   const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
   const float* tb; long tb_bstride;   // gn_apply only: time bias rows
   const int* stepp;                   // gn_apply only: device step index (tb_at), or null
+  // rbout_input only: res_conv over the U-Net input channels {mu, x_t, spk} (level 0): fp32 weight [C][cin], bias
+  const float* mu; const float* xt; const float* spk_s; int cin;
+  const float* rw; const float* rb;
 };
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s);
+// the first ResnetBlock's output: Mish(GN(h2))*m + res_conv(x*m) with x = {mu, x_t (, spk)} (2-3 channels, level 0):
+// an elementwise pass (the 1x1 conv over 2-3 input channels is 2-3 FMAs per output element)
+hipError_t launch_rbout_input(int act_bf16, const RbOutParams& p, hipStream_t s);
 // in place: pre = (Mish(GN(pre))*m + tb)*m   (out must equal pre)
 hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s);
 

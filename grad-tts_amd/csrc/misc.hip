@@ -3,7 +3,9 @@
 //                         the score output (GradLogPEstimator2d.forward, diffusion.py:212-216) or the
 //                         Euler update of Diffusion.reverse_diffusion (diffusion.py:264-267) in place.
 //   gn_mish_kernel        ResnetBlock output with identity residual: Mish(GN(h2))*m + x*m (diffusion.py:77-79),
-//                         or block2's input (Mish(GN(h1))*m + t_emb)*m applied once in place (wide levels)
+//                         with the first block's res_conv over the 2-3 U-Net input channels (mu, x_t, spk:
+//                         diffusion.py:70, 78, 181-184) as 2-3 FMAs per element, or block2's input
+//                         (Mish(GN(h1))*m + t_emb)*m applied once in place (wide levels)
 //   temb_kernel           SinusoidalPosEmb -> time MLP -> every ResnetBlock's Mish+Linear time bias
 //                         (diffusion.py:113-125, 143-144, 64-65, 76); one row per Euler step.
 //   spk_mlp_kernel        spk_mlp (diffusion.py:139-141, 175-176)
@@ -76,7 +78,8 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 #define GT_RB_IPT 8
 #endif
 constexpr int RB_IPT = GT_RB_IPT;
-template <class A, bool APPLY>
+// RES = 1: the residual is res_conv(x*m) over the U-Net input channels (p.mu, p.xt, p.spk_s; level 0) instead of x*m
+template <class A, bool APPLY, int RES = 0>
 __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   __shared__ float s_mean[8], s_rstd[8];
   __shared__ double s_red[272];
@@ -87,24 +90,40 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   const int c0 = e0 % p.C;
   const long ub = (long)b * total;
   const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
-  const A* xin = reinterpret_cast<const A*>(APPLY ? p.pre : p.x) + ub;
+  const A* xin = reinterpret_cast<const A*>(APPLY || RES ? p.pre : p.x) + ub;
   A* out = reinterpret_cast<A*>(p.out) + ub;
   // Data and mask loads go out first; the GroupNorm reduction (its own loads + LDS barriers) overlaps them.
   // Item i is position pos0 + i * pstep (C divides the 256-item block stride): frame index by increments.
   const int pstep = 256 * ICH / p.C;
   int t = (e0 / p.C) % p.T;
   uint4 vp[RB_IPT], vx[RB_IPT];
-  float mk[RB_IPT];
+  float mk[RB_IPT], xr[RES ? RB_IPT : 1][3];
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
     const int e = e0 + i * 256 * ICH;
     if (e < total) {
       vp[i] = *reinterpret_cast<const uint4*>(pre + e);
-      if (!APPLY) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
+      if (!APPLY && !RES) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
       mk[i] = mask_at(p.mask, p.T0, b, t, p.lvl);
+      if (RES) {   // input channels of this position ([B][F][T] fp32 sampler state; spk projected per mel row)
+        const int f = e / p.C / p.T;
+        const long q = ((long)b * p.F + f) * p.T + t;
+        xr[i][0] = p.mu[q];
+        xr[i][1] = p.xt[q];
+        xr[i][2] = p.cin == 3 ? p.spk_s[(long)b * p.F + f] : 0.f;
+      }
     }
     t += pstep;
     while (t >= p.T) t -= p.T;
+  }
+  float rw[RES ? ICH : 1][3], rbias[RES ? ICH : 1];
+  if (RES) {
+#pragma unroll
+    for (int k = 0; k < ICH; ++k) {
+      rbias[k] = p.rb[c0 + k];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) rw[k][j] = j < p.cin ? p.rw[(c0 + k) * p.cin + j] : 0.f;
+    }
   }
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   float sc[ICH], sh[ICH], tb[ICH];
@@ -123,6 +142,13 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
       if (APPLY) {
 #pragma unroll
         for (int k = 0; k < ICH; ++k) v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) * m + tb[k]) * m;
+      } else if (RES) {   // res_conv(x * m): bias + W (x m), fp32
+        const float x0 = xr[i][0] * m, x1 = xr[i][1] * m, x2 = xr[i][2] * m;
+#pragma unroll
+        for (int k = 0; k < ICH; ++k) {
+          const float r = fmaf(rw[k][2], x2, fmaf(rw[k][1], x1, fmaf(rw[k][0], x0, rbias[k])));
+          v[k] = mish_act<A>(v[k] * sc[k] + sh[k]) * m + r;
+        }
       } else {
         float x[ICH];
         item_to_f(vx[i], x, A());
@@ -238,6 +264,16 @@ static hipError_t launch_gn_mish(int act_bf16, bool apply, const RbOutParams& p,
 }
 hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
   return launch_gn_mish(act_bf16, false, p, s);
+}
+hipError_t launch_rbout_input(int act_bf16, const RbOutParams& p, hipStream_t s) {
+  const int ich = act_bf16 ? 8 : 4;
+  const long total = (long)p.F * p.T * p.C;
+  if ((256 * ich) % p.C != 0 || total >= (1L << 31) || p.cin < 2 || p.cin > 3 || p.lvl != 0) return hipErrorInvalidValue;
+  const long items = total / ich;
+  dim3 grid((unsigned)((items + 256 * RB_IPT - 1) / (256 * RB_IPT)), (unsigned)p.B);
+  if (act_bf16) hipLaunchKernelGGL((gn_mish_kernel<bf16, false, 1>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gn_mish_kernel<float, false, 1>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s) {
   return launch_gn_mish(act_bf16, true, p, s);
