@@ -39,11 +39,6 @@ struct gt_text_encoder {
   int ntab = 0;
   bool host_stale = false;
   hipStream_t dev_stream = nullptr;
-  // the last gt_text_encoder_forward_train call (its tape is the backward's input)
-  const void* tr_ws = nullptr;
-  int64_t tr_B = 0, tr_T = 0;
-  uint64_t tr_seed = 0;
-  float tr_p = 0.f, tr_ppre = 0.f;
 };
 
 namespace {
@@ -505,16 +500,14 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
     chk(launch_tt_ew(c, s));
   }
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder training forward: ") + hipGetErrorString(err));
-  e->tr_ws = workspace; e->tr_B = B; e->tr_T = T; e->tr_seed = seed; e->tr_p = p_dropout; e->tr_ppre = p_dropout_prenet;
   return GT_OK;
 }
 
 int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float* dlogw, int64_t B, int64_t T,
-                             float* grads, void* workspace, size_t workspace_bytes, void* stream) {
+                             float p_dropout, float p_dropout_prenet, uint64_t seed, float* grads, void* workspace,
+                             size_t workspace_bytes, void* stream) {
   if (!e || !grads || !workspace) return gt_internal_fail(GT_ERR_ARG, "null argument");
-  if (workspace != e->tr_ws || B != e->tr_B || T != e->tr_T)
-    return gt_internal_fail(GT_ERR_ARG, "gt_text_encoder_backward must follow gt_text_encoder_forward_train with the "
-                                        "same B, Tx and workspace");
+  if (B <= 0 || T <= 0 || T > TT_TMAX) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
   const TrWs w = tr_layout(e, B, T);
   if (workspace_bytes < w.total) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
   if (e->dirty) return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
@@ -527,8 +520,7 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   auto chk = [&](hipError_t x) { if (err == hipSuccess) err = x; };
   const int C = e->C, Bi = (int)B, Ti = (int)T, K = e->K, Fc = e->Fc, Fd = e->Fdp, NF = e->n_feats;
   const long npos = (long)B * T;
-  const uint64_t seed = e->tr_seed;
-  const float pd = e->tr_p, ppre = e->tr_ppre;
+  const float pd = p_dropout, ppre = p_dropout_prenet;
   const float* mask = F(w.mask);
   const Drop none = make_drop(0, 0, 0.f);
   float *G1 = F(w.g1), *G2 = F(w.g2), *DATT = F(w.datt), *DY = F(w.dy), *DH = F(w.dh), *DQKV = F(w.dqkv);

@@ -86,7 +86,7 @@ SIGNATURES = [
     ("gt_text_encoder_forward_train", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 2 + [_c.c_int64, _c.c_int64] +
      [_c.c_float, _c.c_float, _c.c_uint64] + [_c.c_void_p] * 3 + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_text_encoder_backward", _c.c_int, [_c.c_void_p] + [_c.c_void_p] * 2 + [_c.c_int64, _c.c_int64] +
-     [_c.c_void_p] + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
+     [_c.c_float, _c.c_float, _c.c_uint64] + [_c.c_void_p] + [_c.c_void_p, _c.c_size_t, _c.c_void_p]),
     ("gt_path_scatter", _c.c_int, [_c.c_void_p, _c.c_void_p, _c.c_int64, _c.c_int64, _c.c_int64, _c.c_int32,
                                    _c.c_void_p, _c.c_void_p]),
     ("gt_tts_aux_losses_workspace_bytes", _c.c_size_t, [_c.c_int64, _c.c_int64]),

@@ -214,7 +214,7 @@ class _TextEncoderTrain(torch.autograd.Function):
         check(L.gt_text_encoder_forward_train(h, tokens.data_ptr(), lengths.data_ptr(), B, Tx, p, ppre, seed,
                                               mu.data_ptr(), logw.data_ptr(), x_mask.data_ptr(), ws.data_ptr(),
                                               ws.numel(), _stream_ptr(device)), "gt_text_encoder_forward_train")
-        ctx.h, ctx.ws, ctx.shape = h, ws, (B, Tx)
+        ctx.h, ctx.ws, ctx.shape, ctx.drop = h, ws, (B, Tx), (p, ppre, seed)
         ctx.pshapes = [q.shape for q in params]
         ctx.mark_non_differentiable(x_mask)
         return mu, logw, x_mask
@@ -230,8 +230,9 @@ class _TextEncoderTrain(torch.autograd.Function):
         dlogw = dlogw.to(torch.float32).contiguous() if dlogw is not None else None
         with torch.cuda.device(device):
             check(L.gt_text_encoder_backward(ctx.h, dmu.data_ptr() if dmu is not None else None,
-                                             dlogw.data_ptr() if dlogw is not None else None, B, Tx, grads.data_ptr(),
-                                             ctx.ws.data_ptr(), ctx.ws.numel(), _stream_ptr(device)),
+                                             dlogw.data_ptr() if dlogw is not None else None, B, Tx, *ctx.drop,
+                                             grads.data_ptr(), ctx.ws.data_ptr(), ctx.ws.numel(),
+                                             _stream_ptr(device)),
                   "gt_text_encoder_backward")
         out, off = [], 0
         for shp in ctx.pshapes:

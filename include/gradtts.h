@@ -227,7 +227,9 @@ int gt_path_gather(const float* attn, const float* mu_x, int64_t B, int64_t Tx, 
  * gt_text_encoder_backward: given dmu_x [B,n_feats,Tx] and dlogw [B,1,Tx] (either may be NULL = zero), writes the
  * gradient of every encoder parameter into grads (gt_text_encoder_grad_numel floats, state_dict inventory order,
  * reference layouts); the duration predictor sees a detached input (text_encoder.py:332), so dlogw reaches only its
- * parameters. Same encoder, B, Tx and workspace as the forward_train call it follows, parameters unchanged between. */
+ * parameters. Takes the tape (workspace), B, Tx and dropout arguments of the forward_train call it differentiates
+ * (no state in the handle: several taped forwards may precede their backwards, e.g. gradient accumulation); the
+ * parameters must be unchanged in between. */
 size_t gt_text_encoder_train_workspace_bytes(gt_text_encoder* enc, int64_t B, int64_t Tx);
 /* Device-side parameter update (a training loop's optimizer step, no host round trip): params = every parameter in
  * inventory order, fp32 contiguous on the device (the gradient buffer's layout), copied and repacked on `stream`.
@@ -239,7 +241,8 @@ int gt_text_encoder_forward_train(gt_text_encoder* enc, const int64_t* tokens, c
                                   int64_t Tx, float p_dropout, float p_dropout_prenet, uint64_t seed, float* mu_x,
                                   float* logw, float* x_mask, void* workspace, size_t workspace_bytes, void* stream);
 int gt_text_encoder_backward(gt_text_encoder* enc, const float* dmu_x, const float* dlogw, int64_t B, int64_t Tx,
-                             float* grads, void* workspace, size_t workspace_bytes, void* stream);
+                             float p_dropout, float p_dropout_prenet, uint64_t seed, float* grads, void* workspace,
+                             size_t workspace_bytes, void* stream);
 /* dmu_x [B,n_feats,Tx] = attn dmu_y: the backward of mu_y = attn^T mu_x (tts.py:184-185), attn [B,Tx,Ty] 0/1 */
 int gt_path_scatter(const float* attn, const float* dmu_y, int64_t B, int64_t Tx, int64_t Ty, int32_t n_feats,
                     float* dmu_x, void* stream);

@@ -246,3 +246,26 @@ def test_optimizer_step_device_sync_matches_fresh_upload():
     assert a[0] == b[0]
     assert all(torch.equal(x, y) for x, y in zip(a[1], b[1]))
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
+
+
+def test_two_taped_forwards_before_backward():
+    """Gradient accumulation: two compute_loss calls (two encoder tapes alive) and one backward of their sum give the
+    gradients of two separate backward passes (the library's backward is stateless: each tape carries its own)."""
+    g = load_golden("tts_loss_B2.npz")
+    m = make_gradtts(int(g["seed_enc"]), int(g["seed_dec"])).eval()
+    g2 = dict(g)
+    g2["tokens"] = np.ascontiguousarray(g["tokens"][::-1])
+    g2["x_lengths"] = np.ascontiguousarray(g["x_lengths"][::-1])
+    g2["y"] = np.ascontiguousarray(g["y"][::-1])
+    g2["y_lengths"] = np.ascontiguousarray(g["y_lengths"][::-1])
+    m.zero_grad(set_to_none=True)
+    l1 = sum(run_fixture(m, g))
+    l2 = sum(run_fixture(m, g2))
+    (l1 + l2).backward()
+    together = [p.grad.detach().clone() for p in m.parameters()]
+    m.zero_grad(set_to_none=True)
+    sum(run_fixture(m, g)).backward()
+    sum(run_fixture(m, g2)).backward()
+    apart = [p.grad.detach().clone() for p in m.parameters()]
+    for a, b in zip(together, apart):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
