@@ -357,8 +357,8 @@ namespace {
 // tape + backward scratch (floats unless noted), 256-byte aligned pieces
 struct TrWs {
   size_t tokens, mask, x0, pre_c[3], pre_h[3], x1, d1c, d1d, d2c, d2d;
-  std::vector<size_t> qkv, P, Pd, att, y1, xmid, hd, y2, xout;
-  size_t g1, g2, datt, dy, dh, dqkv, ds, drel, wpart, cpart, lpart, dmu;
+  std::vector<size_t> qkv, P, Pd, PdT, att, y1, xmid, hd, y2, xout;
+  size_t g1, g2, datt, dy, dh, dqkv, ds, dsT, drel, wpart, cpart, lpart, dmu;
   long wpart_floats, cpart_floats;
   size_t total;
 };
@@ -374,14 +374,14 @@ TrWs tr_layout(const gt_text_encoder* e, int64_t B, int64_t T) {
   for (int i = 0; i < 3; ++i) { w.pre_c[i] = put(n * C); w.pre_h[i] = put(n * C); }
   w.x1 = put(n * C);
   for (int l = 0; l < e->L; ++l) {
-    w.qkv.push_back(put(n * 3 * C)); w.P.push_back(put(att)); w.Pd.push_back(put(att));
+    w.qkv.push_back(put(n * 3 * C)); w.P.push_back(put(att)); w.Pd.push_back(put(att)); w.PdT.push_back(put(att));
     w.att.push_back(put(n * C)); w.y1.push_back(put(n * C)); w.xmid.push_back(put(n * C));
     w.hd.push_back(put(n * Fc)); w.y2.push_back(put(n * C)); w.xout.push_back(put(n * C));
   }
   w.d1c = put(n * Fd); w.d1d = put(n * Fd); w.d2c = put(n * Fd); w.d2d = put(n * Fd);
   const size_t wide = std::max({C, Fc, Fd, (size_t)e->n_feats});
   w.g1 = put(n * C); w.g2 = put(n * C); w.datt = put(n * C);
-  w.dy = put(n * wide); w.dh = put(n * wide); w.dqkv = put(n * 3 * C); w.ds = put(att);
+  w.dy = put(n * wide); w.dh = put(n * wide); w.dqkv = put(n * 3 * C); w.ds = put(att); w.dsT = put(att);
   w.drel = put((size_t)B * 2 * (2 * e->W + 1) * 96);
   w.wpart_floats = 8L << 20;
   w.wpart = put((size_t)w.wpart_floats);
@@ -469,7 +469,7 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
     conv(x, C, nullptr, a + "conv_k", C, 1, qkv, 3 * C, C, 0, nullptr, nullptr, 0, none);
     conv(x, C, nullptr, a + "conv_v", C, 1, qkv, 3 * C, 2 * C, 0, nullptr, nullptr, 0, none);
     chk(launch_tt_attn_fwd(qkv, mask, P(a + "emb_rel_k"), P(a + "emb_rel_v"), Bi, Ti, C, e->H, e->W,
-                           make_drop(seed, site, p_dropout), F(w.P[l]), F(w.Pd[l]), F(w.att[l]), s));
+                           make_drop(seed, site, p_dropout), F(w.P[l]), F(w.Pd[l]), F(w.PdT[l]), F(w.att[l]), s));
     conv(F(w.att[l]), C, nullptr, a + "conv_o", C, 1, F(w.y1[l]), C, 0, 0, nullptr, nullptr, 0,
          make_drop(seed, site + 1, p_dropout));                                                      // y = drop(attn)
     ln(x, F(w.y1[l]), "encoder.norm_layers_1." + std::to_string(l), C, 0, nullptr, F(w.xmid[l]), none);
@@ -596,9 +596,9 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
     ew(DY, C, G1, C, 0, C, nullptr, make_drop(seed, site + 1, pd), nullptr, 0);
     wgrad(DY, C, F(w.att[l]), C, nullptr, a + "conv_o", C, C, 1);
     dgrad(DY, C, a + "conv_o", C, C, 1, DATT, C, 0, nullptr);
-    chk(launch_tt_attn_bwd(F(w.qkv[l]), F(w.P[l]), F(w.Pd[l]), DATT, mask, P(a + "emb_rel_k"), P(a + "emb_rel_v"), Bi,
-                           Ti, C, e->H, e->W, make_drop(seed, site, pd), F(w.ds), DQKV, F(w.drel), G(a + "emb_rel_k"),
-                           s));
+    chk(launch_tt_attn_bwd(F(w.qkv[l]), F(w.P[l]), F(w.Pd[l]), F(w.PdT[l]), DATT, mask, P(a + "emb_rel_k"),
+                           P(a + "emb_rel_v"), Bi, Ti, C, e->H, e->W, make_drop(seed, site, pd), F(w.ds), F(w.dsT), DQKV,
+                           F(w.drel), G(a + "emb_rel_k"), s));
     const char* qkvn[3] = {"conv_q", "conv_k", "conv_v"};
     for (int j = 0; j < 3; ++j) {
       wgrad(DQKV + j * C, 3 * C, xin, C, nullptr, a + qkvn[j], C, C, 1);
@@ -618,7 +618,7 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
     else dgrad(DY, C, "prenet.conv_layers." + k, C, C, 5, G1, C, 1, mask);
   }
   chk(launch_tt_emb_bwd((const int64_t*)F(w.tokens), npos, G1, e->n_vocab, C, (float)std::sqrt((double)C),
-                        G("emb.weight"), s));
+                        G("emb.weight"), F(w.wpart), w.wpart_floats, s));
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder backward: ") + hipGetErrorString(err));
   return GT_OK;
 }

@@ -10,14 +10,16 @@ namespace gt {
 
 constexpr int TT_TMAX = 4096;   // longest token sequence of the training attention (one LDS score row)
 
-// attention forward with explicit probabilities: P = softmax(masked scores) [B][H][T][T], Pd = dropout(P), out
+// attention forward with explicit probabilities: P = softmax(masked scores) [B][H][T][T], Pd = dropout(P) and its
+// transpose PdT, out
 hipError_t launch_tt_attn_fwd(const float* qkv, const float* x_mask, const float* erk, const float* erv, int B, int T,
-                              int C, int H, int W, Drop drop, float* P, float* Pd, float* out, hipStream_t s);
+                              int C, int H, int W, Drop drop, float* P, float* Pd, float* PdT, float* out,
+                              hipStream_t s);
 // attention backward: datt [B][T][C] -> dqkv [B][T][3C], d emb_rel_k | d emb_rel_v (2 (2W+1) 96 floats);
 // dS [B][H][T][T] and drel_part [B][2][2W+1][96] are scratch
-hipError_t launch_tt_attn_bwd(const float* qkv, const float* P, const float* Pd, const float* datt,
+hipError_t launch_tt_attn_bwd(const float* qkv, const float* P, const float* Pd, const float* PdT, const float* datt,
                               const float* x_mask, const float* erk, const float* erv, int B, int T, int C, int H,
-                              int W, Drop drop, float* dS, float* dqkv, float* drel_part, float* derk_derv,
+                              int W, Drop drop, float* dS, float* dST, float* dqkv, float* drel_part, float* derk_derv,
                               hipStream_t s);
 
 // LayerNorm backward. LN input = x (+ res); dy_eff = dy * dy_mask * drop * [relu_ref > 0]; dx = LN'(dy_eff)
@@ -56,7 +58,7 @@ hipError_t launch_tt_wgrad(WgradParams p, float* dW, float* partial, long partia
 hipError_t launch_tt_colsum(const float* x, int x_cs, long npos, int C, float* part, long part_floats, float* out,
                             hipStream_t s);
 hipError_t launch_tt_emb_bwd(const int64_t* tokens, long npos, const float* dx0, int n_vocab, int C, float scale,
-                             float* demb, hipStream_t s);
+                             float* demb, float* part, long part_floats, hipStream_t s);
 
 // dst[pos][c] = src(pos, c) (0 if src is NULL) * mask[pos] * drop(pos C + c) * [relu_ref[pos][c] > 0]; src channels-last or
 // channel-major [B][C][T]

@@ -76,7 +76,7 @@ GT_DEV float dot96(const float* s, const float* g) {   // s in LDS, g 16-byte al
 // ---------------------------------------------------------------- attention, forward (training)
 // one workgroup per (query i, head h, utterance b); the score row lives in LDS (T <= TT_TMAX)
 __global__ __launch_bounds__(256) void tt_attn_p_kernel(const float* qkv, const float* x_mask, const float* erk, int T,
-                                                        int C, int W, Drop drop, float* P, float* Pd) {
+                                                        int C, int W, Drop drop, float* P, float* Pd, float* PdT) {
   __shared__ float s_q[TT_D], s_ek[TT_WMAX * TT_D], s_row[TT_TMAX], s_red[4];
   const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z, H = gridDim.y, tid = threadIdx.x, nw = 2 * W + 1;
   const long C3 = 3L * C;
@@ -111,7 +111,9 @@ __global__ __launch_bounds__(256) void tt_attn_p_kernel(const float* qkv, const 
   for (int j = tid; j < T; j += 256) {
     const float p = s_row[j] / l;
     P[row + j] = p;
-    Pd[row + j] = p * drop_scale(drop, (uint64_t)(row + j));
+    const float pd = p * drop_scale(drop, (uint64_t)(row + j));
+    Pd[row + j] = pd;
+    PdT[(((long)b * H + h) * T + j) * T + i] = pd;   // transposed copy: the backward's dv reads rows of it
   }
 }
 
@@ -125,6 +127,7 @@ __global__ __launch_bounds__(256) void tt_attn_pv_kernel(const float* qkv, const
   const float* prow = Pd + (((long)b * H + h) * T + i) * T;
   const float* vb = qkv + (long)b * T * C3 + 2 * C + tid;
   float o = 0.f;
+#pragma unroll 8
   for (int j = 0; j < T; ++j) o = fmaf(prow[j], vb[(long)j * C3], o);
   for (int r = -W; r <= W; ++r) {
     const int j = i + r;
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(256) void tt_attn_pv_kernel(const float* qkv, const
 // dPd[j] = g_i . v_j + [|j - i| <= W] g_i . erv[j - i + W]; dP = dPd * drop; dS = P (dP - sum_j P dP), 0 where masked
 __global__ __launch_bounds__(256) void tt_attn_ds_kernel(const float* qkv, const float* P, const float* datt,
                                                          const float* x_mask, const float* erv, int T, int C, int W,
-                                                         Drop drop, float* dS) {
+                                                         Drop drop, float* dS, float* dST) {
   __shared__ float s_g[TT_D], s_ev[TT_WMAX * TT_D], s_dp[TT_TMAX], s_red[4];
   const int i = blockIdx.x, h = blockIdx.y, b = blockIdx.z, H = gridDim.y, tid = threadIdx.x, nw = 2 * W + 1;
   const long C3 = 3L * C;
@@ -165,14 +168,15 @@ __global__ __launch_bounds__(256) void tt_attn_ds_kernel(const float* qkv, const
     float ds = P[row + j] * (s_dp[j] - acc);
     if (!(qi && x_mask[(long)b * T + j] != 0.f)) ds = 0.f;
     dS[row + j] = ds;
+    dST[(((long)b * H + h) * T + j) * T + i] = ds;   // transposed copy: dk reads rows of it
   }
 }
 
 // position i of utterance b, thread = (h, d): dq_i = (sum_j dS[i][j] k_j + sum_r dS[i][i + r] erk[r]) / sqrt(96),
 // dk_i = sum_j dS[j][i] q_j / sqrt(96), dv_i = sum_j Pd[j][i] g_j   -> dqkv [B][T][3C] (q | k | v)
-__global__ __launch_bounds__(256) void tt_attn_dqkv_kernel(const float* qkv, const float* Pd, const float* dS,
-                                                           const float* datt, const float* erk, int T, int C, int H,
-                                                           int W, float* dqkv) {
+__global__ __launch_bounds__(256) void tt_attn_dqkv_kernel(const float* qkv, const float* PdT, const float* dS,
+                                                           const float* dST, const float* datt, const float* erk, int T,
+                                                           int C, int H, int W, float* dqkv) {
   const int i = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   if (tid >= C) return;
   const int h = tid / TT_D, d = tid % TT_D;
@@ -180,10 +184,14 @@ __global__ __launch_bounds__(256) void tt_attn_dqkv_kernel(const float* qkv, con
   const float* q = qkv + (long)b * T * C3 + tid;
   const float* g = datt + (long)b * T * C + tid;
   float dq = 0.f, dk = 0.f, dv = 0.f;
+  const float* ds_r = dS + hb + (long)i * T;    // row i of dS
+  const float* dst_r = dST + hb + (long)i * T;  // column i of dS
+  const float* pdt_r = PdT + hb + (long)i * T;  // column i of Pd
+#pragma unroll 4
   for (int j = 0; j < T; ++j) {
-    dq = fmaf(dS[hb + (long)i * T + j], q[(long)j * C3 + C], dq);
-    dk = fmaf(dS[hb + (long)j * T + i], q[(long)j * C3], dk);
-    dv = fmaf(Pd[hb + (long)j * T + i], g[(long)j * C], dv);
+    dq = fmaf(ds_r[j], q[(long)j * C3 + C], dq);
+    dk = fmaf(dst_r[j], q[(long)j * C3], dk);
+    dv = fmaf(pdt_r[j], g[(long)j * C], dv);
   }
   for (int r = -W; r <= W; ++r) {
     const int j = i + r;
@@ -209,11 +217,10 @@ __global__ __launch_bounds__(128) void tt_attn_drel_kernel(const float* qkv, con
     const long hb = ((long)b * H + h) * T * T;
     const float* v = which ? datt + (long)b * T * C + h * TT_D + d : qkv + (long)b * T * C3 + h * TT_D + d;
     const long vs = which ? C : C3;
-    for (int i = 0; i < T; ++i) {
-      const int j = i + r;
-      if (j < 0 || j >= T) continue;
-      acc = fmaf(M[hb + (long)i * T + j], v[(long)i * vs], acc);
-    }
+    const int i0 = r < 0 ? -r : 0, i1 = r > 0 ? T - r : T;   // rows whose column i + r exists
+    const float* md = M + hb + (long)i0 * T + i0 + r;        // the r-th diagonal, stride T + 1
+#pragma unroll 8
+    for (int i = i0; i < i1; ++i) acc = fmaf(md[(long)(i - i0) * (T + 1)], v[(long)i * vs], acc);
   }
   if (!which) acc = acc / sqrtf((float)TT_D);
   part[(((long)b * 2 + which) * nw + (r + W)) * TT_D + d] = acc;
@@ -370,14 +377,16 @@ __global__ void tt_sum_splits_kernel(const float* part, int nsplit, long n, floa
 }
 
 // ---------------------------------------------------------------- embedding, elementwise
+// part[s][v][c] = scale * sum over split s's positions (in order) with token v of dx0[pos][c]
 __global__ __launch_bounds__(256) void tt_emb_bwd_kernel(const int64_t* tokens, long npos, const float* dx0, int C,
-                                                         float scale, float* demb) {
-  const int v = blockIdx.x, c = threadIdx.x;
+                                                         float scale, int nv, float* part) {
+  const int v = blockIdx.x, sp = blockIdx.y, ns = gridDim.y, c = threadIdx.x;
   if (c >= C) return;
+  const long a = (long)sp * npos / ns, z = (long)(sp + 1) * npos / ns;
   float acc = 0.f;
-  for (long pos = 0; pos < npos; ++pos)
+  for (long pos = a; pos < z; ++pos)
     if (tokens[pos] == v) acc += dx0[pos * C + c];
-  demb[(long)v * C + c] = acc * scale;
+  part[((long)sp * nv + v) * C + c] = acc * scale;
 }
 
 __global__ void tt_ew_kernel(EwParams p) {
@@ -437,21 +446,25 @@ GT_DEV double tt_block_sum_d(double x, double* red) {
   __syncthreads();
   return ((red[0] + red[1]) + red[2]) + red[3];
 }
+// one wave per (b, i) row of attn (coalesced; the 0/1 sum is exact in any order), 4 rows per workgroup
 __global__ __launch_bounds__(256) void tt_dur_kernel(const float* logw, const float* attn, const float* x_mask,
                                                      long n, int Ta, float* dlogw_unit, double* part) {
-  __shared__ double s_red[4];
-  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double s_sq[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 4 + wv;
   double sq = 0.0;
   if (e < n) {
     const float* a = attn + e * Ta;
     float dur = 0.f;
-    for (int j = 0; j < Ta; ++j) dur += a[j];
+    for (int j = lane; j < Ta; j += 64) dur += a[j];
+    dur = tt_wave_sum(dur);
     const float df = logw[e] - logf(1e-8f + dur) * x_mask[e];
-    dlogw_unit[e] = df;
+    if (lane == 0) dlogw_unit[e] = df;
     sq = (double)df * df;
   }
-  sq = tt_block_sum_d(sq, s_red);
-  if (threadIdx.x == 0) part[blockIdx.x] = sq;
+  if (lane == 0) s_sq[wv] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((s_sq[0] + s_sq[1]) + s_sq[2]) + s_sq[3];
 }
 __global__ __launch_bounds__(256) void tt_prior_kernel(const float* y, const float* mu_y, const float* y_mask, int B,
                                                        int F, int Ty, double* part) {
@@ -473,13 +486,19 @@ __global__ __launch_bounds__(256) void tt_prior_kernel(const float* y, const flo
     part[2 * blockIdx.x + 1] = ms;
   }
 }
-__global__ void tt_aux_final_kernel(const double* dpart, int nd, const double* ppart, int np, const int64_t* x_lengths,
-                                    int B, int F, float* out) {
-  if (threadIdx.x != 0) return;
-  double ds = 0.0, ps = 0.0, ms = 0.0, ls = 0.0;
-  for (int i = 0; i < nd; ++i) ds += dpart[i];
-  for (int i = 0; i < np; ++i) { ps += ppart[2 * i]; ms += ppart[2 * i + 1]; }
-  for (int b = 0; b < B; ++b) ls += (double)x_lengths[b];
+__global__ __launch_bounds__(256) void tt_aux_final_kernel(const double* dpart, int nd, const double* ppart, int np,
+                                                           const int64_t* x_lengths, int B, int F, float* out) {
+  __shared__ double s_red[4];
+  const int tid = threadIdx.x;
+  double ds = 0.0, ps = 0.0, ms = 0.0, ls = 0.0;   // per thread strided, then a fixed-order block reduction
+  for (int i = tid; i < nd; i += 256) ds += dpart[i];
+  for (int i = tid; i < np; i += 256) { ps += ppart[2 * i]; ms += ppart[2 * i + 1]; }
+  for (int b = tid; b < B; b += 256) ls += (double)x_lengths[b];
+  ds = tt_block_sum_d(ds, s_red);
+  ps = tt_block_sum_d(ps, s_red);
+  ms = tt_block_sum_d(ms, s_red);
+  ls = tt_block_sum_d(ls, s_red);
+  if (tid != 0) return;
   const double pden = ms * F;
   out[0] = (float)(ds / ls);
   out[1] = (float)(ps / pden);
@@ -514,20 +533,22 @@ __global__ void tt_repack_kernel(const float* raw, const RepackEntry* tab, float
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_tt_attn_fwd(const float* qkv, const float* x_mask, const float* erk, const float* erv, int B, int T,
-                              int C, int H, int W, Drop drop, float* P, float* Pd, float* out, hipStream_t s) {
+                              int C, int H, int W, Drop drop, float* P, float* Pd, float* PdT, float* out,
+                              hipStream_t s) {
   if (C != H * TT_D || 2 * W + 1 > TT_WMAX || T > TT_TMAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tt_attn_p_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, x_mask, erk, T, C, W, drop, P, Pd);
+  hipLaunchKernelGGL(tt_attn_p_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, x_mask, erk, T, C, W, drop, P, Pd, PdT);
   hipLaunchKernelGGL(tt_attn_pv_kernel, dim3(T, B), dim3(256), 0, s, qkv, Pd, erv, T, C, H, W, out);
   return hipGetLastError();
 }
 
-hipError_t launch_tt_attn_bwd(const float* qkv, const float* P, const float* Pd, const float* datt,
+hipError_t launch_tt_attn_bwd(const float* qkv, const float* P, const float* Pd, const float* PdT, const float* datt,
                               const float* x_mask, const float* erk, const float* erv, int B, int T, int C, int H,
-                              int W, Drop drop, float* dS, float* dqkv, float* drel_part, float* derk_derv,
+                              int W, Drop drop, float* dS, float* dST, float* dqkv, float* drel_part, float* derk_derv,
                               hipStream_t s) {
   if (C != H * TT_D || 2 * W + 1 > TT_WMAX || T > TT_TMAX) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tt_attn_ds_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, P, datt, x_mask, erv, T, C, W, drop, dS);
-  hipLaunchKernelGGL(tt_attn_dqkv_kernel, dim3(T, B), dim3(256), 0, s, qkv, Pd, dS, datt, erk, T, C, H, W, dqkv);
+  hipLaunchKernelGGL(tt_attn_ds_kernel, dim3(T, H, B), dim3(256), 0, s, qkv, P, datt, x_mask, erv, T, C, W, drop, dS,
+                     dST);
+  hipLaunchKernelGGL(tt_attn_dqkv_kernel, dim3(T, B), dim3(256), 0, s, qkv, PdT, dS, dST, datt, erk, T, C, H, W, dqkv);
   const int nw = 2 * W + 1;
   hipLaunchKernelGGL(tt_attn_drel_kernel, dim3(nw, 2, B), dim3(128), 0, s, qkv, Pd, dS, datt, T, C, H, W, drel_part);
   // derk_derv = [emb_rel_k grad (nw x 96) | emb_rel_v grad (nw x 96)] summed over utterances in order
@@ -583,9 +604,12 @@ hipError_t launch_tt_colsum(const float* x, int x_cs, long npos, int C, float* p
 }
 
 hipError_t launch_tt_emb_bwd(const int64_t* tokens, long npos, const float* dx0, int n_vocab, int C, float scale,
-                             float* demb, hipStream_t s) {
+                             float* demb, float* part, long part_floats, hipStream_t s) {
   if (C > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tt_emb_bwd_kernel, dim3(n_vocab), dim3(256), 0, s, tokens, npos, dx0, C, scale, demb);
+  const long n = (long)n_vocab * C;
+  const int ns = (int)std::max(1L, std::min(std::min(32L, (npos + 127) / 128), part_floats / n));
+  hipLaunchKernelGGL(tt_emb_bwd_kernel, dim3(n_vocab, ns), dim3(256), 0, s, tokens, npos, dx0, C, scale, n_vocab, part);
+  hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, ns, n, demb);
   return hipGetLastError();
 }
 
@@ -619,12 +643,12 @@ hipError_t launch_tt_aux_loss(const float* logw, const float* attn, const float*
                               const float* y, const float* mu_y, const float* y_mask, int B, int Tx, int Ta, int Ty,
                               int F, float* out, float* dlogw_unit, float* dmu_unit, double* scratch, hipStream_t s) {
   const long nx = (long)B * Tx, ny = (long)B * F * Ty;
-  const int nd = (int)((nx + 255) / 256);
+  const int nd = (int)((nx + 3) / 4);   // tt_dur_kernel: 4 rows per workgroup
   double* dpart = scratch;
   double* ppart = scratch + nd;
   hipLaunchKernelGGL(tt_dur_kernel, dim3(nd), dim3(256), 0, s, logw, attn, x_mask, nx, Ta, dlogw_unit, dpart);
   hipLaunchKernelGGL(tt_prior_kernel, dim3(TT_PRIOR_BLOCKS), dim3(256), 0, s, y, mu_y, y_mask, B, F, Ty, ppart);
-  hipLaunchKernelGGL(tt_aux_final_kernel, dim3(1), dim3(64), 0, s, dpart, nd, ppart, TT_PRIOR_BLOCKS, x_lengths, B, F,
+  hipLaunchKernelGGL(tt_aux_final_kernel, dim3(1), dim3(256), 0, s, dpart, nd, ppart, TT_PRIOR_BLOCKS, x_lengths, B, F,
                      out);
   const long ng = std::max(nx, ny);
   hipLaunchKernelGGL(tt_aux_grad_kernel, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, y, mu_y, y_mask, B, F, Ty,
@@ -632,6 +656,6 @@ hipError_t launch_tt_aux_loss(const float* logw, const float* attn, const float*
   return hipGetLastError();
 }
 
-long tt_aux_loss_scratch_doubles(long B, long Tx) { return (B * Tx + 255) / 256 + 2 * TT_PRIOR_BLOCKS; }
+long tt_aux_loss_scratch_doubles(long B, long Tx) { return (B * Tx + 3) / 4 + 2 * TT_PRIOR_BLOCKS; }
 
 }  // namespace gt
