@@ -353,18 +353,22 @@ __global__ __launch_bounds__(256) void tt_wgrad_kernel(WgradParams p) {
   }
 }
 
-// part[s][c] = sum over split s's positions of x[pos][c] (4 position lanes per channel, combined in order)
-__global__ __launch_bounds__(256) void tt_colsum_kernel(const float* x, int x_cs, long npos, int C, int nsplit,
-                                                        float* part) {
-  __shared__ float s_p[4][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, s = blockIdx.y;
-  const long a = (long)s * npos / nsplit, e = (long)(s + 1) * npos / nsplit;
+// out[c] = sum_pos x[pos][c]: one workgroup per 64 channels, 16 position lanes (strided), combined in lane order
+__global__ __launch_bounds__(1024) void tt_colsum_kernel(const float* x, int x_cs, long npos, int C, float* out) {
+  __shared__ float s_p[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
   float acc = 0.f;
   if (c < C)
-    for (long pos = a + g; pos < e; pos += 4) acc += x[pos * x_cs + c];
+#pragma unroll 4
+    for (long pos = g; pos < npos; pos += 16) acc += x[pos * x_cs + c];
   s_p[g][cl] = acc;
   __syncthreads();
-  if (g == 0 && c < C) part[(long)s * C + c] = ((s_p[0][cl] + s_p[1][cl]) + s_p[2][cl]) + s_p[3][cl];
+  if (g == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += s_p[k][cl];
+    out[c] = t;
+  }
 }
 
 // out[i] = sum_s part[s n + i] in split order
@@ -596,10 +600,8 @@ hipError_t launch_tt_wgrad(WgradParams p, float* dW, float* partial, long partia
 
 hipError_t launch_tt_colsum(const float* x, int x_cs, long npos, int C, float* part, long part_floats, float* out,
                             hipStream_t s) {
-  int ns = (int)std::min<long>(64, std::max(1L, npos / 64));
-  ns = (int)std::max<long>(1, std::min<long>(ns, part_floats / C));
-  hipLaunchKernelGGL(tt_colsum_kernel, dim3((unsigned)((C + 63) / 64), ns), dim3(256), 0, s, x, x_cs, npos, C, ns, part);
-  hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, s, part, ns, (long)C, out);
+  (void)part; (void)part_floats;
+  hipLaunchKernelGGL(tt_colsum_kernel, dim3((unsigned)((C + 63) / 64)), dim3(1024), 0, s, x, x_cs, npos, C, out);
   return hipGetLastError();
 }
 
