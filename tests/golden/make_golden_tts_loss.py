@@ -11,8 +11,8 @@ running the REAL reference in this container (the fixtures are data; the referen
 * The draws: ``random.seed(py_seed)`` before the call fixes the crop offsets (``random.choice``, tts.py:161-165; the
   offsets are stored), ``torch.rand`` (t, diffusion.py:284) and ``torch.randn`` (z, diffusion.py:249) return stored
   values.
-* Stored: the three losses, the MAS path, ``(dur + prior + diff).backward()``'s gradient of every parameter as a
-  digest (sum of squares, projection on ``oracle.decoder.grad_probe``) and a few full gradients.
+* Stored: the three losses, ``(dur + prior + diff).backward()``'s gradient of every parameter as a digest (sum of
+  squares, projection on ``oracle.decoder.grad_probe``) and a few full gradients.
 
 Usage:  make -C oracle ref && PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_tts_loss.py
 """
@@ -110,7 +110,6 @@ def case(tts, name, x_lengths, y_lengths, Tx, Ty, out_size, py_seed, tvals, seed
         if tag == "f64":
             for k in FULL:
                 out["full__" + k] = named[k].grad.numpy()
-    # the MAS path of the fp32 run (recomputed with the reference's own modules, tts.py:136-152)
     out["param_names"] = np.array(list(sd.keys()))
     save(name, **out)
 
@@ -120,6 +119,9 @@ def main():
     import model.tts as tts   # noqa: E402  (model.text_encoder, model.utils, model.monotonic_align as installed above)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     case(tts, "tts_loss_B2.npz", [13, 9], [56, 41], 13, 56, 32, py_seed=3, tvals=[0.63, 0.18], seed_in=61, seed_z=62)
+    # one utterance shorter than out_size: its crop keeps all 21 frames at offset 0 (no random draw, :162-164)
+    case(tts, "tts_loss_B2_short.npz", [13, 6], [56, 21], 13, 56, 32, py_seed=5, tvals=[0.44, 0.91], seed_in=65,
+         seed_z=66)
     case(tts, "tts_loss_B3_nocut.npz", [7, 11, 5], [30, 44, 21], 11, 44, None, py_seed=4, tvals=[0.35, 0.77, 0.52],
          seed_in=63, seed_z=64)
 

@@ -74,7 +74,7 @@ def run_fixture(m, g):
     return dur, prior, diff
 
 
-@pytest.mark.parametrize("name", ["tts_loss_B2.npz", "tts_loss_B3_nocut.npz"])
+@pytest.mark.parametrize("name", ["tts_loss_B2.npz", "tts_loss_B3_nocut.npz", "tts_loss_B2_short.npz"])
 def test_compute_loss_matches_reference_fixture(name):
     from oracle import decoder as odec
     g = load_golden(name)

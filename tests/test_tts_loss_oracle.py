@@ -34,7 +34,7 @@ def run_oracle(g, mas, dtype=torch.float64, drop=None):
     return np.array([float(dur), float(prior), float(diff)]), grads, attn
 
 
-@pytest.mark.parametrize("name", ["tts_loss_B2.npz", "tts_loss_B3_nocut.npz"])
+@pytest.mark.parametrize("name", ["tts_loss_B2.npz", "tts_loss_B3_nocut.npz", "tts_loss_B2_short.npz"])
 def test_oracle_compute_loss_matches_reference(name, mas_oracle):
     g = load_golden(name)
     losses, grads, _ = run_oracle(g, mas_oracle)
