@@ -106,7 +106,8 @@ class TextEncoder(torch.nn.Module):
     kernel_size, p_dropout, window_size=None, spk_emb_dim=64, n_spks=1)``; ``forward(x, x_lengths, spk=None)`` ->
     (mu [B, n_feats, Tx], logw [B, 1, Tx], x_mask [B, 1, Tx]).
 
-    With gradients enabled and parameters that require them, ``forward`` is the training pass
+    With gradients enabled and parameters that require them, or in train mode with p_dropout > 0, ``forward`` is the
+    training pass
     (``gt_text_encoder_forward_train`` + ``gt_text_encoder_backward`` behind an autograd Function): in train mode the
     reference's dropouts apply (``p_dropout`` at the attention probabilities, attention / FFN outputs, FFN hidden
     and duration predictor; 0.5 in the prenet), drawn from the library's counter-based generator with a seed taken
@@ -175,7 +176,9 @@ class TextEncoder(torch.nn.Module):
         tokens = x.to(device=device, dtype=torch.int64).contiguous()
         lengths = x_lengths.to(device=device, dtype=torch.int64).contiguous()
         B, Tx = tokens.shape
-        if torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters()):
+        # the training pass: with gradients, or in train mode with dropout (torch's Dropout drops under no_grad too)
+        if (torch.is_grad_enabled() and any(q.requires_grad for q in self.parameters())) or \
+                (self.training and self.p_dropout > 0):
             p, ppre = (float(self.p_dropout), 0.5) if self.training else (0.0, 0.0)
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (p > 0 or ppre > 0) else 0
             with torch.cuda.device(device):

@@ -30,7 +30,7 @@ def build(compute_dtype=torch.float32, vocoder_dtype=torch.float32):
     voc = Generator(HIFIGAN_V1, compute_dtype=vocoder_dtype)
     voc.load_state_dict({k: torch.from_numpy(v) for k, v in vsd.items()}, strict=True)
     voc.remove_weight_norm()
-    return m.cuda(), voc.cuda().eval(), (esd, dsd, vsd)
+    return m.cuda().eval(), voc.cuda().eval(), (esd, dsd, vsd)   # eval: inference semantics (no dropout)
 
 
 def run(m, voc, tokens, lengths, n_timesteps, drawn=None):

@@ -169,7 +169,7 @@ def test_get_score_model_and_rescoring_chain(mas_oracle):
     from oracle import decoder as odec, likelihood as olik, text_encoder as ote
     from gradtts_amd.params import synthetic_text_encoder_state_dict
     from gradtts_amd.tts import GradTTS
-    m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+    m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000).eval()
     esd, dsd = synthetic_text_encoder_state_dict(2), None
     dec, dsd = make_decoder(1, 0, torch.float32)
     m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)

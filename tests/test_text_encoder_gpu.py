@@ -30,7 +30,7 @@ def make_encoder(seed):
     enc = TextEncoder(149, 80, 192, 768, 256, 2, 6, 3, 0.1, 4)
     sd = synthetic_text_encoder_state_dict(seed)
     enc.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
-    return enc.cuda(), sd
+    return enc.cuda().eval(), sd   # eval: the reference's inference semantics (no dropout)
 
 
 @pytest.mark.parametrize("name", ["te_B3_T37", "te_B2_T130"])
@@ -74,7 +74,7 @@ def test_front_end_exact_on_reference_encoder_outputs(name, ls):
 def test_gradtts_forward_matches_oracle_chain(n_spks):
     from oracle import decoder as odec, text_encoder as ote
     from gradtts_amd.tts import GradTTS
-    m = GradTTS(149, n_spks, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000)
+    m = GradTTS(149, n_spks, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000).eval()
     esd = synthetic_text_encoder_state_dict(2)
     dsd = synthetic_state_dict(seed=0, n_spks=n_spks)
     m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)

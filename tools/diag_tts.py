@@ -8,7 +8,7 @@ m = GradTTS(149, 1, 64, 192, 768, 256, 2, 6, 3, 0.1, 4, 80, 64, 0.05, 20.0, 1000
 esd = synthetic_text_encoder_state_dict(2); dsd = synthetic_state_dict(seed=0, n_spks=1)
 m.encoder.load_state_dict({k: torch.from_numpy(v) for k, v in esd.items()}, strict=True)
 m.decoder.estimator.load_state_dict({k: torch.from_numpy(v) for k, v in dsd.items()}, strict=True)
-m = m.cuda()
+m = m.cuda().eval()
 rng = np.random.default_rng(4)
 tokens = torch.from_numpy(rng.integers(0, 149, (2, 29))); lengths = torch.tensor([29, 21])
 mu_x, logw, xm = m.encoder(tokens.cuda(), lengths.cuda())
