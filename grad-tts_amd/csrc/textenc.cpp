@@ -361,12 +361,18 @@ struct TrWs {
   size_t g1, g2, datt, dy, dh, dqkv, ds, dsT, drel, wpart, cpart, lpart, dmu;
   long wpart_floats, cpart_floats;
   size_t total;
+  std::map<size_t, size_t> bytes;   // piece offset -> its size: tape pointers are checked against it (tape_ptr)
 };
 
 TrWs tr_layout(const gt_text_encoder* e, int64_t B, int64_t T) {
   TrWs w{};
   size_t off = 0;
-  auto put = [&](size_t floats) { const size_t o = off; off += (floats * 4 + 255) & ~size_t(255); return o; };
+  auto put = [&](size_t floats) {
+    const size_t o = off;
+    off += (floats * 4 + 255) & ~size_t(255);
+    w.bytes[o] = floats * 4;
+    return o;
+  };
   const size_t n = (size_t)B * T, C = e->C, Fc = e->Fc, Fd = e->Fdp, att = (size_t)B * e->H * T * T;
   w.tokens = put(2 * n);
   w.mask = put(n);
@@ -391,6 +397,15 @@ TrWs tr_layout(const gt_text_encoder* e, int64_t B, int64_t T) {
   w.dmu = put(n * wide);
   w.total = off + 256;
   return w;
+}
+
+// pointer to the tape piece at byte offset o: a host-side guard against offset misuse. An offset that is not a piece
+// start, or a piece reaching past the workspace, flags the call (it then fails with GT_ERR_WORKSPACE) and yields the
+// workspace base, so the launch that uses it stays inside the caller's allocation instead of faulting the GPU.
+float* tape_ptr(const TrWs& w, char* base, size_t o, size_t ws_usable, bool& bad) {
+  const auto it = w.bytes.find(o);
+  if (it == w.bytes.end() || o + it->second > ws_usable) { bad = true; return (float*)base; }
+  return (float*)(base + o);
 }
 
 }  // namespace
@@ -418,7 +433,9 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  auto F = [&](size_t o) { return (float*)(base + o); };   // o: byte offset (tr_layout)
+  const size_t usable = workspace_bytes - (size_t)(base - (char*)workspace);
+  bool bad_ptr = false;
+  auto F = [&](size_t o) { return tape_ptr(w, base, o, usable, bad_ptr); };   // o: byte offset (tr_layout)
   auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
   auto PK = [&](const std::string& k) {
     const auto it = e->pkoff.find(k);
@@ -500,6 +517,7 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
     chk(launch_tt_ew(c, s));
   }
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder training forward: ") + hipGetErrorString(err));
+  if (bad_ptr) return gt_internal_fail(GT_ERR_WORKSPACE, "text encoder training forward: tape offset outside the layout");
   return GT_OK;
 }
 
@@ -513,7 +531,9 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   if (e->dirty) return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
-  auto F = [&](size_t o) { return (float*)(base + o); };   // o: byte offset (tr_layout)
+  const size_t usable = workspace_bytes - (size_t)(base - (char*)workspace);
+  bool bad_ptr = false;
+  auto F = [&](size_t o) { return tape_ptr(w, base, o, usable, bad_ptr); };   // o: byte offset (tr_layout)
   auto P = [&](const std::string& k) { return e->dev + e->off[e->index.at(k)]; };
   auto G = [&](const std::string& k) { return grads + e->off[e->index.at(k)]; };
   hipError_t err = hipSuccess;
@@ -620,6 +640,7 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   chk(launch_tt_emb_bwd((const int64_t*)F(w.tokens), npos, G1, e->n_vocab, C, (float)std::sqrt((double)C),
                         G("emb.weight"), F(w.wpart), w.wpart_floats, s));
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder backward: ") + hipGetErrorString(err));
+  if (bad_ptr) return gt_internal_fail(GT_ERR_WORKSPACE, "text encoder backward: tape offset outside the layout");
   return GT_OK;
 }
 
