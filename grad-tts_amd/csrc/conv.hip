@@ -49,13 +49,17 @@ namespace gt {
 #ifndef GT_CAP_3W8
 #define GT_CAP_3W8 3
 #endif
+#ifndef GT_SMALL_DBW
+#define GT_SMALL_DBW 1
+#endif
+constexpr int TF1_DBW = 101;   // tile-height code: 1-row tiles with double-buffered weight slabs (ConvCfg::SMALLDB)
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
 struct ConvCfg {
   static constexpr bool CONVT = KIND == CONVT4;
   static constexpr int KS = (KIND == CONV1) ? 1 : 3;
   static constexpr int S = (KIND == CONV3_S2) ? 2 : 1;
-  static constexpr int TF = TF_;
+  static constexpr int TF = TF_ == TF1_DBW ? 1 : TF_;
   static constexpr int TT = (KIND == CONV3_S2) ? 32 : 64;
   static constexpr int RBT = TT / 32;
   static constexpr int WN = NT / 64;
@@ -85,10 +89,15 @@ struct ConvCfg {
   // Split pipeline (bf16, multi-tap, operand from an activation): the two halves of chunk c+1 are staged while
   // the other half of chunk c is in the MFMAs. Every wave issues exactly PA / PB DMA pieces per half and PPT
   // patch loads per chunk, so counted vmcnt waits retire exactly the right ones.
-  static constexpr bool SPLIT = (!W8 && NA < NTAP && IN != IN_INPUT) || A8;
+  // Small-batch plan, 1-row 128-wide 3x3 tiles when the grid has at most one workgroup per CU (TF_ = TF1_DBW, launch_c3):
+  // the whole next weight slab is staged into a second buffer during the current chunk (DBW) instead of the split
+  // half-slab pipeline, whose half-A DMA has only half a chunk of MFMAs to land behind. Same MFMA order, so the same
+  // bits; twice the weight LDS, so one workgroup per CU (slower once the grid exceeds the CUs: B = 4 measured -11 %)
+  static constexpr bool SMALLDB = TF_ == TF1_DBW;
+  static constexpr bool SPLIT = ((!W8 && NA < NTAP && IN != IN_INPUT) || A8) && !SMALLDB;
   // 1x1 convs: two weight slabs, chunk c+1's DMA in flight during chunk c's MFMAs (a 1x1 chunk is one tap, too
   // short to hide a weight round trip behind; the slab is 4-8 KB)
-  static constexpr bool DBW = !SPLIT && KIND == CONV1;
+  static constexpr bool DBW = (!SPLIT && KIND == CONV1) || SMALLDB;
   static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
   static constexpr int CK = A8 ? 32 : CKB / (int)sizeof(A);   // input channels per chunk
   static constexpr int ICH = 16 / (int)sizeof(A);            // channels per item (one 16-B global load)
@@ -794,8 +803,12 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 // 1-row (128-wide) / 2-row (64-wide) tiles for bf16 activations, with bf16 or fp8 weights)
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
-  if constexpr (sizeof(A) == 2)
+  if constexpr (sizeof(A) == 2) {
+    if constexpr (NT == 128 && !W8 && IN != IN_INPUT && GT_SMALL_DBW)
+      if (p.small && (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128) <= 256)   // <= one workgroup per CU
+        return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, TF1_DBW>(p, s);
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
+  }
   if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT && W8 != 2)   // (A8: 4-row tiles)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
