@@ -1,0 +1,12 @@
+#!/bin/bash
+# Latency regime (B = 1, T = 512): bench lines for bf16 and fp8 at N = 50 and a rocprofv3 kernel trace of bf16.
+set -u
+OUT=gpurun_out/b1
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+for dt in bf16 fp8; do
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --batch 1 --dtype $dt --steps 5 > $OUT/bench_$dt.json 2> $OUT/bench_$dt.err || { echo "bench $dt failed"; exit 1; }
+  python3 -c "import json; d=json.loads(open('$OUT/bench_$dt.json').read().strip().splitlines()[-1]); print('$dt B=1', round(d['value']), 'mel-frames/s', round(d['ms_per_step'],2), 'ms per decode')"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --batch 1 --steps 2 --warmup 1 > $OUT/kt.log 2>&1 || { echo "rocprof failed"; exit 1; }
+echo done
