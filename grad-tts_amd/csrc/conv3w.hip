@@ -1,0 +1,554 @@
+// Wide-tile 3x3 convolution (stride 1, pad 1) for the 128- and 256-channel U-Net levels, bf16 (gfx950).
+//
+// Covers Block.block[0] (model/diffusion.py:52) at U-Net levels 1-2 with Cin % 32 == 0 -- the convs that carry half
+// of a U-Net evaluation's FLOPs. conv_kernel (conv.hip) runs them as 128-wide, 4-wave tiles, two workgroups per CU,
+// three barriers per 16-channel chunk: the structure that tops out near 900-1100 TFLOP/s on CDNA4 (every chunk waits
+// on its own weight DMA), with the GroupNorm operand transform recomputed by both 128-channel tiles of a 256-output
+// conv and by the 7/5 halo rows. This kernel is the one-workgroup-per-CU, deep-pipelined form:
+//
+//   * 8 waves (512 threads), ONE workgroup per CU. The workgroup owns ALL output channels of its spatial tile (BN = Cout:
+//     256, 128 or 64), so every input element of the tile is loaded and (IN_GN) GroupNorm + Mish + time-bias transformed
+//     exactly once per tile; halo rows add (TR + 2) / TR (1.2x at 10 rows, 1.1x at 20).
+//   * Tile = TR mel rows x 32 frames. Wave (wn, wm) computes CB x 32 output channels x RB = 5 rows (CB x 5 accumulators
+//     of 32 x 32, v_mfma_f32_32x32x16_bf16, weights as A, positions as B -> channel x position, as conv_kernel).
+//   * K loop = phases: one phase = one tap x 32 input channels (two MFMA k-steps). A weight slot (BN rows x 32 channels,
+//     BN x 64 B) is staged by LDS DMA (global_load_lds, 1 KiB per wave instruction) into a ring of S slots, D = S - 1
+//     phases ahead; the counted `s_waitcnt vmcnt` at the top of phase k retires DMA(k+1), so each slot is visible one
+//     phase before it is read and the first fragments of phase k+1 are read during phase k (no MFMA bubble at the
+//     barrier). One barrier per phase.
+//   * The input patch ((TR + 2) x 34 positions x 32 channels) is double-buffered per 32-channel chunk: the next chunk's
+//     items are loaded into registers at phase 0 (raw buffer loads: padding / masked frames read past the end of the
+//     tensor, zeros), transformed and written one item per phase during phases 2..7, behind the MFMAs.
+//   * LDS layouts are PLANAR: 8-channel planes of 16-B entries, [plane][position] for the patch and [plane][channel] for
+//     a weight slot, so a fragment (32 consecutive positions / channels of one plane) is a contiguous 512 B: conflict-free
+//     ds_read_b128 at any tap shift, and every fragment address is one per-lane base plus a compile-time offset. The patch
+//     plane stride is 2 mod 16 entries, so the item writes (4 planes of one position per lane quad) are conflict-free too.
+//     The weight image in HBM is pre-packed in exactly the slot layout (decoder.cpp pack_conv3w): a slot is one straight
+//     DMA.
+// Epilogue: bias, GroupNorm partial sums of the output (one slot per tile, fixed-order reduction), 16-B bf16 stores, from
+// the accumulators through v_permlane32_swap (as conv_kernel).
+#include "common.h"
+#include "kernels.h"
+#include "wimage.h"
+
+namespace gt {
+
+#ifndef GT_C3W_ASM_DMA
+#define GT_C3W_ASM_DMA 1   // weight DMA by inline asm (see asm_dma16)
+#endif
+#ifndef GT_C3W_SCHED
+#define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
+#endif
+
+namespace c3w {
+constexpr int NTHR = 512, NW = 8, RB = 5, TT = 32, PCOL = TT + 2;
+
+template <int BN, int CB>
+struct Cfg {
+  static constexpr int WN = BN / (32 * CB);        // waves along output channels
+  static constexpr int WM = NW / WN;               // waves along mel rows
+  static constexpr int TR = WM * RB;               // tile rows
+  static constexpr int PR = TR + 2;                // patch rows
+  static constexpr int PP = PR * PCOL;             // patch positions
+  static constexpr int PPAD = PP + ((2 - PP % 16) + 16) % 16;   // plane stride in 16-B entries, == 2 mod 16
+  static constexpr int PLANE = PPAD * 16;
+  static constexpr int PBUF = 4 * PLANE;           // one 32-channel patch buffer
+  static constexpr int SLOT = BN * 64;             // one weight slot: BN channels x 32 input channels
+  static constexpr int PIECES = SLOT / 1024;       // DMA pieces per slot
+  static constexpr int PWMAX = (PIECES + NW - 1) / NW;
+  static constexpr int PWLO = PIECES / NW;         // pieces of waves >= PIECES % NW
+  static constexpr int S = BN == 256 ? 5 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
+  static constexpr int D = S - 1;                  // DMA issue distance in phases
+  static constexpr int ITEMS = PP * 4;             // 16-B patch items per chunk
+  static constexpr int NPT = (ITEMS + NTHR - 1) / NTHR;
+  static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
+  static constexpr int OFF_W = 2 * PBUF;
+  static constexpr int OFF_F = OFF_W + S * SLOT;   // float area
+  // floats: s_sc, s_sh, s_tb [256] each, s_bias [256], s_sub [NW][CB][4][2], s_mean, s_rstd [8]
+  static constexpr int NF = 4 * 256 + NW * CB * 8 + 16;
+  static constexpr int SMEM = OFF_F + NF * 4;
+  static_assert(WN * WM == NW && WN >= 1, "wave grid");
+  static_assert(PIECES * 1024 == SLOT, "whole DMA pieces");
+  static_assert(D >= 2 && D <= 8, "DMA distance");
+  static_assert(NPT <= 6, "items transformed in phases 2..7");
+  static_assert(SMEM <= 160 * 1024, "LDS budget: one workgroup per CU");
+  static_assert(PBUF >= 272 * 8, "s_red aliases patch buffer 1");
+};
+}  // namespace c3w
+
+typedef unsigned u32x4c_t __attribute__((ext_vector_type(4)));
+
+template <int N>
+GT_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+// counted wait that names the registers of an asm load (they are written when it retires)
+template <int N>
+GT_DEV void vm_wait_dep(u32x4c_t& x) { asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x) : "n"(N) : "memory"); }
+// LDS DMA (1 KiB per wave instruction) hidden from hipcc's waitcnt bookkeeping: hipcc models its builtin twin as an LDS
+// access too and then waits lgkmcnt(0) in front of the fragment reads that follow it. M0 is written and restored in the
+// same statement (guide §5.7).
+GT_DEV void asm_dma16(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+}
+// raw buffer load hidden from hipcc's waitcnt bookkeeping (the s_nop covers an SGPR operand written just before)
+GT_DEV void asm_buffer_load(u32x4c_t& dst, int voff, __amdgpu_buffer_rsrc_t rs, int soff) {
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+
+// IN: IN_MASK (x * mask), IN_GN ((Mish(GN(h)) + tb) * mask), IN_PLAIN. OUT: OUT_STATS.
+template <int IN, int BN, int CB>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void conv3w_kernel(ConvParams p) {
+  typedef c3w::Cfg<BN, CB> C;
+  using c3w::NTHR; using c3w::RB; using c3w::PCOL;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];   // ONE LDS object
+  float* const s_sc = reinterpret_cast<float*>(smem + C::OFF_F);
+  float* const s_sh = s_sc + 256;
+  float* const s_tb = s_sh + 256;
+  float* const s_bias = s_tb + 256;
+  float* const s_sub = s_bias + 256;
+  float* const s_mean = s_sub + c3w::NW * CB * 8;
+  float* const s_rstd = s_mean + 8;
+  double* const s_red = reinterpret_cast<double*>(smem + C::PBUF);   // patch buffer 1 is free until chunk 0, phase 2
+
+  const int F = p.Fout, T = p.Tout;
+  const int n_ft = F / C::TR, n_tt = (T + 31) / 32;
+  const int nsp = p.B * n_ft * n_tt;
+  // XCD-aware order (as conv_kernel): XCD x walks the contiguous tile range [x Q, x Q + Q)
+  int bid = (blockIdx.x & 7) * ((nsp + 7) >> 3) + (blockIdx.x >> 3);
+  if (bid >= nsp) return;   // grid padding: the whole workgroup, before any barrier
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int ft = bid % n_ft;
+  const int b = bid / n_ft;
+  const int f0 = ft * C::TR, t0 = tt * 32;
+
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wv % C::WN, wm = wv / C::WN;
+  const int q16 = tid & 3;                       // this thread's 8-channel plane inside a chunk (fixed)
+
+  // ---- prologue loads: GroupNorm slots (IN_GN), per-channel coefficients, bias, masks
+  GnLoad gl;
+  if (IN == IN_GN) gl = gn_load(p.gn_part, p.gn_nparts, b);
+  float c_g = 0.f, c_b = 0.f, c_t = 0.f;
+  if (IN == IN_GN && tid < p.Cin) {
+    c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; c_t = tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid];
+  }
+  const float c_bias = tid < BN ? p.bias[tid] : 0.f;
+
+  const int npos = p.B * F * T;
+  int pidx[C::NPT];
+  float pm[C::NPT];
+  bool frac = false;
+#pragma unroll
+  for (int j = 0; j < C::NPT; ++j) {
+    const int pp = (tid + NTHR * j) >> 2;
+    const int pr = pp / PCOL, pc = pp - pr * PCOL;
+    const int fi = f0 - 1 + pr, ti = t0 - 1 + pc;
+    const bool ok = pp < C::PP && fi >= 0 && fi < F && ti >= 0 && ti < T;
+    const float m = ok ? mask_at(p.mask, p.T0, b, ti, p.lvl_in) : 0.f;
+    int qi = ok ? (b * F + fi) * T + ti : npos;
+    if (IN == IN_MASK && m == 0.f) qi = npos;   // x * 0: the range-checked load returns zeros
+    if (IN != IN_PLAIN) frac |= (m != 0.f && m != 1.f);
+    pidx[j] = qi;
+    pm[j] = (IN == IN_PLAIN) ? (ok ? 1.f : 0.f) : m;
+  }
+  const __amdgpu_buffer_rsrc_t rs0 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * p.C0 * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(p.in1 ? p.in1 : p.in0), (short)0, npos * (p.in1 ? p.C1 : p.C0) * 2, 0x00020000);
+  const int nchunk = p.Cin / 32;
+  const int K = nchunk * 9;
+
+  // The next chunk's patch items are loaded by inline-asm buffer loads: hipcc would otherwise wait for them with a
+  // conservative vmcnt(0) (draining the weight DMAs in flight). Item j is loaded at phase j and transformed at phase
+  // j + 2, behind that phase's MFMAs, after a counted wait naming its registers (guide §5.7 form (ii)): at most three
+  // items are in registers at once.
+  u32x4c_t preg[C::NPT];
+  auto load_items = [&](int c, auto JLO, auto JHI) {   // items [JLO, JHI) of chunk c
+    const int c0 = c * 32;
+    const bool first = c0 < p.C0;
+    const int pb = (first ? p.C0 : p.C1) * 2;
+    const int so = __builtin_amdgcn_readfirstlane((first ? c0 : c0 - p.C0) * 2);
+    const __amdgpu_buffer_rsrc_t rs = first ? rs0 : rs1;
+#pragma unroll
+    for (int j = decltype(JLO)::value; j < decltype(JHI)::value && j < C::NPT; ++j) {
+      const int vo = pidx[j] * pb + q16 * 16;
+      asm_buffer_load(preg[j], vo, rs, so);
+    }
+  };
+  auto load_patch = [&](int c) {   // every item (prologue: hipcc-visible loads are fine there)
+    const int c0 = c * 32;
+    if (c0 < p.C0) {
+      const int pb = p.C0 * 2;
+#pragma unroll
+      for (int j = 0; j < C::NPT; ++j)
+        preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs0, pidx[j] * pb + q16 * 16, c0 * 2, 0);
+    } else {
+      const int pb = p.C1 * 2;
+#pragma unroll
+      for (int j = 0; j < C::NPT; ++j)
+        preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs1, pidx[j] * pb + q16 * 16, (c0 - p.C0) * 2, 0);
+    }
+  };
+  // transform item j of chunk c and write it to patch buffer `buf`. IN_GN: (Mish(GN(h)) + tb) * m in base 2 (common.h
+  // gn_mish_tb_l2), 4 channels at a time with their coefficients read from LDS right before (fewer registers live
+  // across the MFMA stream than one coefficient set per chunk)
+  auto put_item = [&](int j, int c, int buf) {
+    const int pp = (tid + NTHR * j) >> 2;
+    if (C::NPT * NTHR != C::ITEMS && pp >= C::PP) return;
+    u32x4c_t v4 = preg[j];
+    if (IN == IN_GN) {
+      float v[8];
+      item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
+      const int ch = c * 32 + q16 * 8;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(s_sc + ch + 4 * u);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(s_sh + ch + 4 * u);
+        const f32x4 tb = *reinterpret_cast<const f32x4*>(s_tb + ch + 4 * u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * u + k] = gn_mish_tb_l2(v[4 * u + k], sc[k], sh[k], tb[k]);
+      }
+      if (frac) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= pm[j];
+      }
+      const uint4 o = f_to_item(v, bf16());
+      const bool z = !frac && pm[j] == 0.f;
+      v4 = u32x4c_t{z ? 0u : o.x, z ? 0u : o.y, z ? 0u : o.z, z ? 0u : o.w};
+    } else if (IN == IN_MASK) {
+      if (frac) {
+        float v[8];
+        item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= pm[j];
+        const uint4 o = f_to_item(v, bf16());
+        v4 = u32x4c_t{o.x, o.y, o.z, o.w};
+      }
+    }
+    *reinterpret_cast<u32x4c_t*>(smem + buf * C::PBUF + q16 * C::PLANE + pp * 16) = v4;
+  };
+
+  // weight DMA: slot of phase k = image bytes [k SLOT, (k+1) SLOT) (decoder.cpp pack_conv3w). Every wave issues PW
+  // pieces per slot (BN = 64: 4 pieces; waves 4..7 repeat waves 0..3's, same bytes to the same LDS), so the counted
+  // waits below are the same in every wave.
+  constexpr int PW = C::PIECES >= c3w::NW ? C::PIECES / c3w::NW : 1;
+  static_assert(C::PIECES % c3w::NW == 0 || c3w::NW % C::PIECES == 0, "pieces split evenly");
+  const char* const wimg = reinterpret_cast<const char*>(p.w);
+  const unsigned lds_base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem));
+  auto dma = [&](int k, int slot) {
+    const char* src = wimg + (long)k * C::SLOT + lane * 16;
+    char* dst = smem + C::OFF_W + slot * C::SLOT;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int piece = C::PIECES >= c3w::NW ? wv + c3w::NW * i : wv % C::PIECES;
+      if (GT_C3W_ASM_DMA)
+        asm_dma16(src + piece * 1024, lds_base + C::OFF_W + slot * C::SLOT + piece * 1024);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024),
+                                         (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+    }
+  };
+  // items of the next chunk loaded at phases in [lo, hi] (item j at phase j)
+  constexpr auto n_lp = [](int lo, int hi) {
+    int n = 0;
+    for (int j = 0; j < C::NPT; ++j) n += (j >= lo && j <= hi) ? 1 : 0;
+    return n;
+  };
+  // top of phase (t = tap, MORE: chunk c+1 exists): retire DMA(k+1). Younger VMEM ops of this wave: the DMAs of phases
+  // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
+  // DMA of their phase).
+  auto top_wait = [&](auto Tc, auto MOREc) {
+    constexpr int t = decltype(Tc)::value;
+    constexpr bool MORE = decltype(MOREc)::value;
+    constexpr int ndma = MORE ? C::D - 2 : ((7 - t) < (C::D - 2) ? ((7 - t) > 0 ? 7 - t : 0) : C::D - 2);
+    constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
+    vm_wait<ndma * PW + npl>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  // before transforming item j at phase j + 2: younger VMEM ops are items j+1, j+2 (loaded at phases j+1, j+2) and the
+  // DMAs of phases j+1, j+2
+  auto item_wait = [&](auto Jc) {
+    constexpr int j = decltype(Jc)::value;
+    constexpr int n = (C::NPT - 1 - j < 2 ? C::NPT - 1 - j : 2) + 2 * PW;
+    vm_wait_dep<n>(preg[j]);
+  };
+
+  // ---- fragments. A (weights): slot + plane (2s + h) x BN + channel; B (patch): buffer + plane (2s + h) + position.
+  const int a_lane = C::OFF_W + (h * BN + wn * 32 * CB + r) * 16;
+  const int b_lane = h * C::PLANE + (wm * RB * PCOL + r) * 16;
+  auto rd_a = [&](int slot, int s, int cb) {
+    return *reinterpret_cast<const bf16x8*>(smem + a_lane + slot * C::SLOT + (2 * s * BN + cb * 32) * 16);
+  };
+  auto rd_b = [&](int buf, int t, int s, int rb) {
+    const int dr = t / 3, dc = t % 3;
+    return *reinterpret_cast<const bf16x8*>(smem + b_lane + buf * C::PBUF + 2 * s * C::PLANE +
+                                            ((rb + dr) * PCOL + dc) * 16);
+  };
+
+  f32x16 acc[RB][CB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int j = 0; j < CB; ++j)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+
+  // ---- prologue: chunk 0 patch loads, then the first D weight slots, then the GroupNorm reduction
+  load_patch(0);
+#pragma unroll
+  for (int k = 0; k < C::D; ++k)
+    if (k < K) dma(k, k);
+  if (IN == IN_GN) {
+    gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
+    if (tid < p.Cin) {
+      const int g = tid / (p.Cin >> 3);
+      const float sc = c_g * s_rstd[g];
+      s_sc[tid] = sc * kLog2e; s_sh[tid] = (c_b - s_mean[g] * sc) * kLog2e; s_tb[tid] = c_t;
+    }
+  }
+  if (tid < BN) s_bias[tid] = c_bias;
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < C::NPT; ++j) put_item(j, 0, 0);
+  vm_wait<(C::D - 2) * PW>();   // DMA(0), DMA(1) landed (younger: DMA(2 .. D-1)); chunk 0's patch written
+  lds_barrier();
+
+  // MFMA steps i = s * RB + rb of a phase; fragments are read two steps ahead (B: ring of 3 by the chunk-global step
+  // index, a chunk being 90 steps; A: one register set per k-step s), across phase boundaries too: phase k+1's slot and
+  // patch are visible from the top of phase k.
+  bf16x8 fa[2][CB], fb[3];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(0, 0, cb);
+  fb[0] = rd_b(0, 0, 0, 0);
+  fb[1] = rd_b(0, 0, 0, 1);
+
+  int slot = 0;   // weight slot of the current phase (k mod S)
+  // One chunk: 9 phases. MORE: a chunk c+1 exists (its patch is loaded and written during this chunk).
+  auto chunk = [&](int c, auto MOREc) {
+    constexpr bool MORE = decltype(MOREc)::value;
+    const int cur = c & 1, nxt = cur ^ 1;
+    const int k0 = c * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int k = k0 + t;
+      // (a) DMA(k+1) landed for every wave, every read of phase k-1 done
+      switch (t) {   // compile-time t for the wait immediates
+        case 0: top_wait(std::integral_constant<int, 0>{}, MOREc); break;
+        case 1: top_wait(std::integral_constant<int, 1>{}, MOREc); break;
+        case 2: top_wait(std::integral_constant<int, 2>{}, MOREc); break;
+        case 3: top_wait(std::integral_constant<int, 3>{}, MOREc); break;
+        case 4: top_wait(std::integral_constant<int, 4>{}, MOREc); break;
+        case 5: top_wait(std::integral_constant<int, 5>{}, MOREc); break;
+        case 6: top_wait(std::integral_constant<int, 6>{}, MOREc); break;
+        case 7: top_wait(std::integral_constant<int, 7>{}, MOREc); break;
+        default: top_wait(std::integral_constant<int, 8>{}, MOREc); break;
+      }
+      // (b) DMA of phase k + D into the slot phase k - 1 used
+      if (MORE || t + C::D < 9) {
+        int ds = slot + C::D;
+        ds = ds >= C::S ? ds - C::S : ds;
+        dma(k + C::D, ds);
+      }
+      int nslot = slot + 1;
+      nslot = nslot == C::S ? 0 : nslot;
+      // (c) the next chunk's patch item of this phase (item t)
+      if (MORE) {
+        if (t < C::NPT) {
+          switch (t) {
+            case 0: load_items(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}); break;
+            case 1: load_items(c + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}); break;
+            case 2: load_items(c + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{}); break;
+            case 3: load_items(c + 1, std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{}); break;
+            case 4: load_items(c + 1, std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{}); break;
+            default: load_items(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 6>{}); break;
+          }
+        }
+      }
+      // (d) MFMAs of phase k
+#pragma unroll
+      for (int i = 0; i < C::NS; ++i) {
+        const int s = i / RB, rb = i % RB;
+        const int g = t * C::NS + i;          // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
+        const int n = i + 2;                  // step whose fragments are read now
+        int nrd = 0;
+        if (n < C::NS) {
+          const int s1 = n / RB, rb1 = n % RB;
+          if (rb1 == 0) {
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) fa[s1 & 1][cb] = rd_a(slot, s1, cb);
+            nrd += CB;
+          }
+          fb[(g + 2) % 3] = rd_b(cur, t, s1, rb1);
+          nrd += 1;
+        } else if (MORE || t < 8) {           // phase k+1's steps 0 and 1
+          const int rb1 = n - C::NS;
+          if (rb1 == 0) {
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(nslot, 0, cb);
+            nrd += CB;
+          }
+          fb[(g + 2) % 3] = t < 8 ? rd_b(cur, t + 1, 0, rb1) : rd_b(nxt, 0, 0, rb1);
+          nrd += 1;
+        }
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][cb], fb[g % 3], acc[rb][cb], 0, 0, 0);
+        if (GT_C3W_SCHED) {
+          if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
+          else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
+        }
+        // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
+        if (MORE && i == 3 && t >= 2 && t - 2 < C::NPT) {
+          switch (t - 2) {
+            case 0: item_wait(std::integral_constant<int, 0>{}); break;
+            case 1: if constexpr (C::NPT > 1) item_wait(std::integral_constant<int, 1>{}); break;
+            case 2: if constexpr (C::NPT > 2) item_wait(std::integral_constant<int, 2>{}); break;
+            case 3: if constexpr (C::NPT > 3) item_wait(std::integral_constant<int, 3>{}); break;
+            case 4: if constexpr (C::NPT > 4) item_wait(std::integral_constant<int, 4>{}); break;
+            default: if constexpr (C::NPT > 5) item_wait(std::integral_constant<int, 5>{}); break;
+          }
+          put_item(t - 2, c + 1, nxt);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      slot = nslot;
+    }
+  };
+  int c = 0;
+  for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
+  chunk(c, std::false_type{});
+
+  // ---- epilogue: bias, GroupNorm partial sums, 16-B stores (lane (r, h) of block (rb, cb) holds channels
+  // cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r; v_permlane32_swap leaves it 8 consecutive channels)
+  float gs[CB][2], gq[CB][2];
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb) { gs[cb][0] = gs[cb][1] = gq[cb][0] = gq[cb][1] = 0.f; }
+  bf16* out = reinterpret_cast<bf16*>(p.out);
+  const int tcol = t0 + r;
+  const bool valid = tcol < T;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int frow = f0 + wm * RB + rb;
+    const long ob = (((long)b * F + frow) * T + tcol) * BN;
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = acc[rb][cb][q];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]),
+                                                           __float_as_uint(v[8 * pr + 4 + q]), false, false);
+          v[8 * pr + q] = __uint_as_float(sw[0]);
+          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int cl = wn * 32 * CB + cb * 32 + pr * 16 + 8 * h;
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
+        float o[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] + b1[k]; }
+        if (valid) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            gs[cb][pr] += o[k]; gq[cb][pr] += o[k] * o[k];
+            asm volatile("" : "+v"(gs[cb][pr]), "+v"(gq[cb][pr]));   // scalar chains (conv.hip, packed-FP32 hazard)
+          }
+          *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(o, bf16());
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const float s = half_sum32(gs[cb][pr]), q = half_sum32(gq[cb][pr]);
+      if (r == 0) {
+        s_sub[((wv * CB + cb) * 4 + pr * 2 + h) * 2 + 0] = s;
+        s_sub[((wv * CB + cb) * 4 + pr * 2 + h) * 2 + 1] = q;
+      }
+    }
+  lds_barrier();
+  if (tid < 8) {   // per GroupNorm group, over waves and 8-channel sub-groups in a fixed order: one slot per tile
+    const int gshift = __builtin_ctz(BN >> 3);
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w = 0; w < c3w::NW; ++w)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int g8 = 0; g8 < 4; ++g8) {
+          const int co = (w % C::WN) * 32 * CB + cb * 32 + g8 * 8;
+          if ((co >> gshift) == tid) {
+            S += s_sub[((w * CB + cb) * 4 + g8) * 2 + 0];
+            Q += s_sub[((w * CB + cb) * 4 + g8) * 2 + 1];
+          }
+        }
+    const int nparts = n_ft * n_tt;
+    float* dst = p.out_part + ((long)b * nparts + ft * n_tt + tt) * 16 + tid * 2;
+    dst[0] = S;
+    dst[1] = Q;
+  }
+}
+
+// (BN, CB) of a conv on an F-row grid with Cout outputs, or 0 if conv3w does not cover it
+static int c3w_cfg(int Cout, int F) {
+  if (Cout == 256 && F % 10 == 0) return 1;    // <256, 2>: 10-row tiles (level 2)
+  if (Cout == 128 && F % 20 == 0 && F >= 40) return 2;   // <128, 2>: 20-row tiles (level 1)
+  if (Cout == 128 && F % 10 == 0) return 3;    // <128, 1>: 10-row tiles (level 2)
+  if (Cout == 64 && F % 20 == 0 && F >= 40) return 4;    // <64, 1>: 20-row tiles (level 1)
+  return 0;
+}
+static int c3w_rows(int cfg) { return (cfg == 1 || cfg == 3) ? 10 : 20; }
+
+bool conv3w_eligible(const ConvParams& p, InMode im) {
+  if (im != IN_MASK && im != IN_GN && im != IN_PLAIN) return false;
+  if (p.small || p.wscale || p.w_bstride || p.Fin != p.Fout || p.Tin != p.Tout) return false;
+  if (p.Cin % 32 || p.C0 % 32 || (p.in1 && p.C1 % 32) || p.Cin_pad != p.Cin || p.Cin != p.C0 + (p.in1 ? p.C1 : 0)) return false;
+  if (im == IN_GN && p.Cin > 256) return false;
+  if (!c3w_cfg(p.Cout, p.Fout)) return false;
+  return (long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * 2 < (1L << 31);
+}
+
+int conv3w_nparts(int F, int T, int Cout) {
+  const int cfg = c3w_cfg(Cout, F);
+  return cfg ? (F / c3w_rows(cfg)) * ((T + 31) / 32) : 0;
+}
+
+template <int IN, int BN, int CB>
+static hipError_t launch_c3w_t(const ConvParams& p, hipStream_t s) {
+  typedef c3w::Cfg<BN, CB> C;
+  if (p.Fout % C::TR || p.Cout != BN) return hipErrorInvalidValue;
+  const long nsp = (long)p.B * (p.Fout / C::TR) * ((p.Tout + 31) / 32);
+  hipLaunchKernelGGL((conv3w_kernel<IN, BN, CB>), dim3((unsigned)(8 * ((nsp + 7) / 8))), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+template <int BN, int CB>
+static hipError_t launch_c3w_in(InMode im, const ConvParams& p, hipStream_t s) {
+  if (im == IN_MASK) return launch_c3w_t<IN_MASK, BN, CB>(p, s);
+  if (im == IN_GN) return launch_c3w_t<IN_GN, BN, CB>(p, s);
+  if (im == IN_PLAIN) return launch_c3w_t<IN_PLAIN, BN, CB>(p, s);
+  return hipErrorNotSupported;
+}
+
+hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s) {
+  if (!conv3w_eligible(p, im)) return hipErrorInvalidValue;
+  switch (c3w_cfg(p.Cout, p.Fout)) {
+    case 1: return launch_c3w_in<256, 2>(im, p, s);
+    case 2: return launch_c3w_in<128, 2>(im, p, s);
+    case 3: return launch_c3w_in<128, 1>(im, p, s);
+    case 4: return launch_c3w_in<64, 1>(im, p, s);
+  }
+  return hipErrorNotSupported;
+}
+
+}  // namespace gt

@@ -177,13 +177,16 @@ struct gt_decoder {
   // bf16 calls on at most small_b utterances run the small-batch tile plan (small_plan below);
   // GT_SMALL_B at creation or gt_decoder_set_small_batch
   int64_t small_b = kSmallB;
+  // bf16 throughput-plan 3x3 convs at levels 1-2 on conv3w (one 8-wave workgroup per CU owning all output channels of
+  // a tile); GT_CONV3W=0 at creation or gt_decoder_set_wide_conv(dec, 0) runs them on conv_kernel
+  bool wide = true;
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
   // gt_decoder_set_params_device wrote the fp32 block on the device: the host copies (and every weight image
   // packed from them) are stale until refresh_host() reads the block back
   bool host_stale = false;
-  hipStream_t dev_stream = nullptr;
+  hipEvent_t dev_done = nullptr;   // recorded on the caller's stream by set_params_device (refresh_host waits on it)
   float* raw = nullptr;
   std::vector<int64_t> raw_off;
   int64_t raw_numel = 0;
@@ -384,6 +387,20 @@ void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w
   blob.put(key, img.data(), img.size() * 2);
 }
 
+// pack a 3x3 [Cout][Cin][3][3] weight (Cin % 32 == 0) in conv3w's slot order (conv3w.hip), bf16: one slot per
+// (32-channel chunk c, tap t) in phase order k = 9 c + t, each [plane q 0..3][co][8 channels 32 c + 8 q ..] -- the LDS
+// image of a weight slot, so staging one is a straight DMA
+void pack_conv3w(Blob& blob, const std::string& key, const std::vector<float>& w, int cout, int cin) {
+  std::vector<uint16_t> img((size_t)(cin / 32) * 9 * cout * 32);
+  size_t i = 0;
+  for (int c = 0; c < cin / 32; ++c)
+    for (int t = 0; t < 9; ++t)
+      for (int q = 0; q < 4; ++q)
+        for (int co = 0; co < cout; ++co)
+          for (int e = 0; e < 8; ++e) img[i++] = f2bf(w[((size_t)co * cin + 32 * c + 8 * q + e) * 9 + t]);
+  blob.put(key, img.data(), img.size() * 2);
+}
+
 // e4m3 values (codes decoded, without the scale) of a [rows][...] weight quantized per row as gt_quantize_e4m3 does:
 // exact in bf16, for the conv64 image of an fp8-weight conv (the scale is applied in conv64's epilogue)
 std::vector<float> e4m3_values(const std::vector<float>& w, int rows) {
@@ -439,6 +456,9 @@ int prepare(gt_decoder* d, int code) {
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
       if (c64) pack_conv64(blob, k + ".w64", w);
+      if (code == GT_BF16 && ends_with(k, ".block.0.weight") && !c64 && shp[2] == 3 && shp[3] == 3 && shp[1] % 32 == 0 &&
+          (shp[0] == 64 || shp[0] == 128 || shp[0] == 256))
+        pack_conv3w(blob, k + ".w3w", w, (int)shp[0], (int)shp[1]);
       if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
@@ -522,6 +542,7 @@ int max_gn_parts(int dt, int64_t T) {
     for (int small = 0; small < 2; ++small) {
       if (small && !dt) continue;
       m = std::max(m, conv64_nparts(80 >> l, (int)(T >> l), small));
+      for (int cout : {64, 128, 256}) m = std::max(m, conv3w_nparts(80 >> l, (int)(T >> l), cout));
       for (int cout : {64, 128, 256})
         for (int im : {IN_INPUT, IN_MASK, IN_GN, IN_PLAIN})
           for (int a8 = 0; a8 <= dt; ++a8)   // fp8-operand convs (GT_FP8) tile differently
@@ -622,6 +643,18 @@ struct Run {
       timed(std::string("conv64_kernel<") + std::to_string((int)im) + (p.wscale ? ",w8" : "") + ">@64x64x" +
                 std::to_string(p.Fout),
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
+      return np;
+    }
+    if (dt && wi == GT_BF16 && d->wide && conv3w_eligible(p, im) && d->dp[wi].count(wkey + ".w3w")) {
+      p.w = W(wkey + ".w3w");
+      const int np = conv3w_nparts(p.Fout, p.Tout, p.Cout);
+      if (np <= 0 || np > L.pmax) { chk(hipErrorInvalidValue); return np; }
+      const double pos = (double)p.B * p.Fout * p.Tout;
+      const int cb = (p.Cout == 256 || (p.Cout == 128 && p.Fout % 20 == 0 && p.Fout >= 40)) ? 2 : 1;
+      timed(std::string("conv3w_kernel<") + std::to_string((int)im) + "," + std::to_string(p.Cout) + "," +
+                std::to_string(cb) + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout),
+            2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + 9.0 * p.Cin * p.Cout * 2,
+            [&] { return launch_conv3w(im, p, s); });
       return np;
     }
     const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
@@ -956,6 +989,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_GRAPHS")) d->graphs = atoi(e) != 0;
   if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
   if (const char* e = getenv("GT_SMALL_B")) d->small_b = atoll(e);
+  if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
   *out = d;
   return GT_OK;
 }
@@ -966,6 +1000,7 @@ void gt_decoder_destroy(gt_decoder* d) {
   if (d->cap_stream) (void)hipStreamDestroy(d->cap_stream);
   if (d->raw) (void)hipFree(d->raw);
   for (auto e : d->pool) (void)hipEventDestroy(e);
+  if (d->dev_done) (void)hipEventDestroy(d->dev_done);
   for (int i = 0; i < gt_decoder::kCodes; ++i)
     if (d->arena[i]) (void)hipFree(d->arena[i]);
   delete d;
@@ -1135,7 +1170,8 @@ float gt_internal_host_scalar(gt_decoder* d, const std::string& name) {
 // image, a host scalar or a host-side parameter change needs them)
 int gt_internal_refresh_host(gt_decoder* d) {
   if (!d->host_stale) return GT_OK;
-  if (hipStreamSynchronize(d->dev_stream) != hipSuccess) return fail(GT_ERR_HIP, "hipStreamSynchronize failed");
+  // the update's own completion event, not its stream: the caller may have destroyed the stream since
+  if (d->dev_done && hipEventSynchronize(d->dev_done) != hipSuccess) return fail(GT_ERR_HIP, "hipEventSynchronize failed");
   std::vector<float> h((size_t)d->raw_numel);
   if (hipMemcpy(h.data(), d->raw, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     return fail(GT_ERR_HIP, "hipMemcpy(raw params -> host) failed");
@@ -1151,9 +1187,11 @@ int gt_decoder_set_params_device(gt_decoder* d, const float* params, int64_t num
   if (numel != d->raw_numel) return fail(GT_ERR_ARG, "numel != gt_decoder_grad_numel");
   const hipError_t e = launch_copy_f32(d->raw, params, (long)numel, (hipStream_t)stream);
   if (e != hipSuccess) return fail(GT_ERR_HIP, std::string("parameter copy: ") + hipGetErrorString(e));
+  if (!d->dev_done && hipEventCreateWithFlags(&d->dev_done, hipEventDisableTiming) != hipSuccess)
+    return fail(GT_ERR_HIP, "hipEventCreate failed");
+  if (hipEventRecord(d->dev_done, (hipStream_t)stream) != hipSuccess) return fail(GT_ERR_HIP, "hipEventRecord failed");
   for (bool& x : d->dirty) x = true;
   d->host_stale = true;
-  d->dev_stream = (hipStream_t)stream;
   return GT_OK;
 }
 const float* gt_internal_freqs(gt_decoder* d) { return d->raw + d->raw_numel; }
@@ -1390,6 +1428,13 @@ int gt_decoder_set_betas(gt_decoder* d, float beta_min, float beta_max) {
     d->beta_min = beta_min; d->beta_max = beta_max;
     d->drop_graphs();   // captured sampler graphs hold the old beta table
   }
+  return GT_OK;
+}
+
+int gt_decoder_set_wide_conv(gt_decoder* d, int on) {
+  if (!d) return fail(GT_ERR_ARG, "null decoder");
+  d->wide = on != 0;
+  d->drop_graphs();
   return GT_OK;
 }
 

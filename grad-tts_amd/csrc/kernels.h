@@ -114,4 +114,11 @@ int conv64_nparts(int F, int T, int small);
 bool conv64_eligible(const ConvParams& p);
 hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s);
 
+// wide-tile 3x3 conv for the 64/128/256-output convs of levels 1-2, bf16, throughput plan (conv3w.hip): one 8-wave
+// workgroup per CU owns all output channels of a tile; weight image decoder.cpp pack_conv3w (key ".w3w"). GroupNorm
+// partial slots: one per tile (conv3w_nparts, 0 if the shape is not covered). GT_CONV3W=0 disables it.
+bool conv3w_eligible(const ConvParams& p, InMode im);
+int conv3w_nparts(int F, int T, int Cout);
+hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s);
+
 }  // namespace gt

@@ -38,7 +38,11 @@ struct gt_text_encoder {
   RepackEntry* devtab = nullptr;
   int ntab = 0;
   bool host_stale = false;
-  hipStream_t dev_stream = nullptr;
+  hipEvent_t dev_done = nullptr;   // recorded on the caller's stream by set_params_device (refresh_host waits on it)
+  // parameter generation: bumped by every host or device parameter change; forward_train records it per tape (keyed by
+  // the workspace base) and backward refuses a tape taken under other parameters
+  uint64_t gen = 0;
+  std::map<const void*, uint64_t> tape_gen;
 };
 
 namespace {
@@ -174,6 +178,7 @@ void gt_text_encoder_destroy(gt_text_encoder* e) {
   if (e->devtab) (void)hipFree(e->devtab);
   if (e->dev) (void)hipFree(e->dev);
   if (e->devpk) (void)hipFree(e->devpk);
+  if (e->dev_done) (void)hipEventDestroy(e->dev_done);
   delete e;
 }
 
@@ -188,7 +193,8 @@ int64_t gt_text_encoder_param_numel(gt_text_encoder* e, int i) {
 // host copies <- the device block after gt_text_encoder_set_params_device (only when a host-side change needs them)
 static int refresh_host(gt_text_encoder* e) {
   if (!e->host_stale) return GT_OK;
-  if (hipStreamSynchronize(e->dev_stream) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipStreamSynchronize failed");
+  // the update's own completion event, not its stream: the caller may have destroyed the stream since
+  if (e->dev_done && hipEventSynchronize(e->dev_done) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipEventSynchronize failed");
   std::vector<float> h((size_t)e->numel);
   if (hipMemcpy(h.data(), e->dev, h.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
     return gt_internal_fail(GT_ERR_HIP, "hipMemcpy failed");
@@ -206,6 +212,7 @@ int gt_text_encoder_set_param(gt_text_encoder* e, const char* name, const float*
   e->host[it->second].assign(data, data + numel);
   e->set[it->second] = true;
   e->dirty = true;
+  e->gen += 1;
   return GT_OK;
 }
 
@@ -217,8 +224,11 @@ int gt_text_encoder_set_params_device(gt_text_encoder* e, const float* params, i
   hipError_t err = launch_copy_f32(e->dev, params, (long)numel, s);
   if (err == hipSuccess) err = launch_tt_repack(e->dev, e->devtab, e->ntab, e->devpk, s);
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("parameter update: ") + hipGetErrorString(err));
+  if (!e->dev_done && hipEventCreateWithFlags(&e->dev_done, hipEventDisableTiming) != hipSuccess)
+    return gt_internal_fail(GT_ERR_HIP, "hipEventCreate failed");
+  if (hipEventRecord(e->dev_done, s) != hipSuccess) return gt_internal_fail(GT_ERR_HIP, "hipEventRecord failed");
   e->host_stale = true;
-  e->dev_stream = s;
+  e->gen += 1;
   return GT_OK;
 }
 
@@ -518,6 +528,8 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
   }
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder training forward: ") + hipGetErrorString(err));
   if (bad_ptr) return gt_internal_fail(GT_ERR_WORKSPACE, "text encoder training forward: tape offset outside the layout");
+  if (e->tape_gen.size() >= 256 && !e->tape_gen.count(base)) e->tape_gen.erase(e->tape_gen.begin());
+  e->tape_gen[base] = e->gen;
   return GT_OK;
 }
 
@@ -528,9 +540,14 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   if (B <= 0 || T <= 0 || T > TT_TMAX) return gt_internal_fail(GT_ERR_ARG, "bad B / T");
   const TrWs w = tr_layout(e, B, T);
   if (workspace_bytes < w.total) return gt_internal_fail(GT_ERR_WORKSPACE, "workspace too small");
-  if (e->dirty) return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
   hipStream_t s = (hipStream_t)stream;
   char* base = (char*)(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  {
+    const auto it = e->tape_gen.find(base);
+    if (it == e->tape_gen.end()) return gt_internal_fail(GT_ERR_ARG, "backward: no forward_train tape in this workspace");
+    if (e->dirty || it->second != e->gen)
+      return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
+  }
   const size_t usable = workspace_bytes - (size_t)(base - (char*)workspace);
   bool bad_ptr = false;
   auto F = [&](size_t o) { return tape_ptr(w, base, o, usable, bad_ptr); };   // o: byte offset (tr_layout)

@@ -610,6 +610,11 @@ hipError_t launch_tt_emb_bwd(const int64_t* tokens, long npos, const float* dx0,
   if (C > 256) return hipErrorInvalidValue;
   const long n = (long)n_vocab * C;
   const int ns = (int)std::max(1L, std::min(std::min(32L, (npos + 127) / 128), part_floats / n));
+  if (ns == 1) {   // one position split (short inputs, or a vocabulary whose n_vocab x C exceeds the partials): straight
+                   // into demb, as launch_tt_wgrad does -- never more than part_floats into the partials
+    hipLaunchKernelGGL(tt_emb_bwd_kernel, dim3(n_vocab, 1), dim3(256), 0, s, tokens, npos, dx0, C, scale, n_vocab, demb);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(tt_emb_bwd_kernel, dim3(n_vocab, ns), dim3(256), 0, s, tokens, npos, dx0, C, scale, n_vocab, part);
   hipLaunchKernelGGL(tt_sum_splits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, part, ns, n, demb);
   return hipGetLastError();

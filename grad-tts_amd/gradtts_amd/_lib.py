@@ -43,6 +43,7 @@ SIGNATURES = [
     ("gt_decoder_set_graphs", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_graph_captures", _c.c_int64, [_c.c_void_p]),
     ("gt_decoder_set_small_batch", _c.c_int, [_c.c_void_p, _c.c_int64]),
+    ("gt_decoder_set_wide_conv", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_profile_enable", _c.c_int, [_c.c_void_p, _c.c_int]),
     ("gt_decoder_profile_read", _c.c_int, [_c.c_void_p, _c.c_char_p, _c.c_size_t]),
     ("gt_decoder_profile_filter", _c.c_int, [_c.c_void_p, _c.c_char_p]),

@@ -242,7 +242,8 @@ class _TextEncoderTrain(torch.autograd.Function):
             n = int(np.prod(shp)) if len(shp) else 1
             out.append(grads[off:off + n].view(shp))
             off += n
-        ctx.ws = None
+        # the tape stays in ctx.ws until autograd frees ctx: backward only writes the workspace's scratch pieces, so a
+        # second backward through the same graph (retain_graph=True) differentiates the same tape again
         return (None, None, None, None, None, None, None, *out)
 
 

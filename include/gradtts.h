@@ -109,6 +109,11 @@ int64_t gt_decoder_graph_captures(const gt_decoder* dec);
  * use 1-/2-row conv tiles and (GT_BF16) one-tile conv64 segments, so a single utterance fills the GPU (latency). Default 4. Each plan
  * is batch-invariant on its own; across plans results agree to fp32 rounding of the GroupNorm sums. 0 disables. */
 int gt_decoder_set_small_batch(gt_decoder* dec, int64_t max_b);
+/* Wide-tile 3x3 convs (default on; env GT_CONV3W=0 at creation turns them off): GT_BF16 throughput-plan calls run the
+ * level-1/2 Block convs (model/diffusion.py:52; Cout 64/128/256, Cin % 32 == 0) as one 8-wave workgroup per CU that owns
+ * every output channel of a 10- or 20-row x 32-frame tile (csrc/conv3w.hip). Off: the 128-wide conv_kernel tiles. The
+ * two agree to fp32 accumulation order (different K order and GroupNorm partition). */
+int gt_decoder_set_wide_conv(gt_decoder* dec, int on);
 
 /* Batches of any size: a compute call runs the batch in chunks of at most
  * floor((2^31 - 1) / (80 * T * 64 * element_size)) utterances (the kernels' 32-bit buffer ranges), each a

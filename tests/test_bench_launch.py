@@ -49,3 +49,25 @@ def test_bench_single_rank_dry_run():
 def test_bench_world_size_mismatch_is_an_error():
     r = _run([sys.executable, "bench.py", "--gpus", "2", *SMALL], WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_external_launcher_without_gpus_flag():
+    """`torchrun --nproc-per-node 2 bench.py` with no --gpus: the world size comes from WORLD_SIZE."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    d = _line(_run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", *SMALL]))
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
+
+
+def test_launcher_parent_makes_no_hip_call():
+    """The self-launching parent must not touch the HIP runtime (not even a device count): its launch path is plain
+    subprocess plumbing. Checked on the source of launch_ranks and of main() up to the launch."""
+    import inspect
+    sys.path.insert(0, REPO)
+    import bench
+    src = inspect.getsource(bench.launch_ranks)
+    head = inspect.getsource(bench.main).split("launch_ranks(args)")[0]
+    for s in (src, head):
+        assert "torch.cuda" not in s and "_lib." not in s

@@ -269,3 +269,72 @@ def test_two_taped_forwards_before_backward():
     apart = [p.grad.detach().clone() for p in m.parameters()]
     for a, b in zip(together, apart):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+
+
+def _encoder_inputs(seed, lengths, n_vocab=149):
+    rng = np.random.default_rng(seed)
+    tokens = rng.integers(0, n_vocab, size=(len(lengths), max(lengths))).astype(np.int64)
+    return torch.from_numpy(tokens).cuda(), torch.tensor(lengths).cuda()
+
+
+def test_encoder_retain_graph_second_backward():
+    """A second backward through the same graph (retain_graph=True) differentiates the same tape again and gives the
+    same gradients, as the reference's autograd does (the tape stays alive until autograd frees the graph)."""
+    enc = make_gradtts().encoder.eval()
+    tokens, lengths = _encoder_inputs(9, [21, 13])
+    mu, logw, _ = enc(tokens, lengths)
+    loss = mu.square().sum() + logw.sum()
+    loss.backward(retain_graph=True)
+    g1 = [p.grad.detach().clone() for p in enc.parameters()]
+    enc.zero_grad(set_to_none=True)
+    loss.backward()
+    g2 = [p.grad.detach().clone() for p in enc.parameters()]
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+
+
+def test_encoder_backward_refuses_parameters_changed_on_device():
+    """A device-side parameter update (gt_text_encoder_set_params_device, as after an optimizer step) between the
+    taped forward and its backward: the tape holds activations of the old weights, so the backward must fail with
+    GT_ERR_PARAM instead of returning silently wrong gradients."""
+    from gradtts_amd import _lib
+    from gradtts_amd.diffusion import _stream_ptr
+    enc = make_gradtts().encoder.eval()
+    tokens, lengths = _encoder_inputs(10, [17, 9])
+    mu, logw, _ = enc(tokens, lengths)
+    loss = mu.sum() + logw.sum()
+    L = _lib.lib()
+    h = enc._native()
+    named = dict(enc.named_parameters())
+    names = [L.gt_text_encoder_param_name(h, i).decode() for i in range(L.gt_text_encoder_num_params(h))]
+    flat = torch.cat([named[n].detach().reshape(-1) for n in names]) * 1.01
+    _lib.check(L.gt_text_encoder_set_params_device(h, flat.data_ptr(), flat.numel(), _stream_ptr(flat.device)),
+               "gt_text_encoder_set_params_device")
+    with pytest.raises(_lib.GradTTSError, match="parameters changed"):
+        loss.backward()
+
+
+def test_text_encoder_large_vocabulary_embedding_gradient():
+    """n_vocab x C above the backward's 8 M-float partial buffer (C = 192: n_vocab > 43,690, e.g. a BPE vocabulary):
+    the embedding gradient goes straight into the gradient buffer instead of past the partials. Checked elementwise
+    on the rows of the tokens used (ids up to 44,999) against fp64 autograd through the oracle."""
+    from oracle import text_encoder as ote
+    from gradtts_amd.text_encoder import TextEncoder
+    nv = 45000
+    enc = TextEncoder(nv, 80, 192, 768, 256, 2, 6, 3, 0.1, 4)
+    sd = synthetic_text_encoder_state_dict(5, n_vocab=nv)
+    enc.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    enc = enc.cuda().eval()
+    lengths = [19, 12]
+    tokens, lens = _encoder_inputs(11, lengths, nv)
+    tokens[0, :3] = torch.tensor([nv - 1, 43691, 0])
+    mu, logw, _ = enc(tokens, lens)
+    (mu.sum() + 0.5 * logw.sum()).backward()
+    p = {k: torch.as_tensor(v).double().requires_grad_() for k, v in sd.items()}
+    rmu, rlw, _ = ote.text_encoder(p, tokens.cpu(), lens.cpu())
+    (rmu.sum() + 0.5 * rlw.sum()).backward()
+    used = torch.unique(tokens.cpu()).numpy()
+    ours = enc.emb.weight.grad.detach().cpu().numpy()[used]
+    ref = p["emb.weight"].grad.numpy()[used]
+    report("large-vocabulary embedding gradient (n_vocab 45000)", rel_err(ours, ref), 5e-5)
+    unused = np.setdiff1d(np.arange(nv), used)
+    assert not np.any(enc.emb.weight.grad.detach().cpu().numpy()[unused])
