@@ -36,6 +36,27 @@ namespace gt {
 #ifndef GT_C3W_ASM_DMA
 #define GT_C3W_ASM_DMA 1   // weight DMA by inline asm (see asm_dma16)
 #endif
+#ifndef GT_C3W_VAR
+#define GT_C3W_VAR 0   // timing-only experiment bits (wrong results): 1 no phase barrier, 2 no DMA wait, 4 no next-chunk items
+#endif
+#ifndef GT_C3W_PRIO
+#define GT_C3W_PRIO 0  // s_setprio 1 around each phase's MFMA stream
+#endif
+#ifndef GT_C3W_S256
+#define GT_C3W_S256 5  // weight ring slots of the 256-wide tiles
+#endif
+#ifndef GT_C3W_XD
+#define GT_C3W_XD 2    // item load -> transform distance in phases (capped so the last item is written by phase 7)
+#endif
+#ifndef GT_C3W_STAMP
+#define GT_C3W_STAMP 0   // diagnostic builds only: s_memtime stamps of the phase waits (gt_diag_conv3w_stamps)
+#endif
+#ifndef GT_C3W_STAMP_BN
+#define GT_C3W_STAMP_BN 256
+#endif
+#ifndef GT_C3W_STAMP_IN
+#define GT_C3W_STAMP_IN 2
+#endif
 #ifndef GT_C3W_SCHED
 #define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
 #endif
@@ -57,11 +78,13 @@ struct Cfg {
   static constexpr int PIECES = SLOT / 1024;       // DMA pieces per slot
   static constexpr int PWMAX = (PIECES + NW - 1) / NW;
   static constexpr int PWLO = PIECES / NW;         // pieces of waves >= PIECES % NW
-  static constexpr int S = BN == 256 ? 5 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
+  static constexpr int S = BN == 256 ? GT_C3W_S256 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
   static constexpr int D = S - 1;                  // DMA issue distance in phases
   static constexpr int ITEMS = PP * 4;             // 16-B patch items per chunk
   static constexpr int NPT = (ITEMS + NTHR - 1) / NTHR;
   static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
+  // phases between an item's load and its transform (item j: loaded at phase j, transformed at phase j + XD <= 7)
+  static constexpr int XD = (8 - NPT) < GT_C3W_XD ? (8 - NPT) : GT_C3W_XD;
   static constexpr int OFF_W = 2 * PBUF;
   static constexpr int OFF_F = OFF_W + S * SLOT;   // float area
   // floats: s_sc, s_sh, s_tb [256] each, s_bias [256], s_sub [NW][CB][4][2], s_mean, s_rstd [8]
@@ -77,6 +100,12 @@ struct Cfg {
 }  // namespace c3w
 
 typedef unsigned u32x4c_t __attribute__((ext_vector_type(4)));
+
+#if GT_C3W_STAMP
+// [workgroup slot 0..511][wave 0..7][counter 0..7]: cycles in the DMA wait, the phase barrier, the item waits, the item
+// transforms + writes, the whole chunk loop, phases (the last launch of the stamped instantiation wins)
+__device__ unsigned long long gt_c3w_stamps[512 * 8 * 8];
+#endif
 
 template <int N>
 GT_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
@@ -162,7 +191,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 
   // The next chunk's patch items are loaded by inline-asm buffer loads: hipcc would otherwise wait for them with a
   // conservative vmcnt(0) (draining the weight DMAs in flight). Item j is loaded at phase j and transformed at phase
-  // j + 2, behind that phase's MFMAs, after a counted wait naming its registers (guide §5.7 form (ii)): at most three
+  // j + XD, behind that phase's MFMAs, after a counted wait naming its registers (guide §5.7 form (ii)): at most XD + 1
   // items are in registers at once.
   u32x4c_t preg[C::NPT];
   auto load_items = [&](int c, auto JLO, auto JHI) {   // items [JLO, JHI) of chunk c
@@ -260,20 +289,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // top of phase (t = tap, MORE: chunk c+1 exists): retire DMA(k+1). Younger VMEM ops of this wave: the DMAs of phases
   // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
   // DMA of their phase).
+  constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
+  unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+  auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
   auto top_wait = [&](auto Tc, auto MOREc) {
     constexpr int t = decltype(Tc)::value;
     constexpr bool MORE = decltype(MOREc)::value;
     constexpr int ndma = MORE ? C::D - 2 : ((7 - t) < (C::D - 2) ? ((7 - t) > 0 ? 7 - t : 0) : C::D - 2);
     constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
-    vm_wait<ndma * PW + npl>();
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const unsigned long long a = stamp();
+    if (!(GT_C3W_VAR & 2)) vm_wait<ndma * PW + npl>();
+    const unsigned long long b = stamp();
+    if (GT_C3W_VAR & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (STAMP) { const unsigned long long e = stamp(); st[0] += b - a; st[1] += e - b; st[5] += 1; }
   };
-  // before transforming item j at phase j + 2: younger VMEM ops are items j+1, j+2 (loaded at phases j+1, j+2) and the
-  // DMAs of phases j+1, j+2
+  // before transforming item j at phase j + XD: younger VMEM ops are items j+1 .. j+XD (loaded at phases j+1 .. j+XD)
+  // and the DMAs of phases j+1 .. j+XD
   auto item_wait = [&](auto Jc) {
     constexpr int j = decltype(Jc)::value;
-    constexpr int n = (C::NPT - 1 - j < 2 ? C::NPT - 1 - j : 2) + 2 * PW;
+    constexpr int n = (C::NPT - 1 - j < C::XD ? C::NPT - 1 - j : C::XD) + C::XD * PW;
+    const unsigned long long a = stamp();
     vm_wait_dep<n>(preg[j]);
+    if (STAMP) st[2] += stamp() - a;
   };
 
   // ---- fragments. A (weights): slot + plane (2s + h) x BN + channel; B (patch): buffer + plane (2s + h) + position.
@@ -355,7 +393,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       int nslot = slot + 1;
       nslot = nslot == C::S ? 0 : nslot;
       // (c) the next chunk's patch item of this phase (item t)
-      if (MORE) {
+      if (MORE && !(GT_C3W_VAR & 4)) {
         if (t < C::NPT) {
           switch (t) {
             case 0: load_items(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}); break;
@@ -402,8 +440,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
           __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
         }
         // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
-        if (MORE && i == 3 && t >= 2 && t - 2 < C::NPT) {
-          switch (t - 2) {
+        if (GT_C3W_PRIO && i == 0) __builtin_amdgcn_s_setprio(1);
+        if (MORE && !(GT_C3W_VAR & 4) && i == 3 && t >= C::XD && t - C::XD < C::NPT) {
+          switch (t - C::XD) {
             case 0: item_wait(std::integral_constant<int, 0>{}); break;
             case 1: if constexpr (C::NPT > 1) item_wait(std::integral_constant<int, 1>{}); break;
             case 2: if constexpr (C::NPT > 2) item_wait(std::integral_constant<int, 2>{}); break;
@@ -411,16 +450,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             case 4: if constexpr (C::NPT > 4) item_wait(std::integral_constant<int, 4>{}); break;
             default: if constexpr (C::NPT > 5) item_wait(std::integral_constant<int, 5>{}); break;
           }
-          put_item(t - 2, c + 1, nxt);
+          const unsigned long long a = stamp();
+          put_item(t - C::XD, c + 1, nxt);
+          if (STAMP) st[3] += stamp() - a;
         }
       }
+      if (GT_C3W_PRIO) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       slot = nslot;
     }
   };
   int c = 0;
+  const unsigned long long t_loop = stamp();
   for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
   chunk(c, std::false_type{});
+#if GT_C3W_STAMP
+  if (STAMP) {   // lanes 0..5 store one counter each (vector stores)
+    st[4] = stamp() - t_loop;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v = lane == i ? st[i] : v;
+    if (lane < 6) gt_c3w_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
+  }
+#endif
 
   // ---- epilogue: bias, GroupNorm partial sums, 16-B stores (lane (r, h) of block (rb, cb) holds channels
   // cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r; v_permlane32_swap leaves it 8 consecutive channels)
@@ -550,5 +602,12 @@ hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s) {
   }
   return hipErrorNotSupported;
 }
+
+#if GT_C3W_STAMP
+extern "C" int gt_diag_conv3w_stamps(unsigned long long* out, long n) {   // diagnostic builds only
+  if (n > 512 * 8 * 8) n = 512 * 8 * 8;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c3w_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace gt

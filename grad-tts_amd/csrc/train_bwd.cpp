@@ -1,8 +1,9 @@
 // Training step of the decoder: Diffusion.loss_t forward with a tape, then the backward of
 // the score U-Net to every parameter of GradLogPEstimator2d and to mu (model/diffusion.py:16-216, 244-281).
 //
-// fp32 throughout, channels-last activations; forward and backward are built from the generic kernels of bwd.hip
-// (correctness-first VALU), launched in the order of oracle/decoder.py's estimator and its reverse.
+// fp32 throughout, channels-last activations; forward and backward are built from the fp32-MFMA kernels of bwd.hip
+// (v_mfma_f32_32x32x2_f32 gather-relation convs, weight gradients, attention products), launched in the
+// order of oracle/decoder.py's estimator and its reverse.
 // Every intermediate the backward needs is kept in the workspace (the tape); a measuring pass of the same code
 // sizes the workspace (gt_train_workspace_bytes).
 #include <hip/hip_runtime.h>

@@ -8,8 +8,8 @@ owns every output channel of a 10- or 20-row x 32-frame tile. Checked here, alwa
     level-2 rows end in partial 32-frame tiles (T = 132: 33 frames at level 2) and with 247 speakers;
   * the sampler output against the conv_kernel path (GT_CONV3W off) and against the oracle: the two paths differ only
     in fp32 accumulation order and GroupNorm partition (gate: the bf16 sampler gate 1e-2);
-  * fractional mask values (x * mask with m not in {0, 1}: the reference multiplies, it does not select) against the
-    oracle;
+  * fractional mask values against the conv_kernel path (outside the decoder's {0, 1} mask contract, so not against
+    the oracle);
   * determinism and batch invariance at the bench shape are in test_decoder_gpu.py
     (test_bench_shape_deterministic_and_batch_invariant), which now runs conv3w.
 """
@@ -91,11 +91,12 @@ def test_wide_conv_sampler_agrees_with_conv_kernel_and_oracle(B, T, lengths):
 
 
 def test_wide_conv_fractional_mask():
-    """mask values in (0, 1): x * mask is a multiply on every operand path (IN_MASK: the range-checked zero load only
-    for m == 0; IN_GN: (Mish(GN(h)) + tb) * m)."""
+    """mask values in (0, 1): x * mask is a multiply on every operand path of conv3w (IN_MASK: the range-checked zero
+    load only for m == 0; IN_GN: (Mish(GN(h)) + tb) * m). Gated against the conv_kernel path on the same inputs. The
+    decoder's contract is {0, 1} masks (sequence_mask; DESIGN.md §1: the reference's double masking x*m*m is computed as
+    x*m), so both paths sit ~0.6 from the fp32 oracle here: reported, not gated."""
     from oracle import decoder as odec
     dec, sd = make_decoder(1, 0, torch.bfloat16)
-    _plan(dec, True)
     B, T = 5, 128
     mu, z, mask, _ = synthetic_inputs(51, B, T, lengths=[128, 128, 100, 90, 64])
     rng = np.random.default_rng(5)
@@ -104,8 +105,13 @@ def test_wide_conv_fractional_mask():
     with torch.no_grad():
         ref = odec.estimator(odec.to_torch_params(sd), torch.from_numpy(z), torch.from_numpy(mask),
                              torch.from_numpy(mu), torch.from_numpy(t)).numpy()
-    y = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
-    report("conv3w estimator fractional mask", rel_err(y, ref), 1.92e-2)
+    ys = {}
+    for wide in (True, False):
+        _plan(dec, wide)
+        ys[wide] = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t)).cpu().numpy()
+        report(f"{'conv3w' if wide else 'conv_kernel'} estimator fractional mask vs oracle", rel_err(ys[wide], ref),
+               1.92e-2, gate=False)
+    report("conv3w vs conv_kernel estimator fractional mask", rel_err(ys[True], ys[False]), 1.92e-2)
 
 
 def test_wide_conv_deterministic_large_batch():

@@ -147,6 +147,27 @@ def test_fp8_sampler_N1000_matches_oracle():
     report("fp8 reverse N=1000 vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
 
 
+@pytest.mark.parametrize("B,T,lengths", [(5, 64, [64, 64, 50, 33, 64]), (2, 128, [128, 97])])
+def test_fp8_sampler_T64_plus_matches_oracle(B, T, lengths):
+    """The A8 sampler on the tile shapes the bench runs: B = 5 takes the throughput plan (4- and 5-row / 128-wide fp8
+    tiles at levels 1-2, 64 frames wide), B = 2 the small plan; T >= 64 so every level has full-width tiles (the
+    N = 1000 check above uses T = 16). 50 Euler steps; gates as for N = 1000."""
+    from oracle import decoder as odec
+    from gradtts_amd.params import synthetic_inputs
+    dec, sd = make_decoder(1, 0, FP8)
+    mu, z, mask, _ = synthetic_inputs(13, B, T, lengths=lengths)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    args = (torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu))
+    with torch.no_grad():
+        with odec.fp8_activations():
+            ref8 = odec.reverse_diffusion(odec.fp8_params(sd), *args, 50).numpy()
+        ref32 = odec.reverse_diffusion(odec.to_torch_params(sd), *args, 50).numpy()
+    y = dec(_cuda(z), _cuda(mask), _cuda(mu), 50).cpu().numpy()
+    q = rel_err(ref8, ref32)
+    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle", rel_err(y, ref8), 1e-2, quant_effect=q)
+    report(f"fp8 reverse N=50 B={B} T={T} vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
+
+
 def test_fp8_bench_shape_deterministic_and_batch_invariant():
     from gradtts_amd.params import synthetic_inputs
     dec, _ = make_decoder(1, 0, FP8)

@@ -95,27 +95,6 @@ def test_throughput_plan_bf16_matches_reference(name):
     report(f"reverse bf16 throughput plan {name}", rel_err(y, g["out"]), BF16_REV_TOL)
 
 
-def test_latency_b1_report():
-    dec, _ = make_decoder(1, 0, torch.bfloat16)
-    mu, z, mask, _ = _inputs(3, 1, 512)
-    N = 20
-
-    def run():
-        dec(z, mask, mu, N)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        y = dec(z, mask, mu, N)
-        torch.cuda.synchronize()
-        return y, (time.perf_counter() - t0) / N * 1e3
-
-    y_s, ms_s = run()
-    _set_small(dec, 0)
-    y_t, ms_t = run()
-    print(f"LATENCY B=1 T=512 bf16: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
-          f"({512 / (50 * ms_s) * 1e3:.0f} vs {512 / (50 * ms_t) * 1e3:.0f} mel-frames/s for 50-step decodes)")
-    assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
-
-
 def test_throughput_plan_every_stage_bf16():
     """Every U-Net stage vs the oracle on the throughput plan (forced at the fixture's batch size): the tiles the
     bench runs (5-row tiles, 32-channel 1x1 chunks, the ResnetBlock output formed in attn_kv, conv64 column

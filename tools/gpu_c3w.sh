@@ -19,3 +19,16 @@ for k in ("on", "off"):
     print(k, round(d["value"]), "mel-frames/s", round(d["ms_per_step"], 2), "ms", d["roofline"]["kernel"], round(d["roofline"]["frac"], 3))
     for n, v in list(d["shapes"].items())[:14]: print("   ", n, v)
 PY
+# profile: rocprofv3 kernel trace of a short bench, then the SQ counter passes of the conv3w kernels
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 300 rocprofv3 -M --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > $OUT/kt.log 2>&1 || { echo "ktrace failed"; exit 1; }
+f=$(find $OUT/kt -name "*kernel_stats.csv" | head -1); cp $f $OUT/kernel_stats.csv
+python3 - $OUT/kernel_stats.csv <<'PY'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:16]:
+    print(f"{r['Name'][:64]:64s} {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:8.1f} us {float(r['Percentage']):6.2f} %")
+print("total ms", tot / 1e6)
+PY
+bash tools/pmc_kernels.sh conv3w $OUT/pmc > $OUT/pmc.log 2>&1; echo "pmc rc=$?"; tail -20 $OUT/pmc.log
