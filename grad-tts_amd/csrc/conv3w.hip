@@ -57,6 +57,18 @@ namespace gt {
 #ifndef GT_C3W_STAMP_IN
 #define GT_C3W_STAMP_IN 2
 #endif
+#ifndef GT_C3W_STAG
+#define GT_C3W_STAG 1  // stagger the next-chunk item work between the two waves of a SIMD
+#endif
+#ifndef GT_C3W_PF
+#define GT_C3W_PF 2    // fragment prefetch distance in MFMA steps (2, 4 or 5: the B ring must divide 90 steps)
+#endif
+#ifndef GT_C3W_DMAS
+#define GT_C3W_DMAS 0  // stagger the LDS-DMA / item-load issue between the two waves of a SIMD
+#endif
+#ifndef GT_C3W_LGK
+#define GT_C3W_LGK 1   // phase barrier waits for all LDS ops but the next phase's pre-reads (0: lgkmcnt(0))
+#endif
 #ifndef GT_C3W_SCHED
 #define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
 #endif
@@ -151,6 +163,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int b = bid / n_ft;
   const int f0 = ft * C::TR, t0 = tt * 32;
 
+#if GT_C3W_STAMP
+  const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
+#endif
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wv % C::WN, wm = wv / C::WN;
@@ -290,18 +305,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
   // DMA of their phase).
   constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
-  unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+  constexpr int NPRE = GT_C3W_PF + CB;   // LDS reads of the next phase's first PF steps (top_wait)
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
   auto top_wait = [&](auto Tc, auto MOREc) {
     constexpr int t = decltype(Tc)::value;
     constexpr bool MORE = decltype(MOREc)::value;
     constexpr int ndma = MORE ? C::D - 2 : ((7 - t) < (C::D - 2) ? ((7 - t) > 0 ? 7 - t : 0) : C::D - 2);
+    // waves 0-3 issue a phase's DMA before its item, waves 4-7 (GT_C3W_DMAS) after it: an item loaded in phase
+    // k + 1 - D is younger than DMA(k+1) only in the first half
     constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
+    constexpr int npl4 = MORE ? n_lp(t + 2 - C::D, t - 1) : 0;
     const unsigned long long a = stamp();
-    if (!(GT_C3W_VAR & 2)) vm_wait<ndma * PW + npl>();
+    if (!(GT_C3W_VAR & 2)) {
+      if (!GT_C3W_DMAS || wv < c3w::NW / 2) vm_wait<ndma * PW + npl>();
+      else vm_wait<ndma * PW + npl4>();
+    }
     const unsigned long long b = stamp();
+    // LDS: every access of this wave but its last NPRE (the next phase's first fragments, read at the end of the
+    // previous phase; they need no barrier, so their latency stays hidden) has completed -- the reads of the slot the
+    // DMA below overwrites and the item writes of the next chunk's patch included (LDS ops complete in order)
     if (GT_C3W_VAR & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (GT_C3W_STAMP || !GT_C3W_LGK) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(NPRE) : "memory");
     if (STAMP) { const unsigned long long e = stamp(); st[0] += b - a; st[1] += e - b; st[5] += 1; }
   };
   // before transforming item j at phase j + XD: younger VMEM ops are items j+1 .. j+XD (loaded at phases j+1 .. j+XD)
@@ -357,13 +383,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // MFMA steps i = s * RB + rb of a phase; fragments are read two steps ahead (B: ring of 3 by the chunk-global step
   // index, a chunk being 90 steps; A: one register set per k-step s), across phase boundaries too: phase k+1's slot and
   // patch are visible from the top of phase k.
-  bf16x8 fa[2][CB], fb[3];
+  constexpr int PF = GT_C3W_PF, NB = PF + 1;   // fragment prefetch distance in steps; B ring of NB registers
+  static_assert(9 * C::NS % NB == 0 && PF <= RB, "B ring index chunk-periodic; A frags double-buffered by k-step");
+  bf16x8 fa[2][CB], fb[NB];
 #pragma unroll
   for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(0, 0, cb);
-  fb[0] = rd_b(0, 0, 0, 0);
-  fb[1] = rd_b(0, 0, 0, 1);
+#pragma unroll
+  for (int n = 0; n < PF; ++n) fb[n] = rd_b(0, 0, 0, n);
 
   int slot = 0;   // weight slot of the current phase (k mod S)
+  constexpr int DS1 = C::NS / 2;   // MFMA step of the DMA issue of waves 4-7 (GT_C3W_DMAS, below)
+  // MFMA steps of the item transforms: waves 0-3 at XS0, waves 4-7 at XS1
+  constexpr int XS0 = GT_C3W_STAG ? 1 : 3, XS1 = GT_C3W_STAG ? C::NS - 3 : 3;
   // One chunk: 9 phases. MORE: a chunk c+1 exists (its patch is loaded and written during this chunk).
   auto chunk = [&](int c, auto MOREc) {
     constexpr bool MORE = decltype(MOREc)::value;
@@ -384,15 +415,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         case 7: top_wait(std::integral_constant<int, 7>{}, MOREc); break;
         default: top_wait(std::integral_constant<int, 8>{}, MOREc); break;
       }
-      // (b) DMA of phase k + D into the slot phase k - 1 used
-      if (MORE || t + C::D < 9) {
-        int ds = slot + C::D;
-        ds = ds >= C::S ? ds - C::S : ds;
-        dma(k + C::D, ds);
-      }
       int nslot = slot + 1;
       nslot = nslot == C::S ? 0 : nslot;
-      // (c) the next chunk's patch item of this phase (item t)
+      // (b) DMA of phase k + D into the slot phase k - 1 used: waves 0-3 here, waves 4-7 at MFMA step DS1
+      // (GT_C3W_DMAS), so the two waves of a SIMD do not both stop issuing MFMAs for their LDS-DMA pieces at once
+      auto issue_dma = [&]() {
+        if (MORE || t + C::D < 9) {
+          int ds = slot + C::D;
+          ds = ds >= C::S ? ds - C::S : ds;
+          dma(k + C::D, ds);
+        }
+      };
+      if (!GT_C3W_DMAS || wv < c3w::NW / 2) issue_dma();
+      // (c) the next chunk's patch item of this phase (item t), and the counted wait for item t - XD's registers
+      // (loaded XD phases ago; younger: items t-XD+1 .. t and the DMAs of XD phases -- the same count in both wave
+      // halves). Unconditional in every wave: an asm load whose wait a wave skipped would land in a reused register.
       if (MORE && !(GT_C3W_VAR & 4)) {
         if (t < C::NPT) {
           switch (t) {
@@ -404,44 +441,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             default: load_items(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 6>{}); break;
           }
         }
-      }
-      // (d) MFMAs of phase k
-#pragma unroll
-      for (int i = 0; i < C::NS; ++i) {
-        const int s = i / RB, rb = i % RB;
-        const int g = t * C::NS + i;          // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
-        const int n = i + 2;                  // step whose fragments are read now
-        int nrd = 0;
-        if (n < C::NS) {
-          const int s1 = n / RB, rb1 = n % RB;
-          if (rb1 == 0) {
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb) fa[s1 & 1][cb] = rd_a(slot, s1, cb);
-            nrd += CB;
-          }
-          fb[(g + 2) % 3] = rd_b(cur, t, s1, rb1);
-          nrd += 1;
-        } else if (MORE || t < 8) {           // phase k+1's steps 0 and 1
-          const int rb1 = n - C::NS;
-          if (rb1 == 0) {
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(nslot, 0, cb);
-            nrd += CB;
-          }
-          fb[(g + 2) % 3] = t < 8 ? rd_b(cur, t + 1, 0, rb1) : rd_b(nxt, 0, 0, rb1);
-          nrd += 1;
-        }
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-          acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][cb], fb[g % 3], acc[rb][cb], 0, 0, 0);
-        if (GT_C3W_SCHED) {
-          if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
-          else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
-        }
-        // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
-        if (GT_C3W_PRIO && i == 0) __builtin_amdgcn_s_setprio(1);
-        if (MORE && !(GT_C3W_VAR & 4) && i == 3 && t >= C::XD && t - C::XD < C::NPT) {
+        if (t >= C::XD && t - C::XD < C::NPT) {
           switch (t - C::XD) {
             case 0: item_wait(std::integral_constant<int, 0>{}); break;
             case 1: if constexpr (C::NPT > 1) item_wait(std::integral_constant<int, 1>{}); break;
@@ -450,9 +450,55 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             case 4: if constexpr (C::NPT > 4) item_wait(std::integral_constant<int, 4>{}); break;
             default: if constexpr (C::NPT > 5) item_wait(std::integral_constant<int, 5>{}); break;
           }
-          const unsigned long long a = stamp();
-          put_item(t - C::XD, c + 1, nxt);
-          if (STAMP) st[3] += stamp() - a;
+        }
+      }
+      // (d) MFMAs of phase k
+#pragma unroll
+      for (int i = 0; i < C::NS; ++i) {
+        if (GT_C3W_DMAS && i == DS1 && wv >= c3w::NW / 2) issue_dma();
+        const int s = i / RB, rb = i % RB;
+        const int g = t * C::NS + i;          // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
+        const int n = i + PF;                 // step whose fragments are read now
+        int nrd = 0;
+        if (n < C::NS) {
+          const int s1 = n / RB, rb1 = n % RB;
+          if (rb1 == 0) {
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) fa[s1 & 1][cb] = rd_a(slot, s1, cb);
+            nrd += CB;
+          }
+          fb[(g + PF) % NB] = rd_b(cur, t, s1, rb1);
+          nrd += 1;
+        } else if (MORE || t < 8) {           // phase k+1's steps 0 .. PF-1
+          const int rb1 = n - C::NS;
+          if (rb1 == 0) {
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(nslot, 0, cb);
+            nrd += CB;
+          }
+          fb[(g + PF) % NB] = t < 8 ? rd_b(cur, t + 1, 0, rb1) : rd_b(nxt, 0, 0, rb1);
+          nrd += 1;
+        }
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb)
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][cb], fb[g % NB], acc[rb][cb], 0, 0, 0);
+        if (GT_C3W_SCHED) {
+          if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
+          else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
+        }
+        // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
+        if (GT_C3W_PRIO && i == 0) __builtin_amdgcn_s_setprio(1);
+        // Staggered between the two waves of a SIMD (waves w and w + 4 share one; MI355X_MICROARCH.md, two waves per
+        // SIMD, item 9): waves 0-3 at step XS0, waves 4-7 at step XS1, so one wave's transform VALU runs beside its
+        // partner's MFMAs instead of both leaving the matrix pipe idle at the same step.
+        if (MORE && !(GT_C3W_VAR & 4) && (i == XS0 || i == XS1) && t >= C::XD && t - C::XD < C::NPT) {
+          if ((i == XS0 && wv < c3w::NW / 2) || (i == XS1 && wv >= c3w::NW / 2)) {
+            const unsigned long long a = stamp();
+            put_item(t - C::XD, c + 1, nxt);
+            asm volatile("" ::: "memory");   // the item's LDS write stays ahead of the phase-end fragment reads (NPRE)
+            if (STAMP) st[3] += stamp() - a;
+          }
         }
       }
       if (GT_C3W_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -464,14 +510,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const unsigned long long t_loop = stamp();
   for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
   chunk(c, std::false_type{});
+  const unsigned long long t_loop_end = stamp();
 #if GT_C3W_STAMP
-  if (STAMP) {   // lanes 0..5 store one counter each (vector stores)
-    st[4] = stamp() - t_loop;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) v = lane == i ? st[i] : v;
-    if (lane < 6) gt_c3w_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
-  }
+  if (STAMP) { st[4] = t_loop_end - t_loop; st[6] = t_loop - t_entry; }
 #endif
 
   // ---- epilogue: bias, GroupNorm partial sums, 16-B stores (lane (r, h) of block (rb, cb) holds channels
@@ -550,6 +591,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = S;
     dst[1] = Q;
   }
+#if GT_C3W_STAMP
+  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
+    st[7] = stamp() - t_loop_end;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
+    if (lane < 8) gt_c3w_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
+  }
+#endif
 }
 
 // (BN, CB) of a conv on an F-row grid with Cout outputs, or 0 if conv3w does not cover it

@@ -31,7 +31,7 @@ buf = np.zeros(512 * 8 * 8, dtype=np.uint64)
 assert f(buf.ctypes.data, buf.size) == 0
 a = buf.reshape(512, 8, 8).astype(np.float64)
 used = a[:, :, 5] > 0
-names = ["dma_wait", "barrier", "item_wait", "item_put", "loop", "phases"]
+names = ["dma_wait", "barrier", "item_wait", "item_put", "loop", "phases", "prologue", "epilogue"]
 print(f"workgroups with stamps: {int(used.any(1).sum())}")
 for i, n in enumerate(names):
     v = a[:, :, i][used]
@@ -40,4 +40,6 @@ loop = a[:, :, 4][used]
 for i, n in enumerate(names[:4]):
     print(f"{n:10s} share of loop {(a[:, :, i][used] / loop).mean():.3f}")
 ph = a[:, :, 5][used].mean()
+tot = (a[:, :, 4] + a[:, :, 6] + a[:, :, 7])[used]
+print(f"prologue {(a[:, :, 6][used] / tot).mean():.3f}  loop {(loop / tot).mean():.3f}  epilogue {(a[:, :, 7][used] / tot).mean():.3f} of {tot.mean():.0f} cycles")
 print(f"cycles per phase {loop.mean() / ph:.0f} (MFMA floor 2 waves x 20 x 32 = 1280)")
