@@ -35,6 +35,15 @@ namespace gt {
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef GT_C64_VAR
+#define GT_C64_VAR 0  // timing-only experiment bits (wrong results): 1 no new-row staging, 2 no output stores, 4 no barrier
+#endif
+#ifndef GT_C64_STAMP
+#define GT_C64_STAMP 0  // diagnostic builds only: s_memtime stamps (gt_diag_conv64_stamps), instantiation GT_C64_STAMP_IN, F = 80
+#endif
+#ifndef GT_C64_STAMP_IN
+#define GT_C64_STAMP_IN 1
+#endif
 #ifndef GT_C64_PF
 #define GT_C64_PF 2   // MFMA steps a fragment read is issued ahead
 #endif
@@ -65,6 +74,12 @@ static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 // work overlaps the other's MFMAs.
 // W8: fp8 weights (GT_BF16_W8 / GT_FP8) -- the image holds the e4m3 values (exact in bf16) and p.wscale the
 // per-output-channel scale: the accumulator starts at bias / scale and the epilogue multiplies by the scale.
+#if GT_C64_STAMP
+// [workgroup 0..511][wave 0..3][counter 0..7]: prologue, loop, barrier wait, pass MFMA streams, pass epilogues, tiles,
+// segment end, unused
+__device__ unsigned long long gt_c64_stamps[512 * 4 * 8];
+#endif
+
 template <int IN, bool W8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
@@ -79,6 +94,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
 
+  const bool STAMP = GT_C64_STAMP && IN == GT_C64_STAMP_IN && !W8 && p.Fout == 80;
+  auto stamp = [&]() -> unsigned long long { return (GT_C64_STAMP && STAMP) ? __builtin_amdgcn_s_memtime() : 0ull; };
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_entry = stamp();
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: ring-row addressing stays scalar
   const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
@@ -236,6 +255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // per-lane GroupNorm partials of the whole segment (group cb*4 + pr*2 + h), accumulated tile by tile, pass by
   // pass in a fixed order; reduced across lanes and waves once, at the end
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
+  const unsigned long long t_loop = stamp();
   for (int k = 0; k < L; ++k) {
     const int ft = ft0 + k;
 #pragma unroll
@@ -247,6 +267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const char* rowp1 = sR + ((sbase + 1) % RING) * ROWB + r * POSB + h * 16;
       const char* rowp2 = sR + ((sbase + 2) % RING) * ROWB + r * POSB + h * 16;
       f32x16 acc;
+      const unsigned long long t_pass = stamp();
       // 36 MFMAs (4 chunks x 9 taps), fragment reads software-pipelined GT_C64_PF steps ahead (issued in the natural
       // order the compiler waited on each read right before its MFMA); behind each chunk's MFMAs one staging item of
       // tile k+1's new rows is stored and reloaded for tile k+2 (items spread over the 8 chunk slots of two passes)
@@ -276,7 +297,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
         if (st % 9 == 8) {
           const int j = ps * NCH + st / 9;
-          if (j < PPT) {
+          if (j < PPT && !(GT_C64_VAR & 1)) {
             put_new(j, k + 1);
             issue_new(j, k + 2);
           }
@@ -289,6 +310,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       float v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) v[q] = acc[q];
+      unsigned long long t_epi = 0;
+      if (GT_C64_STAMP && STAMP) {   // the MFMA stream retired (the stamp would otherwise read the issue time)
+        asm volatile("" :: "v"(v[15]));
+        t_epi = stamp();
+        st[3] += t_epi - t_pass;
+      }
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
@@ -318,13 +345,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
           asm volatile("" : "+v"(s), "+v"(q));   // scalar chains: see conv.hip (packed-FP32 op_sel hazard)
         }
         const uint4 ov = f_to_item(o, bf16());
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
+        if (!(GT_C64_VAR & 2))
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
+        else
+          asm volatile("" :: "v"(ov.x), "v"(ov.y), "v"(ov.z), "v"(ov.w));
         gs[pr] += valid ? s : 0.f;
         gq[pr] += valid ? q : 0.f;
       }
+      if (GT_C64_STAMP && STAMP) { asm volatile("" :: "v"(gs[1]), "v"(gq[1])); st[4] += stamp() - t_epi; }
     }
-    lds_barrier();   // tile k+1's rows complete
+    const unsigned long long t_bar = stamp();
+    if (!(GT_C64_VAR & 4)) lds_barrier();   // tile k+1's rows complete
+    if (GT_C64_STAMP && STAMP) { st[2] += stamp() - t_bar; st[5] += 1; }
   }
+  const unsigned long long t_loop_end = stamp();
   // segment done: this wave's groups over its positions, then the 2 waves of each channel half -> one slot
 #pragma unroll
   for (int pr = 0; pr < 2; ++pr) {
@@ -348,6 +382,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = S;
     dst[1] = Q;
   }
+#if GT_C64_STAMP
+  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
+    st[0] = t_loop - t_entry; st[1] = t_loop_end - t_loop; st[6] = stamp() - t_loop_end;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
+    if (lane < 8) gt_c64_stamps[((blockIdx.x & 511) * 4 + wv) * 8 + lane] = v;
+  }
+#endif
 }
 
 static int cu_count() {
@@ -397,5 +440,12 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   }
   return hipGetLastError();
 }
+
+#if GT_C64_STAMP
+extern "C" int gt_diag_conv64_stamps(unsigned long long* out, long n) {   // diagnostic builds only
+  if (n > 512 * 4 * 8) n = 512 * 4 * 8;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c64_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace gt

@@ -11,7 +11,7 @@ run() {   # run <name> <limit> <bench args...>
   timeout -k 10 $lim python3 bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -3 $OUT/$name.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$OUT/$name.json')); print('$name', round(d['value'],1), d['unit'], round(d['ms_per_step'],2), 'ms/step', d['roofline']['kernel'], round(d['roofline']['frac'],3), 'cpu', round(d.get('cpu_baseline',{}).get('value',0),2))"
   timeout -k 10 $lim rocprofv3 -M --kernel-trace --stats --output-format csv -d $OUT/kt_$name -o kt -- python3 bench.py --no-cpu-baseline "$@" > $OUT/kt_$name.log 2>&1 || { echo "$name ktrace failed"; exit 1; }
-  cp $(find $OUT/kt_$name -name "*kernel_stats.csv" | head -1) $OUT/${name}_kernel_stats.csv
+  cp $(find $OUT/kt_$name -name "*kernel_stats.csv" | head -1) $OUT/${name}_kernel_stats.csv && rm -rf $OUT/kt_$name
 }
 run c2_bf16 300 --steps 5 --warmup 2
 run c2_fp32 300 --steps 2 --warmup 1 --dtype fp32
