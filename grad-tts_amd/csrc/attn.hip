@@ -343,6 +343,138 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
   }
 }
 
+// grid (B, C/64, C/64): attn_merge + attn_fold in one launch. Each workgroup merges the tiles' partials of all four heads
+// itself (the (C/64)^2 workgroups of an utterance repeat this small, L2-resident pass), forms its 64 rows of A_b in LDS
+// and multiplies them by its 64 columns of Wq: two launches and the A_b round trip through HBM fewer per attention
+// block. Same operations in the same order as attn_merge_kernel + attn_fold_kernel (four tile groups merged online, then
+// combined in a fixed order; A by the same e-ordered fp32 chain), so the folded weights are bit-identical.
+template <class A>
+__global__ __launch_bounds__(1024) void attn_mf_kernel(const float* part, int ntile, const float* wout, const float* g,
+                                                       const float* wq, int C, char* Mw, WImg W) {
+  __shared__ float s_ctx[4][32][33];   // normalised context per head [d][e]
+  __shared__ float s_a[64][129];       // A rows co0..co0+63, k = 0..127
+  __shared__ float s_q[64][129];       // first W_out rows co0..co0+63 (all 128 columns), then Wq^T: [ci - ci0][k]
+  __shared__ float s_g[4][4][32][33];  // [head][tile group][d][e] unnormalised group contexts
+  __shared__ float s_gm[4][4][32], s_gl[4][4][32];
+  const int b = blockIdx.x, co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64, tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {   // W_out rows of this block (float4 loads)
+    const int i = tid + 1024 * j, rr = i >> 5, k4 = (i & 31) * 4;
+    const f32x4 w = *reinterpret_cast<const f32x4*>(wout + (long)(co0 + rr) * 128 + k4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_q[rr][k4 + k] = w[k];
+  }
+  // merge, as attn_merge_kernel: thread (tile group grp, d, 4 e's) merges tiles [t0, t1) of each head online in tile
+  // order (the four heads interleaved, so their loads are in flight together), then the four groups are combined in
+  // group order
+  {
+    const int grp = tid >> 8, lt = tid & 255, d = lt >> 3, e0 = (lt & 7) * 4;
+    const int per = (ntile + 3) / 4, t0 = grp * per, t1 = min(ntile, t0 + per);
+    const long tstride = 4 * 1088;
+    const float* base = part + (long)b * ntile * 4 * 1088;
+    float M[4], L[4], c[4][4];
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) {
+      M[hd] = -__builtin_huge_valf(); L[hd] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c[hd][k] = 0.f;
+    }
+    for (int t = t0; t < t1; ++t) {
+      float mt[4], lt_[4];
+      f32x4 v[4];
+#pragma unroll
+      for (int hd = 0; hd < 4; ++hd) {
+        const float* pt = base + t * tstride + hd * 1088;
+        mt[hd] = pt[d]; lt_[hd] = pt[32 + d];
+        v[hd] = *reinterpret_cast<const f32x4*>(pt + 64 + d * 32 + e0);
+      }
+#pragma unroll
+      for (int hd = 0; hd < 4; ++hd) {
+        if (mt[hd] > M[hd]) {   // rescale what was merged so far (m in log2 units)
+          const float r = __builtin_amdgcn_exp2f(M[hd] - mt[hd]);
+          L[hd] *= r;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) c[hd][k] *= r;
+          M[hd] = mt[hd];
+        }
+        const float w = __builtin_amdgcn_exp2f(mt[hd] - M[hd]);
+        L[hd] += w * lt_[hd];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[hd][k] += w * v[hd][k];
+      }
+    }
+#pragma unroll
+    for (int hd = 0; hd < 4; ++hd) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_g[hd][grp][d][e0 + k] = c[hd][k];
+      if ((lt & 7) == 0) { s_gm[hd][grp][d] = M[hd]; s_gl[hd][grp][d] = L[hd]; }
+    }
+  }
+  __syncthreads();
+  {   // combine the groups in a fixed order: thread (head, d, 4 e's)
+    const int hd = tid >> 8, lt = tid & 255, d = lt >> 3, e0 = (lt & 7) * 4;
+    float Mt = -__builtin_huge_valf();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Mt = fmaxf(Mt, s_gm[hd][q][d]);
+    float Lt = 0.f, ct[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (s_gl[hd][q][d] == 0.f) continue;   // empty group (ntile < 4)
+      const float r = __builtin_amdgcn_exp2f(s_gm[hd][q][d] - Mt);
+      Lt += r * s_gl[hd][q][d];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ct[k] += r * s_g[hd][q][d][e0 + k];
+    }
+    const float inv = 1.f / Lt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_ctx[hd][d][e0 + k] = ct[k] * inv;
+  }
+  __syncthreads();
+  const float gg = g[0];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {   // A[co][32 hd + dd] = g sum_e Wout[co][32 hd + e] ctx_hd[dd][e] (dd fastest)
+    const int idx = tid + 1024 * j, co = idx >> 7, kk = idx & 127, hd = kk >> 5, dd = kk & 31;
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < 32; ++e) acc += s_q[co][hd * 32 + e] * s_ctx[hd][dd][e];
+    s_a[co][kk] = gg * acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {   // Wq^T block, coalesced along ci
+    const int i = tid + 1024 * j, k = i >> 4, c4 = (i & 15) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(wq + (long)k * C + ci0 + c4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s_q[c4 + c][k] = v[c];
+  }
+  __syncthreads();
+  if (tid >= 256) return;   // the fold: 4 waves, one 32 x 32 block each (no barrier below)
+  const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int bm = (wv >> 1) * 32, bn = (wv & 1) * 32;
+  f32x16 acc;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll 8
+  for (int k = 0; k < 128; k += 2)
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_a[bm + r][k + h], s_q[bn + r][k + h], acc, 0, 0, 0);
+  char* img = Mw + (long)b * W.total;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int co = co0 + bm + acc_row(j, h), ci = ci0 + bn + r;
+    *reinterpret_cast<A*>(img + conv_wimg_off(W, co, 0, ci, (int)sizeof(A))) = Act<A>::from_f(acc[j]);
+  }
+}
+
+hipError_t launch_attn_merge_fold(int act_bf16, const float* part, int B, int ntile, const float* wout, const float* g,
+                                  const float* wq, int C, void* Mw, hipStream_t s) {
+  if (C % 64 != 0 || C > 256) return hipErrorInvalidValue;
+  const WImg W = conv_wimg(act_bf16, 1, C, C);
+  const dim3 grid(B, C / 64, C / 64);
+  if (act_bf16) hipLaunchKernelGGL(attn_mf_kernel<bf16>, grid, dim3(1024), 0, s, part, ntile, wout, g, wq, C, (char*)Mw, W);
+  else hipLaunchKernelGGL(attn_mf_kernel<float>, grid, dim3(1024), 0, s, part, ntile, wout, g, wq, C, (char*)Mw, W);
+  return hipGetLastError();
+}
+
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels

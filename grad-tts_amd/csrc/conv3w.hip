@@ -99,8 +99,8 @@ struct Cfg {
   static constexpr int XD = (8 - NPT) < GT_C3W_XD ? (8 - NPT) : GT_C3W_XD;
   static constexpr int OFF_W = 2 * PBUF;
   static constexpr int OFF_F = OFF_W + S * SLOT;   // float area
-  // floats: s_sc, s_sh, s_tb [256] each, s_bias [256], s_sub [NW][CB][4][2], s_mean, s_rstd [8]
-  static constexpr int NF = 4 * 256 + NW * CB * 8 + 16;
+  // floats: s_sc, s_sh, s_tb [256] each, s_bias [256], s_wsc [256], s_sub [NW][CB][4][2], s_mean, s_rstd [8]
+  static constexpr int NF = 5 * 256 + NW * CB * 8 + 16;
   static constexpr int SMEM = OFF_F + NF * 4;
   static_assert(WN * WM == NW && WN >= 1, "wave grid");
   static_assert(PIECES * 1024 == SLOT, "whole DMA pieces");
@@ -147,7 +147,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   float* const s_sh = s_sc + 256;
   float* const s_tb = s_sh + 256;
   float* const s_bias = s_tb + 256;
-  float* const s_sub = s_bias + 256;
+  float* const s_wsc = s_bias + 256;   // fp8-weight images (GT_BF16_W8): per-output-channel weight scale
+  float* const s_sub = s_wsc + 256;
   float* const s_mean = s_sub + c3w::NW * CB * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(smem + C::PBUF);   // patch buffer 1 is free until chunk 0, phase 2
@@ -179,6 +180,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     c_g = p.gn_gamma[tid]; c_b = p.gn_beta[tid]; c_t = tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid];
   }
   const float c_bias = tid < BN ? p.bias[tid] : 0.f;
+  // fp8 weights (the image holds their e4m3 values, exact in bf16): out = acc * scale + bias, as conv_kernel's W8
+  const bool w8 = p.wscale != nullptr;
+  const float c_wsc = (w8 && tid < BN) ? p.wscale[tid] : 1.f;
 
   const int npos = p.B * F * T;
   int pidx[C::NPT];
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       s_sc[tid] = sc * kLog2e; s_sh[tid] = (c_b - s_mean[g] * sc) * kLog2e; s_tb[tid] = c_t;
     }
   }
-  if (tid < BN) s_bias[tid] = c_bias;
+  if (tid < BN) { s_bias[tid] = c_bias; s_wsc[tid] = c_wsc; }
   lds_barrier();
 #pragma unroll
   for (int j = 0; j < C::NPT; ++j) put_item(j, 0, 0);
@@ -547,8 +551,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
         const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
         float o[8];
+        if (w8) {   // wave-uniform
+          const f32x4 s0 = *reinterpret_cast<const f32x4*>(s_wsc + cl);
+          const f32x4 s1 = *reinterpret_cast<const f32x4*>(s_wsc + cl + 4);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] + b1[k]; }
+          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] * s0[k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] * s1[k] + b1[k]; }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] + b1[k]; }
+        }
         if (valid) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
@@ -614,7 +625,7 @@ static int c3w_rows(int cfg) { return (cfg == 1 || cfg == 3) ? 10 : 20; }
 
 bool conv3w_eligible(const ConvParams& p, InMode im) {
   if (im != IN_MASK && im != IN_GN && im != IN_PLAIN) return false;
-  if (p.small || p.wscale || p.w_bstride || p.Fin != p.Fout || p.Tin != p.Tout) return false;
+  if (p.small || p.a8 || p.w_bstride || p.Fin != p.Fout || p.Tin != p.Tout) return false;
   if (p.Cin % 32 || p.C0 % 32 || (p.in1 && p.C1 % 32) || p.Cin_pad != p.Cin || p.Cin != p.C0 + (p.in1 ? p.C1 : 0)) return false;
   if (im == IN_GN && p.Cin > 256) return false;
   if (!c3w_cfg(p.Cout, p.Fout)) return false;

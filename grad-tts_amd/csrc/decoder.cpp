@@ -180,6 +180,10 @@ struct gt_decoder {
   // bf16 throughput-plan 3x3 convs at levels 1-2 on conv3w (one 8-wave workgroup per CU owning all output channels of
   // a tile); GT_CONV3W=0 at creation or gt_decoder_set_wide_conv(dec, 0) runs them on conv_kernel
   bool wide = true;
+  // attention merge + fold as one launch (attn_mf_kernel); GT_ATTN_MF=1 at creation (off: slower at B = 32)
+  bool attn_mf = false;
+  // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
+  bool attn_ds = true;
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -417,6 +421,12 @@ std::vector<float> e4m3_values(const std::vector<float>& w, int rows) {
   return v;
 }
 
+// a 3x3 [Cout][Cin][3][3] weight conv3w covers (Cin % 32 == 0, Cout 64 / 128 / 256; not the 64 -> 64 convs of conv64)
+static bool conv3w_shape(const std::vector<int64_t>& shp) {
+  return shp.size() == 4 && shp[2] == 3 && shp[3] == 3 && shp[1] % 32 == 0 && (shp[0] == 64 || shp[0] == 128 || shp[0] == 256) &&
+         !(shp[0] == 64 && shp[1] == 64);
+}
+
 // conv64 (persistent weight-resident 64-channel 3x3 conv, conv64.hip) for bf16; GT_CONV64=0 disables it (A/B)
 static bool conv64_enabled() {
   static const bool v = [] {
@@ -450,15 +460,18 @@ int prepare(gt_decoder* d, int code) {
       pack_conva8(blob, d, code, k, w, shp);
     } else if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
       pack_conv8(blob, d, code, k, w, shp, false);
+      if (code == GT_BF16_W8 && ends_with(k, ".block.0.weight") && conv3w_shape(shp))   // conv3w: the e4m3 values
+        pack_conv3w(blob, k + ".w3w", e4m3_values(w, (int)shp[0]), (int)shp[0], (int)shp[1]);
     } else if (w8 && starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv8(blob, d, code, k, w, shp, true);
     } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
       if (c64) pack_conv64(blob, k + ".w64", w);
-      if (code == GT_BF16 && ends_with(k, ".block.0.weight") && !c64 && shp[2] == 3 && shp[3] == 3 && shp[1] % 32 == 0 &&
-          (shp[0] == 64 || shp[0] == 128 || shp[0] == 256))
+      if (code == GT_BF16 && ends_with(k, ".block.0.weight") && !c64 && conv3w_shape(shp))
         pack_conv3w(blob, k + ".w3w", w, (int)shp[0], (int)shp[1]);
+      if (code == GT_BF16 && starts_with(k, "downs.") && ends_with(k, ".3.conv.weight") && shp[0] == 64 && shp[1] == 64)
+        pack_conv64(blob, k + ".w64", w);   // the level-0 Downsample of attn_down_kernel
       if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
@@ -645,14 +658,15 @@ struct Run {
             2.0 * 64 * 64 * 9 * pos, pos * 128 * 2.0 + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(im, p, s); });
       return np;
     }
-    if (dt && wi == GT_BF16 && d->wide && conv3w_eligible(p, im) && d->dp[wi].count(wkey + ".w3w")) {
+    if (dt && (wi == GT_BF16 || wi == GT_BF16_W8) && d->wide && conv3w_eligible(p, im) && d->dp[wi].count(wkey + ".w3w")) {
       p.w = W(wkey + ".w3w");
       const int np = conv3w_nparts(p.Fout, p.Tout, p.Cout);
       if (np <= 0 || np > L.pmax) { chk(hipErrorInvalidValue); return np; }
       const double pos = (double)p.B * p.Fout * p.Tout;
       const int cb = (p.Cout == 256 || (p.Cout == 128 && p.Fout % 20 == 0 && p.Fout >= 40)) ? 2 : 1;
       timed(std::string("conv3w_kernel<") + std::to_string((int)im) + "," + std::to_string(p.Cout) + "," +
-                std::to_string(cb) + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout),
+                std::to_string(cb) + (p.wscale ? ",w8" : "") + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) +
+                "x" + std::to_string(p.Fout),
             2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + 9.0 * p.Cin * p.Cout * 2,
             [&] { return launch_conv3w(im, p, s); });
       return np;
@@ -811,6 +825,32 @@ struct Run {
 
   // Residual(Rezero(LinearAttention)) (diffusion.py:82-110)
   void attention(const std::string& k, int lvl, const void* in, int C, void* out) {
+    attention_fold(k, lvl, in, C);
+    attention_out(k, lvl, in, C, out);
+  }
+
+  // level 0: the attention output and the Downsample after it as one pass (attn_down.hip; the attention output is
+  // never materialised). false (nothing launched) when not applicable: another dtype, the fused form disabled
+  // (GT_ATTN_DS=0), or a probe of the attention output itself.
+  bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* out) {
+    if (!(dt && wi == GT_BF16 && d->attn_ds && lvl == 0 && C == 64 && d->dp[wi].count(kd + "conv.weight.w64")))
+      return false;
+    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
+    AttnDownParams a{};
+    a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
+    a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
+    a.wds = W(kd + "conv.weight.w64"); a.bds = Fp(kd + "conv.bias"); a.out = out;
+    if (!attn_down_eligible(a)) return false;
+    attention_fold(ka, lvl, in, C);
+    const double pin = (double)B * a.F * a.T, pout = pin / 4;
+    timed("attn_down_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
+          2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin + pout) * C * 2.0, [&] { return launch_attn_down(a, s); });
+    tap(kd.substr(0, kd.size() - 1), lvl + 1, out, C);
+    return true;
+  }
+
+  // attn_kv + merge/fold: M_b for every utterance in the workspace (the ResnetBlock output before it formed on the way)
+  void attention_fold(const std::string& k, int lvl, const void* in, int C) {
     float* part = (float*)(ws + L.part);
     float* G = (float*)(ws + L.G);
     void* Mw = ws + L.Mw;
@@ -838,11 +878,22 @@ struct Run {
               "x" + std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
           npos * C * esize(dt) * (rb ? 3.0 : 1.0), [&] { return launch_attn_kv(dt, a, s); });
     if (rb) tap(pend.name, lvl, in, C);
-    timed("attn_merge_kernel", 0.0, 0.0, [&] {
-      return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);
-    });
-    timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>"), 2.0 * B * C * 128.0 * C, 0.0,
-          [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
+    if (d->attn_mf) {
+      timed(std::string("attn_mf_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0, [&] {
+        return launch_attn_merge_fold(dt, part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"),
+                                      Fp(k + "fn.fn.to_qkv.weight.q"), C, Mw, s);
+      });
+    } else {
+      timed("attn_merge_kernel@" + std::to_string(C), 0.0, 0.0, [&] {
+        return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);
+      });
+      timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0,
+            [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
+    }
+  }
+
+  void attention_out(const std::string& k, int lvl, const void* in, int C, void* out) {   // y = x + M_b x + g b_out
+    void* Mw = ws + L.Mw;
     ConvParams p = base(lvl, lvl);
     p.Cin = C; p.Cout = C; p.Cin_pad = C;
     p.in0 = in; p.C0 = C;
@@ -878,8 +929,10 @@ struct Run {
     // down 0 (80 x T, 64 ch)
     resnet("downs.0.0.", 0, nullptr, 0, nullptr, 0, 64, act(0, 0), next_tb(64));
     resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64), true);
-    attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
-    downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
+    if (!attention_down("downs.0.2.", "downs.0.3.", 0, act(0, 1), 64, act(1, 0))) {
+      attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
+      downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
+    }
     // down 1 (40 x T/2, 128 ch); hidden 1 -> act(1,2)
     resnet("downs.1.0.", 1, act(1, 0), 64, nullptr, 0, 128, act(1, 1), next_tb(128));
     resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128), true);
@@ -990,6 +1043,8 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
   if (const char* e = getenv("GT_SMALL_B")) d->small_b = atoll(e);
   if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
+  if (const char* e = getenv("GT_ATTN_MF")) d->attn_mf = atoi(e) != 0;
+  if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   *out = d;
   return GT_OK;
 }

@@ -60,9 +60,26 @@ struct AttnKVParams {
   void* rb_out; const float* mask; int T, T0, lvl;
 };
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
+
+// level-0 attention output (y = x + M_b x + g b_out, per-utterance 1x1) + Downsample (3x3 stride 2) in one pass, bf16,
+// C = 64 (attn_down.hip): y is never written (hiddens[0] is never read by the up path, diffusion.py:186-201)
+struct AttnDownParams {
+  const void* x; int B, F, T, C;   // attention input [B][F][T][C] (level-0 grid)
+  int T0; const float* mask; int lvl;
+  const void* mw; long mw_bstride;  // per-utterance 1x1 weight image M_b (wimage.h conv_wimg(1, 1, C, C)), stride in BYTES
+  const float* gb;                  // g * b_out [C]
+  const void* wds;                  // downsample weight in conv64's fragment order (decoder.cpp pack_conv64)
+  const float* bds;                 // downsample bias [C]
+  void* out;                        // [B][F/2][T/2][C]
+};
+bool attn_down_eligible(const AttnDownParams& p);
+hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s);
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              hipStream_t s);
 hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s);
+// attn_merge + attn_fold as one launch (bit-identical folded weights)
+hipError_t launch_attn_merge_fold(int act_bf16, const float* part, int B, int ntile, const float* wout, const float* g,
+                                  const float* wq, int C, void* Mw, hipStream_t s);
 
 struct FinalParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
