@@ -1,24 +1,25 @@
-// Level-0 attention output + Downsample as one pass (bf16, C = 64).
+// Attention output + Downsample as one pass (bf16): levels 0 (C = 64) and 1 (C = 128).
 //
-// Reference (model/diffusion.py:186-191, 30-36, 103-110): at the first U-Net level
+// Reference (model/diffusion.py:186-191, 30-36, 103-110): at the first two U-Net levels
 //     y = x + g * to_out(attn(x))                      Residual(Rezero(LinearAttention))
-//     hiddens.append(y); x = downsample(y * mask)      Conv2d(64, 64, 3, stride 2, padding 1)
-// and hiddens[0] is never popped (the up path has two levels; it pops the level-2 and level-1 entries), so the
-// 168 MB (B = 32, T = 512) level-0 attention output is only ever read by the downsample. With the attention folded
-// into one per-utterance 1x1 (attn.hip: y = x + M_b x + g b_out) both convolutions fit one kernel that never writes y:
+//     hiddens.append(y); x = downsample(y * mask)      Conv2d(C, C, 3, stride 2, padding 1)
+// hiddens[0] is never popped (the up path has two levels; it pops the level-2 and level-1 entries), so the 168 MB
+// (B = 32, T = 512) level-0 attention output is only ever read by the downsample; the level-1 one is also the skip
+// connection of ups.1. With the attention folded into one per-utterance 1x1 (attn.hip: y = x + M_b x + g b_out) both
+// convolutions fit one kernel:
 //
 //   stage 1  a workgroup's input patch (5 mel rows x 65 frames: the stride-2 3x3 window of 2 output rows x 32 output
 //            frames) -> y = (M_b x + g b_out) + x on MFMA (M_b as A, positions as B; the residual x is the B fragment
-//            itself), masked, rounded to bf16 into LDS;
-//   stage 2  the 3x3 stride-2 conv of the LDS patch (weights as A from the conv64-ordered image, L2-resident) + bias.
+//            itself), masked, rounded to bf16 into LDS (level 1: also stored to HBM, each position once);
+//   stage 2  the 3x3 stride-2 conv of the LDS patch (weights as A from a fragment-ordered image, L2-resident) + bias.
 //
 // Same operations in the same order as conv_kernel CONV1/OUT_RESID followed by conv_kernel CONV3_S2/IN_MASK (1x1 over
-// k-steps 0..3; the residual added after the bias; y rounded to bf16; x * m as a select for {0,1} masks; the 3x3 over
-// 16-channel chunks outer, taps inner; bias after), so the output is bit-identical to the two-kernel path
-// (tests/test_attn_down_gpu.py) while the HBM traffic drops from read x + write y + read y + write out to read x
-// (1.27x: the 5 x 65 patch of a 2 x 32 output tile) + write out.
+// k-steps in order; the residual added after the bias; y rounded to bf16; x * m as a select for {0,1} masks; the 3x3
+// over 16-channel chunks outer, taps inner; bias after), so the outputs are bit-identical to the two-kernel path
+// (tests/test_attn_down_gpu.py) while the HBM traffic drops from read x + write y + read y + write out to read x (1.27x:
+// the 5 x 65 patch of a 2 x 32 output tile) (+ write y at level 1) + write out.
 //
-// LDS patch: 8 planes (8 channels each) x 5 rows x 68 entries of 16 B, the 65 columns deinterleaved by parity (even
+// LDS patch: C/8 planes (8 channels each) x 5 rows x 68 entries of 16 B, the 65 columns deinterleaved by parity (even
 // columns at entries 0..32, odd ones at 36..67): a stride-2 tap then reads 32 CONSECUTIVE entries (conflict-free
 // ds_read_b128), and the stage-1 item writes (even and odd columns alternating) land 16 banks apart.
 #include "common.h"
@@ -28,19 +29,23 @@
 namespace gt {
 
 namespace ad {
-constexpr int C = 64, NTHR = 256;
 constexpr int PROWS = 5, PCOLS = 65, NPOS = PROWS * PCOLS;   // input patch of one 2 x 32 output tile
 constexpr int NPB = (NPOS + 31) / 32;                        // 11 position blocks of 32
 constexpr int ODD = 36, RS = 68;                             // odd-column offset and row stride (entries)
 constexpr int PLANE = PROWS * RS;                            // 340 entries
-constexpr int SMEM = 8 * PLANE * 16;                         // 43,520 B
+template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   // 43,520 B (C = 64) / 87,040 B (128)
 }  // namespace ad
 
 typedef unsigned u32x4a_t __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void attn_down_kernel(AttnDownParams p) {
+// C = 64: 4 waves, the level-0 form (the attention output is not needed). C = 128, WY: 8 waves, the level-1 form, which
+// also stores the attention output from stage 1 -- each position by the one tile whose patch holds it away from the
+// top / left halo (patch row >= 1, column >= 1).
+template <int C, bool WY>
+__global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ? 3 : 2))) void attn_down_kernel(AttnDownParams p) {
   using namespace ad;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  constexpr int NCB = C / 32;   // 32-channel blocks
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<C>()];
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int F = p.F, T = p.T, Fo = F / 2, To = T / 2;
@@ -54,47 +59,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 
   const int npos_all = p.B * F * T;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, npos_all * C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, WY ? npos_all * C * 2 : 0, 0x00020000);
   const int oob = npos_all * C * 2;
-
-  // ---- stage 1: y = (M_b x + g b_out) + x over the patch. Wave w: position blocks w, w+4, w+8 (< 11), both
-  // 32-channel halves (the x fragments are shared by the two halves). M_b fragments (A: output channel cb*32 + r,
-  // input channels 16 ks + 8h ..) from the per-utterance 1x1 image (wimage.h conv_wimg, as conv_kernel reads it).
   const WImg W1 = conv_wimg(1, 1, C, C);
   const char* mimg = reinterpret_cast<const char*>(p.mw) + (long)b * p.mw_bstride;
-  bf16x8 ma[2][4];
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-      ma[cb][ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
-  float gb[2][2][8];   // g b_out of this lane's channels after the swap: cb*32 + 16 pr + 8h + 0..7
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) gb[cb][pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
 
-  auto xfrags = [&](int pb, u32x4a_t* xf, float& m, bool& inside, int& ent) {
+  // position pb*32 + r of the patch: its x fragments (k-steps 0 .. C/16-1; out-of-range positions read zeros), mask,
+  // LDS entry, and (WY) the byte offset its attention output goes to (-1: not this tile's to store)
+  auto xfrags = [&](int pb, u32x4a_t* xf, float& m, int& ent, int& yoff) __attribute__((always_inline)) {
     const int pos = pb * 32 + r;
     const int prow = pos / PCOLS, pcol = pos - prow * PCOLS;
     const int fi = fi0 + prow, ti = ti0 + pcol;
-    inside = pos < NPOS && fi >= 0 && fi < F && ti >= 0 && ti < T;
+    const bool inside = pos < NPOS && fi >= 0 && fi < F && ti >= 0 && ti < T;
     const int off = inside ? ((b * F + fi) * T + ti) * (C * 2) + h * 16 : oob;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) xf[ks] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + ks * 32, 0, 0);
+    for (int ks = 0; ks < C / 16; ++ks) xf[ks] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + ks * 32, 0, 0);
     m = inside ? mask_at(p.mask, p.T0, b, ti, p.lvl) : 0.f;
     ent = pos < NPOS ? prow * RS + (pcol & 1) * ODD + (pcol >> 1) : -1;
+    yoff = (inside && prow >= 1 && pcol >= 1) ? ((b * F + fi) * T + ti) * (C * 2) : -1;
   };
-  {
-    // every x fragment of this wave's (up to 3) position blocks in flight at once: one HBM round trip, not three
+  // the epilogue of one 32 x 32 stage-1 block (channels cb*32.., positions of one block): the accumulator (M_b x), the
+  // bias g b_out, the residual (this lane's own x fragments of k-steps 2cb, 2cb+1) -> bf16 y -> LDS (masked), HBM (WY)
+  auto y_block = [&](const f32x16& acc, int cb, const float (*gbc)[8], const u32x4a_t* xf, float m, int ent,
+                     int yoff) __attribute__((always_inline)) {
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]), __float_as_uint(v[8 * pr + 4 + q]),
+                                                         false, false);
+        v[8 * pr + q] = __uint_as_float(sw[0]);
+        v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+      }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      float e[8], o[8];
+      const u32x4a_t xr = xf[2 * cb + pr];   // (cb compile-time at every call: no dynamic register indexing)
+      item_to_f(make_uint4(xr[0], xr[1], xr[2], xr[3]), e, bf16());
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o[k] = v[8 * pr + k] + gbc[pr][k];   // conv_kernel OUT_RESID: bias, then the residual
+        o[k] += e[k];
+      }
+      const uint4 ov = f_to_item(o, bf16());
+      const int c0 = cb * 32 + pr * 16 + 8 * h;
+      if (WY)   // the unmasked attention output, as conv_kernel OUT_RESID stores it
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4a_t{ov.x, ov.y, ov.z, ov.w}, rsy, yoff >= 0 ? yoff + c0 * 2 : oob, 0, 0);
+      // y * mask as the downsample's IN_MASK select ({0,1} masks; a fractional mask multiplies the bf16 value)
+      u32x4a_t y;
+      if (m == 1.f) {
+        y = u32x4a_t{ov.x, ov.y, ov.z, ov.w};
+      } else if (m == 0.f) {
+        y = u32x4a_t{0u, 0u, 0u, 0u};
+      } else {
+        float t[8];
+        item_to_f(ov, t, bf16());
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k] *= m;
+        const uint4 tv = f_to_item(t, bf16());
+        y = u32x4a_t{tv.x, tv.y, tv.z, tv.w};
+      }
+      if (ent >= 0) *reinterpret_cast<u32x4a_t*>(smem + ((c0 >> 3) * PLANE + ent) * 16) = y;   // plane = c0 / 8
+    }
+  };
+
+  if constexpr (C == 64) {
+    // ---- stage 1, 4 waves: wave w takes position blocks w, w+4, w+8 (< 11) and both 32-channel halves (the x fragments
+    // are shared by the two halves); every x fragment of the wave in flight at once (one HBM round trip)
+    bf16x8 ma[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        ma[cb][ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+    float gb[2][2][8];   // g b_out of this lane's channels after the swap: cb*32 + 16 pr + 8h + 0..7
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gb[cb][pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
     constexpr int NPW = (NPB + 3) / 4;
     u32x4a_t xf[NPW][4];
     float m[NPW];
-    bool inside[NPW];
-    int ent[NPW];
+    int ent[NPW], yoff[NPW];
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) xfrags(wv + 4 * i < NPB ? wv + 4 * i : NPB, xf[i], m[i], inside[i], ent[i]);
+    for (int i = 0; i < NPW; ++i) xfrags(wv + 4 * i < NPB ? wv + 4 * i : NPB, xf[i], m[i], ent[i], yoff[i]);
 #pragma unroll
     for (int i = 0; i < NPW; ++i) {
       if (wv + 4 * i >= NPB) break;   // wave-uniform
@@ -109,57 +162,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
           __builtin_memcpy(&xb, &xf[i][ks], 16);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb][ks], xb, acc, 0, 0, 0);
         }
-        float v[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = acc[q];
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]),
-                                                             __float_as_uint(v[8 * pr + 4 + q]), false, false);
-            v[8 * pr + q] = __uint_as_float(sw[0]);
-            v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
-          }
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          // the residual: channels cb*32 + 16 pr + 8h .. of this lane's position = its own x fragment of k-step 2cb+pr
-          float e[8], o[8];
-          const u32x4a_t xr = xf[i][2 * cb + pr];
-          item_to_f(make_uint4(xr[0], xr[1], xr[2], xr[3]), e, bf16());
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            o[k] = v[8 * pr + k] + gb[cb][pr][k];   // conv_kernel OUT_RESID: bias, then the residual
-            o[k] += e[k];
-          }
-          const uint4 ov = f_to_item(o, bf16());
-          // y * mask as the downsample's IN_MASK select ({0,1} masks; a fractional mask multiplies the bf16 value)
-          u32x4a_t y;
-          if (m[i] == 1.f) {
-            y = u32x4a_t{ov.x, ov.y, ov.z, ov.w};
-          } else if (m[i] == 0.f) {
-            y = u32x4a_t{0u, 0u, 0u, 0u};
-          } else {
-            float t[8];
-            item_to_f(ov, t, bf16());
-#pragma unroll
-            for (int k = 0; k < 8; ++k) t[k] *= m[i];
-            const uint4 tv = f_to_item(t, bf16());
-            y = u32x4a_t{tv.x, tv.y, tv.z, tv.w};
-          }
-          if (ent[i] >= 0) {
-            const int q = cb * 4 + pr * 2 + h;   // 8-channel plane
-            *reinterpret_cast<u32x4a_t*>(smem + (q * PLANE + ent[i]) * 16) = y;
-          }
-        }
+        y_block(acc, cb, gb[cb], xf[i], m[i], ent[i], yoff[i]);
       }
+    }
+  } else {
+    // ---- stage 1, C / 16 waves: wave w takes the 32-channel block cb = w % NCB (its M_b fragments stay in registers)
+    // and position blocks w / NCB, + 2, + 4, ... (< 11); the next block's x fragments are loaded during this one's MFMAs
+    const int grp = wv / NCB;
+    constexpr int NKS = C / 16;
+    auto stage1 = [&](auto CBc) __attribute__((always_inline)) {
+      constexpr int cb = decltype(CBc)::value;
+      static_assert(4 * C / 64 == 2 * NCB, "two position-block groups");
+      bf16x8 ma[NKS];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        ma[ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+      float gb[2][8];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gb[pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
+      u32x4a_t xf[2][NKS];
+      float m[2];
+      int ent[2], yoff[2];
+      xfrags(grp, xf[0], m[0], ent[0], yoff[0]);
+      auto step = [&](auto Ic) __attribute__((always_inline)) {   // position block grp + 2 i (i compile-time)
+        constexpr int i = decltype(Ic)::value, cur = i & 1;
+        const int pb = grp + 2 * i;
+        if (pb >= NPB) return;   // wave-uniform
+        if (pb + 2 < NPB) xfrags(pb + 2, xf[cur ^ 1], m[cur ^ 1], ent[cur ^ 1], yoff[cur ^ 1]);
+        f32x16 acc;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          bf16x8 xb;
+          __builtin_memcpy(&xb, &xf[cur][ks], 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[ks], xb, acc, 0, 0, 0);
+        }
+        y_block(acc, cb, gb, xf[cur], m[cur], ent[cur], yoff[cur]);
+      };
+      static_assert((NPB + 1) / 2 == 6, "six position blocks per group");
+      step(std::integral_constant<int, 0>{}); step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{}); step(std::integral_constant<int, 3>{});
+      step(std::integral_constant<int, 4>{}); step(std::integral_constant<int, 5>{});
+    };
+    switch (wv % NCB) {   // wave-uniform
+      case 0: stage1(std::integral_constant<int, 0>{}); break;
+      case 1: stage1(std::integral_constant<int, 1>{}); break;
+      case 2: stage1(std::integral_constant<int, 2 % NCB>{}); break;
+      default: stage1(std::integral_constant<int, 3 % NCB>{}); break;
     }
   }
 
-  // ---- stage 2: 3x3 stride-2 conv of the patch. Wave w: output channels cb*32.. (cb = w & 1) of output row orow =
-  // w >> 1, 32 output frames; k-steps (16-channel chunk ch, tap) in conv_kernel's order (chunk outer, tap inner).
-  const int cb = wv & 1, orow = wv >> 1;
-  const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(p.wds) + cb * 4 * 9 * 64 + lane;   // pack_conv64 order
+  // ---- stage 2: 3x3 stride-2 conv of the patch. Wave w: output channels cb*32.. (cb = w % NCB) of output row
+  // orow = w / NCB, 32 output frames; k-steps (16-channel chunk ch, tap) in conv_kernel's order (chunk outer, tap inner).
+  const int cb = wv % NCB, orow = wv / NCB;
+  const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(p.wds) + cb * (C / 16) * 9 * 64 + lane;   // pack_frag3x3 order
   auto aread = [&](int st) { return wsrc[st * 64]; };   // st = ch * 9 + tap
   auto bread = [&](int st) {
     const int ch = st / 9, tap = st % 9, dr = tap / 3, dc = tap - 3 * dr;
@@ -167,7 +226,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
     return *reinterpret_cast<const bf16x8*>(smem + ((2 * ch + h) * PLANE + ent) * 16);
   };
   // weight fragments (L2) PFA steps ahead, patch fragments (LDS) PFB steps ahead
-  constexpr int PFA = 10, NBA = PFA + 1, PFB = 3, NBB = PFB + 1, NST = 36;
+  constexpr int PFA = 10, NBA = PFA + 1, PFB = 3, NBB = PFB + 1, NST = 9 * C / 16;
   bf16x8 af[NBA], bf[NBB];
 #pragma unroll
   for (int st = 0; st < PFA; ++st) af[st] = aread(st);
@@ -210,13 +269,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void a
 }
 
 bool attn_down_eligible(const AttnDownParams& p) {
-  return p.C == 64 && p.F % 4 == 0 && p.T % 2 == 0 && (long)p.B * p.F * p.T * 128 < (1L << 31);
+  return ((p.C == 64 && !p.y) || (p.C == 128 && p.y)) && p.F % 4 == 0 && p.T % 2 == 0 && (long)p.B * p.F * p.T * p.C * 2 < (1L << 31);
 }
 
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
   if (!attn_down_eligible(p)) return hipErrorInvalidValue;
   const long grid = (long)p.B * (p.F / 4) * ((p.T / 2 + 31) / 32);
-  hipLaunchKernelGGL(attn_down_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
+  if (p.C == 64) {
+    hipLaunchKernelGGL((attn_down_kernel<64, false>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((attn_down_kernel<128, true>), dim3((unsigned)grid), dim3(512), 0, s, p);
+  }
   return hipGetLastError();
 }
 

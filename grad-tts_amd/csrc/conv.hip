@@ -69,6 +69,12 @@ struct ConvCfg {
   static constexpr int PAD = (KIND == CONV1) ? 0 : 1;
   static constexpr int PR = (TF - 1) * S + KS;
   static constexpr int PC = (TT - 1) * S + KS;
+  // stride 2: the patch columns of a row are stored deinterleaved by parity (even columns at 0 .. ODDC-1, odd ones from
+  // ODDC), so a tap's 32 lanes (columns 2r + dc) read 32 CONSECUTIVE positions: with 48-B positions a stride of two
+  // (96 B = 6 slots) put lanes 8 apart on the same banks (2-way conflicts); consecutive ones (3 slots) never do
+  static constexpr bool DEINT = KIND == CONV3_S2;
+  static constexpr int ODDC = (PC + 1) / 2;
+  static constexpr __host__ __device__ int pcol(int pc) { return DEINT ? ((pc & 1) ? ODDC + (pc >> 1) : (pc >> 1)) : pc; }
   // W8 == 2 (A8): fp8 operands on v_mfma_scale_f32_32x32x64_f8f6f4 -- 32-channel chunks of e4m3 activations
   // (32 B per position in LDS + an E8M0 scale byte in the pad) and the conv_wimga8 weight image
   static constexpr bool A8 = W8 == 2;
@@ -322,7 +328,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
     for (int j = 0; j < C::PPT; ++j) {
       const int it = tid + 256 * j;
       if (it < C::PITEMS) {
-        char* dst = sA + (it / C::SUBS) * C::POSB + sub * 16;
+        const int ipos = it / C::SUBS, ipr = ipos / C::PC;
+        char* dst = sA + (ipr * C::PC + C::pcol(ipos - ipr * C::PC)) * C::POSB + sub * 16;
         const u32x4 u = preg[j];
         if (IN == IN_PLAIN || (IN == IN_MASK && !frac)) {   // zeros already came from the range check
           *reinterpret_cast<u32x4*>(dst) = u;
@@ -422,12 +429,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   // ConvTranspose2d(k4, s2, p1): out[2j+p] takes in[j] (k=1) & in[j-1] (k=3) for p=0, in[j+1] (k=0) & in[j]
   // (k=2) for p=1; with the patch origin at (j0-1, j0'-1) tap (a, b) reads patch row 1 + pf - a, column
   // 1 + pt - b. The parity part goes into the base.
-  const int a_base = ((wm / C::RBT) * C::S * C::PC + ((wm % C::RBT) * 32 + r) * C::S +
+  const int a_base = ((wm / C::RBT) * C::S * C::PC + ((wm % C::RBT) * 32 + r) * (C::DEINT ? 1 : C::S) +
                       (CONVT ? (1 + pf) * C::PC + 1 + pt : 0)) * C::POSB + h * (C::KSTEP_B / 2);
   auto load_a = [&](int tap, int rb, int ks) {
     const int dr = CONVT ? -(tap >> 1) : tap / C::KS;
     const int dc = CONVT ? -(tap & 1) : tap % C::KS;
-    const int off = ((rb * (C::WM / C::RBT) * C::S + dr) * C::PC + dc) * C::POSB + ks * C::KSTEP_B;
+    const int dci = C::DEINT ? (dc == 1 ? C::ODDC : dc >> 1) : dc;   // (stride 2: column 2r + dc, deinterleaved)
+    const int off = ((rb * (C::WM / C::RBT) * C::S + dr) * C::PC + dci) * C::POSB + ks * C::KSTEP_B;
     return Mma<A>::load(sA + a_base + off);
   };
   auto load_b = [&](int tap, int cb, int ks) {

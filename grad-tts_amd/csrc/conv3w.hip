@@ -69,6 +69,10 @@ namespace gt {
 #ifndef GT_C3W_LGK
 #define GT_C3W_LGK 1   // phase barrier waits for all LDS ops but the next phase's pre-reads (0: lgkmcnt(0))
 #endif
+#ifndef GT_C3W_BAR2
+#define GT_C3W_BAR2 0  // one workgroup barrier per TWO phases (even taps of a chunk, plus tap 8): the weight ring keeps
+                       // one more slot between the DMA target and the slots still being read (D = S - 2)
+#endif
 #ifndef GT_C3W_SCHED
 #define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
 #endif
@@ -91,7 +95,7 @@ struct Cfg {
   static constexpr int PWMAX = (PIECES + NW - 1) / NW;
   static constexpr int PWLO = PIECES / NW;         // pieces of waves >= PIECES % NW
   static constexpr int S = BN == 256 ? GT_C3W_S256 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
-  static constexpr int D = S - 1;                  // DMA issue distance in phases
+  static constexpr int D = GT_C3W_BAR2 ? S - 2 : S - 1;   // DMA issue distance in phases
   static constexpr int ITEMS = PP * 4;             // 16-B patch items per chunk
   static constexpr int NPT = (ITEMS + NTHR - 1) / NTHR;
   static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
@@ -104,7 +108,8 @@ struct Cfg {
   static constexpr int SMEM = OFF_F + NF * 4;
   static_assert(WN * WM == NW && WN >= 1, "wave grid");
   static_assert(PIECES * 1024 == SLOT, "whole DMA pieces");
-  static_assert(D >= 2 && D <= 8, "DMA distance");
+  static_assert(D >= (GT_C3W_BAR2 ? 3 : 2) && D <= 8, "DMA distance");
+  static_assert(!(GT_C3W_BAR2 && GT_C3W_DMAS), "two-phase barriers assume the DMA issue at the top of the phase");
   static_assert(NPT <= 6, "items transformed in phases 2..7");
   static_assert(SMEM <= 160 * 1024, "LDS budget: one workgroup per CU");
   static_assert(PBUF >= 272 * 8, "s_red aliases patch buffer 1");
@@ -315,11 +320,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   auto top_wait = [&](auto Tc, auto MOREc) {
     constexpr int t = decltype(Tc)::value;
     constexpr bool MORE = decltype(MOREc)::value;
-    constexpr int ndma = MORE ? C::D - 2 : ((7 - t) < (C::D - 2) ? ((7 - t) > 0 ? 7 - t : 0) : C::D - 2);
+    // GT_C3W_BAR2: phases at odd taps have no wait and no barrier; an even one (taps 0, 2, 4, 6, 8) retires DMA(k+1)
+    // AND DMA(k+2): slot k+1 is pre-read at the end of this phase, slot k+2 at the end of phase k+1, which has no
+    // barrier of its own (W = 2). The DMA of an odd phase overwrites the slot of phase k+D-S = k-2, finished by every
+    // wave before this barrier.
+    constexpr bool skip = GT_C3W_BAR2 && (t & 1);
+    constexpr int W = GT_C3W_BAR2 ? 2 : 1;
+    // DMAs issued after DMA(k+W) before the top of phase k: up to DMA(k-1+D), or DMA(K-1) in the last chunk
+    constexpr int ndma0 = MORE ? C::D - 1 - W : ((8 - t - W) < (C::D - 1 - W) ? (8 - t - W) : (C::D - 1 - W));
+    constexpr int ndma = ndma0 > 0 ? ndma0 : 0;
     // waves 0-3 issue a phase's DMA before its item, waves 4-7 (GT_C3W_DMAS) after it: an item loaded in phase
-    // k + 1 - D is younger than DMA(k+1) only in the first half
-    constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
-    constexpr int npl4 = MORE ? n_lp(t + 2 - C::D, t - 1) : 0;
+    // k + W - D is younger than DMA(k+W) only in the first half
+    constexpr int npl = MORE ? n_lp(t + W - C::D, t - 1) : 0;
+    constexpr int npl4 = MORE ? n_lp(t + W + 1 - C::D, t - 1) : 0;
+    if (skip) { if (STAMP) st[5] += 1; return; }
     const unsigned long long a = stamp();
     if (!(GT_C3W_VAR & 2)) {
       if (!GT_C3W_DMAS || wv < c3w::NW / 2) vm_wait<ndma * PW + npl>();
@@ -381,7 +395,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   lds_barrier();
 #pragma unroll
   for (int j = 0; j < C::NPT; ++j) put_item(j, 0, 0);
-  vm_wait<(C::D - 2) * PW>();   // DMA(0), DMA(1) landed (younger: DMA(2 .. D-1)); chunk 0's patch written
+  // DMA(0) .. DMA(W) landed (W = 2 with two-phase barriers, else 1; younger: DMA(W+1 .. D-1)); chunk 0's patch written
+  vm_wait<(C::D - 1 - (GT_C3W_BAR2 ? 2 : 1)) * PW>();
   lds_barrier();
 
   // MFMA steps i = s * RB + rb of a phase; fragments are read two steps ahead (B: ring of 3 by the chunk-global step

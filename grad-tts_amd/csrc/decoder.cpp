@@ -182,8 +182,10 @@ struct gt_decoder {
   bool wide = true;
   // attention merge + fold as one launch (attn_mf_kernel); GT_ATTN_MF=1 at creation (off: slower at B = 32)
   bool attn_mf = false;
-  // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
+  // level-0/1 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
   bool attn_ds = true;
+  // ... and at level 1 (GT_ATTN_DS1=1; off: the C = 128 form measured 236 us against 101 us for the two launches)
+  bool attn_ds1 = false;
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -391,6 +393,23 @@ void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w
   blob.put(key, img.data(), img.size() * 2);
 }
 
+// pack a 3x3 [Cout][Cin][3][3] weight as MFMA A fragments (attn_down.hip's stride-2 stage), bf16:
+// [cb Cout/32][chunk Cin/16][tap 9][lane 64][8 ci]: lane (r, h) = output channel 32 cb + r, input channels 16 chunk + 8h ..
+// (for 64 -> 64 the same bytes as pack_conv64)
+void pack_frag3x3(Blob& blob, const std::string& key, const std::vector<float>& w, int cout, int cin) {
+  std::vector<uint16_t> img((size_t)cout * cin * 9);
+  size_t i = 0;
+  for (int cb = 0; cb < cout / 32; ++cb)
+    for (int ch = 0; ch < cin / 16; ++ch)
+      for (int tap = 0; tap < 9; ++tap)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int k = 0; k < 8; ++k) {
+            const int co = cb * 32 + (lane & 31), ci = ch * 16 + (lane >> 5) * 8 + k;
+            img[i++] = f2bf(w[((size_t)co * cin + ci) * 9 + tap]);
+          }
+  blob.put(key, img.data(), img.size() * 2);
+}
+
 // pack a 3x3 [Cout][Cin][3][3] weight (Cin % 32 == 0) in conv3w's slot order (conv3w.hip), bf16: one slot per
 // (32-channel chunk c, tap t) in phase order k = 9 c + t, each [plane q 0..3][co][8 channels 32 c + 8 q ..] -- the LDS
 // image of a weight slot, so staging one is a straight DMA
@@ -470,8 +489,9 @@ int prepare(gt_decoder* d, int code) {
       if (c64) pack_conv64(blob, k + ".w64", w);
       if (code == GT_BF16 && ends_with(k, ".block.0.weight") && !c64 && conv3w_shape(shp))
         pack_conv3w(blob, k + ".w3w", w, (int)shp[0], (int)shp[1]);
-      if (code == GT_BF16 && starts_with(k, "downs.") && ends_with(k, ".3.conv.weight") && shp[0] == 64 && shp[1] == 64)
-        pack_conv64(blob, k + ".w64", w);   // the level-0 Downsample of attn_down_kernel
+      if (code == GT_BF16 && starts_with(k, "downs.") && ends_with(k, ".3.conv.weight") && shp[0] == shp[1] &&
+          (shp[0] == 64 || shp[0] == 128))
+        pack_frag3x3(blob, k + ".wfr", w, (int)shp[0], (int)shp[1]);   // the Downsample of attn_down_kernel
       if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
@@ -832,19 +852,22 @@ struct Run {
   // level 0: the attention output and the Downsample after it as one pass (attn_down.hip; the attention output is
   // never materialised). false (nothing launched) when not applicable: another dtype, the fused form disabled
   // (GT_ATTN_DS=0), or a probe of the attention output itself.
-  bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* out) {
-    if (!(dt && wi == GT_BF16 && d->attn_ds && lvl == 0 && C == 64 && d->dp[wi].count(kd + "conv.weight.w64")))
-      return false;
-    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
+  // y: where the attention output goes (level 1: the skip connection of ups.1), or null (level 0: never read)
+  bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* y, void* out) {
+    if (!(dt && wi == GT_BF16 && d->attn_ds && d->dp[wi].count(kd + "conv.weight.wfr"))) return false;
+    if (lvl == 1 && !d->attn_ds1) return false;
+    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1) && !y) return false;
     AttnDownParams a{};
     a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
     a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
-    a.wds = W(kd + "conv.weight.w64"); a.bds = Fp(kd + "conv.bias"); a.out = out;
+    a.wds = W(kd + "conv.weight.wfr"); a.bds = Fp(kd + "conv.bias"); a.out = out; a.y = y;
     if (!attn_down_eligible(a)) return false;
     attention_fold(ka, lvl, in, C);
     const double pin = (double)B * a.F * a.T, pout = pin / 4;
     timed("attn_down_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
-          2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin + pout) * C * 2.0, [&] { return launch_attn_down(a, s); });
+          2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin * (y ? 2.0 : 1.0) + pout) * C * 2.0,
+          [&] { return launch_attn_down(a, s); });
+    if (y) tap(ka.substr(0, ka.size() - 1), lvl, y, C);
     tap(kd.substr(0, kd.size() - 1), lvl + 1, out, C);
     return true;
   }
@@ -929,15 +952,17 @@ struct Run {
     // down 0 (80 x T, 64 ch)
     resnet("downs.0.0.", 0, nullptr, 0, nullptr, 0, 64, act(0, 0), next_tb(64));
     resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64), true);
-    if (!attention_down("downs.0.2.", "downs.0.3.", 0, act(0, 1), 64, act(1, 0))) {
+    if (!attention_down("downs.0.2.", "downs.0.3.", 0, act(0, 1), 64, nullptr, act(1, 0))) {
       attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
       downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
     }
     // down 1 (40 x T/2, 128 ch); hidden 1 -> act(1,2)
     resnet("downs.1.0.", 1, act(1, 0), 64, nullptr, 0, 128, act(1, 1), next_tb(128));
     resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128), true);
-    attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
-    downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
+    if (!attention_down("downs.1.2.", "downs.1.3.", 1, act(1, 0), 128, act(1, 2), act(2, 0))) {
+      attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
+      downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
+    }
     // down 2 (20 x T/4, 256 ch); hidden 2 -> act(2,2); Identity(x*mask) is absorbed by the next block's mask
     resnet("downs.2.0.", 2, act(2, 0), 128, nullptr, 0, 256, act(2, 1), next_tb(256));
     resnet("downs.2.1.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256), true);
@@ -1045,6 +1070,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_MF")) d->attn_mf = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
+  if (const char* e = getenv("GT_ATTN_DS1")) d->attn_ds1 = atoi(e) != 0;
   *out = d;
   return GT_OK;
 }

@@ -61,16 +61,18 @@ struct AttnKVParams {
 };
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
 
-// level-0 attention output (y = x + M_b x + g b_out, per-utterance 1x1) + Downsample (3x3 stride 2) in one pass, bf16,
-// C = 64 (attn_down.hip): y is never written (hiddens[0] is never read by the up path, diffusion.py:186-201)
+// attention output (y = x + M_b x + g b_out, per-utterance 1x1) + Downsample (3x3 stride 2) in one pass, bf16
+// (attn_down.hip): level 0 (C = 64, y = null: hiddens[0] is never read by the up path, diffusion.py:186-201) and level 1
+// (C = 128, y = the skip connection, written once per position)
 struct AttnDownParams {
   const void* x; int B, F, T, C;   // attention input [B][F][T][C] (level-0 grid)
   int T0; const float* mask; int lvl;
   const void* mw; long mw_bstride;  // per-utterance 1x1 weight image M_b (wimage.h conv_wimg(1, 1, C, C)), stride in BYTES
   const float* gb;                  // g * b_out [C]
-  const void* wds;                  // downsample weight in conv64's fragment order (decoder.cpp pack_conv64)
+  const void* wds;                  // downsample weight in fragment order (decoder.cpp pack_frag3x3)
   const float* bds;                 // downsample bias [C]
   void* out;                        // [B][F/2][T/2][C]
+  void* y;                          // C = 128: the attention output [B][F][T][C]; C = 64: null
 };
 bool attn_down_eligible(const AttnDownParams& p);
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s);

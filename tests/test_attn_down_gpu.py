@@ -1,8 +1,9 @@
-"""attn_down_kernel (csrc/attn_down.hip): the level-0 attention output and the Downsample after it in one pass.
+"""attn_down_kernel (csrc/attn_down.hip): the attention output and the Downsample after it in one pass (levels 0, 1).
 
 The kernel performs the same operations in the same order as conv_kernel CONV1/OUT_RESID followed by conv_kernel
 CONV3_S2/IN_MASK, so a decoder built with GT_ATTN_DS=1 (the default) must produce bit-identical estimator outputs,
-samples and level-1 activations to one built with GT_ATTN_DS=0, on ragged batches (frames past an utterance's length
+samples, downsample outputs and (level 1) attention outputs -- the skip connection the fused kernel stores -- to one
+built with GT_ATTN_DS=0, on ragged batches (frames past an utterance's length
 masked; T not a multiple of 64: a partial last 32-frame output tile) and with 247 speakers. The fused path's
 downsample output is also checked against the fp32 oracle (the "downs.0.3" stage probe takes the fused path; probing
 "downs.0.2", the attention output the fused path never writes, falls back to the two launches)."""
@@ -35,14 +36,17 @@ def test_attn_down_bit_identical(monkeypatch, n_spks, B, T, lengths):
     res = {}
     for ds in (1, 0):
         monkeypatch.setenv("GT_ATTN_DS", str(ds))
+        monkeypatch.setenv("GT_ATTN_DS1", str(ds))   # the level-1 form (off by default) checked too
         dec, _ = make_decoder(n_spks, 11, torch.bfloat16)
         z_, m_, mu_, t_, s_ = args
         est = dec.estimator(z_, m_, mu_, t_, s_)
         y = dec(z_, m_, mu_, 3, spk=s_)
         _, lvl1 = probe(dec.estimator, torch.bfloat16, z_, m_, mu_, t_, s_, "downs.0.3", (B, 64, 40, T // 2))
+        _, att1 = probe(dec.estimator, torch.bfloat16, z_, m_, mu_, t_, s_, "downs.1.2", (B, 128, 40, T // 2))
+        _, lvl2 = probe(dec.estimator, torch.bfloat16, z_, m_, mu_, t_, s_, "downs.1.3", (B, 128, 20, T // 4))
         torch.cuda.synchronize()
-        res[ds] = (est.cpu(), y.cpu(), lvl1.cpu())
-    for a, b_, name in zip(res[1], res[0], ("estimator", "sampler N=3", "downs.0.3")):
+        res[ds] = (est.cpu(), y.cpu(), lvl1.cpu(), att1.cpu(), lvl2.cpu())
+    for a, b_, name in zip(res[1], res[0], ("estimator", "sampler N=3", "downs.0.3", "downs.1.2", "downs.1.3")):
         assert torch.isfinite(a).all(), name
         assert torch.equal(a, b_), f"{name}: max |diff| {float((a - b_).abs().max())}"
 
@@ -58,7 +62,7 @@ def test_attn_down_stage_vs_oracle():
         odec.estimator(odec.to_torch_params(sd), torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu),
                        torch.from_numpy(t), None, n_spks=1, taps=taps)
     args = [_cuda(a) for a in (z, mask, mu, t)]
-    for st in ("downs.0.2", "downs.0.3"):
+    for st in ("downs.0.2", "downs.0.3", "downs.1.2", "downs.1.3"):
         r = taps[st].numpy()
         _, pr = probe(dec.estimator, torch.bfloat16, *args, None, st, r.shape)
         report(f"attn_down stage {st}", rel_err(pr.cpu().numpy(), r), 2e-2)
