@@ -283,4 +283,185 @@ hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- attention output + Upsample (ConvTranspose2d(64, 64, 4, 2, 1)) as one pass: ups.1 (diffusion.py:201-205), whose
+// attention output (level 1, 64 channels) feeds only the upsample. Stage 1 as above on a coarse patch of 6 rows x 34
+// frames (the 4 x 32 coarse positions of the tile plus a one-position halo); stage 2 the four sub-pixel 2x2 convs of
+// conv_kernel CONVT4 (out[2J + pf][2K + pt] from coarse rows J + pf - a, columns K + pt - b, taps (a, b)), wave w taking
+// parity w, in conv_kernel's order (16-channel chunk outer, tap inner): bit-identical to the two launches.
+namespace au {
+constexpr int PROWS = 6, PCOLS = 34, NPOS = PROWS * PCOLS, NPB = (NPOS + 31) / 32;   // 204 positions, 7 blocks
+constexpr int PLANE = NPOS;                                                          // entries per 8-channel plane
+constexpr int SMEM = 8 * PLANE * 16;                                                 // 26,112 B
+}  // namespace au
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_up_kernel(AttnUpParams p) {
+  using namespace au;
+  constexpr int C = 64;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int F = p.F, T = p.T;                     // coarse grid
+  const int n_tt = (T + 31) / 32, n_ft = F / 4;
+  int bid = blockIdx.x;
+  const int tt = bid % n_tt; bid /= n_tt;
+  const int ft = bid % n_ft;
+  const int b = bid / n_ft;
+  const int J0 = 4 * ft, K0 = 32 * tt;
+  const int fi0 = J0 - 1, ti0 = K0 - 1;           // patch origin (coarse)
+  const int npos_all = p.B * F * T;
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, npos_all * C * 2, 0x00020000);
+  const int oob = npos_all * C * 2;
+
+  // ---- stage 1: y = (M_b x + g b_out) + x, masked, into LDS. Wave w: position blocks w, w + 4 (< 7), both halves.
+  {
+    const WImg W1 = conv_wimg(1, 1, C, C);
+    const char* mimg = reinterpret_cast<const char*>(p.mw) + (long)b * p.mw_bstride;
+    bf16x8 ma[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        ma[cb][ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+    u32x4a_t xf[2][4];
+    float m[2];
+    int ent[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int pos = (wv + 4 * i) * 32 + r;
+      const int prow = pos / PCOLS, pcol = pos - prow * PCOLS;
+      const int fi = fi0 + prow, ti = ti0 + pcol;
+      const bool inside = pos < NPOS && fi >= 0 && fi < F && ti >= 0 && ti < T;
+      const int off = inside ? ((b * F + fi) * T + ti) * (C * 2) + h * 16 : oob;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) xf[i][ks] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + ks * 32, 0, 0);
+      m[i] = inside ? mask_at(p.mask, p.T0, b, ti, p.lvl) : 0.f;
+      ent[i] = pos < NPOS ? pos : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (wv + 4 * i >= NPB) break;   // wave-uniform
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        f32x16 acc;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          bf16x8 xb;
+          __builtin_memcpy(&xb, &xf[i][ks], 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb][ks], xb, acc, 0, 0, 0);
+        }
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]),
+                                                             __float_as_uint(v[8 * pr + 4 + q]), false, false);
+            v[8 * pr + q] = __uint_as_float(sw[0]);
+            v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+          }
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int c0 = cb * 32 + pr * 16 + 8 * h;
+          float e[8], o[8];
+          const u32x4a_t xr = xf[i][2 * cb + pr];
+          item_to_f(make_uint4(xr[0], xr[1], xr[2], xr[3]), e, bf16());
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            o[k] = v[8 * pr + k] + p.gb[c0 + k];   // conv_kernel OUT_RESID: bias, then the residual
+            o[k] += e[k];
+          }
+          const uint4 ov = f_to_item(o, bf16());
+          u32x4a_t y;   // y * mask: conv_kernel CONVT4 IN_MASK's select ({0,1} masks), multiply otherwise
+          if (m[i] == 1.f) {
+            y = u32x4a_t{ov.x, ov.y, ov.z, ov.w};
+          } else if (m[i] == 0.f) {
+            y = u32x4a_t{0u, 0u, 0u, 0u};
+          } else {
+            float t[8];
+            item_to_f(ov, t, bf16());
+#pragma unroll
+            for (int k = 0; k < 8; ++k) t[k] *= m[i];
+            const uint4 tv = f_to_item(t, bf16());
+            y = u32x4a_t{tv.x, tv.y, tv.z, tv.w};
+          }
+          if (ent[i] >= 0) *reinterpret_cast<u32x4a_t*>(smem + ((c0 >> 3) * PLANE + ent[i]) * 16) = y;
+        }
+      }
+    }
+  }
+
+  // ---- stage 2: wave w = sub-pixel parity (pf, pt) = (w >> 1, w & 1); for each 32-channel half cb and coarse row j of
+  // the tile: 16 k-steps (chunk ch of 16 channels, tap (a, b) = (t >> 1, t & 1)) -> fine row 2 (J0 + j) + pf, fine
+  // columns 2 (K0 + r) + pt. Weights: the parity's fragment image (pack_fragT), A operand, 16 fragments per half.
+  const int pf = wv >> 1, pt = wv & 1;
+  const int Ff = 2 * F, Tf = 2 * T;
+  const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(p.wup) + wv * 2 * 16 * 64 + lane;   // [par][cb][ch][tap][lane]
+  lds_barrier();
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    bf16x8 wa[16];
+#pragma unroll
+    for (int st = 0; st < 16; ++st) wa[st] = wsrc[(cb * 16 + st) * 64];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      auto bread = [&](int st) {
+        const int ch = st >> 2, tap = st & 3, a = tap >> 1, bb = tap & 1;
+        const int ent = (j + 1 + pf - a) * PCOLS + (r + 1 + pt - bb);
+        return *reinterpret_cast<const bf16x8*>(smem + ((2 * ch + h) * PLANE + ent) * 16);
+      };
+      constexpr int PFB = 3, NBB = PFB + 1;
+      bf16x8 bf[NBB];
+#pragma unroll
+      for (int st = 0; st < PFB; ++st) bf[st] = bread(st);
+      f32x16 acc;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        if (st + PFB < 16) bf[(st + PFB) % NBB] = bread(st + PFB);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[st], bf[st % NBB], acc, 0, 0, 0);
+      }
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]),
+                                                           __float_as_uint(v[8 * pr + 4 + q]), false, false);
+          v[8 * pr + q] = __uint_as_float(sw[0]);
+          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        }
+      const int frow = 2 * (J0 + j) + pf, fcol = 2 * (K0 + r) + pt;
+      if (K0 + r < T) {
+        bf16* out = reinterpret_cast<bf16*>(p.out) + (((long)b * Ff + frow) * Tf + fcol) * C;
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int c0 = cb * 32 + pr * 16 + 8 * h;
+          float o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] + p.bup[c0 + k];
+          *reinterpret_cast<uint4*>(out + c0) = f_to_item(o, bf16());
+        }
+      }
+    }
+  }
+}
+
+bool attn_up_eligible(const AttnUpParams& p) {
+  return p.C == 64 && p.F % 4 == 0 && (long)p.B * 4 * p.F * p.T * 128 < (1L << 31);
+}
+
+hipError_t launch_attn_up(const AttnUpParams& p, hipStream_t s) {
+  if (!attn_up_eligible(p)) return hipErrorInvalidValue;
+  const long grid = (long)p.B * (p.F / 4) * ((p.T + 31) / 32);
+  hipLaunchKernelGGL(attn_up_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 }  // namespace gt

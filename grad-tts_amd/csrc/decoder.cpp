@@ -186,6 +186,8 @@ struct gt_decoder {
   bool attn_ds = true;
   // ... and at level 1 (GT_ATTN_DS1=1; off: the C = 128 form measured 236 us against 101 us for the two launches)
   bool attn_ds1 = false;
+  // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
+  bool attn_us = true;
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -410,6 +412,26 @@ void pack_frag3x3(Blob& blob, const std::string& key, const std::vector<float>& 
   blob.put(key, img.data(), img.size() * 2);
 }
 
+// pack a ConvTranspose2d [Cin][Cout][4][4] weight (stride 2, padding 1) as MFMA A fragments of its four sub-pixel 2x2
+// convs (attn_up_kernel), bf16: [parity 2 pf + pt][cb Cout/32][chunk Cin/16][tap 2a + b][lane 64][8 ci], kernel index
+// kh = K[pf][a], kw = K[pt][b] with K = {{1, 3}, {0, 2}} (as pack_conv's transposed images)
+void pack_fragT(Blob& blob, const std::string& key, const std::vector<float>& w, int cin, int cout) {
+  const int K[2][2] = {{1, 3}, {0, 2}};
+  std::vector<uint16_t> img((size_t)4 * cout * cin * 4);
+  size_t i = 0;
+  for (int par = 0; par < 4; ++par)
+    for (int cb = 0; cb < cout / 32; ++cb)
+      for (int ch = 0; ch < cin / 16; ++ch)
+        for (int tap = 0; tap < 4; ++tap)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int k = 0; k < 8; ++k) {
+              const int co = cb * 32 + (lane & 31), ci = ch * 16 + (lane >> 5) * 8 + k;
+              const int kh = K[par >> 1][tap >> 1], kw = K[par & 1][tap & 1];
+              img[i++] = f2bf(w[(((size_t)ci * cout + co) * 4 + kh) * 4 + kw]);
+            }
+  blob.put(key, img.data(), img.size() * 2);
+}
+
 // pack a 3x3 [Cout][Cin][3][3] weight (Cin % 32 == 0) in conv3w's slot order (conv3w.hip), bf16: one slot per
 // (32-channel chunk c, tap t) in phase order k = 9 c + t, each [plane q 0..3][co][8 channels 32 c + 8 q ..] -- the LDS
 // image of a weight slot, so staging one is a straight DMA
@@ -495,6 +517,8 @@ int prepare(gt_decoder* d, int code) {
       if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
+      if (code == GT_BF16 && shp[0] == 64 && shp[1] == 64)
+        pack_fragT(blob, k + ".wfr", w, (int)shp[0], (int)shp[1]);   // the Upsample of attn_up_kernel
     } else if (ends_with(k, "to_qkv.weight")) {
       const int C = (int)shp[1];
       std::vector<float> q(w.begin(), w.begin() + 128 * C);
@@ -873,6 +897,24 @@ struct Run {
   }
 
   // attn_kv + merge/fold: M_b for every utterance in the workspace (the ResnetBlock output before it formed on the way)
+  // ups.1: the attention output and the Upsample after it as one pass (attn_up.hip); false (nothing launched) when not
+  // applicable: another dtype, disabled (GT_ATTN_US=0), or a probe of the attention output
+  bool attention_up(const std::string& ka, const std::string& ku, int lvl, const void* in, int C, void* out) {
+    if (!(dt && wi == GT_BF16 && d->attn_us && d->dp[wi].count(ku + "conv.weight.wfr"))) return false;
+    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
+    AttnUpParams a{};
+    a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
+    a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
+    a.wup = W(ku + "conv.weight.wfr"); a.bup = Fp(ku + "conv.bias"); a.out = out;
+    if (!attn_up_eligible(a)) return false;
+    attention_fold(ka, lvl, in, C);
+    const double pin = (double)B * a.F * a.T, pout = pin * 4;
+    timed("attn_up_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
+          2.0 * C * C * pin + 2.0 * C * C * 16 * pin, (pin + pout) * C * 2.0, [&] { return launch_attn_up(a, s); });
+    tap(ku.substr(0, ku.size() - 1), lvl - 1, out, C);
+    return true;
+  }
+
   void attention_fold(const std::string& k, int lvl, const void* in, int C) {
     float* part = (float*)(ws + L.part);
     float* G = (float*)(ws + L.G);
@@ -979,8 +1021,10 @@ struct Run {
     // up 1 at level 1: cat(x, hidden1) -> 64 ch, then ConvTranspose to level 0
     resnet("ups.1.0.", 1, act(1, 0), 128, act(1, 2), 128, 64, act(1, 1), next_tb(64));
     resnet("ups.1.1.", 1, act(1, 1), 64, nullptr, 0, 64, act(1, 0), next_tb(64), true);
-    attention("ups.1.2.", 1, act(1, 0), 64, act(1, 1));
-    upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
+    if (!attention_up("ups.1.2.", "ups.1.3.", 1, act(1, 0), 64, act(0, 0))) {
+      attention("ups.1.2.", 1, act(1, 0), 64, act(1, 1));
+      upsample("ups.1.3.", 1, act(1, 1), 64, act(0, 0));
+    }
     // final_block conv (+GN sums), then the fused GN/Mish/final_conv/(Euler) kernel
     float* st = stats();
     int fnp = 0;
@@ -1071,6 +1115,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_ATTN_MF")) d->attn_mf = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS1")) d->attn_ds1 = atoi(e) != 0;
+  if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   *out = d;
   return GT_OK;
 }

@@ -76,6 +76,20 @@ struct AttnDownParams {
 };
 bool attn_down_eligible(const AttnDownParams& p);
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s);
+
+// ups.1's attention output (never read but by the upsample) + Upsample (ConvTranspose 4x4 stride 2) in one pass, bf16,
+// C = 64 (attn_down.hip): level-1 input, level-0 output
+struct AttnUpParams {
+  const void* x; int B, F, T, C;   // attention input [B][F][T][C] (coarse grid)
+  int T0; const float* mask; int lvl;
+  const void* mw; long mw_bstride;  // per-utterance 1x1 weight image M_b
+  const float* gb;                  // g * b_out [C]
+  const void* wup;                  // upsample weight, four parities in fragment order (decoder.cpp pack_fragT)
+  const float* bup;                 // upsample bias [C]
+  void* out;                        // [B][2F][2T][C]
+};
+bool attn_up_eligible(const AttnUpParams& p);
+hipError_t launch_attn_up(const AttnUpParams& p, hipStream_t s);
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              hipStream_t s);
 hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s);

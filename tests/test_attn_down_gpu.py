@@ -66,3 +66,26 @@ def test_attn_down_stage_vs_oracle():
         r = taps[st].numpy()
         _, pr = probe(dec.estimator, torch.bfloat16, *args, None, st, r.shape)
         report(f"attn_down stage {st}", rel_err(pr.cpu().numpy(), r), 2e-2)
+
+
+@pytest.mark.parametrize("n_spks,B,T,lengths", [(1, 3, 132, [132, 100, 44]), (247, 2, 512, [512, 301]), (1, 2, 72, None)])
+def test_attn_up_bit_identical(monkeypatch, n_spks, B, T, lengths):
+    """attn_up_kernel (ups.1's attention output + Upsample, one pass) against the two launches (GT_ATTN_US=0): the
+    estimator, a 3-step sample and the level-0 upsample output ("ups.1.3") bit-identical; T = 132 / 72: partial
+    32-frame coarse tiles."""
+    mu, z, mask, spk = synthetic_inputs(29, B, T, lengths=lengths)
+    t = np.linspace(0.85, 0.25, B).astype(np.float32)
+    args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), _cuda(spk) if n_spks > 1 else None)
+    res = {}
+    for us in (1, 0):
+        monkeypatch.setenv("GT_ATTN_US", str(us))
+        dec, _ = make_decoder(n_spks, 13, torch.bfloat16)
+        z_, m_, mu_, t_, s_ = args
+        est = dec.estimator(z_, m_, mu_, t_, s_)
+        y = dec(z_, m_, mu_, 3, spk=s_)
+        _, up = probe(dec.estimator, torch.bfloat16, z_, m_, mu_, t_, s_, "ups.1.3", (B, 64, 80, T))
+        torch.cuda.synchronize()
+        res[us] = (est.cpu(), y.cpu(), up.cpu())
+    for a, b_, name in zip(res[1], res[0], ("estimator", "sampler N=3", "ups.1.3")):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, b_), f"{name}: max |diff| {float((a - b_).abs().max())}"
