@@ -166,53 +166,49 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
       }
     }
   } else {
-    // ---- stage 1, C / 16 waves: wave w takes the 32-channel block cb = w % NCB (its M_b fragments stay in registers)
-    // and position blocks w / NCB, + 2, + 4, ... (< 11); the next block's x fragments are loaded during this one's MFMAs
-    const int grp = wv / NCB;
-    constexpr int NKS = C / 16;
-    auto stage1 = [&](auto CBc) __attribute__((always_inline)) {
-      constexpr int cb = decltype(CBc)::value;
-      static_assert(4 * C / 64 == 2 * NCB, "two position-block groups");
-      bf16x8 ma[NKS];
+    // ---- stage 1, C / 16 waves: wave w takes position blocks w and w + 8 (< 11) and every 32-channel block; all its x
+    // fragments are loaded up front (one HBM round trip per workgroup, as the C = 64 form), the M_b fragments of block
+    // cb + 1 (L2) while block cb is in the MFMAs
+    constexpr int NKS = C / 16, NWV = 4 * C / 64;
+    const bool two = wv + NWV < NPB;   // wave-uniform
+    u32x4a_t xf[2][NKS];
+    float m[2];
+    int ent[2], yoff[2];
+    xfrags(wv, xf[0], m[0], ent[0], yoff[0]);
+    xfrags(two ? wv + NWV : NPB, xf[1], m[1], ent[1], yoff[1]);
+    bf16x8 ma[2][NKS];
+    auto mload = [&](int cb, bf16x8* dst) __attribute__((always_inline)) {
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks)
-        ma[ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+        dst[ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+    };
+    mload(0, ma[0]);
+    auto cbstep = [&](auto CBc) __attribute__((always_inline)) {
+      constexpr int cb = decltype(CBc)::value;
+      if (cb + 1 < NCB) mload(cb + 1, ma[(cb + 1) & 1]);
       float gb[2][8];
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
         for (int k = 0; k < 8; ++k) gb[pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
-      u32x4a_t xf[2][NKS];
-      float m[2];
-      int ent[2], yoff[2];
-      xfrags(grp, xf[0], m[0], ent[0], yoff[0]);
-      auto step = [&](auto Ic) __attribute__((always_inline)) {   // position block grp + 2 i (i compile-time)
-        constexpr int i = decltype(Ic)::value, cur = i & 1;
-        const int pb = grp + 2 * i;
-        if (pb >= NPB) return;   // wave-uniform
-        if (pb + 2 < NPB) xfrags(pb + 2, xf[cur ^ 1], m[cur ^ 1], ent[cur ^ 1], yoff[cur ^ 1]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i == 1 && !two) break;
         f32x16 acc;
 #pragma unroll
         for (int k = 0; k < 16; ++k) acc[k] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           bf16x8 xb;
-          __builtin_memcpy(&xb, &xf[cur][ks], 16);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[ks], xb, acc, 0, 0, 0);
+          __builtin_memcpy(&xb, &xf[i][ks], 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb & 1][ks], xb, acc, 0, 0, 0);
         }
-        y_block(acc, cb, gb, xf[cur], m[cur], ent[cur], yoff[cur]);
-      };
-      static_assert((NPB + 1) / 2 == 6, "six position blocks per group");
-      step(std::integral_constant<int, 0>{}); step(std::integral_constant<int, 1>{});
-      step(std::integral_constant<int, 2>{}); step(std::integral_constant<int, 3>{});
-      step(std::integral_constant<int, 4>{}); step(std::integral_constant<int, 5>{});
+        y_block(acc, cb, gb, xf[i], m[i], ent[i], yoff[i]);
+      }
     };
-    switch (wv % NCB) {   // wave-uniform
-      case 0: stage1(std::integral_constant<int, 0>{}); break;
-      case 1: stage1(std::integral_constant<int, 1>{}); break;
-      case 2: stage1(std::integral_constant<int, 2 % NCB>{}); break;
-      default: stage1(std::integral_constant<int, 3 % NCB>{}); break;
-    }
+    static_assert(NCB == 4, "four 32-channel blocks");
+    cbstep(std::integral_constant<int, 0>{}); cbstep(std::integral_constant<int, 1>{});
+    cbstep(std::integral_constant<int, 2>{}); cbstep(std::integral_constant<int, 3>{});
   }
 
   // ---- stage 2: 3x3 stride-2 conv of the patch. Wave w: output channels cb*32.. (cb = w % NCB) of output row

@@ -60,8 +60,8 @@ def norm(name: str) -> str:
                     ("" if tf == "4" else ",tf" + tf) + ">")
         if base == "conv64_kernel":          # <IN>
             return f"conv64_kernel<{args[0]}>"
-        if base == "conv3w_kernel":          # <IN, COUT, CB>
-            return f"conv3w_kernel<{','.join(args)}>"
+        if base in ("conv3w_kernel", "attn_down_kernel"):   # <IN, COUT, CB> / <C, WY>
+            return f"{base}<{','.join(args)}>"
         if base == "gn_mish_kernel":         # <A, APPLY>: the ResnetBlock output or block2's in-place input
             return ("gn_apply_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
         if base in ("attn_kv_kernel", "final_kernel", "to_nchw_kernel"):
