@@ -73,6 +73,9 @@ namespace gt {
 #define GT_C3W_BAR2 0  // one workgroup barrier per TWO phases (even taps of a chunk, plus tap 8): the weight ring keeps
                        // one more slot between the DMA target and the slots still being read (D = S - 2)
 #endif
+#ifndef GT_C3W_SPREAD
+#define GT_C3W_SPREAD 1  // next-chunk items transformed at odd phases 1, 3, 5, 7 (NPT <= 4) instead of phases XD ..
+#endif
 #ifndef GT_C3W_SCHED
 #define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
 #endif
@@ -101,6 +104,20 @@ struct Cfg {
   static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
   // phases between an item's load and its transform (item j: loaded at phase j, transformed at phase j + XD <= 7)
   static constexpr int XD = (8 - NPT) < GT_C3W_XD ? (8 - NPT) : GT_C3W_XD;
+  // phase of item j's transform (TP) and of its load (LP): XD phases apart, consecutive items in consecutive phases;
+  // GT_C3W_SPREAD (NPT <= 4): transforms every other phase (1, 3, 5, 7), each load two phases ahead, so the VALU of the
+  // operand transform is spread over the chunk instead of filling phases XD .. XD + NPT - 1
+  static constexpr bool SPREAD = GT_C3W_SPREAD && NPT <= 4;
+  static constexpr int TP(int j) { return SPREAD ? 1 + 2 * j : j + XD; }
+  static constexpr int LP(int j) { return SPREAD ? (TP(j) >= 2 ? TP(j) - 2 : 0) : j; }
+  static constexpr int jl(int t) {   // item loaded at phase t, or -1
+    for (int j = 0; j < NPT; ++j) if (LP(j) == t) return j;
+    return -1;
+  }
+  static constexpr int jt(int t) {   // item transformed at phase t, or -1
+    for (int j = 0; j < NPT; ++j) if (TP(j) == t) return j;
+    return -1;
+  }
   static constexpr int OFF_W = 2 * PBUF;
   static constexpr int OFF_F = OFF_W + S * SLOT;   // float area
   // floats: s_sc, s_sh, s_tb [256] each, s_bias [256], s_wsc [256], s_sub [NW][CB][4][2], s_mean, s_rstd [8]
@@ -304,10 +321,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
                                          (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
     }
   };
-  // items of the next chunk loaded at phases in [lo, hi] (item j at phase j)
+  // items of the next chunk loaded at phases in [lo, hi] (item j at phase LP(j))
   constexpr auto n_lp = [](int lo, int hi) {
     int n = 0;
-    for (int j = 0; j < C::NPT; ++j) n += (j >= lo && j <= hi) ? 1 : 0;
+    for (int j = 0; j < C::NPT; ++j) n += (C::LP(j) >= lo && C::LP(j) <= hi) ? 1 : 0;
     return n;
   };
   // top of phase (t = tap, MORE: chunk c+1 exists): retire DMA(k+1). Younger VMEM ops of this wave: the DMAs of phases
@@ -348,11 +365,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(NPRE) : "memory");
     if (STAMP) { const unsigned long long e = stamp(); st[0] += b - a; st[1] += e - b; st[5] += 1; }
   };
-  // before transforming item j at phase j + XD: younger VMEM ops are items j+1 .. j+XD (loaded at phases j+1 .. j+XD)
-  // and the DMAs of phases j+1 .. j+XD
+  // before transforming item j at phase TP(j): younger VMEM ops are the items loaded at phases LP(j)+1 .. TP(j) and the
+  // DMAs of those phases (each phase issues its DMA, then its item load, then this wait)
   auto item_wait = [&](auto Jc) {
     constexpr int j = decltype(Jc)::value;
-    constexpr int n = (C::NPT - 1 - j < C::XD ? C::NPT - 1 - j : C::XD) + C::XD * PW;
+    constexpr int n = n_lp(C::LP(j) + 1, C::TP(j)) + (C::TP(j) - C::LP(j)) * PW;
     const unsigned long long a = stamp();
     vm_wait_dep<n>(preg[j]);
     if (STAMP) st[2] += stamp() - a;
@@ -450,8 +467,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       // (loaded XD phases ago; younger: items t-XD+1 .. t and the DMAs of XD phases -- the same count in both wave
       // halves). Unconditional in every wave: an asm load whose wait a wave skipped would land in a reused register.
       if (MORE && !(GT_C3W_VAR & 4)) {
-        if (t < C::NPT) {
-          switch (t) {
+        if (C::jl(t) >= 0) {
+          switch (C::jl(t)) {
             case 0: load_items(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}); break;
             case 1: load_items(c + 1, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}); break;
             case 2: load_items(c + 1, std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{}); break;
@@ -460,8 +477,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             default: load_items(c + 1, std::integral_constant<int, 5>{}, std::integral_constant<int, 6>{}); break;
           }
         }
-        if (t >= C::XD && t - C::XD < C::NPT) {
-          switch (t - C::XD) {
+        if (C::jt(t) >= 0) {
+          switch (C::jt(t)) {
             case 0: item_wait(std::integral_constant<int, 0>{}); break;
             case 1: if constexpr (C::NPT > 1) item_wait(std::integral_constant<int, 1>{}); break;
             case 2: if constexpr (C::NPT > 2) item_wait(std::integral_constant<int, 2>{}); break;
@@ -511,10 +528,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         // Staggered between the two waves of a SIMD (waves w and w + 4 share one; MI355X_MICROARCH.md, two waves per
         // SIMD, item 9): waves 0-3 at step XS0, waves 4-7 at step XS1, so one wave's transform VALU runs beside its
         // partner's MFMAs instead of both leaving the matrix pipe idle at the same step.
-        if (MORE && !(GT_C3W_VAR & 4) && (i == XS0 || i == XS1) && t >= C::XD && t - C::XD < C::NPT) {
+        if (MORE && !(GT_C3W_VAR & 4) && (i == XS0 || i == XS1) && C::jt(t) >= 0) {
           if ((i == XS0 && wv < c3w::NW / 2) || (i == XS1 && wv >= c3w::NW / 2)) {
             const unsigned long long a = stamp();
-            put_item(t - C::XD, c + 1, nxt);
+            put_item(C::jt(t), c + 1, nxt);
             asm volatile("" ::: "memory");   // the item's LDS write stays ahead of the phase-end fragment reads (NPRE)
             if (STAMP) st[3] += stamp() - a;
           }
