@@ -157,9 +157,12 @@ constexpr int GN_Q = 24;   // slot loads per thread issued up front: 16 thread g
 struct GnLoad {
   float v[GN_Q];
 };
-GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
+// t: the calling thread's index among the 256 that take part (default threadIdx.x; a 512-thread workgroup running two
+// independent 256-thread halves passes threadIdx.x & 255 -- both halves then call gn_finish, whose barriers they share)
+GT_DEV GnLoad gn_load(const float* part, int nparts, int b, int t = -1) {
   GnLoad g;
-  const int t = threadIdx.x, k = t & 15, grp = t >> 4;
+  if (t < 0) t = threadIdx.x;
+  const int k = t & 15, grp = t >> 4;
   const float* pb = part + (long)b * nparts * 16 + k;
 #pragma unroll
   for (int q = 0; q < GN_Q; ++q) {
@@ -170,8 +173,9 @@ GT_DEV GnLoad gn_load(const float* part, int nparts, int b) {
 }
 // s_red: LDS scratch of >= 272 doubles
 GT_DEV void gn_finish(const GnLoad& g, const float* part, int nparts, int b, long count, float* s_mean, float* s_rstd,
-                      double* s_red) {
-  const int t = threadIdx.x, k = t & 15, grp = t >> 4;
+                      double* s_red, int t = -1) {
+  if (t < 0) t = threadIdx.x;
+  const int k = t & 15, grp = t >> 4;
   if (t < 256) {
     double acc = 0.0;
 #pragma unroll

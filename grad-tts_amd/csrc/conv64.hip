@@ -38,6 +38,9 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef GT_C64_VAR
 #define GT_C64_VAR 0  // timing-only experiment bits (wrong results): 1 no new-row staging, 2 no output stores, 4 no barrier
 #endif
+#ifndef GT_C64_PAIR
+#define GT_C64_PAIR 0  // two segments per 8-wave workgroup sharing the tile barrier (0: one 4-wave workgroup per segment)
+#endif
 #ifndef GT_C64_STAMP
 #define GT_C64_STAMP 0  // diagnostic builds only: s_memtime stamps (gt_diag_conv64_stamps), instantiation GT_C64_STAMP_IN, F = 80
 #endif
@@ -65,6 +68,7 @@ constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + NW * 8
 // taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room
 constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
+constexpr int NSEG = GT_C64_PAIR ? 2 : 1;                 // segments (4-wave halves) per workgroup
 }  // namespace c64
 
 // IN: IN_MASK / IN_GN / IN_PLAIN. Masks from sequence_mask are 0/1: x * m is then a select, decided per item on
@@ -80,10 +84,16 @@ static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 __device__ unsigned long long gt_c64_stamps[512 * 4 * 8];
 #endif
 
+// GT_C64_PAIR: one 8-wave workgroup runs two segments, one per 4-wave half, each with its own LDS region, sharing the
+// tile barrier: the two halves advance in lockstep. (As two workgroups per CU, one gets issue priority and finishes its
+// loop ~25 % before the other, which then runs alone on the CU: tools/diag_c64_stamps.py. In lockstep, though, the two
+// halves' staging and epilogues coincide instead of overlapping each other's MFMAs: 96.1 -> 99.9 us, so off.)
 template <int IN, bool W8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
+__global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
+  __shared__ __attribute__((aligned(16))) char smem_all[NSEG * SMEM];   // one LDS object
+  const int half = NSEG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+  char* const smem = smem_all + half * SMEM;
   char* const sR = smem;                                     // ring of RING patch rows
   constexpr int WREG = wreg_of(IN);
   char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
@@ -98,13 +108,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   auto stamp = [&]() -> unsigned long long { return (GT_C64_STAMP && STAMP) ? __builtin_amdgcn_s_memtime() : 0ull; };
   unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long t_entry = stamp();
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int tid = threadIdx.x & 255, lane = tid & 63, r = lane & 31, h = lane >> 5;   // (thread of this half)
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: ring-row addressing stays scalar
   const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
   const int F = p.Fout, T = p.Tout;
   const int n_ft = F / TF, n_tt = (T + TT - 1) / TT;
   const int kseg = n_ft / L;                                 // segments per column
-  const int col = blockIdx.x / kseg, part = blockIdx.x - col * kseg;
+  // this half's segment; a half past the last segment (odd count) runs segment 0 again without storing anything
+  const int nseg_all = p.B * n_tt * kseg;
+  const int seg_raw = blockIdx.x * NSEG + half;
+  const bool dummy = seg_raw >= nseg_all;
+  const int seg = dummy ? 0 : seg_raw;
+  const int col = seg / kseg, part = seg - col * kseg;
   const int b = col / n_tt, tt = col - b * n_tt;
   const int ft0 = part * L;
 
@@ -189,9 +204,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   if (IN == IN_GN) {
     const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
     static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
-    const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b);
+    const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b, tid);
     const float tbv = tid < 64 ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid] : 0.f;
-    gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
+    gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red, tid);
     if (tid < 64) {
       const float sc = c_g * s_rstd[tid >> 3];   // the affine in base 2 (common.h gn_mish_tb_l2)
       s_coef[tid] = sc * kLog2e; s_coef[64 + tid] = (c_b - s_mean[tid >> 3] * sc) * kLog2e; s_coef[128 + tid] = tbv;
@@ -327,7 +342,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
       const int t = t0 + r;
       const bool valid = t < T;
-      const int obyte = valid ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
+      const int obyte = (valid && !dummy) ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
@@ -369,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   }
   lds_barrier();
-  if (tid < 8) {   // fixed-order sum over the 2 waves of the group's channel half
+  if (tid < 8 && !dummy) {   // fixed-order sum over the 2 waves of the group's channel half
     const int g = tid, gcb = g >> 2, e = (g & 3) * 2;
     float S = 0.f, Q = 0.f;
 #pragma unroll
@@ -388,7 +403,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     unsigned long long v = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
-    if (lane < 8) gt_c64_stamps[((blockIdx.x & 511) * 4 + wv) * 8 + lane] = v;
+    if (lane < 8) gt_c64_stamps[((seg_raw & 511) * 4 + wv) * 8 + lane] = v;
   }
 #endif
 }
@@ -426,16 +441,18 @@ int conv64_nparts(int F, int T, int small) { return ((T + 31) / 32) * ((F / 4) /
 hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
   const int L = conv64_seg(p.Fout, p.small);
-  const unsigned grid = (unsigned)((long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L));
+  const long nseg = (long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L);
+  const unsigned grid = (unsigned)((nseg + c64::NSEG - 1) / c64::NSEG);
+  const dim3 block(256 * c64::NSEG);
   if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)
-    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), dim3(256), 0, s, p, L);
-    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, true>), dim3(grid), dim3(256), 0, s, p, L);
-    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, true>), dim3(grid), dim3(256), 0, s, p, L);
+    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), block, 0, s, p, L);
+    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, true>), dim3(grid), block, 0, s, p, L);
+    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, true>), dim3(grid), block, 0, s, p, L);
     else return hipErrorNotSupported;
   } else {
-    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), dim3(256), 0, s, p, L);
-    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), dim3(256), 0, s, p, L);
-    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), dim3(256), 0, s, p, L);
+    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), block, 0, s, p, L);
+    else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), block, 0, s, p, L);
+    else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), block, 0, s, p, L);
     else return hipErrorNotSupported;
   }
   return hipGetLastError();

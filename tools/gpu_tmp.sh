@@ -1,3 +1,2 @@
-timeout -k 10 600 python3 -u -m pytest tests/test_attn_down_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; tail -2 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
-for v in 0 1 0 1; do GT_ATTN_US=$v GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 2 --n-timesteps 10 > gpurun_out/us_$v.json 2>/dev/null || exit 1; python3 -c "
-import json; d=json.load(open('gpurun_out/us_$v.json')); print('US=$v', round(d['ms_per_step'],2), 'ms/step', round(d['value']), {k[:28]:v['avg_us'] for k,v in d['shapes'].items() if 'attn_up' in k or '@64x64x40' in k or '<bf16,3,1,1,64>' in k or 'attn_down' in k})"; done
+timeout -k 10 900 python3 -u -m pytest tests/test_decoder_gpu.py tests/test_fp8_gpu.py tests/test_small_batch_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; tail -1 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+AB_ROWS=8 bash tools/ab_variants.sh nopair tree nopair tree
