@@ -284,6 +284,10 @@ hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
 // frames (the 4 x 32 coarse positions of the tile plus a one-position halo); stage 2 the four sub-pixel 2x2 convs of
 // conv_kernel CONVT4 (out[2J + pf][2K + pt] from coarse rows J + pf - a, columns K + pt - b, taps (a, b)), wave w taking
 // parity w, in conv_kernel's order (16-channel chunk outer, tap inner): bit-identical to the two launches.
+#ifndef GT_AU_PF
+#define GT_AU_PF 0   // attn_up: stage-2 weight fragments requested ahead (0: at use, 1: first half before stage 1, 2: both;
+                     // 1 and 2 cost the third wave per SIMD: 82 -> 91 / 88 us)
+#endif
 namespace au {
 constexpr int PROWS = 6, PCOLS = 34, NPOS = PROWS * PCOLS, NPB = (NPOS + 31) / 32;   // 204 positions, 7 blocks
 constexpr int PLANE = NPOS;                                                          // entries per 8-channel plane
@@ -308,6 +312,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, npos_all * C * 2, 0x00020000);
   const int oob = npos_all * C * 2;
 
+  bf16x8 wpre[GT_AU_PF >= 1 ? 16 : 1];   // stage 2's first-half weight fragments, requested now (see below)
+  if (GT_AU_PF >= 1) {
+    const bf16x8* w0 = reinterpret_cast<const bf16x8*>(p.wup) + wv * 2 * 16 * 64 + lane;
+#pragma unroll
+    for (int st = 0; st < (GT_AU_PF >= 1 ? 16 : 1); ++st) wpre[st] = w0[st * 64];
+  }
   // ---- stage 1: y = (M_b x + g b_out) + x, masked, into LDS. Wave w: position blocks w, w + 4 (< 7), both halves.
   {
     const WImg W1 = conv_wimg(1, 1, C, C);
@@ -396,12 +406,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int pf = wv >> 1, pt = wv & 1;
   const int Ff = 2 * F, Tf = 2 * T;
   const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(p.wup) + wv * 2 * 16 * 64 + lane;   // [par][cb][ch][tap][lane]
+  // the first half's weight fragments were requested before stage 1 (their L2 latency hidden behind it); GT_AU_PF = 2
+  // also requests the second half's during the first half's MFMAs (64 more registers: two waves per SIMD)
   lds_barrier();
+  bf16x8 wb[GT_AU_PF >= 2 ? 16 : 1];
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) {
     bf16x8 wa[16];
 #pragma unroll
-    for (int st = 0; st < 16; ++st) wa[st] = wsrc[(cb * 16 + st) * 64];
+    for (int st = 0; st < 16; ++st) {
+      if (GT_AU_PF >= 1 && cb == 0) wa[st] = wpre[st];
+      else if (GT_AU_PF >= 2) wa[st] = wb[st < (GT_AU_PF >= 2 ? 16 : 1) ? st : 0];
+      else wa[st] = wsrc[(cb * 16 + st) * 64];
+    }
+    if (GT_AU_PF >= 2 && cb == 0) {
+#pragma unroll
+      for (int st = 0; st < 16; ++st) wb[st] = wsrc[(16 + st) * 64];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       auto bread = [&](int st) {
