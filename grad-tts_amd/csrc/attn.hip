@@ -19,25 +19,35 @@
 #include "kernels.h"
 #include "wimage.h"
 
+#ifndef GT_KV_WPF
+#define GT_KV_WPF 1    // chunked attn_kv: the next k/v weight slice loaded into registers during the current chunk
+#endif
+#ifndef GT_KV_SB
+#define GT_KV_SB 64    // positions per sub-block of the chunked (C > 64) bf16 attn_kv (128: spills at 256 VGPRs)
+#endif
+
 namespace gt {
 
 // RB: the input is formed from the ResnetBlock's block2 pre-activation and its residual in the operand load
 // (AttnKVParams::rb_pre); the formed rows also go to rb_out. Same expression and GroupNorm reduction as
 // gn_mish_kernel, so the stored activation is bit-identical to the separate pass it replaces.
-template <class A, int CPR, bool RB>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
+// SB: positions per sub-block (64 or 128; the chunked path stages every k/v weight slice once per sub-block, so 128 halves
+// that traffic and the barriers per position)
+template <class A, int CPR, bool RB, int SB = 64>   // CPR > 0: all CPR input channels resident in LDS; 0: chunked (large C)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_kv_kernel(AttnKVParams p) {
+  constexpr int NRB = SB / 32;                                  // 32-position row blocks per sub-block
   constexpr bool RES = CPR > 0;
   constexpr int CK = 64 / (int)sizeof(A);
   constexpr int ICH = 16 / (int)sizeof(A);
   constexpr int KSTEP_B = 16 * (int)sizeof(A);
   constexpr int ROWB = RES ? CPR * (int)sizeof(A) + 16 : 80;   // LDS row stride: odd number of 16-B slots
   constexpr int IPR = RES ? CPR / ICH : 4;                      // 16-B items per staged row
-  constexpr int XIT = 64 * IPR / 256;                           // x items per thread per sub-block
-  static_assert(64 * IPR % 256 == 0, "x staging must split evenly");
+  constexpr int XIT = SB * IPR / 256;                           // x items per thread per sub-block
+  static_assert(SB * IPR % 256 == 0, "x staging must split evenly");
   typedef typename Mma<A>::frag frag;
-  __shared__ __attribute__((aligned(16))) char smem[(64 + 256) * ROWB];
+  __shared__ __attribute__((aligned(16))) char smem[(SB + 256) * ROWB];
   char* sX = smem;
-  char* sW = smem + 64 * ROWB;
+  char* sW = smem + SB * ROWB;
 
   const int b = blockIdx.x / p.ntile, tile = blockIdx.x % p.ntile;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -111,10 +121,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
     for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
   }
-  for (int pos0 = tbeg; pos0 < tend; pos0 += 64) {
-    f32x16 ak[2], av[2];
+  uint4 w0, w1, w2, w3;   // GT_KV_WPF: the next weight slice (rows tid/4 + 64 i), loaded during the current chunk
+  bool wpf_ok = false;
+  const A* wrow = wkv + (long)(tid >> 2) * p.Cpad + (tid & 3) * ICH;
+  const long wstep = 64L * p.Cpad;
+  auto load_w = [&](int ch) __attribute__((always_inline)) {
+    if (GT_KV_WPF && !RES) {
+      w0 = *reinterpret_cast<const uint4*>(wrow + ch * CK);
+      w1 = *reinterpret_cast<const uint4*>(wrow + wstep + ch * CK);
+      w2 = *reinterpret_cast<const uint4*>(wrow + 2 * wstep + ch * CK);
+      w3 = *reinterpret_cast<const uint4*>(wrow + 3 * wstep + ch * CK);
+    }
+  };
+  for (int pos0 = tbeg; pos0 < tend; pos0 += SB) {
+    f32x16 ak[NRB], av[NRB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NRB; ++i)
 #pragma unroll
       for (int k = 0; k < 16; ++k) { ak[i][k] = 0.f; av[i][k] = 0.f; }
 
@@ -123,19 +145,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       lds_barrier();                                   // every wave is done with the previous chunk's fragments
       store_x(pos0, ch * CK);
       if (!RES) {                                      // the k/v weight slice: L2-resident, loaded straight into LDS
-        for (int it = tid; it < 256 * 4; it += 256) {
-          const int row = it >> 2, sub = it & 3;
-          *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
-              *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
+        if (GT_KV_WPF) {                               // (prefetched into registers during the previous chunk)
+          if (!wpf_ok) load_w(ch);
+          char* wd = sW + (tid >> 2) * 80 + (tid & 3) * 16;   // rows tid/4 + 64 i
+          *reinterpret_cast<uint4*>(wd) = w0;
+          *reinterpret_cast<uint4*>(wd + 64 * 80) = w1;
+          *reinterpret_cast<uint4*>(wd + 128 * 80) = w2;
+          *reinterpret_cast<uint4*>(wd + 192 * 80) = w3;
+        } else {
+          for (int it = tid; it < 256 * 4; it += 256) {
+            const int row = it >> 2, sub = it & 3;
+            *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
+                *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
+          }
         }
       }
       lds_barrier();
       if (RES) {
-        if (pos0 + 64 < tend) load_x(pos0 + 64, 0);   // next sub-block in flight during the MFMAs
+        if (pos0 + SB < tend) load_x(pos0 + SB, 0);   // next sub-block in flight during the MFMAs
       } else if (ch + 1 < nch) {
         load_x(pos0, (ch + 1) * CK);
-      } else if (pos0 + 64 < tend) {
-        load_x(pos0 + 64, 0);
+      } else if (pos0 + SB < tend) {
+        load_x(pos0 + SB, 0);
+      }
+      if (GT_KV_WPF && !RES) {   // the next chunk's weight slice (chunk 0 again after the last: the next sub-block)
+        load_w(ch + 1 < nch ? ch + 1 : 0);
+        wpf_ok = true;
       }
       const int nks = RES ? CPR / 16 : CK / 16;
       for (int ks = 0; ks < nks; ++ks) {
@@ -143,7 +178,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         const frag bk = Mma<A>::load(sW + (wv * 32 + r) * ROWB + off);
         const frag bv = Mma<A>::load(sW + (128 + wv * 32 + r) * ROWB + off);
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int rb = 0; rb < NRB; ++rb) {
           const frag a = Mma<A>::load(sX + (rb * 32 + r) * ROWB + off);
           Mma<A>::mma(a, bk, ak[rb]);
           Mma<A>::mma(a, bv, av[rb]);
@@ -152,16 +187,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     }
 
   // ---- online softmax over positions (k.softmax(dim=-1), diffusion.py:95) for column d = r
-    const bool full = pos0 + 64 <= tend;             // wave-uniform: no per-element validity test
+    const bool full = pos0 + SB <= tend;             // wave-uniform: no per-element validity test
     float mloc = NEG_INF;
     if (full) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j) mloc = fmaxf(mloc, ak[rb][j]);
     } else {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j)
           if (pos0 + rb * 32 + acc_row(j, h) < tend) mloc = fmaxf(mloc, ak[rb][j]);
@@ -176,7 +211,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     float lsum = 0.f;
     if (full) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(ak[rb][j], L2E, -mL));
@@ -185,7 +220,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         }
     } else {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const bool valid = pos0 + rb * 32 + acc_row(j, h) < tend;
@@ -207,7 +242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     // ---- ctx[d][e] += sum_pos P[pos][d] V[pos][e]   (einsum 'bhdn,bhen->bhde', diffusion.py:96)
     if constexpr (sizeof(A) == 2) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           typedef float f32x8_t __attribute__((ext_vector_type(8)));
@@ -219,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         }
     } else {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
         for (int j = 0; j < 16; ++j) ctx = __builtin_amdgcn_mfma_f32_32x32x2f32(ak[rb][j], av[rb][j], ctx, 0, 0, 0);
     }
@@ -480,15 +515,15 @@ hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels
   // resident k/v weights only for C = 64; wider inputs stream 32-channel chunks (3 workgroups/CU,
   // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
-#define GT_KV(A_, CPR_)                                                                           \
-  do {                                                                                            \
-    if (p.rb_pre) hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, true>), grid, dim3(256), 0, s, p);  \
-    else hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, false>), grid, dim3(256), 0, s, p);          \
+#define GT_KV(A_, CPR_, SB_)                                                                          \
+  do {                                                                                                \
+    if (p.rb_pre) hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, true, SB_>), grid, dim3(256), 0, s, p);  \
+    else hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, false, SB_>), grid, dim3(256), 0, s, p);          \
   } while (0)
   if (act_bf16) {
-    if (p.Cpad <= 64) GT_KV(bf16, 64); else GT_KV(bf16, 0);
+    if (p.Cpad <= 64) GT_KV(bf16, 64, 64); else GT_KV(bf16, 0, GT_KV_SB);
   } else {
-    if (p.Cpad <= 64) GT_KV(float, 64); else GT_KV(float, 0);
+    if (p.Cpad <= 64) GT_KV(float, 64, 64); else GT_KV(float, 0, 64);
   }
 #undef GT_KV
   return hipGetLastError();

@@ -1,3 +1,1 @@
-timeout -k 10 300 python3 -u -m pytest tests/test_attn_down_gpu.py -x -q --timeout 200 --timeout-method thread 2>&1 | tail -1
-for v in au0 tree au2 au0 tree au2; do if [ $v = tree ]; then unset GRADTTS_LIB; else export GRADTTS_LIB=$PWD/ab/$v/libgradtts.so; fi; GRADTTS_BENCH_NO_FINITE_CHECK=1 timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 3 --warmup 2 --n-timesteps 10 > gpurun_out/au_$v.json 2>/dev/null || exit 1; python3 -c "
-import json; d=json.load(open('gpurun_out/au_$v.json')); print('$v', round(d['ms_per_step'],2), {k[:26]:v['avg_us'] for k,v in d['shapes'].items() if 'attn_up' in k})"; done
+AB_ROWS=40 bash tools/ab_variants.sh wpf0 tree wpf0 tree > gpurun_out/ab_wpf.txt 2>&1; rc=$?; grep -E "variant|ms/step|attn_kv" gpurun_out/ab_wpf.txt; exit $rc
