@@ -22,6 +22,10 @@
 #ifndef GT_KV_WPF
 #define GT_KV_WPF 1    // chunked attn_kv: the next k/v weight slice loaded into registers during the current chunk
 #endif
+#ifndef GT_KV_CKB
+#define GT_KV_CKB 128  // bytes per position of a bf16 chunk of the chunked attn_kv (128: 64 channels, half the
+                       // barriers of 64; measured 48.8 -> 42.2 us at C = 256, 82.4 -> 72.4 us at C = 128)
+#endif
 #ifndef GT_KV_SB
 #define GT_KV_SB 64    // positions per sub-block of the chunked (C > 64) bf16 attn_kv (128: spills at 256 VGPRs)
 #endif
@@ -37,11 +41,13 @@ template <class A, int CPR, bool RB, int SB = 64>   // CPR > 0: all CPR input ch
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_kv_kernel(AttnKVParams p) {
   constexpr int NRB = SB / 32;                                  // 32-position row blocks per sub-block
   constexpr bool RES = CPR > 0;
-  constexpr int CK = 64 / (int)sizeof(A);
+  constexpr int CKB = (sizeof(A) == 2 && !RES) ? GT_KV_CKB : 64;   // bytes of a position's channel chunk
+  constexpr int CK = CKB / (int)sizeof(A);
   constexpr int ICH = 16 / (int)sizeof(A);
   constexpr int KSTEP_B = 16 * (int)sizeof(A);
-  constexpr int ROWB = RES ? CPR * (int)sizeof(A) + 16 : 80;   // LDS row stride: odd number of 16-B slots
-  constexpr int IPR = RES ? CPR / ICH : 4;                      // 16-B items per staged row
+  constexpr int ROWB = RES ? CPR * (int)sizeof(A) + 16 : CKB + 16;   // LDS row stride: odd number of 16-B slots
+  constexpr int IPR = RES ? CPR / ICH : CKB / 16;                    // 16-B items per staged row
+  constexpr int WPT = RES ? 1 : CKB / 16;                            // weight-slice items per thread (256 rows)
   constexpr int XIT = SB * IPR / 256;                           // x items per thread per sub-block
   static_assert(SB * IPR % 256 == 0, "x staging must split evenly");
   typedef typename Mma<A>::frag frag;
@@ -121,18 +127,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
     for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
   }
-  uint4 w0, w1, w2, w3;   // GT_KV_WPF: the next weight slice (rows tid/4 + 64 i), loaded during the current chunk
+  // GT_KV_WPF: the next weight slice (item i of thread tid: row tid / IPR + (256 / IPR) i, 16 B at (tid % IPR) * 16),
+  // loaded into registers during the current chunk
+  static_assert(WPT == 4 || WPT == 8 || RES, "weight-slice prefetch holds 4 or 8 items");
+  uint4 w0, w1, w2, w3, w4, w5, w6, w7;   // named: an array here lands in scratch
   bool wpf_ok = false;
-  const A* wrow = wkv + (long)(tid >> 2) * p.Cpad + (tid & 3) * ICH;
-  const long wstep = 64L * p.Cpad;
-  auto load_w = [&](int ch) __attribute__((always_inline)) {
-    if (GT_KV_WPF && !RES) {
-      w0 = *reinterpret_cast<const uint4*>(wrow + ch * CK);
-      w1 = *reinterpret_cast<const uint4*>(wrow + wstep + ch * CK);
-      w2 = *reinterpret_cast<const uint4*>(wrow + 2 * wstep + ch * CK);
-      w3 = *reinterpret_cast<const uint4*>(wrow + 3 * wstep + ch * CK);
-    }
-  };
+  const A* wrow = wkv + (long)(tid / IPR) * p.Cpad + (tid % IPR) * ICH;
+  const long wstep = (long)(256 / IPR) * p.Cpad;
+#define GT_KV_W_(I_, CH_) (*reinterpret_cast<const uint4*>(wrow + (I_) * wstep + (CH_) * CK))
+#define GT_KV_LOAD_W(CH_)                                                                    \
+  do {                                                                                       \
+    if constexpr (!RES) {                                                                    \
+      w0 = GT_KV_W_(0, CH_); w1 = GT_KV_W_(1, CH_); w2 = GT_KV_W_(2, CH_); w3 = GT_KV_W_(3, CH_); \
+      if constexpr (WPT == 8) {                                                              \
+        w4 = GT_KV_W_(4, CH_); w5 = GT_KV_W_(5, CH_); w6 = GT_KV_W_(6, CH_); w7 = GT_KV_W_(7, CH_); \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
   for (int pos0 = tbeg; pos0 < tend; pos0 += SB) {
     f32x16 ak[NRB], av[NRB];
 #pragma unroll
@@ -146,16 +157,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       store_x(pos0, ch * CK);
       if (!RES) {                                      // the k/v weight slice: L2-resident, loaded straight into LDS
         if (GT_KV_WPF) {                               // (prefetched into registers during the previous chunk)
-          if (!wpf_ok) load_w(ch);
-          char* wd = sW + (tid >> 2) * 80 + (tid & 3) * 16;   // rows tid/4 + 64 i
+          if (!wpf_ok) GT_KV_LOAD_W(ch);
+          char* wd = sW + (tid / IPR) * ROWB + (tid % IPR) * 16;
+          constexpr int WS = (256 / IPR) * ROWB;
           *reinterpret_cast<uint4*>(wd) = w0;
-          *reinterpret_cast<uint4*>(wd + 64 * 80) = w1;
-          *reinterpret_cast<uint4*>(wd + 128 * 80) = w2;
-          *reinterpret_cast<uint4*>(wd + 192 * 80) = w3;
+          *reinterpret_cast<uint4*>(wd + WS) = w1;
+          *reinterpret_cast<uint4*>(wd + 2 * WS) = w2;
+          *reinterpret_cast<uint4*>(wd + 3 * WS) = w3;
+          if constexpr (WPT == 8) {
+            *reinterpret_cast<uint4*>(wd + 4 * WS) = w4;
+            *reinterpret_cast<uint4*>(wd + 5 * WS) = w5;
+            *reinterpret_cast<uint4*>(wd + 6 * WS) = w6;
+            *reinterpret_cast<uint4*>(wd + 7 * WS) = w7;
+          }
         } else {
-          for (int it = tid; it < 256 * 4; it += 256) {
-            const int row = it >> 2, sub = it & 3;
-            *reinterpret_cast<uint4*>(sW + row * 80 + sub * 16) =
+          for (int it = tid; it < 256 * IPR; it += 256) {
+            const int row = it / IPR, sub = it % IPR;
+            *reinterpret_cast<uint4*>(sW + row * ROWB + sub * 16) =
                 *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
           }
         }
@@ -169,7 +187,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         load_x(pos0 + SB, 0);
       }
       if (GT_KV_WPF && !RES) {   // the next chunk's weight slice (chunk 0 again after the last: the next sub-block)
-        load_w(ch + 1 < nch ? ch + 1 : 0);
+        GT_KV_LOAD_W(ch + 1 < nch ? ch + 1 : 0);
         wpf_ok = true;
       }
       const int nks = RES ? CPR / 16 : CK / 16;
@@ -266,6 +284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
   for (int j = 0; j < 16; ++j) part[64 + acc_row(j, h) * 32 + r] = ctx[j];
 }
+#undef GT_KV_LOAD_W
+#undef GT_KV_W_
 
 // grid (B, 4 heads): merge the tiles' online-softmax partials, normalise, and fold the head's part of
 // the output projection (m_t, M: running maxima in log2 units, as attn_kv keeps them):
@@ -513,7 +533,8 @@ hipError_t launch_attn_merge_fold(int act_bf16, const float* part, int B, int nt
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels
-  // resident k/v weights only for C = 64; wider inputs stream 32-channel chunks (3 workgroups/CU,
+  if (p.Cpad > 64 && p.Cpad % (act_bf16 ? GT_KV_CKB / 2 : 16) != 0) return hipErrorInvalidValue;   // whole chunks
+  // resident k/v weights only for C = 64; wider inputs stream 64-channel chunks (bf16; 3 workgroups/CU,
   // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
 #define GT_KV(A_, CPR_, SB_)                                                                          \
   do {                                                                                                \
