@@ -287,21 +287,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #undef GT_KV_LOAD_W
 #undef GT_KV_W_
 
-// grid (B, 4 heads): merge the tiles' online-softmax partials, normalise, and fold the head's part of
+// grid (B, 4 heads, 32 / DR): merge the tiles' online-softmax partials, normalise, and fold the head's part of
 // the output projection (m_t, M: running maxima in log2 units, as attn_kv keeps them):
 //   ctx_h[d][e]  = sum_t 2^(m_t[d] - M[d]) ctx_t[d][e] / sum_t 2^(m_t[d] - M[d]) l_t[d]
 //   A[co][32h+d] = g * sum_e Wout[co][32h+e] ctx_h[d][e]     (einsum 'bhde,bhdn->bhen' + to_out + Rezero)
+// Rows d are independent, so a workgroup owns DR of them: DR = 32 (throughput plan) merges in NG = 4 tile groups;
+// DR = 4 (small-batch plan: few utterances, up to 256 tiles each) spreads a head over 8 workgroups and merges in
+// NG = 32 groups of a few tiles each (the serial chain of dependent loads is what a B = 1 merge waits on).
+template <int DR>
 __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int ntile, const float* wout, const float* g,
                                                           int C, float* Aout) {
-  __shared__ float s_ctx[32][33];
+  constexpr int NG = 1024 / (DR * 8);   // tile groups
+  __shared__ float s_ctx[DR][33];
   __shared__ float s_w[256][33];
-  __shared__ float s_gc[4][32][33];   // per tile group: unnormalised context, running max, running sum
-  __shared__ float s_gm[4][32], s_gl[4][32];
-  const int b = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
-  const int grp = tid >> 8, lt = tid & 255;
-  const int d = lt >> 3, e0 = (lt & 7) * 4;
+  __shared__ float s_gc[NG][DR][33];   // per tile group: unnormalised context, running max, running sum
+  __shared__ float s_gm[NG][DR], s_gl[NG][DR];
+  const int b = blockIdx.x, hd = blockIdx.y, d0 = blockIdx.z * DR, tid = threadIdx.x;
+  const int grp = tid / (DR * 8), lt = tid % (DR * 8);
+  const int dl = lt >> 3, d = d0 + dl, e0 = (lt & 7) * 4;
   // tile group grp merges tiles [t0, t1) online (running max), in tile order
-  const int per = (ntile + 3) / 4, t0 = grp * per, t1 = min(ntile, t0 + per);
+  const int per = (ntile + NG - 1) / NG, t0 = grp * per, t1 = min(ntile, t0 + per);
   const float* base = part + ((long)b * ntile * 4 + hd) * 1088;
   const long tstride = 4 * 1088;
   float M = -__builtin_huge_valf(), L = 0.f, c[4] = {0.f, 0.f, 0.f, 0.f};
@@ -323,8 +328,8 @@ __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int
     for (int k = 0; k < 4; ++k) c[k] += w * v[k];
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) s_gc[grp][d][e0 + k] = c[k];
-  if ((lt & 7) == 0) { s_gm[grp][d] = M; s_gl[grp][d] = L; }
+  for (int k = 0; k < 4; ++k) s_gc[grp][dl][e0 + k] = c[k];
+  if ((lt & 7) == 0) { s_gm[grp][dl] = M; s_gl[grp][dl] = L; }
   for (int i = tid; i < C * 8; i += 1024) {            // Wout[:, 32h : 32h+32] -> LDS (float4 loads)
     const int co = i >> 3, e4 = (i & 7) * 4;
     const f32x4 w = *reinterpret_cast<const f32x4*>(wout + (long)co * 128 + hd * 32 + e4);
@@ -332,31 +337,31 @@ __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int
     for (int k = 0; k < 4; ++k) s_w[co][e4 + k] = w[k];
   }
   __syncthreads();
-  if (grp == 0) {                                      // combine the 4 groups in a fixed order
+  if (grp == 0) {                                      // combine the groups in a fixed order
     float Mt = -__builtin_huge_valf();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Mt = fmaxf(Mt, s_gm[q][d]);
+    for (int q = 0; q < NG; ++q) Mt = fmaxf(Mt, s_gm[q][dl]);
     float Lt = 0.f, ct[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int q = 0; q < NG; ++q) {
+      if (s_gl[q][dl] == 0.f) continue;                // empty group (ntile < NG)
+      const float r = __builtin_amdgcn_exp2f(s_gm[q][dl] - Mt);
+      Lt += r * s_gl[q][dl];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (s_gl[q][d] == 0.f) continue;                 // empty group (ntile < 4)
-      const float r = __builtin_amdgcn_exp2f(s_gm[q][d] - Mt);
-      Lt += r * s_gl[q][d];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ct[k] += r * s_gc[q][d][e0 + k];
+      for (int k = 0; k < 4; ++k) ct[k] += r * s_gc[q][dl][e0 + k];
     }
     const float inv = 1.f / Lt;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s_ctx[d][e0 + k] = ct[k] * inv;
+    for (int k = 0; k < 4; ++k) s_ctx[dl][e0 + k] = ct[k] * inv;
   }
   __syncthreads();
   const float gg = g[0];
-  for (int idx = tid; idx < C * 32; idx += 1024) {     // (co, d), d fastest: s_w broadcast, s_ctx stride 33
-    const int co = idx >> 5, dd = idx & 31;
+  for (int idx = tid; idx < C * DR; idx += 1024) {     // (co, d), d fastest: s_w broadcast, s_ctx stride 33
+    const int co = idx / DR, dd = idx % DR;
     float acc = 0.f;
 #pragma unroll
     for (int e = 0; e < 32; ++e) acc += s_w[co][e] * s_ctx[dd][e];
-    Aout[((long)b * C + co) * 128 + hd * 32 + dd] = gg * acc;
+    Aout[((long)b * C + co) * 128 + hd * 32 + d0 + dd] = gg * acc;
   }
 }
 
@@ -551,9 +556,11 @@ hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
 }
 
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
-                             hipStream_t s) {
+                             int dr, hipStream_t s) {
   if (C > 256 || C % 4 != 0) return hipErrorInvalidValue;    // s_w holds at most 256 output rows
-  hipLaunchKernelGGL(attn_merge_kernel, dim3(B, 4), dim3(1024), 0, s, part, ntile, wout, g, C, Aout);
+  if (dr == 32) hipLaunchKernelGGL(attn_merge_kernel<32>, dim3(B, 4, 1), dim3(1024), 0, s, part, ntile, wout, g, C, Aout);
+  else if (dr == 4) hipLaunchKernelGGL(attn_merge_kernel<4>, dim3(B, 4, 8), dim3(1024), 0, s, part, ntile, wout, g, C, Aout);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -139,6 +139,14 @@ struct Blob {   // host staging of one packed device arena
 // largest call batch on the small-batch tile plan (small_plan). Measured (50-step decodes, T = 512, one box):
 // B = 1 47.3 vs 78.9 ms, B = 2 50.7 vs 80.6, B = 4 61.0 vs 82.7, B = 8 94.9 vs 94.3, B = 16 152.9 vs 116.3
 constexpr int64_t kSmallB = 4;
+// small-batch plan attention tiles per utterance and merge rows per workgroup. Measured (B = 1, T = 512, N = 50, one
+// box): 64 tiles + one merge workgroup per head 43.9 ms per decode, + 8 merge workgroups 42.9, 128 tiles 42.3, 256 42.0
+constexpr int kSmallTiles = 256;
+constexpr int kMergeDrSmall = 4;
+// small-batch plan split-K target: workgroups per utterance the 128-wide 3x3 convs aim for (conv_small_ksplit; 0 off).
+// Measured (T = 512, N = 50, one box, ms per decode, off / 256): B = 1 42.4 / 37.8, B = 2 45.7 / 42.6, B = 4 57.2 / 59.4;
+// targets 384 and 512 38.4 at B = 1 (level-1 tiles split too: two workgroup rounds)
+constexpr int kSkTarget = 256;
 
 }  // namespace
 
@@ -188,6 +196,11 @@ struct gt_decoder {
   bool attn_ds1 = false;
   // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
   bool attn_us = true;
+  // small-batch plan attention: tiles per utterance (GT_ATTN_TILES_SMALL) and the merge's rows per workgroup
+  // (GT_MERGE_DR_SMALL: 4 spreads a head's merge over 8 workgroups; 32 is the throughput plan's single workgroup)
+  int small_tiles = kSmallTiles;
+  int merge_dr_small = kMergeDrSmall;
+  int sk_target = kSkTarget;   // GT_SK_TARGET
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -570,6 +583,7 @@ int prepare(gt_decoder* d, int code) {
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
   size_t stats, part, G, Mw, tb, spk, betas, step, total;
+  size_t skcnt, skpart; long skcnt_n, skpart_n;   // small plan split-K: counters, fp32 partials (0: not allocated)
   int pmax;
   int tile_pos[3], ntile[3];
 };
@@ -577,9 +591,9 @@ struct Layout {
 // Attention tile size depends only on the positions per utterance and the tile plan (never on B), so an utterance gets
 // the same online-softmax partition -- hence bit-identical arithmetic -- whatever batch or GPU shard it
 // is decoded in (sharded runs must match the single-GPU run).
-// `target` tiles per utterance: the workspace is sized for 64 (the most); the throughput plan takes 16 for utterances
-// of 8192+ positions and 32 below (fewer online-softmax partials to merge, longer streams per workgroup: same-box
-// +1.0-1.3 %), the small-batch plan keeps 64 so that one utterance still spreads over the GPU.
+// `target` tiles per utterance: the throughput plan takes 16 for utterances of 8192+ positions and 32 below (fewer
+// online-softmax partials to merge, longer streams per workgroup: same-box +1.0-1.3 %), the small-batch plan 256
+// (kSmallTiles) so that one utterance still spreads over the GPU; the workspace is sized for the larger of the two.
 void attn_tiles(int64_t n, int target, int& tile_pos, int& ntile) {
   int64_t tp = (n + target - 1) / target;
   tp = (tp + 63) / 64 * 64;
@@ -608,7 +622,7 @@ int max_gn_parts(int dt, int64_t T) {
   return m;
 }
 
-Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
+Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles, int small) {
   Layout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = (o + bytes + 255) & ~size_t(255); return r; };
@@ -621,8 +635,11 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.stats = take((size_t)25 * B * L.pmax * 16 * sizeof(float));
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
-    attn_tiles((int64_t)(80 >> l) * (T >> l), 64, L.tile_pos[l], L.ntile[l]);
+    attn_tiles((int64_t)(80 >> l) * (T >> l), small_tiles, L.tile_pos[l], L.ntile[l]);   // small-batch plan
     maxtile = std::max(maxtile, L.ntile[l]);
+    int tp, nt;
+    attn_tiles((int64_t)(80 >> l) * (T >> l), 32, tp, nt);   // the throughput plan takes at most 32
+    maxtile = std::max(maxtile, nt);
   }
   L.part = take((size_t)B * maxtile * 4 * 1088 * 4);
   L.G = take((size_t)B * 128 * 256 * 4);
@@ -631,6 +648,12 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N) {
   L.spk = take((size_t)B * 80 * 4);
   L.betas = take((size_t)std::max<int32_t>(N, 1) * 4);
   L.step = take(4);
+  if (small) {   // 128-wide 3x3 tiles of levels 1-2 (at most 2 x 128 output channels), up to 4 splits of 8192 floats
+    L.skcnt_n = (long)B * 40 * (((T >> 1) + 63) / 64) * 2;
+    L.skpart_n = L.skcnt_n * 4 * 8192;
+    L.skcnt = take((size_t)L.skcnt_n * 4);
+    L.skpart = take((size_t)L.skpart_n * 4);
+  }
   L.total = o;
   return L;
 }
@@ -717,6 +740,12 @@ struct Run {
     }
     const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
     if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
+    if (small && dt && !p.wscale && p.Cout % 128 == 0 && im != IN_INPUT && L.skcnt_n) {   // split-K (conv.hip ConvCfg::SK)
+      p.ksplit = conv_small_ksplit(p.Fout, p.Tout, p.Cout, p.Cin_pad, d->sk_target);
+      const long tiles = (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128);
+      if (p.ksplit > 1 && (tiles > L.skcnt_n || tiles * p.ksplit * 8192 > L.skpart_n)) { chk(hipErrorInvalidValue); return np; }
+      p.sk_part = (float*)(ws + L.skpart); p.sk_cnt = (int*)(ws + L.skcnt);
+    }
     conv(CONV3, im, OUT_STATS, p);
     return np;
   }
@@ -950,7 +979,8 @@ struct Run {
       });
     } else {
       timed("attn_merge_kernel@" + std::to_string(C), 0.0, 0.0, [&] {
-        return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G, s);
+        return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G,
+                                 small ? d->merge_dr_small : 32, s);
       });
       timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0,
             [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
@@ -1116,6 +1146,9 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS1")) d->attn_ds1 = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
+  if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
+  if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
+  if (const char* e = getenv("GT_SK_TARGET")) d->sk_target = atoi(e);
   *out = d;
   return GT_OK;
 }
@@ -1200,7 +1233,7 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int
   (void)d;
   if (B <= 0 || T <= 0) return 0;
   const int dt = dtype ? 1 : 0;
-  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps).total + 256;
+  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps, d->small_tiles, small_plan(d, dtype, B)).total + 256;
 }
 
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
@@ -1220,7 +1253,8 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = (hipStream_t)stream;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, 0);
+    R.L = layout(R.dt, nb, T, 0, d->small_tiles, R.small);
+    if (R.L.skcnt_n) R.chk(hipMemsetAsync(R.ws + R.L.skcnt, 0, (size_t)R.L.skcnt_n * 4, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = x + fo; R.spk_s = nullptr;
     R.probe = probe; R.probe_out = probe_out;
     float* tbuf = (float*)(R.ws + R.L.tb);
@@ -1480,7 +1514,8 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = st;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, n_timesteps);
+    R.L = layout(R.dt, nb, T, n_timesteps, d->small_tiles, R.small);
+    if (R.L.skcnt_n) R.chk(hipMemsetAsync(R.ws + R.L.skcnt, 0, (size_t)R.L.skcnt_n * 4, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = out + fo; R.spk_s = nullptr;
     float* xt = out + fo;
     R.chk(launch_mask_copy(z + fo, R.mask, (int)nb, 80, (int)T, xt, R.s));   // xt = z * mask  (diffusion.py:257)

@@ -27,6 +27,9 @@ def _cuda(a):
 
 def _run(monkeypatch, mf, dtype, n_spks, args, N):
     monkeypatch.setenv("GT_ATTN_MF", "1" if mf else "0")   # (default: off)
+    # attn_mf merges in attn_merge_kernel<32>'s four tile groups; the small-batch plan (these batches) defaults to the
+    # 32-group merge (GT_MERGE_DR_SMALL=4), so both runs take the four-group merge here
+    monkeypatch.setenv("GT_MERGE_DR_SMALL", "32")
     dec, _ = make_decoder(n_spks, 7, dtype)
     z, mask, mu, t, spk = args
     est = dec.estimator(z, mask, mu, t, spk)
