@@ -66,6 +66,8 @@ def norm(name: str) -> str:
             return ("gn_apply_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
         if base in ("attn_kv_kernel", "final_kernel", "to_nchw_kernel"):
             return f"{base}<{ty(args[0])}>"
+        if base == "attn_merge_kernel" and args:   # <DR>: rows per workgroup
+            return f"{base}<{args[0]}>"
         if base == "attn_fold_kernel" and args:
             return f"{base}<{ty(args[0])}>"
         if not args:
