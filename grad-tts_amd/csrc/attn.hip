@@ -19,18 +19,13 @@
 #include "kernels.h"
 #include "wimage.h"
 
-#ifndef GT_KV_WPF
-#define GT_KV_WPF 1    // chunked attn_kv: the next k/v weight slice loaded into registers during the current chunk
-#endif
-#ifndef GT_KV_CKB
-#define GT_KV_CKB 128  // bytes per position of a bf16 chunk of the chunked attn_kv (128: 64 channels, half the
-                       // barriers of 64; measured 48.8 -> 42.2 us at C = 256, 82.4 -> 72.4 us at C = 128)
-#endif
-#ifndef GT_KV_SB
-#define GT_KV_SB 64    // positions per sub-block of the chunked (C > 64) bf16 attn_kv (128: spills at 256 VGPRs)
-#endif
-
 namespace gt {
+
+// bytes per position of a bf16 chunk of the chunked attn_kv (128: 64 channels, half the barriers of 64 B; measured
+// 48.8 -> 42.2 us at C = 256, 82.4 -> 72.4 us at C = 128)
+constexpr int kKvCkb = 128;
+// positions per sub-block of the chunked (C > 64) bf16 attn_kv (128 spills at 256 VGPRs)
+constexpr int kKvSb = 64;
 
 // RB: the input is formed from the ResnetBlock's block2 pre-activation and its residual in the operand load
 // (AttnKVParams::rb_pre); the formed rows also go to rb_out. Same expression and GroupNorm reduction as
@@ -41,7 +36,7 @@ template <class A, int CPR, bool RB, int SB = 64>   // CPR > 0: all CPR input ch
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_kv_kernel(AttnKVParams p) {
   constexpr int NRB = SB / 32;                                  // 32-position row blocks per sub-block
   constexpr bool RES = CPR > 0;
-  constexpr int CKB = (sizeof(A) == 2 && !RES) ? GT_KV_CKB : 64;   // bytes of a position's channel chunk
+  constexpr int CKB = (sizeof(A) == 2 && !RES) ? kKvCkb : 64;   // bytes of a position's channel chunk
   constexpr int CK = CKB / (int)sizeof(A);
   constexpr int ICH = 16 / (int)sizeof(A);
   constexpr int KSTEP_B = 16 * (int)sizeof(A);
@@ -127,20 +122,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
     for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
   }
-  // GT_KV_WPF: the next weight slice (item i of thread tid: row tid / IPR + (256 / IPR) i, 16 B at (tid % IPR) * 16),
-  // loaded into registers during the current chunk
+  // chunked path: the next k/v weight slice (item i of thread tid: row tid / IPR + (256 / IPR) i, 16 B at
+  // (tid % IPR) * 16) is loaded into registers during the current chunk (level 1: 94.5 -> 82.4 us)
   static_assert(WPT == 4 || WPT == 8 || RES, "weight-slice prefetch holds 4 or 8 items");
   uint4 w0, w1, w2, w3, w4, w5, w6, w7;   // named: an array here lands in scratch
   bool wpf_ok = false;
   const A* wrow = wkv + (long)(tid / IPR) * p.Cpad + (tid % IPR) * ICH;
   const long wstep = (long)(256 / IPR) * p.Cpad;
-#define GT_KV_W_(I_, CH_) (*reinterpret_cast<const uint4*>(wrow + (I_) * wstep + (CH_) * CK))
-#define GT_KV_LOAD_W(CH_)                                                                    \
+#define KV_W_(I_, CH_) (*reinterpret_cast<const uint4*>(wrow + (I_) * wstep + (CH_) * CK))
+#define KV_LOAD_W(CH_)                                                                    \
   do {                                                                                       \
     if constexpr (!RES) {                                                                    \
-      w0 = GT_KV_W_(0, CH_); w1 = GT_KV_W_(1, CH_); w2 = GT_KV_W_(2, CH_); w3 = GT_KV_W_(3, CH_); \
+      w0 = KV_W_(0, CH_); w1 = KV_W_(1, CH_); w2 = KV_W_(2, CH_); w3 = KV_W_(3, CH_); \
       if constexpr (WPT == 8) {                                                              \
-        w4 = GT_KV_W_(4, CH_); w5 = GT_KV_W_(5, CH_); w6 = GT_KV_W_(6, CH_); w7 = GT_KV_W_(7, CH_); \
+        w4 = KV_W_(4, CH_); w5 = KV_W_(5, CH_); w6 = KV_W_(6, CH_); w7 = KV_W_(7, CH_); \
       }                                                                                      \
     }                                                                                        \
   } while (0)
@@ -156,26 +151,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       lds_barrier();                                   // every wave is done with the previous chunk's fragments
       store_x(pos0, ch * CK);
       if (!RES) {                                      // the k/v weight slice: L2-resident, loaded straight into LDS
-        if (GT_KV_WPF) {                               // (prefetched into registers during the previous chunk)
-          if (!wpf_ok) GT_KV_LOAD_W(ch);
-          char* wd = sW + (tid / IPR) * ROWB + (tid % IPR) * 16;
-          constexpr int WS = (256 / IPR) * ROWB;
-          *reinterpret_cast<uint4*>(wd) = w0;
-          *reinterpret_cast<uint4*>(wd + WS) = w1;
-          *reinterpret_cast<uint4*>(wd + 2 * WS) = w2;
-          *reinterpret_cast<uint4*>(wd + 3 * WS) = w3;
-          if constexpr (WPT == 8) {
-            *reinterpret_cast<uint4*>(wd + 4 * WS) = w4;
-            *reinterpret_cast<uint4*>(wd + 5 * WS) = w5;
-            *reinterpret_cast<uint4*>(wd + 6 * WS) = w6;
-            *reinterpret_cast<uint4*>(wd + 7 * WS) = w7;
-          }
-        } else {
-          for (int it = tid; it < 256 * IPR; it += 256) {
-            const int row = it / IPR, sub = it % IPR;
-            *reinterpret_cast<uint4*>(sW + row * ROWB + sub * 16) =
-                *reinterpret_cast<const uint4*>(wkv + (long)row * p.Cpad + ch * CK + sub * ICH);
-          }
+        if (!wpf_ok) KV_LOAD_W(ch);                    // (prefetched into registers during the previous chunk)
+        char* wd = sW + (tid / IPR) * ROWB + (tid % IPR) * 16;
+        constexpr int WS = (256 / IPR) * ROWB;
+        *reinterpret_cast<uint4*>(wd) = w0;
+        *reinterpret_cast<uint4*>(wd + WS) = w1;
+        *reinterpret_cast<uint4*>(wd + 2 * WS) = w2;
+        *reinterpret_cast<uint4*>(wd + 3 * WS) = w3;
+        if constexpr (WPT == 8) {
+          *reinterpret_cast<uint4*>(wd + 4 * WS) = w4;
+          *reinterpret_cast<uint4*>(wd + 5 * WS) = w5;
+          *reinterpret_cast<uint4*>(wd + 6 * WS) = w6;
+          *reinterpret_cast<uint4*>(wd + 7 * WS) = w7;
         }
       }
       lds_barrier();
@@ -186,8 +173,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
       } else if (pos0 + SB < tend) {
         load_x(pos0 + SB, 0);
       }
-      if (GT_KV_WPF && !RES) {   // the next chunk's weight slice (chunk 0 again after the last: the next sub-block)
-        GT_KV_LOAD_W(ch + 1 < nch ? ch + 1 : 0);
+      if (!RES) {   // the next chunk's weight slice (chunk 0 again after the last: the next sub-block)
+        KV_LOAD_W(ch + 1 < nch ? ch + 1 : 0);
         wpf_ok = true;
       }
       const int nks = RES ? CPR / 16 : CK / 16;
@@ -284,8 +271,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
 #pragma unroll
   for (int j = 0; j < 16; ++j) part[64 + acc_row(j, h) * 32 + r] = ctx[j];
 }
-#undef GT_KV_LOAD_W
-#undef GT_KV_W_
+#undef KV_LOAD_W
+#undef KV_W_
 
 // grid (B, 4 heads, 32 / DR): merge the tiles' online-softmax partials, normalise, and fold the head's part of
 // the output projection (m_t, M: running maxima in log2 units, as attn_kv keeps them):
@@ -403,155 +390,23 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
   }
 }
 
-// grid (B, C/64, C/64): attn_merge + attn_fold in one launch. Each workgroup merges the tiles' partials of all four heads
-// itself (the (C/64)^2 workgroups of an utterance repeat this small, L2-resident pass), forms its 64 rows of A_b in LDS
-// and multiplies them by its 64 columns of Wq: two launches and the A_b round trip through HBM fewer per attention
-// block. Same operations in the same order as attn_merge_kernel + attn_fold_kernel (four tile groups merged online, then
-// combined in a fixed order; A by the same e-ordered fp32 chain), so the folded weights are bit-identical.
-template <class A>
-__global__ __launch_bounds__(1024) void attn_mf_kernel(const float* part, int ntile, const float* wout, const float* g,
-                                                       const float* wq, int C, char* Mw, WImg W) {
-  __shared__ float s_ctx[4][32][33];   // normalised context per head [d][e]
-  __shared__ float s_a[64][129];       // A rows co0..co0+63, k = 0..127
-  __shared__ float s_q[64][129];       // first W_out rows co0..co0+63 (all 128 columns), then Wq^T: [ci - ci0][k]
-  __shared__ float s_g[4][4][32][33];  // [head][tile group][d][e] unnormalised group contexts
-  __shared__ float s_gm[4][4][32], s_gl[4][4][32];
-  const int b = blockIdx.x, co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64, tid = threadIdx.x;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {   // W_out rows of this block (float4 loads)
-    const int i = tid + 1024 * j, rr = i >> 5, k4 = (i & 31) * 4;
-    const f32x4 w = *reinterpret_cast<const f32x4*>(wout + (long)(co0 + rr) * 128 + k4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s_q[rr][k4 + k] = w[k];
-  }
-  // merge, as attn_merge_kernel: thread (tile group grp, d, 4 e's) merges tiles [t0, t1) of each head online in tile
-  // order (the four heads interleaved, so their loads are in flight together), then the four groups are combined in
-  // group order
-  {
-    const int grp = tid >> 8, lt = tid & 255, d = lt >> 3, e0 = (lt & 7) * 4;
-    const int per = (ntile + 3) / 4, t0 = grp * per, t1 = min(ntile, t0 + per);
-    const long tstride = 4 * 1088;
-    const float* base = part + (long)b * ntile * 4 * 1088;
-    float M[4], L[4], c[4][4];
-#pragma unroll
-    for (int hd = 0; hd < 4; ++hd) {
-      M[hd] = -__builtin_huge_valf(); L[hd] = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) c[hd][k] = 0.f;
-    }
-    for (int t = t0; t < t1; ++t) {
-      float mt[4], lt_[4];
-      f32x4 v[4];
-#pragma unroll
-      for (int hd = 0; hd < 4; ++hd) {
-        const float* pt = base + t * tstride + hd * 1088;
-        mt[hd] = pt[d]; lt_[hd] = pt[32 + d];
-        v[hd] = *reinterpret_cast<const f32x4*>(pt + 64 + d * 32 + e0);
-      }
-#pragma unroll
-      for (int hd = 0; hd < 4; ++hd) {
-        if (mt[hd] > M[hd]) {   // rescale what was merged so far (m in log2 units)
-          const float r = __builtin_amdgcn_exp2f(M[hd] - mt[hd]);
-          L[hd] *= r;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) c[hd][k] *= r;
-          M[hd] = mt[hd];
-        }
-        const float w = __builtin_amdgcn_exp2f(mt[hd] - M[hd]);
-        L[hd] += w * lt_[hd];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) c[hd][k] += w * v[hd][k];
-      }
-    }
-#pragma unroll
-    for (int hd = 0; hd < 4; ++hd) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s_g[hd][grp][d][e0 + k] = c[hd][k];
-      if ((lt & 7) == 0) { s_gm[hd][grp][d] = M[hd]; s_gl[hd][grp][d] = L[hd]; }
-    }
-  }
-  __syncthreads();
-  {   // combine the groups in a fixed order: thread (head, d, 4 e's)
-    const int hd = tid >> 8, lt = tid & 255, d = lt >> 3, e0 = (lt & 7) * 4;
-    float Mt = -__builtin_huge_valf();
-#pragma unroll
-    for (int q = 0; q < 4; ++q) Mt = fmaxf(Mt, s_gm[hd][q][d]);
-    float Lt = 0.f, ct[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (s_gl[hd][q][d] == 0.f) continue;   // empty group (ntile < 4)
-      const float r = __builtin_amdgcn_exp2f(s_gm[hd][q][d] - Mt);
-      Lt += r * s_gl[hd][q][d];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ct[k] += r * s_g[hd][q][d][e0 + k];
-    }
-    const float inv = 1.f / Lt;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s_ctx[hd][d][e0 + k] = ct[k] * inv;
-  }
-  __syncthreads();
-  const float gg = g[0];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {   // A[co][32 hd + dd] = g sum_e Wout[co][32 hd + e] ctx_hd[dd][e] (dd fastest)
-    const int idx = tid + 1024 * j, co = idx >> 7, kk = idx & 127, hd = kk >> 5, dd = kk & 31;
-    float acc = 0.f;
-#pragma unroll
-    for (int e = 0; e < 32; ++e) acc += s_q[co][hd * 32 + e] * s_ctx[hd][dd][e];
-    s_a[co][kk] = gg * acc;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {   // Wq^T block, coalesced along ci
-    const int i = tid + 1024 * j, k = i >> 4, c4 = (i & 15) * 4;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(wq + (long)k * C + ci0 + c4);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s_q[c4 + c][k] = v[c];
-  }
-  __syncthreads();
-  if (tid >= 256) return;   // the fold: 4 waves, one 32 x 32 block each (no barrier below)
-  const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int bm = (wv >> 1) * 32, bn = (wv & 1) * 32;
-  f32x16 acc;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < 128; k += 2)
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_a[bm + r][k + h], s_q[bn + r][k + h], acc, 0, 0, 0);
-  char* img = Mw + (long)b * W.total;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int co = co0 + bm + acc_row(j, h), ci = ci0 + bn + r;
-    *reinterpret_cast<A*>(img + conv_wimg_off(W, co, 0, ci, (int)sizeof(A))) = Act<A>::from_f(acc[j]);
-  }
-}
-
-hipError_t launch_attn_merge_fold(int act_bf16, const float* part, int B, int ntile, const float* wout, const float* g,
-                                  const float* wq, int C, void* Mw, hipStream_t s) {
-  if (C % 64 != 0 || C > 256) return hipErrorInvalidValue;
-  const WImg W = conv_wimg(act_bf16, 1, C, C);
-  const dim3 grid(B, C / 64, C / 64);
-  if (act_bf16) hipLaunchKernelGGL(attn_mf_kernel<bf16>, grid, dim3(1024), 0, s, part, ntile, wout, g, wq, C, (char*)Mw, W);
-  else hipLaunchKernelGGL(attn_mf_kernel<float>, grid, dim3(1024), 0, s, part, ntile, wout, g, wq, C, (char*)Mw, W);
-  return hipGetLastError();
-}
-
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels
-  if (p.Cpad > 64 && p.Cpad % (act_bf16 ? GT_KV_CKB / 2 : 16) != 0) return hipErrorInvalidValue;   // whole chunks
+  if (p.Cpad > 64 && p.Cpad % (act_bf16 ? kKvCkb / 2 : 16) != 0) return hipErrorInvalidValue;   // whole chunks
   // resident k/v weights only for C = 64; wider inputs stream 64-channel chunks (bf16; 3 workgroups/CU,
   // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)
-#define GT_KV(A_, CPR_, SB_)                                                                          \
+#define KV_LAUNCH(A_, CPR_, SB_)                                                                          \
   do {                                                                                                \
     if (p.rb_pre) hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, true, SB_>), grid, dim3(256), 0, s, p);  \
     else hipLaunchKernelGGL((attn_kv_kernel<A_, CPR_, false, SB_>), grid, dim3(256), 0, s, p);          \
   } while (0)
   if (act_bf16) {
-    if (p.Cpad <= 64) GT_KV(bf16, 64, 64); else GT_KV(bf16, 0, GT_KV_SB);
+    if (p.Cpad <= 64) KV_LAUNCH(bf16, 64, 64); else KV_LAUNCH(bf16, 0, kKvSb);
   } else {
-    if (p.Cpad <= 64) GT_KV(float, 64, 64); else GT_KV(float, 0, 64);
+    if (p.Cpad <= 64) KV_LAUNCH(float, 64, 64); else KV_LAUNCH(float, 0, 64);
   }
-#undef GT_KV
+#undef KV_LAUNCH
   return hipGetLastError();
 }
 

@@ -1,23 +1,24 @@
-// Attention output + Downsample as one pass (bf16): levels 0 (C = 64) and 1 (C = 128).
+// Attention output + Downsample as one pass (bf16), U-Net level 0 (C = 64).
 //
 // Reference (model/diffusion.py:186-191, 30-36, 103-110): at the first two U-Net levels
 //     y = x + g * to_out(attn(x))                      Residual(Rezero(LinearAttention))
 //     hiddens.append(y); x = downsample(y * mask)      Conv2d(C, C, 3, stride 2, padding 1)
 // hiddens[0] is never popped (the up path has two levels; it pops the level-2 and level-1 entries), so the 168 MB
-// (B = 32, T = 512) level-0 attention output is only ever read by the downsample; the level-1 one is also the skip
-// connection of ups.1. With the attention folded into one per-utterance 1x1 (attn.hip: y = x + M_b x + g b_out) both
-// convolutions fit one kernel:
+// (B = 32, T = 512) level-0 attention output is only ever read by the downsample. (The level-1 one is also the skip
+// connection of ups.1: that level keeps the two launches -- a fused form that also stored y measured 236 us against
+// 101 us, one 87 KB workgroup per CU.) With the attention folded into one per-utterance 1x1 (attn.hip:
+// y = x + M_b x + g b_out) both convolutions fit one kernel:
 //
 //   stage 1  a workgroup's input patch (5 mel rows x 65 frames: the stride-2 3x3 window of 2 output rows x 32 output
 //            frames) -> y = (M_b x + g b_out) + x on MFMA (M_b as A, positions as B; the residual x is the B fragment
-//            itself), masked, rounded to bf16 into LDS (level 1: also stored to HBM, each position once);
+//            itself), masked, rounded to bf16 into LDS;
 //   stage 2  the 3x3 stride-2 conv of the LDS patch (weights as A from a fragment-ordered image, L2-resident) + bias.
 //
 // Same operations in the same order as conv_kernel CONV1/OUT_RESID followed by conv_kernel CONV3_S2/IN_MASK (1x1 over
 // k-steps in order; the residual added after the bias; y rounded to bf16; x * m as a select for {0,1} masks; the 3x3
 // over 16-channel chunks outer, taps inner; bias after), so the outputs are bit-identical to the two-kernel path
 // (tests/test_attn_down_gpu.py) while the HBM traffic drops from read x + write y + read y + write out to read x (1.27x:
-// the 5 x 65 patch of a 2 x 32 output tile) (+ write y at level 1) + write out.
+// the 5 x 65 patch of a 2 x 32 output tile) + write out.
 //
 // LDS patch: C/8 planes (8 channels each) x 5 rows x 68 entries of 16 B, the 65 columns deinterleaved by parity (even
 // columns at entries 0..32, odd ones at 36..67): a stride-2 tap then reads 32 CONSECUTIVE entries (conflict-free
@@ -33,16 +34,14 @@ constexpr int PROWS = 5, PCOLS = 65, NPOS = PROWS * PCOLS;   // input patch of o
 constexpr int NPB = (NPOS + 31) / 32;                        // 11 position blocks of 32
 constexpr int ODD = 36, RS = 68;                             // odd-column offset and row stride (entries)
 constexpr int PLANE = PROWS * RS;                            // 340 entries
-template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   // 43,520 B (C = 64) / 87,040 B (128)
+template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   // 43,520 B (C = 64)
 }  // namespace ad
 
 typedef unsigned u32x4a_t __attribute__((ext_vector_type(4)));
 
-// C = 64: 4 waves, the level-0 form (the attention output is not needed). C = 128, WY: 8 waves, the level-1 form, which
-// also stores the attention output from stage 1 -- each position by the one tile whose patch holds it away from the
-// top / left halo (patch row >= 1, column >= 1).
-template <int C, bool WY>
-__global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ? 3 : 2))) void attn_down_kernel(AttnDownParams p) {
+// 4 waves (the attention output itself is not needed at level 0).
+template <int C>
+__global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void attn_down_kernel(AttnDownParams p) {
   using namespace ad;
   constexpr int NCB = C / 32;   // 32-channel blocks
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<C>()];
@@ -59,14 +58,13 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
 
   const int npos_all = p.B * F * T;
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, npos_all * C * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, WY ? npos_all * C * 2 : 0, 0x00020000);
   const int oob = npos_all * C * 2;
   const WImg W1 = conv_wimg(1, 1, C, C);
   const char* mimg = reinterpret_cast<const char*>(p.mw) + (long)b * p.mw_bstride;
 
   // position pb*32 + r of the patch: its x fragments (k-steps 0 .. C/16-1; out-of-range positions read zeros), mask,
-  // LDS entry, and (WY) the byte offset its attention output goes to (-1: not this tile's to store)
-  auto xfrags = [&](int pb, u32x4a_t* xf, float& m, int& ent, int& yoff) __attribute__((always_inline)) {
+  // LDS entry
+  auto xfrags = [&](int pb, u32x4a_t* xf, float& m, int& ent) __attribute__((always_inline)) {
     const int pos = pb * 32 + r;
     const int prow = pos / PCOLS, pcol = pos - prow * PCOLS;
     const int fi = fi0 + prow, ti = ti0 + pcol;
@@ -76,12 +74,11 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
     for (int ks = 0; ks < C / 16; ++ks) xf[ks] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + ks * 32, 0, 0);
     m = inside ? mask_at(p.mask, p.T0, b, ti, p.lvl) : 0.f;
     ent = pos < NPOS ? prow * RS + (pcol & 1) * ODD + (pcol >> 1) : -1;
-    yoff = (inside && prow >= 1 && pcol >= 1) ? ((b * F + fi) * T + ti) * (C * 2) : -1;
   };
   // the epilogue of one 32 x 32 stage-1 block (channels cb*32.., positions of one block): the accumulator (M_b x), the
-  // bias g b_out, the residual (this lane's own x fragments of k-steps 2cb, 2cb+1) -> bf16 y -> LDS (masked), HBM (WY)
-  auto y_block = [&](const f32x16& acc, int cb, const float (*gbc)[8], const u32x4a_t* xf, float m, int ent,
-                     int yoff) __attribute__((always_inline)) {
+  // bias g b_out, the residual (this lane's own x fragments of k-steps 2cb, 2cb+1) -> bf16 y -> LDS (masked)
+  auto y_block = [&](const f32x16& acc, int cb, const float (*gbc)[8], const u32x4a_t* xf, float m, int ent)
+      __attribute__((always_inline)) {
     float v[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) v[q] = acc[q];
@@ -106,8 +103,6 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
       }
       const uint4 ov = f_to_item(o, bf16());
       const int c0 = cb * 32 + pr * 16 + 8 * h;
-      if (WY)   // the unmasked attention output, as conv_kernel OUT_RESID stores it
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4a_t{ov.x, ov.y, ov.z, ov.w}, rsy, yoff >= 0 ? yoff + c0 * 2 : oob, 0, 0);
       // y * mask as the downsample's IN_MASK select ({0,1} masks; a fractional mask multiplies the bf16 value)
       u32x4a_t y;
       if (m == 1.f) {
@@ -126,89 +121,43 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
     }
   };
 
-  if constexpr (C == 64) {
-    // ---- stage 1, 4 waves: wave w takes position blocks w, w+4, w+8 (< 11) and both 32-channel halves (the x fragments
-    // are shared by the two halves); every x fragment of the wave in flight at once (one HBM round trip)
-    bf16x8 ma[2][4];
+  // ---- stage 1, 4 waves: wave w takes position blocks w, w+4, w+8 (< 11) and both 32-channel halves (the x fragments
+  // are shared by the two halves); every x fragment of the wave in flight at once (one HBM round trip)
+  bf16x8 ma[2][4];
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-        ma[cb][ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
-    float gb[2][2][8];   // g b_out of this lane's channels after the swap: cb*32 + 16 pr + 8h + 0..7
+    for (int ks = 0; ks < 4; ++ks)
+      ma[cb][ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
+  float gb[2][2][8];   // g b_out of this lane's channels after the swap: cb*32 + 16 pr + 8h + 0..7
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
+    for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) gb[cb][pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
-    constexpr int NPW = (NPB + 3) / 4;
-    u32x4a_t xf[NPW][4];
-    float m[NPW];
-    int ent[NPW], yoff[NPW];
+      for (int k = 0; k < 8; ++k) gb[cb][pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
+  constexpr int NPW = (NPB + 3) / 4;
+  u32x4a_t xf[NPW][4];
+  float m[NPW];
+  int ent[NPW];
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) xfrags(wv + 4 * i < NPB ? wv + 4 * i : NPB, xf[i], m[i], ent[i], yoff[i]);
+  for (int i = 0; i < NPW; ++i) xfrags(wv + 4 * i < NPB ? wv + 4 * i : NPB, xf[i], m[i], ent[i]);
 #pragma unroll
-    for (int i = 0; i < NPW; ++i) {
-      if (wv + 4 * i >= NPB) break;   // wave-uniform
+  for (int i = 0; i < NPW; ++i) {
+    if (wv + 4 * i >= NPB) break;   // wave-uniform
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        f32x16 acc;
+    for (int cb = 0; cb < 2; ++cb) {
+      f32x16 acc;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) acc[k] = 0.f;
+      for (int k = 0; k < 16; ++k) acc[k] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          bf16x8 xb;
-          __builtin_memcpy(&xb, &xf[i][ks], 16);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb][ks], xb, acc, 0, 0, 0);
-        }
-        y_block(acc, cb, gb[cb], xf[i], m[i], ent[i], yoff[i]);
+      for (int ks = 0; ks < 4; ++ks) {
+        bf16x8 xb;
+        __builtin_memcpy(&xb, &xf[i][ks], 16);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb][ks], xb, acc, 0, 0, 0);
       }
+      y_block(acc, cb, gb[cb], xf[i], m[i], ent[i]);
     }
-  } else {
-    // ---- stage 1, C / 16 waves: wave w takes position blocks w and w + 8 (< 11) and every 32-channel block; all its x
-    // fragments are loaded up front (one HBM round trip per workgroup, as the C = 64 form), the M_b fragments of block
-    // cb + 1 (L2) while block cb is in the MFMAs
-    constexpr int NKS = C / 16, NWV = 4 * C / 64;
-    const bool two = wv + NWV < NPB;   // wave-uniform
-    u32x4a_t xf[2][NKS];
-    float m[2];
-    int ent[2], yoff[2];
-    xfrags(wv, xf[0], m[0], ent[0], yoff[0]);
-    xfrags(two ? wv + NWV : NPB, xf[1], m[1], ent[1], yoff[1]);
-    bf16x8 ma[2][NKS];
-    auto mload = [&](int cb, bf16x8* dst) __attribute__((always_inline)) {
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        dst[ks] = *reinterpret_cast<const bf16x8*>(mimg + conv_wimg_off(W1, cb * 32 + r, 0, 16 * ks + 8 * h, 2));
-    };
-    mload(0, ma[0]);
-    auto cbstep = [&](auto CBc) __attribute__((always_inline)) {
-      constexpr int cb = decltype(CBc)::value;
-      if (cb + 1 < NCB) mload(cb + 1, ma[(cb + 1) & 1]);
-      float gb[2][8];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) gb[pr][k] = p.gb[cb * 32 + pr * 16 + 8 * h + k];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (i == 1 && !two) break;
-        f32x16 acc;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          bf16x8 xb;
-          __builtin_memcpy(&xb, &xf[i][ks], 16);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma[cb & 1][ks], xb, acc, 0, 0, 0);
-        }
-        y_block(acc, cb, gb, xf[i], m[i], ent[i], yoff[i]);
-      }
-    };
-    static_assert(NCB == 4, "four 32-channel blocks");
-    cbstep(std::integral_constant<int, 0>{}); cbstep(std::integral_constant<int, 1>{});
-    cbstep(std::integral_constant<int, 2>{}); cbstep(std::integral_constant<int, 3>{});
   }
 
   // ---- stage 2: 3x3 stride-2 conv of the patch. Wave w: output channels cb*32.. (cb = w % NCB) of output row
@@ -265,17 +214,13 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(C == 64 ?
 }
 
 bool attn_down_eligible(const AttnDownParams& p) {
-  return ((p.C == 64 && !p.y) || (p.C == 128 && p.y)) && p.F % 4 == 0 && p.T % 2 == 0 && (long)p.B * p.F * p.T * p.C * 2 < (1L << 31);
+  return p.C == 64 && p.F % 4 == 0 && p.T % 2 == 0 && (long)p.B * p.F * p.T * p.C * 2 < (1L << 31);
 }
 
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
   if (!attn_down_eligible(p)) return hipErrorInvalidValue;
   const long grid = (long)p.B * (p.F / 4) * ((p.T / 2 + 31) / 32);
-  if (p.C == 64) {
-    hipLaunchKernelGGL((attn_down_kernel<64, false>), dim3((unsigned)grid), dim3(256), 0, s, p);
-  } else {
-    hipLaunchKernelGGL((attn_down_kernel<128, true>), dim3((unsigned)grid), dim3(512), 0, s, p);
-  }
+  hipLaunchKernelGGL((attn_down_kernel<64>), dim3((unsigned)grid), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -284,10 +229,6 @@ hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
 // frames (the 4 x 32 coarse positions of the tile plus a one-position halo); stage 2 the four sub-pixel 2x2 convs of
 // conv_kernel CONVT4 (out[2J + pf][2K + pt] from coarse rows J + pf - a, columns K + pt - b, taps (a, b)), wave w taking
 // parity w, in conv_kernel's order (16-channel chunk outer, tap inner): bit-identical to the two launches.
-#ifndef GT_AU_PF
-#define GT_AU_PF 0   // attn_up: stage-2 weight fragments requested ahead (0: at use, 1: first half before stage 1, 2: both;
-                     // 1 and 2 cost the third wave per SIMD: 82 -> 91 / 88 us)
-#endif
 namespace au {
 constexpr int PROWS = 6, PCOLS = 34, NPOS = PROWS * PCOLS, NPB = (NPOS + 31) / 32;   // 204 positions, 7 blocks
 constexpr int PLANE = NPOS;                                                          // entries per 8-channel plane
@@ -312,12 +253,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, npos_all * C * 2, 0x00020000);
   const int oob = npos_all * C * 2;
 
-  bf16x8 wpre[GT_AU_PF >= 1 ? 16 : 1];   // stage 2's first-half weight fragments, requested now (see below)
-  if (GT_AU_PF >= 1) {
-    const bf16x8* w0 = reinterpret_cast<const bf16x8*>(p.wup) + wv * 2 * 16 * 64 + lane;
-#pragma unroll
-    for (int st = 0; st < (GT_AU_PF >= 1 ? 16 : 1); ++st) wpre[st] = w0[st * 64];
-  }
   // ---- stage 1: y = (M_b x + g b_out) + x, masked, into LDS. Wave w: position blocks w, w + 4 (< 7), both halves.
   {
     const WImg W1 = conv_wimg(1, 1, C, C);
@@ -406,23 +341,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int pf = wv >> 1, pt = wv & 1;
   const int Ff = 2 * F, Tf = 2 * T;
   const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(p.wup) + wv * 2 * 16 * 64 + lane;   // [par][cb][ch][tap][lane]
-  // the first half's weight fragments were requested before stage 1 (their L2 latency hidden behind it); GT_AU_PF = 2
-  // also requests the second half's during the first half's MFMAs (64 more registers: two waves per SIMD)
+  // (weight fragments requested before stage 1 or during the first half's MFMAs measured slower: the extra registers
+  // cost the third wave per SIMD, 82 -> 88-91 us)
   lds_barrier();
-  bf16x8 wb[GT_AU_PF >= 2 ? 16 : 1];
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) {
     bf16x8 wa[16];
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      if (GT_AU_PF >= 1 && cb == 0) wa[st] = wpre[st];
-      else if (GT_AU_PF >= 2) wa[st] = wb[st < (GT_AU_PF >= 2 ? 16 : 1) ? st : 0];
-      else wa[st] = wsrc[(cb * 16 + st) * 64];
-    }
-    if (GT_AU_PF >= 2 && cb == 0) {
-#pragma unroll
-      for (int st = 0; st < 16; ++st) wb[st] = wsrc[(16 + st) * 64];
-    }
+    for (int st = 0; st < 16; ++st) wa[st] = wsrc[(cb * 16 + st) * 64];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       auto bread = [&](int st) {

@@ -336,13 +336,13 @@ __global__ __launch_bounds__(256, NY == 1 ? 3 : 2) void mconv_pk_kernel(GConvPar
     for (int st = 0; st < NST; ++st) {
       if (st + 1 < NST) rd(st + 1, opd[(st + 1) & 1]);
       const float4 x0 = opd[st & 1][0], x1 = opd[st & 1][1], w0 = opd[st & 1][2], w1 = opd[st & 1][3];
-#define GT_MC4(E)                                                                                    \
+#define MC4_STEP(E)                                                                                    \
   acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.E, w0.E, acc[0][0], 0, 0, 0);                  \
   if (NY == 2) acc[0][NY - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0.E, w1.E, acc[0][NY - 1], 0, 0, 0); \
   acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.E, w0.E, acc[1][0], 0, 0, 0);                  \
   if (NY == 2) acc[1][NY - 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1.E, w1.E, acc[1][NY - 1], 0, 0, 0);
-      GT_MC4(x) GT_MC4(y) GT_MC4(z) GT_MC4(w)
-#undef GT_MC4
+      MC4_STEP(x) MC4_STEP(y) MC4_STEP(z) MC4_STEP(w)
+#undef MC4_STEP
     }
     __syncthreads();
     if (more) {
@@ -632,12 +632,12 @@ __global__ __launch_bounds__(256, 2) void mwgrad_pk_kernel(WGradParams p, int sp
         const float4 q1 = make_float4(q[1], q[2], q[3], q[4]);
         const float2 q2a = *reinterpret_cast<const float2*>(q + 2), q2b = *reinterpret_cast<const float2*>(q + 4);
         const float4 q2 = make_float4(q2a.x, q2a.y, q2b.x, q2b.y);
-#define GT_WG3(E)                                                                          \
+#define WG3_STEP(E)                                                                          \
   acc[3 * kh] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q0.E, acc[3 * kh], 0, 0, 0);         \
   acc[3 * kh + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q1.E, acc[3 * kh + 1], 0, 0, 0); \
   acc[3 * kh + 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.E, q2.E, acc[3 * kh + 2], 0, 0, 0);
-        GT_WG3(x) GT_WG3(y) GT_WG3(z) GT_WG3(w)   // three independent accumulator chains interleaved
-#undef GT_WG3
+        WG3_STEP(x) WG3_STEP(y) WG3_STEP(z) WG3_STEP(w)   // three independent accumulator chains interleaved
+#undef WG3_STEP
       }
     }
   }
@@ -1174,24 +1174,24 @@ hipError_t launch_gconv(const GConvParams& p, hipStream_t s) {
     auto g2 = [&](int rh, int tw, int ct) {
       return dim3((unsigned)((long)p.B * slots(rh, tw)), (unsigned)((p.Cout + ct - 1) / ct));
     };
-#define GT_MPK(KS_, RH_, TW_, KC_)                                                                            \
+#define MPK_LAUNCH(KS_, RH_, TW_, KC_)                                                                            \
   do {                                                                                                        \
     if (ny1(RH_, TW_)) hipLaunchKernelGGL((mconv_pk_kernel<KS_, RH_, TW_, KC_, 1>), g2(RH_, TW_, 32), dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((mconv_pk_kernel<KS_, RH_, TW_, KC_, 2>), g2(RH_, TW_, 64), dim3(256), 0, s, p);           \
   } while (0)
     const long s4 = slots(4, 64), s8 = slots(8, 32), s5 = slots(5, 48);
     const int shape = (s4 <= s8 && s4 <= s5) ? 4 : (s8 <= s5) ? 8 : 5;
-    if (p.KS == 4) GT_MPK(4, 4, 64, 8);
+    if (p.KS == 4) MPK_LAUNCH(4, 4, 64, 8);
     else if (p.KS == 1) {   // 1x1: 32-channel chunks
-      if (shape == 4) GT_MPK(1, 4, 64, 32);
-      else if (shape == 8) GT_MPK(1, 8, 32, 32);
-      else GT_MPK(1, 5, 48, 32);
+      if (shape == 4) MPK_LAUNCH(1, 4, 64, 32);
+      else if (shape == 8) MPK_LAUNCH(1, 8, 32, 32);
+      else MPK_LAUNCH(1, 5, 48, 32);
     } else {
-      if (shape == 4) GT_MPK(3, 4, 64, 16);
-      else if (shape == 8) GT_MPK(3, 8, 32, 16);
-      else GT_MPK(3, 5, 48, 16);
+      if (shape == 4) MPK_LAUNCH(3, 4, 64, 16);
+      else if (shape == 8) MPK_LAUNCH(3, 8, 32, 16);
+      else MPK_LAUNCH(3, 5, 48, 16);
     }
-#undef GT_MPK
+#undef MPK_LAUNCH
     return hipGetLastError();
   }
   if (cfg == 11) {

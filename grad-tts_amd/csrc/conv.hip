@@ -29,29 +29,6 @@
 
 namespace gt {
 
-// 1-D XCD-aware workgroup order (conv_kernel prologue): 2 contiguous spatial range per XCD, 1 interleaved, 0 the
-// (spatial, channel tile, parity) 3-D grid
-#ifndef GT_XCD_MAP
-#define GT_XCD_MAP 2
-#endif
-#ifndef GT_CAP_T
-#define GT_CAP_T 3
-#endif
-#ifndef GT_CAP_1
-#define GT_CAP_1 3
-#endif
-#ifndef GT_CAP_S2
-#define GT_CAP_S2 2
-#endif
-#ifndef GT_CAP_3
-#define GT_CAP_3 0
-#endif
-#ifndef GT_CAP_3W8
-#define GT_CAP_3W8 3
-#endif
-#ifndef GT_SMALL_DBW
-#define GT_SMALL_DBW 1
-#endif
 constexpr int TF1_DBW = 101;   // tile-height code: 1-row tiles with double-buffered weight slabs (ConvCfg::SMALLDB)
 
 template <class A, int KIND, int IN, int OUT, int NT, int W8, int TF_>
@@ -118,8 +95,7 @@ struct ConvCfg {
   // contention, not latency hiding, bounds them): CAP = 0 leaves occupancy to registers and LDS.
   // (measured, tools/ab_variants.sh: 64-wide 1x1 and sub-pixel convs 3, stride-2 64-wide 2; the fp8-weight
   // 3x3 tiles need fewer registers than the bf16 ones and would otherwise run 4 per CU)
-  static constexpr int CAP = NT != 64 ? 0 : KIND == CONVT4 ? GT_CAP_T : KIND == CONV1 ? GT_CAP_1
-                           : KIND == CONV3_S2 ? GT_CAP_S2 : (W8 ? GT_CAP_3W8 : GT_CAP_3);
+  static constexpr int CAP = NT != 64 ? 0 : KIND == CONVT4 ? 3 : KIND == CONV1 ? 3 : KIND == CONV3_S2 ? 2 : (W8 ? 3 : 0);
   static constexpr int SMEM = (CAP && SMEM0 <= 160 * 1024 / (CAP + 1)) ? 160 * 1024 / (CAP + 1) + 512 : SMEM0;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(TF * RBT % WM == 0, "row blocks split evenly over the waves");
@@ -171,18 +147,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   // sub-pixel parities for CONVT4) of one spatial tile -- which all read the same input patch -- get ids 8 apart: the
   // same XCD, dispatched together, the patch fetched into that XCD's L2 once instead of once per tile.
   const int ny = p.Cout / NT, nyz = ny * (CONVT ? 4 : 1);
-  int bid, ntile, par;
-  if (GT_XCD_MAP) {
-    const int nsp = p.B * n_ft * n_tt, lin = blockIdx.x, j = lin >> 3, yz = j % nyz;
-    // GT_XCD_MAP 2: XCD x walks the contiguous spatial range [x S, x S + S) in order (S = ceil(nsp / 8)), so the
-    // tiles one XCD runs together are vertical neighbours whose halo rows its L2 already holds; 1: interleaved
-    bid = GT_XCD_MAP == 2 ? (lin & 7) * ((nsp + 7) >> 3) + j / nyz : (j / nyz) * 8 + (lin & 7);
-    ntile = yz % ny;
-    par = yz / ny;
-    if (bid >= nsp) return;   // grid padding: the whole workgroup, before any barrier
-  } else {
-    bid = blockIdx.x; ntile = blockIdx.y; par = blockIdx.z;
-  }
+  // XCD x walks the contiguous spatial range [x S, x S + S) in order (S = ceil(nsp / 8)), so the tiles one XCD runs
+  // together are vertical neighbours whose halo rows its L2 already holds (round 2: -19 % fetched bytes per U-Net
+  // evaluation against the 3-D grid, +0.9 % against an interleaved 1-D order)
+  const int nsp = p.B * n_ft * n_tt, lin = blockIdx.x, j = lin >> 3, yz = j % nyz;
+  int bid = (lin & 7) * ((nsp + 7) >> 3) + j / nyz;
+  const int ntile = yz % ny;
+  const int par = yz / ny;
+  if (bid >= nsp) return;   // grid padding: the whole workgroup, before any barrier
   const int tt = bid % n_tt; bid /= n_tt;
   const int ft = bid % n_ft;
   const int b = bid / n_ft;
@@ -812,12 +784,12 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s);
 template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
   if constexpr (sizeof(A) == 2) {
-    if constexpr (NT == 128 && !W8 && IN != IN_INPUT && GT_SMALL_DBW)
+    if constexpr (NT == 128 && !W8 && IN != IN_INPUT)
       if (p.small && (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128) <= 256)   // <= one workgroup per CU
         return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, TF1_DBW>(p, s);
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
   }
-  if constexpr (NT == 128 && (IN != IN_GN || GT_L1_TF5_GN) && IN != IN_INPUT && W8 != 2)   // (A8: 4-row tiles)
+  if constexpr (NT == 128 && IN != IN_INPUT && W8 != 2)   // (A8: 4-row tiles)
     if (conv_tf(CONV3, IN, NT, p.Cout, p.Fout) == 5) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 5>(p, s);
   return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, 4>(p, s);
 }
@@ -847,8 +819,7 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
     return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
   const long nsp = (long)p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT);   // spatial tiles
   const unsigned nyz = (unsigned)(p.Cout / NT) * (KIND == CONVT4 ? 4u : 1u);
-  const dim3 grid = GT_XCD_MAP ? dim3((unsigned)(8 * nyz * ((nsp + 7) / 8)))
-                               : dim3((unsigned)nsp, (unsigned)(p.Cout / NT), KIND == CONVT4 ? 4u : 1u);
+  const dim3 grid((unsigned)(8 * nyz * ((nsp + 7) / 8)));
   if (W8 && !p.wscale) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8, TF_>), grid, dim3(256), 0, s, p);
   return hipGetLastError();

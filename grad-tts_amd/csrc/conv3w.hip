@@ -33,21 +33,6 @@
 
 namespace gt {
 
-#ifndef GT_C3W_ASM_DMA
-#define GT_C3W_ASM_DMA 1   // weight DMA by inline asm (see asm_dma16)
-#endif
-#ifndef GT_C3W_VAR
-#define GT_C3W_VAR 0   // timing-only experiment bits (wrong results): 1 no phase barrier, 2 no DMA wait, 4 no next-chunk items
-#endif
-#ifndef GT_C3W_PRIO
-#define GT_C3W_PRIO 0  // s_setprio 1 around each phase's MFMA stream
-#endif
-#ifndef GT_C3W_S256
-#define GT_C3W_S256 5  // weight ring slots of the 256-wide tiles
-#endif
-#ifndef GT_C3W_XD
-#define GT_C3W_XD 2    // item load -> transform distance in phases (capped so the last item is written by phase 7)
-#endif
 #ifndef GT_C3W_STAMP
 #define GT_C3W_STAMP 0   // diagnostic builds only: s_memtime stamps of the phase waits (gt_diag_conv3w_stamps)
 #endif
@@ -57,31 +42,11 @@ namespace gt {
 #ifndef GT_C3W_STAMP_IN
 #define GT_C3W_STAMP_IN 2
 #endif
-#ifndef GT_C3W_STAG
-#define GT_C3W_STAG 1  // stagger the next-chunk item work between the two waves of a SIMD
-#endif
-#ifndef GT_C3W_PF
-#define GT_C3W_PF 2    // fragment prefetch distance in MFMA steps (2, 4 or 5: the B ring must divide 90 steps)
-#endif
-#ifndef GT_C3W_DMAS
-#define GT_C3W_DMAS 0  // stagger the LDS-DMA / item-load issue between the two waves of a SIMD
-#endif
-#ifndef GT_C3W_LGK
-#define GT_C3W_LGK 1   // phase barrier waits for all LDS ops but the next phase's pre-reads (0: lgkmcnt(0))
-#endif
-#ifndef GT_C3W_BAR2
-#define GT_C3W_BAR2 0  // one workgroup barrier per TWO phases (even taps of a chunk, plus tap 8): the weight ring keeps
-                       // one more slot between the DMA target and the slots still being read (D = S - 2)
-#endif
-#ifndef GT_C3W_SPREAD
-#define GT_C3W_SPREAD 1  // next-chunk items transformed at odd phases 1, 3, 5, 7 (NPT <= 4) instead of phases XD ..
-#endif
-#ifndef GT_C3W_SCHED
-#define GT_C3W_SCHED 1   // pin the fragment-read / MFMA interleave with sched_group_barrier
-#endif
 
 namespace c3w {
 constexpr int NTHR = 512, NW = 8, RB = 5, TT = 32, PCOL = TT + 2;
+constexpr int S256 = 5;   // weight ring slots of the 256-wide tiles
+constexpr int PF = 2;     // fragment prefetch distance in MFMA steps (the B ring of PF + 1 must divide a chunk's 90 steps)
 
 template <int BN, int CB>
 struct Cfg {
@@ -97,17 +62,17 @@ struct Cfg {
   static constexpr int PIECES = SLOT / 1024;       // DMA pieces per slot
   static constexpr int PWMAX = (PIECES + NW - 1) / NW;
   static constexpr int PWLO = PIECES / NW;         // pieces of waves >= PIECES % NW
-  static constexpr int S = BN == 256 ? GT_C3W_S256 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
-  static constexpr int D = GT_C3W_BAR2 ? S - 2 : S - 1;   // DMA issue distance in phases
+  static constexpr int S = BN == 256 ? S256 : (CB == 2 ? 6 : 8);   // weight ring slots (LDS budget below)
+  static constexpr int D = S - 1;                  // DMA issue distance in phases
   static constexpr int ITEMS = PP * 4;             // 16-B patch items per chunk
   static constexpr int NPT = (ITEMS + NTHR - 1) / NTHR;
   static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
   // phases between an item's load and its transform (item j: loaded at phase j, transformed at phase j + XD <= 7)
-  static constexpr int XD = (8 - NPT) < GT_C3W_XD ? (8 - NPT) : GT_C3W_XD;
+  static constexpr int XD = (8 - NPT) < 2 ? (8 - NPT) : 2;
   // phase of item j's transform (TP) and of its load (LP): XD phases apart, consecutive items in consecutive phases;
-  // GT_C3W_SPREAD (NPT <= 4): transforms every other phase (1, 3, 5, 7), each load two phases ahead, so the VALU of the
+  // NPT <= 4 (SPREAD): transforms every other phase (1, 3, 5, 7), each load two phases ahead, so the VALU of the
   // operand transform is spread over the chunk instead of filling phases XD .. XD + NPT - 1
-  static constexpr bool SPREAD = GT_C3W_SPREAD && NPT <= 4;
+  static constexpr bool SPREAD = NPT <= 4;
   static constexpr int TP(int j) { return SPREAD ? 1 + 2 * j : j + XD; }
   static constexpr int LP(int j) { return SPREAD ? (TP(j) >= 2 ? TP(j) - 2 : 0) : j; }
   static constexpr int jl(int t) {   // item loaded at phase t, or -1
@@ -125,8 +90,7 @@ struct Cfg {
   static constexpr int SMEM = OFF_F + NF * 4;
   static_assert(WN * WM == NW && WN >= 1, "wave grid");
   static_assert(PIECES * 1024 == SLOT, "whole DMA pieces");
-  static_assert(D >= (GT_C3W_BAR2 ? 3 : 2) && D <= 8, "DMA distance");
-  static_assert(!(GT_C3W_BAR2 && GT_C3W_DMAS), "two-phase barriers assume the DMA issue at the top of the phase");
+  static_assert(D >= 2 && D <= 8, "DMA distance");
   static_assert(NPT <= 6, "items transformed in phases 2..7");
   static_assert(SMEM <= 160 * 1024, "LDS budget: one workgroup per CU");
   static_assert(PBUF >= 272 * 8, "s_red aliases patch buffer 1");
@@ -310,15 +274,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem));
   auto dma = [&](int k, int slot) {
     const char* src = wimg + (long)k * C::SLOT + lane * 16;
-    char* dst = smem + C::OFF_W + slot * C::SLOT;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int piece = C::PIECES >= c3w::NW ? wv + c3w::NW * i : wv % C::PIECES;
-      if (GT_C3W_ASM_DMA)
-        asm_dma16(src + piece * 1024, lds_base + C::OFF_W + slot * C::SLOT + piece * 1024);
-      else
-        __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024),
-                                         (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16, 0, 0);
+      asm_dma16(src + piece * 1024, lds_base + C::OFF_W + slot * C::SLOT + piece * 1024);
     }
   };
   // items of the next chunk loaded at phases in [lo, hi] (item j at phase LP(j))
@@ -331,37 +290,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
   // DMA of their phase).
   constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
-  constexpr int NPRE = GT_C3W_PF + CB;   // LDS reads of the next phase's first PF steps (top_wait)
+  constexpr int NPRE = c3w::PF + CB;   // LDS reads of the next phase's first PF steps (top_wait)
   unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
   auto top_wait = [&](auto Tc, auto MOREc) {
     constexpr int t = decltype(Tc)::value;
     constexpr bool MORE = decltype(MOREc)::value;
-    // GT_C3W_BAR2: phases at odd taps have no wait and no barrier; an even one (taps 0, 2, 4, 6, 8) retires DMA(k+1)
-    // AND DMA(k+2): slot k+1 is pre-read at the end of this phase, slot k+2 at the end of phase k+1, which has no
-    // barrier of its own (W = 2). The DMA of an odd phase overwrites the slot of phase k+D-S = k-2, finished by every
-    // wave before this barrier.
-    constexpr bool skip = GT_C3W_BAR2 && (t & 1);
-    constexpr int W = GT_C3W_BAR2 ? 2 : 1;
-    // DMAs issued after DMA(k+W) before the top of phase k: up to DMA(k-1+D), or DMA(K-1) in the last chunk
-    constexpr int ndma0 = MORE ? C::D - 1 - W : ((8 - t - W) < (C::D - 1 - W) ? (8 - t - W) : (C::D - 1 - W));
+    // DMAs issued after DMA(k+1) before the top of phase k: up to DMA(k-1+D), or DMA(K-1) in the last chunk
+    constexpr int ndma0 = MORE ? C::D - 2 : ((8 - t - 1) < (C::D - 2) ? (8 - t - 1) : (C::D - 2));
     constexpr int ndma = ndma0 > 0 ? ndma0 : 0;
-    // waves 0-3 issue a phase's DMA before its item, waves 4-7 (GT_C3W_DMAS) after it: an item loaded in phase
-    // k + W - D is younger than DMA(k+W) only in the first half
-    constexpr int npl = MORE ? n_lp(t + W - C::D, t - 1) : 0;
-    constexpr int npl4 = MORE ? n_lp(t + W + 1 - C::D, t - 1) : 0;
-    if (skip) { if (STAMP) st[5] += 1; return; }
+    // items loaded in phases k + 1 - D .. k - 1 (each issued after the DMA of its phase)
+    constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
     const unsigned long long a = stamp();
-    if (!(GT_C3W_VAR & 2)) {
-      if (!GT_C3W_DMAS || wv < c3w::NW / 2) vm_wait<ndma * PW + npl>();
-      else vm_wait<ndma * PW + npl4>();
-    }
+    vm_wait<ndma * PW + npl>();
     const unsigned long long b = stamp();
     // LDS: every access of this wave but its last NPRE (the next phase's first fragments, read at the end of the
     // previous phase; they need no barrier, so their latency stays hidden) has completed -- the reads of the slot the
     // DMA below overwrites and the item writes of the next chunk's patch included (LDS ops complete in order)
-    if (GT_C3W_VAR & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    else if (GT_C3W_STAMP || !GT_C3W_LGK) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (GT_C3W_STAMP) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(NPRE) : "memory");
     if (STAMP) { const unsigned long long e = stamp(); st[0] += b - a; st[1] += e - b; st[5] += 1; }
   };
@@ -412,14 +358,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   lds_barrier();
 #pragma unroll
   for (int j = 0; j < C::NPT; ++j) put_item(j, 0, 0);
-  // DMA(0) .. DMA(W) landed (W = 2 with two-phase barriers, else 1; younger: DMA(W+1 .. D-1)); chunk 0's patch written
-  vm_wait<(C::D - 1 - (GT_C3W_BAR2 ? 2 : 1)) * PW>();
+  // DMA(0), DMA(1) landed (younger: DMA(2 .. D-1)); chunk 0's patch written
+  vm_wait<(C::D - 2) * PW>();
   lds_barrier();
 
   // MFMA steps i = s * RB + rb of a phase; fragments are read two steps ahead (B: ring of 3 by the chunk-global step
   // index, a chunk being 90 steps; A: one register set per k-step s), across phase boundaries too: phase k+1's slot and
   // patch are visible from the top of phase k.
-  constexpr int PF = GT_C3W_PF, NB = PF + 1;   // fragment prefetch distance in steps; B ring of NB registers
+  constexpr int PF = c3w::PF, NB = PF + 1;   // fragment prefetch distance in steps; B ring of NB registers
   static_assert(9 * C::NS % NB == 0 && PF <= RB, "B ring index chunk-periodic; A frags double-buffered by k-step");
   bf16x8 fa[2][CB], fb[NB];
 #pragma unroll
@@ -428,9 +374,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   for (int n = 0; n < PF; ++n) fb[n] = rd_b(0, 0, 0, n);
 
   int slot = 0;   // weight slot of the current phase (k mod S)
-  constexpr int DS1 = C::NS / 2;   // MFMA step of the DMA issue of waves 4-7 (GT_C3W_DMAS, below)
   // MFMA steps of the item transforms: waves 0-3 at XS0, waves 4-7 at XS1
-  constexpr int XS0 = GT_C3W_STAG ? 1 : 3, XS1 = GT_C3W_STAG ? C::NS - 3 : 3;
+  constexpr int XS0 = 1, XS1 = C::NS - 3;
   // One chunk: 9 phases. MORE: a chunk c+1 exists (its patch is loaded and written during this chunk).
   auto chunk = [&](int c, auto MOREc) {
     constexpr bool MORE = decltype(MOREc)::value;
@@ -453,20 +398,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       }
       int nslot = slot + 1;
       nslot = nslot == C::S ? 0 : nslot;
-      // (b) DMA of phase k + D into the slot phase k - 1 used: waves 0-3 here, waves 4-7 at MFMA step DS1
-      // (GT_C3W_DMAS), so the two waves of a SIMD do not both stop issuing MFMAs for their LDS-DMA pieces at once
-      auto issue_dma = [&]() {
-        if (MORE || t + C::D < 9) {
-          int ds = slot + C::D;
-          ds = ds >= C::S ? ds - C::S : ds;
-          dma(k + C::D, ds);
-        }
-      };
-      if (!GT_C3W_DMAS || wv < c3w::NW / 2) issue_dma();
+      // (b) DMA of phase k + D into the slot phase k - 1 used
+      if (MORE || t + C::D < 9) {
+        int ds = slot + C::D;
+        ds = ds >= C::S ? ds - C::S : ds;
+        dma(k + C::D, ds);
+      }
       // (c) the next chunk's patch item of this phase (item t), and the counted wait for item t - XD's registers
       // (loaded XD phases ago; younger: items t-XD+1 .. t and the DMAs of XD phases -- the same count in both wave
       // halves). Unconditional in every wave: an asm load whose wait a wave skipped would land in a reused register.
-      if (MORE && !(GT_C3W_VAR & 4)) {
+      if (MORE) {
         if (C::jl(t) >= 0) {
           switch (C::jl(t)) {
             case 0: load_items(c + 1, std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{}); break;
@@ -491,7 +432,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       // (d) MFMAs of phase k
 #pragma unroll
       for (int i = 0; i < C::NS; ++i) {
-        if (GT_C3W_DMAS && i == DS1 && wv >= c3w::NW / 2) issue_dma();
         const int s = i / RB, rb = i % RB;
         const int g = t * C::NS + i;          // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
         const int n = i + PF;                 // step whose fragments are read now
@@ -518,17 +458,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
           acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][cb], fb[g % NB], acc[rb][cb], 0, 0, 0);
-        if (GT_C3W_SCHED) {
-          if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
-          else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
-        }
+        if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
+        else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
         // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
-        if (GT_C3W_PRIO && i == 0) __builtin_amdgcn_s_setprio(1);
         // Staggered between the two waves of a SIMD (waves w and w + 4 share one; MI355X_MICROARCH.md, two waves per
         // SIMD, item 9): waves 0-3 at step XS0, waves 4-7 at step XS1, so one wave's transform VALU runs beside its
         // partner's MFMAs instead of both leaving the matrix pipe idle at the same step.
-        if (MORE && !(GT_C3W_VAR & 4) && (i == XS0 || i == XS1) && C::jt(t) >= 0) {
+        if (MORE && (i == XS0 || i == XS1) && C::jt(t) >= 0) {
           if ((i == XS0 && wv < c3w::NW / 2) || (i == XS1 && wv >= c3w::NW / 2)) {
             const unsigned long long a = stamp();
             put_item(C::jt(t), c + 1, nxt);
@@ -537,7 +474,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
           }
         }
       }
-      if (GT_C3W_PRIO) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       slot = nslot;
     }

@@ -35,20 +35,11 @@ namespace gt {
 
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-#ifndef GT_C64_VAR
-#define GT_C64_VAR 0  // timing-only experiment bits (wrong results): 1 no new-row staging, 2 no output stores, 4 no barrier
-#endif
-#ifndef GT_C64_PAIR
-#define GT_C64_PAIR 0  // two segments per 8-wave workgroup sharing the tile barrier (0: one 4-wave workgroup per segment)
-#endif
 #ifndef GT_C64_STAMP
 #define GT_C64_STAMP 0  // diagnostic builds only: s_memtime stamps (gt_diag_conv64_stamps), instantiation GT_C64_STAMP_IN, F = 80
 #endif
 #ifndef GT_C64_STAMP_IN
 #define GT_C64_STAMP_IN 1
-#endif
-#ifndef GT_C64_PF
-#define GT_C64_PF 2   // MFMA steps a fragment read is issued ahead
 #endif
 
 namespace c64 {
@@ -68,7 +59,6 @@ constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + NW * 8
 // taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room
 constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
-constexpr int NSEG = GT_C64_PAIR ? 2 : 1;                 // segments (4-wave halves) per workgroup
 }  // namespace c64
 
 // IN: IN_MASK / IN_GN / IN_PLAIN. Masks from sequence_mask are 0/1: x * m is then a select, decided per item on
@@ -84,16 +74,10 @@ constexpr int NSEG = GT_C64_PAIR ? 2 : 1;                 // segments (4-wave ha
 __device__ unsigned long long gt_c64_stamps[512 * 4 * 8];
 #endif
 
-// GT_C64_PAIR: one 8-wave workgroup runs two segments, one per 4-wave half, each with its own LDS region, sharing the
-// tile barrier: the two halves advance in lockstep. (As two workgroups per CU, one gets issue priority and finishes its
-// loop ~25 % before the other, which then runs alone on the CU: tools/diag_c64_stamps.py. In lockstep, though, the two
-// halves' staging and epilogues coincide instead of overlapping each other's MFMAs: 96.1 -> 99.9 us, so off.)
 template <int IN, bool W8>
-__global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
-  __shared__ __attribute__((aligned(16))) char smem_all[NSEG * SMEM];   // one LDS object
-  const int half = NSEG == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
-  char* const smem = smem_all + half * SMEM;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
   char* const sR = smem;                                     // ring of RING patch rows
   constexpr int WREG = wreg_of(IN);
   char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
@@ -108,17 +92,13 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
   auto stamp = [&]() -> unsigned long long { return (GT_C64_STAMP && STAMP) ? __builtin_amdgcn_s_memtime() : 0ull; };
   unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const unsigned long long t_entry = stamp();
-  const int tid = threadIdx.x & 255, lane = tid & 63, r = lane & 31, h = lane >> 5;   // (thread of this half)
+  const int tid = threadIdx.x & 255, lane = tid & 63, r = lane & 31, h = lane >> 5;   // (range known: 256 threads)
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: ring-row addressing stays scalar
   const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
   const int F = p.Fout, T = p.Tout;
   const int n_ft = F / TF, n_tt = (T + TT - 1) / TT;
   const int kseg = n_ft / L;                                 // segments per column
-  // this half's segment; a half past the last segment (odd count) runs segment 0 again without storing anything
-  const int nseg_all = p.B * n_tt * kseg;
-  const int seg_raw = blockIdx.x * NSEG + half;
-  const bool dummy = seg_raw >= nseg_all;
-  const int seg = dummy ? 0 : seg_raw;
+  const int seg = blockIdx.x;
   const int col = seg / kseg, part = seg - col * kseg;
   const int b = col / n_tt, tt = col - b * n_tt;
   const int ft0 = part * L;
@@ -283,7 +263,7 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
       const char* rowp2 = sR + ((sbase + 2) % RING) * ROWB + r * POSB + h * 16;
       f32x16 acc;
       const unsigned long long t_pass = stamp();
-      // 36 MFMAs (4 chunks x 9 taps), fragment reads software-pipelined GT_C64_PF steps ahead (issued in the natural
+      // 36 MFMAs (4 chunks x 9 taps), fragment reads software-pipelined PF steps ahead (issued in the natural
       // order the compiler waited on each read right before its MFMA); behind each chunk's MFMAs one staging item of
       // tile k+1's new rows is stored and reloaded for tile k+2 (items spread over the 8 chunk slots of two passes)
       auto xread = [&](int st) {
@@ -296,7 +276,7 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
         return tap < WREG ? wf[ch][tap < WREG ? tap : 0]
                           : *reinterpret_cast<const bf16x8*>(wlp + (tap - WREG) * WTAP_B + ch * 1024);
       };
-      constexpr int PF = GT_C64_PF, NB = PF + 1, NST = NCH * 9;
+      constexpr int PF = 2, NB = PF + 1, NST = NCH * 9;   // (3, 4, 6 steps ahead: unchanged or spilling)
       bf16x8 xb[NB], wb[NB];
 #pragma unroll
       for (int st = 0; st < PF; ++st) { xb[st] = xread(st); wb[st] = wread(st); }
@@ -312,7 +292,7 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
         }
         if (st % 9 == 8) {
           const int j = ps * NCH + st / 9;
-          if (j < PPT && !(GT_C64_VAR & 1)) {
+          if (j < PPT) {
             put_new(j, k + 1);
             issue_new(j, k + 2);
           }
@@ -342,7 +322,7 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
         }
       const int t = t0 + r;
       const bool valid = t < T;
-      const int obyte = (valid && !dummy) ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
+      const int obyte = valid ? (((b * F + ft * TF + lrow) * T + t) * 64) * 2 : oob;   // past the end: dropped
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
         const int c0 = cb * 32 + pr * 16 + 8 * h;   // first of this lane's 8 channels
@@ -360,17 +340,14 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
           asm volatile("" : "+v"(s), "+v"(q));   // scalar chains: see conv.hip (packed-FP32 op_sel hazard)
         }
         const uint4 ov = f_to_item(o, bf16());
-        if (!(GT_C64_VAR & 2))
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
-        else
-          asm volatile("" :: "v"(ov.x), "v"(ov.y), "v"(ov.z), "v"(ov.w));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{ov.x, ov.y, ov.z, ov.w}, rs_out, obyte + c0 * 2, 0, 0);
         gs[pr] += valid ? s : 0.f;
         gq[pr] += valid ? q : 0.f;
       }
       if (GT_C64_STAMP && STAMP) { asm volatile("" :: "v"(gs[1]), "v"(gq[1])); st[4] += stamp() - t_epi; }
     }
     const unsigned long long t_bar = stamp();
-    if (!(GT_C64_VAR & 4)) lds_barrier();   // tile k+1's rows complete
+    lds_barrier();   // tile k+1's rows complete
     if (GT_C64_STAMP && STAMP) { st[2] += stamp() - t_bar; st[5] += 1; }
   }
   const unsigned long long t_loop_end = stamp();
@@ -384,7 +361,7 @@ __global__ __launch_bounds__(256 * c64::NSEG) __attribute__((amdgpu_waves_per_eu
     }
   }
   lds_barrier();
-  if (tid < 8 && !dummy) {   // fixed-order sum over the 2 waves of the group's channel half
+  if (tid < 8) {   // fixed-order sum over the 2 waves of the group's channel half
     const int g = tid, gcb = g >> 2, e = (g & 3) * 2;
     float S = 0.f, Q = 0.f;
 #pragma unroll
@@ -442,8 +419,8 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv64_eligible(p)) return hipErrorInvalidValue;
   const int L = conv64_seg(p.Fout, p.small);
   const long nseg = (long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L);
-  const unsigned grid = (unsigned)((nseg + c64::NSEG - 1) / c64::NSEG);
-  const dim3 block(256 * c64::NSEG);
+  const unsigned grid = (unsigned)nseg;
+  const dim3 block(256);
   if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)
     if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), block, 0, s, p, L);
     else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, true>), dim3(grid), block, 0, s, p, L);

@@ -139,6 +139,9 @@ struct Blob {   // host staging of one packed device arena
 // largest call batch on the small-batch tile plan (small_plan). Measured (50-step decodes, T = 512, one box):
 // B = 1 47.3 vs 78.9 ms, B = 2 50.7 vs 80.6, B = 4 61.0 vs 82.7, B = 8 94.9 vs 94.3, B = 16 152.9 vs 116.3
 constexpr int64_t kSmallB = 4;
+// the largest small_b accepted (gt_decoder_set_small_batch, GT_SMALL_B): chunks of more utterances never take the
+// small-batch plan, so the workspace holds its 256 attention tiles per utterance only up to this batch size
+constexpr int64_t kSmallBMax = 16;
 // small-batch plan attention tiles per utterance and merge rows per workgroup. Measured (B = 1, T = 512, N = 50, one
 // box): 64 tiles + one merge workgroup per head 43.9 ms per decode, + 8 merge workgroups 42.9, 128 tiles 42.3, 256 42.0
 constexpr int kSmallTiles = 256;
@@ -184,12 +187,8 @@ struct gt_decoder {
   // bf16 throughput-plan 3x3 convs at levels 1-2 on conv3w (one 8-wave workgroup per CU owning all output channels of
   // a tile); GT_CONV3W=0 at creation or gt_decoder_set_wide_conv(dec, 0) runs them on conv_kernel
   bool wide = true;
-  // attention merge + fold as one launch (attn_mf_kernel); GT_ATTN_MF=1 at creation (off: slower at B = 32)
-  bool attn_mf = false;
-  // level-0/1 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
+  // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
   bool attn_ds = true;
-  // ... and at level 1 (GT_ATTN_DS1=1; off: the C = 128 form measured 236 us against 101 us for the two launches)
-  bool attn_ds1 = false;
   // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
   bool attn_us = true;
   // small-batch plan attention: tiles per utterance (GT_ATTN_TILES_SMALL) and the merge's rows per workgroup
@@ -225,25 +224,6 @@ namespace {
 int ck_of(int dt) { return dt ? 32 : 16; }
 size_t esize(int dt) { return dt ? 2 : 4; }
 
-// channel count from which block2's GroupNorm/Mish transform runs as a separate in-place pass (gn_apply_kernel)
-// instead of in the conv's operand load. Default: never (1024). Round 2: with the 256-channel GroupNorm-input conv
-// on 5-row tiles the in-register transform (recomputed by both 128-channel tiles and the halo rows) costs
-// 103 us per launch against 87 + 35 us for the plain conv plus the pass (same box, tools/ab_env.sh); the
-// knob (GT_GN_APPLY_MIN_C=256 restores the round-1 split) stays for A/B runs.
-// the first ResnetBlock's output + res_conv over the input channels as an elementwise pass (GT_RB_INPUT=0: the
-// 1x1 conv_kernel with IN_INPUT / OUT_RBOUT, as before round 3)
-static bool rb_input_on() {
-  static const bool v = [] { const char* e = getenv("GT_RB_INPUT"); return !e || atoi(e) != 0; }();
-  return v;
-}
-
-static int gn_apply_min_c() {
-  static const int v = [] {
-    const char* e = getenv("GT_GN_APPLY_MIN_C");
-    return e ? atoi(e) : 1024;
-  }();
-  return v;
-}
 
 // pack [Cout][Cin][KH][KW] (or ConvTranspose [Cin][Cout][4][4], as 4 parity images) into the
 // conv_kernel weight image (wimage.h) in the compute dtype
@@ -630,7 +610,7 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles) {
   int maxtile = 0;
   for (int l = 0; l < 3; ++l) {
     attn_tiles((int64_t)(80 >> l) * (T >> l), small_tiles, L.tile_pos[l], L.ntile[l]);   // small-batch plan
-    maxtile = std::max(maxtile, L.ntile[l]);
+    if (B <= kSmallBMax) maxtile = std::max(maxtile, L.ntile[l]);   // (larger chunks never run it)
     int tp, nt;
     attn_tiles((int64_t)(80 >> l) * (T >> l), 32, tp, nt);   // the throughput plan takes at most 32
     maxtile = std::max(maxtile, nt);
@@ -811,22 +791,8 @@ struct Run {
       tap(k + "pre1", lvl, pre1, Cout);
       tap_part(stat_slot - 2);
     }
-    {   // block2 conv on (Mish(GN(h1))*m + tb)*m
-      // The transform runs once per element in place (one extra read+write of h1) on wide levels
-      // (GT_GN_APPLY_MIN_C, default 256 channels), where the operand-load transform of conv_kernel would be
-      // recomputed by every 128-channel tile and halo row.
-      const bool apply = Cout >= gn_apply_min_c() ||
-                         (dt && GT_L1_TF5 && !GT_L1_TF5_GN && Cout == 128 && Fl(lvl) == 40);   // level 1: plain 5-row tiles
-      if (apply) {
-        RbOutParams a{};
-        a.pre = pre1; a.part = st1; a.nparts = np1; a.gamma = Fp(k + "block1.block.1.weight");
-        a.beta = Fp(k + "block1.block.1.bias"); a.count = count; a.out = pre1; a.mask = mask;
-        a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = Cout; a.T0 = T; a.lvl = lvl;
-        a.tb = tb + tb_off; a.tb_bstride = tb_bstride; a.stepp = stepp;
-        timed(std::string("gn_apply_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
-                  std::to_string(Fl(lvl)), 0.0, 2.0 * B * Fl(lvl) * Tl(lvl) * Cout * esize(dt),
-              [&] { return launch_gn_apply(dt, a, s); });
-      }
+    {   // block2 conv on (Mish(GN(h1))*m + tb)*m: the transform in the conv's operand load (IN_GN). (Round 1 ran it as a
+        // separate in-place pass at 256 channels; since round 2 the operand-load form is faster everywhere.)
       ConvParams p = base(lvl, lvl);
       p.Cin = Cout; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "block2.block.0.weight");
       p.in0 = pre1; p.C0 = Cout;
@@ -834,12 +800,13 @@ struct Run {
       p.gn_count = count; p.tb = tb + tb_off; p.tb_bstride = tb_bstride;
       setw(p, k + "block2.block.0.weight"); p.bias = Fp(k + "block2.block.0.bias");
       p.out = pre2; p.out_part = st2;
-      np2 = conv3_stats(apply ? IN_PLAIN : IN_GN, p, k + "block2.block.0.weight");
+      np2 = conv3_stats(IN_GN, p, k + "block2.block.0.weight");
       tap(k + "pre2", lvl, pre2, Cout);
       tap_part(stat_slot - 1);
     }
-    if (d->index.count(k + "res_conv.weight") && input && rb_input_on()) {
-      // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m) as an elementwise pass
+    if (d->index.count(k + "res_conv.weight") && input) {
+      // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m) as an elementwise pass (a 1x1 conv_kernel
+      // over 2-3 channels measured slower: 100.4 vs 86.3 us, round 3)
       RbOutParams p{};
       p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight");
       p.beta = Fp(k + "block2.block.1.bias"); p.count = count; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl);
@@ -860,7 +827,7 @@ struct Run {
       p.pre_beta = Fp(k + "block2.block.1.bias"); p.pre_count = count;
       p.out = out;
       conv(CONV1, input ? IN_INPUT : IN_MASK, OUT_RBOUT, p);
-    } else if (defer && GT_RB_ATTN) {              // Mish(GN(h2))*m + x*m, formed by the next attn_kv
+    } else if (defer) {                            // Mish(GN(h2))*m + x*m, formed by the next attn_kv
       pend.on = true; pend.name = k.substr(0, k.size() - 1);
       pend.pre = pre2; pend.part = st2; pend.nparts = np2; pend.gamma = Fp(k + "block2.block.1.weight");
       pend.beta = Fp(k + "block2.block.1.bias"); pend.count = count; pend.x = in0; pend.out = out;
@@ -887,22 +854,18 @@ struct Run {
   // level 0: the attention output and the Downsample after it as one pass (attn_down.hip; the attention output is
   // never materialised). false (nothing launched) when not applicable: another dtype, the fused form disabled
   // (GT_ATTN_DS=0), or a probe of the attention output itself.
-  // y: where the attention output goes (level 1: the skip connection of ups.1), or null (level 0: never read)
-  bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* y, void* out) {
-    if (!(dt && wi == GT_BF16 && d->attn_ds && d->dp[wi].count(kd + "conv.weight.wfr"))) return false;
-    if (lvl == 1 && !d->attn_ds1) return false;
-    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1) && !y) return false;
+  bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* out) {
+    if (!(dt && wi == GT_BF16 && d->attn_ds && lvl == 0 && d->dp[wi].count(kd + "conv.weight.wfr"))) return false;
+    if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
     AttnDownParams a{};
     a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
     a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
-    a.wds = W(kd + "conv.weight.wfr"); a.bds = Fp(kd + "conv.bias"); a.out = out; a.y = y;
+    a.wds = W(kd + "conv.weight.wfr"); a.bds = Fp(kd + "conv.bias"); a.out = out;
     if (!attn_down_eligible(a)) return false;
     attention_fold(ka, lvl, in, C);
     const double pin = (double)B * a.F * a.T, pout = pin / 4;
     timed("attn_down_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
-          2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin * (y ? 2.0 : 1.0) + pout) * C * 2.0,
-          [&] { return launch_attn_down(a, s); });
-    if (y) tap(ka.substr(0, ka.size() - 1), lvl, y, C);
+          2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin + pout) * C * 2.0, [&] { return launch_attn_down(a, s); });
     tap(kd.substr(0, kd.size() - 1), lvl + 1, out, C);
     return true;
   }
@@ -954,19 +917,12 @@ struct Run {
               "x" + std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
           npos * C * esize(dt) * (rb ? 3.0 : 1.0), [&] { return launch_attn_kv(dt, a, s); });
     if (rb) tap(pend.name, lvl, in, C);
-    if (d->attn_mf) {
-      timed(std::string("attn_mf_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0, [&] {
-        return launch_attn_merge_fold(dt, part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"),
-                                      Fp(k + "fn.fn.to_qkv.weight.q"), C, Mw, s);
-      });
-    } else {
-      timed("attn_merge_kernel@" + std::to_string(C), 0.0, 0.0, [&] {
-        return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G,
-                                 small ? d->merge_dr_small : 32, s);
-      });
-      timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0,
-            [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
-    }
+    timed("attn_merge_kernel@" + std::to_string(C), 0.0, 0.0, [&] {
+      return launch_attn_merge(part, B, a.ntile, Fp(k + "fn.fn.to_out.weight"), Fp(k + "fn.g"), C, G,
+                               small ? d->merge_dr_small : 32, s);
+    });
+    timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0,
+          [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
   }
 
   void attention_out(const std::string& k, int lvl, const void* in, int C, void* out) {   // y = x + M_b x + g b_out
@@ -1006,17 +962,15 @@ struct Run {
     // down 0 (80 x T, 64 ch)
     resnet("downs.0.0.", 0, nullptr, 0, nullptr, 0, 64, act(0, 0), next_tb(64));
     resnet("downs.0.1.", 0, act(0, 0), 64, nullptr, 0, 64, act(0, 1), next_tb(64), true);
-    if (!attention_down("downs.0.2.", "downs.0.3.", 0, act(0, 1), 64, nullptr, act(1, 0))) {
+    if (!attention_down("downs.0.2.", "downs.0.3.", 0, act(0, 1), 64, act(1, 0))) {
       attention("downs.0.2.", 0, act(0, 1), 64, act(0, 0));
       downsample("downs.0.3.", 0, act(0, 0), 64, act(1, 0));
     }
     // down 1 (40 x T/2, 128 ch); hidden 1 -> act(1,2)
     resnet("downs.1.0.", 1, act(1, 0), 64, nullptr, 0, 128, act(1, 1), next_tb(128));
     resnet("downs.1.1.", 1, act(1, 1), 128, nullptr, 0, 128, act(1, 0), next_tb(128), true);
-    if (!attention_down("downs.1.2.", "downs.1.3.", 1, act(1, 0), 128, act(1, 2), act(2, 0))) {
-      attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
-      downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
-    }
+    attention("downs.1.2.", 1, act(1, 0), 128, act(1, 2));
+    downsample("downs.1.3.", 1, act(1, 2), 128, act(2, 0));
     // down 2 (20 x T/4, 256 ch); hidden 2 -> act(2,2); Identity(x*mask) is absorbed by the next block's mask
     resnet("downs.2.0.", 2, act(2, 0), 128, nullptr, 0, 256, act(2, 1), next_tb(256));
     resnet("downs.2.1.", 2, act(2, 1), 256, nullptr, 0, 256, act(2, 0), next_tb(256), true);
@@ -1122,11 +1076,9 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   for (int k = 0; k < 32; ++k) d->freqs[k] = expf((float)k * negc);
   if (const char* e = getenv("GT_GRAPHS")) d->graphs = atoi(e) != 0;
   if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
-  if (const char* e = getenv("GT_SMALL_B")) d->small_b = atoll(e);
+  if (const char* e = getenv("GT_SMALL_B")) d->small_b = std::max<int64_t>(0, std::min<int64_t>(kSmallBMax, atoll(e)));
   if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
-  if (const char* e = getenv("GT_ATTN_MF")) d->attn_mf = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
-  if (const char* e = getenv("GT_ATTN_DS1")) d->attn_ds1 = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
@@ -1580,7 +1532,7 @@ int gt_decoder_set_wide_conv(gt_decoder* d, int on) {
 
 int gt_decoder_set_small_batch(gt_decoder* d, int64_t max_b) {
   if (!d) return fail(GT_ERR_ARG, "null decoder");
-  if (max_b < 0) return fail(GT_ERR_ARG, "max_b must be >= 0");
+  if (max_b < 0 || max_b > kSmallBMax) return fail(GT_ERR_ARG, "max_b must be in [0, 16]");
   d->small_b = max_b;
   d->drop_graphs();
   return GT_OK;

@@ -62,8 +62,7 @@ struct AttnKVParams {
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s);
 
 // attention output (y = x + M_b x + g b_out, per-utterance 1x1) + Downsample (3x3 stride 2) in one pass, bf16
-// (attn_down.hip): level 0 (C = 64, y = null: hiddens[0] is never read by the up path, diffusion.py:186-201) and level 1
-// (C = 128, y = the skip connection, written once per position)
+// (attn_down.hip): level 0 (C = 64; y is never written: hiddens[0] is never read by the up path, diffusion.py:186-201)
 struct AttnDownParams {
   const void* x; int B, F, T, C;   // attention input [B][F][T][C] (level-0 grid)
   int T0; const float* mask; int lvl;
@@ -72,7 +71,6 @@ struct AttnDownParams {
   const void* wds;                  // downsample weight in fragment order (decoder.cpp pack_frag3x3)
   const float* bds;                 // downsample bias [C]
   void* out;                        // [B][F/2][T/2][C]
-  void* y;                          // C = 128: the attention output [B][F][T][C]; C = 64: null
 };
 bool attn_down_eligible(const AttnDownParams& p);
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s);
@@ -94,9 +92,6 @@ hipError_t launch_attn_up(const AttnUpParams& p, hipStream_t s);
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              int dr, hipStream_t s);
 hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s);
-// attn_merge + attn_fold as one launch (bit-identical folded weights)
-hipError_t launch_attn_merge_fold(int act_bf16, const float* part, int B, int ntile, const float* wout, const float* g,
-                                  const float* wq, int C, void* Mw, hipStream_t s);
 
 struct FinalParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
@@ -111,8 +106,6 @@ hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s);
 struct RbOutParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
   const void* x; void* out; const float* mask; int B, F, T, C, T0, lvl;
-  const float* tb; long tb_bstride;   // gn_apply only: time bias rows
-  const int* stepp;                   // gn_apply only: device step index (tb_at), or null
   // rbout_input only: res_conv over the U-Net input channels {mu, x_t, spk} (level 0): fp32 weight [C][cin], bias
   const float* mu; const float* xt; const float* spk_s; int cin;
   const float* rw; const float* rb;
@@ -121,8 +114,6 @@ hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t
 // the first ResnetBlock's output: Mish(GN(h2))*m + res_conv(x*m) with x = {mu, x_t (, spk)} (2-3 channels, level 0):
 // an elementwise pass (the 1x1 conv over 2-3 input channels is 2-3 FMAs per output element)
 hipError_t launch_rbout_input(int act_bf16, const RbOutParams& p, hipStream_t s);
-// in place: pre = (Mish(GN(pre))*m + tb)*m   (out must equal pre)
-hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s);
 
 struct TembParams {
   int rows; const float* tvals;   // tvals == nullptr: row i is Euler step i of n_steps (t computed on device)

@@ -72,14 +72,10 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 
 // 8 x 16-B items per thread; the block stride (256 items) is a multiple of C, so every thread keeps one
 // channel group (and its GroupNorm scale/shift) for all of its items.
-//   APPLY = false: ResnetBlock output, out = Mish(GN(pre))*m + x*m               (diffusion.py:57-58, 77-79)
-//   APPLY = true : block2's conv input in place, pre = (Mish(GN(pre))*m + tb)*m   (diffusion.py:57-58, 76, 52)
-#ifndef GT_RB_IPT
-#define GT_RB_IPT 8
-#endif
-constexpr int RB_IPT = GT_RB_IPT;
+// ResnetBlock output, out = Mish(GN(pre))*m + x*m (diffusion.py:57-58, 77-79).
+constexpr int RB_IPT = 8;   // items per thread (4 / 16 measured no faster, round 3)
 // RES = 1: the residual is res_conv(x*m) over the U-Net input channels (p.mu, p.xt, p.spk_s; level 0) instead of x*m
-template <class A, bool APPLY, int RES = 0>
+template <class A, int RES = 0>
 __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   __shared__ float s_mean[8], s_rstd[8];
   __shared__ double s_red[272];
@@ -90,7 +86,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   const int c0 = e0 % p.C;
   const long ub = (long)b * total;
   const A* pre = reinterpret_cast<const A*>(p.pre) + ub;
-  const A* xin = reinterpret_cast<const A*>(APPLY || RES ? p.pre : p.x) + ub;
+  const A* xin = reinterpret_cast<const A*>(RES ? p.pre : p.x) + ub;
   A* out = reinterpret_cast<A*>(p.out) + ub;
   // Data and mask loads go out first; the GroupNorm reduction (its own loads + LDS barriers) overlaps them.
   // Item i is position pos0 + i * pstep (C divides the 256-item block stride): frame index by increments.
@@ -103,7 +99,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
     const int e = e0 + i * 256 * ICH;
     if (e < total) {
       vp[i] = *reinterpret_cast<const uint4*>(pre + e);
-      if (!APPLY && !RES) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
+      if (!RES) vx[i] = *reinterpret_cast<const uint4*>(xin + e);
       mk[i] = mask_at(p.mask, p.T0, b, t, p.lvl);
       if (RES) {   // input channels of this position ([B][F][T] fp32 sampler state; spk projected per mel row)
         const int f = e / p.C / p.T;
@@ -126,12 +122,9 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
     }
   }
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
-  float sc[ICH], sh[ICH], tb[ICH];
+  float sc[ICH], sh[ICH];
 #pragma unroll
-  for (int k = 0; k < ICH; ++k) {
-    gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
-    tb[k] = APPLY ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + c0 + k] : 0.f;
-  }
+  for (int k = 0; k < ICH; ++k) gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
     const int e = e0 + i * 256 * ICH;
@@ -139,10 +132,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
       const float m = mk[i];
       float v[ICH];
       item_to_f(vp[i], v, A());
-      if (APPLY) {
-#pragma unroll
-        for (int k = 0; k < ICH; ++k) v[k] = (mish_act<A>(v[k] * sc[k] + sh[k]) * m + tb[k]) * m;
-      } else if (RES) {   // res_conv(x * m): bias + W (x m), fp32
+      if (RES) {   // res_conv(x * m): bias + W (x m), fp32
         const float x0 = xr[i][0] * m, x1 = xr[i][1] * m, x2 = xr[i][2] * m;
 #pragma unroll
         for (int k = 0; k < ICH; ++k) {
@@ -247,23 +237,15 @@ hipError_t launch_final(int act_bf16, const FinalParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-static hipError_t launch_gn_mish(int act_bf16, bool apply, const RbOutParams& p, hipStream_t s) {
+hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
   const int ich = act_bf16 ? 8 : 4;
   const long total = (long)p.F * p.T * p.C;
   if ((256 * ich) % p.C != 0 || total >= (1L << 31)) return hipErrorInvalidValue;
   const long items = total / ich;
   dim3 grid((unsigned)((items + 256 * RB_IPT - 1) / (256 * RB_IPT)), (unsigned)p.B);
-  if (act_bf16) {
-    if (apply) hipLaunchKernelGGL((gn_mish_kernel<bf16, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gn_mish_kernel<bf16, false>), grid, dim3(256), 0, s, p);
-  } else {
-    if (apply) hipLaunchKernelGGL((gn_mish_kernel<float, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((gn_mish_kernel<float, false>), grid, dim3(256), 0, s, p);
-  }
+  if (act_bf16) hipLaunchKernelGGL((gn_mish_kernel<bf16>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gn_mish_kernel<float>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
-}
-hipError_t launch_rbout_identity(int act_bf16, const RbOutParams& p, hipStream_t s) {
-  return launch_gn_mish(act_bf16, false, p, s);
 }
 hipError_t launch_rbout_input(int act_bf16, const RbOutParams& p, hipStream_t s) {
   const int ich = act_bf16 ? 8 : 4;
@@ -271,12 +253,9 @@ hipError_t launch_rbout_input(int act_bf16, const RbOutParams& p, hipStream_t s)
   if ((256 * ich) % p.C != 0 || total >= (1L << 31) || p.cin < 2 || p.cin > 3 || p.lvl != 0) return hipErrorInvalidValue;
   const long items = total / ich;
   dim3 grid((unsigned)((items + 256 * RB_IPT - 1) / (256 * RB_IPT)), (unsigned)p.B);
-  if (act_bf16) hipLaunchKernelGGL((gn_mish_kernel<bf16, false, 1>), grid, dim3(256), 0, s, p);
-  else hipLaunchKernelGGL((gn_mish_kernel<float, false, 1>), grid, dim3(256), 0, s, p);
+  if (act_bf16) hipLaunchKernelGGL((gn_mish_kernel<bf16, 1>), grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((gn_mish_kernel<float, 1>), grid, dim3(256), 0, s, p);
   return hipGetLastError();
-}
-hipError_t launch_gn_apply(int act_bf16, const RbOutParams& p, hipStream_t s) {
-  return launch_gn_mish(act_bf16, true, p, s);
 }
 
 hipError_t launch_temb(const TembParams& p, hipStream_t s) {

@@ -40,9 +40,12 @@ struct gt_text_encoder {
   bool host_stale = false;
   hipEvent_t dev_done = nullptr;   // recorded on the caller's stream by set_params_device (refresh_host waits on it)
   // parameter generation: bumped by every host or device parameter change; forward_train records it per tape (keyed by
-  // the workspace base) and backward refuses a tape taken under other parameters
+  // the workspace base) and backward refuses a tape taken under other parameters. The 256 most recently written
+  // tapes are tracked (kMaxTapes): past that the OLDEST by insertion order is dropped, so a backward on a tape that is
+  // older than the last 256 forward_train calls of this encoder reports "no forward_train tape".
   uint64_t gen = 0;
-  std::map<const void*, uint64_t> tape_gen;
+  uint64_t tape_seq = 0;
+  std::map<const void*, std::pair<uint64_t, uint64_t>> tape_gen;   // base -> (parameter generation, insertion number)
 };
 
 namespace {
@@ -528,8 +531,14 @@ int gt_text_encoder_forward_train(gt_text_encoder* e, const int64_t* tokens, con
   }
   if (err != hipSuccess) return gt_internal_fail(GT_ERR_HIP, std::string("text encoder training forward: ") + hipGetErrorString(err));
   if (bad_ptr) return gt_internal_fail(GT_ERR_WORKSPACE, "text encoder training forward: tape offset outside the layout");
-  if (e->tape_gen.size() >= 256 && !e->tape_gen.count(base)) e->tape_gen.erase(e->tape_gen.begin());
-  e->tape_gen[base] = e->gen;
+  constexpr size_t kMaxTapes = 256;
+  if (e->tape_gen.size() >= kMaxTapes && !e->tape_gen.count(base)) {
+    auto oldest = e->tape_gen.begin();
+    for (auto it = e->tape_gen.begin(); it != e->tape_gen.end(); ++it)
+      if (it->second.second < oldest->second.second) oldest = it;
+    e->tape_gen.erase(oldest);
+  }
+  e->tape_gen[base] = {e->gen, e->tape_seq++};
   return GT_OK;
 }
 
@@ -545,7 +554,7 @@ int gt_text_encoder_backward(gt_text_encoder* e, const float* dmu_x, const float
   {
     const auto it = e->tape_gen.find(base);
     if (it == e->tape_gen.end()) return gt_internal_fail(GT_ERR_ARG, "backward: no forward_train tape in this workspace");
-    if (e->dirty || it->second != e->gen)
+    if (e->dirty || it->second.first != e->gen)
       return gt_internal_fail(GT_ERR_PARAM, "parameters changed between forward_train and backward");
   }
   const size_t usable = workspace_bytes - (size_t)(base - (char*)workspace);

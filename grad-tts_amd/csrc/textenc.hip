@@ -328,7 +328,7 @@ hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
     const int nb = fill(n1) > fill(n2) + 0.2 ? 1 : 2;
     const dim3 g((unsigned)(p.B * ((p.Q + (nb == 2 ? ft2 : ft2 / 2) - 1) / (nb == 2 ? ft2 : ft2 / 2))),
                  (unsigned)((p.Cout + ct - 1) / ct));
-#define GT_C1D_PK(KM, KC, SP)                                                                               \
+#define C1D_PK_LAUNCH(KM, KC, SP)                                                                               \
   do {                                                                                                      \
     if (narrow) {                                                                                           \
       if (nb == 2) hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 32, 2>), g, dim3(256), 0, s, p);           \
@@ -338,11 +338,11 @@ hipError_t launch_c1d(const C1dParams& p, hipStream_t s) {
       else hipLaunchKernelGGL((c1d_pk_kernel<KM, KC, SP, 64, 1>), g, dim3(256), 0, s, p);                   \
     }                                                                                                       \
   } while (0)
-    if (p.K <= 3 && span <= 10) GT_C1D_PK(3, 32, 10);
-    else if (p.K <= 7 && span <= 30) GT_C1D_PK(7, 16, 30);
-    else if (span <= 50) GT_C1D_PK(11, 16, 50);
-    else GT_C1D_PK(11, 16, C1_SPAN);
-#undef GT_C1D_PK
+    if (p.K <= 3 && span <= 10) C1D_PK_LAUNCH(3, 32, 10);
+    else if (p.K <= 7 && span <= 30) C1D_PK_LAUNCH(7, 16, 30);
+    else if (span <= 50) C1D_PK_LAUNCH(11, 16, 50);
+    else C1D_PK_LAUNCH(11, 16, C1_SPAN);
+#undef C1D_PK_LAUNCH
     return hipGetLastError();
   }
   if (p.K <= 3 && span <= 10) hipLaunchKernelGGL((c1d_kernel<3, 32, 10>), grid, dim3(256), 0, s, p);

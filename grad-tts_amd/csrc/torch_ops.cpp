@@ -71,6 +71,20 @@ at::Tensor f32c(const at::Tensor& t, const at::Device& dev) { return t.to(dev, a
 
 hipStream_t stream_of(const at::Device& dev) { return c10::hip::getCurrentHIPStream(dev.index()).stream(); }
 
+// Masks are 0/1 (sequence_mask, model/utils.py:6-10; the reference's callers never build others). The decoder's fused
+// kernels rely on it: the reference masks some operands twice (Block: (Mish(GN(h))*m + tb)*m, diffusion.py:56-58,
+// 74-77), which the library computes as one multiply -- exact for 0/1 masks, 40-60 % off for fractional ones. A
+// fractional mask is therefore rejected here instead of decoded wrongly. The check reads one flag back (a host
+// sync); inside a HIP-graph capture, where no host read is allowed, it is skipped (the captured call was checked when
+// its inputs were made, or is the caller's contract).
+void check_binary_mask(const at::Tensor& m32, hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return;
+  const bool bad = (m32.ne(0) & m32.ne(1)).any().item<bool>();
+  TORCH_CHECK(!bad, "gradtts: mask values must be 0 or 1 (sequence_mask); fractional masks are not supported by the "
+              "fused decoder (the reference's double masking x*m*m is computed as x*m)");
+}
+
 at::Tensor reverse_diffusion_hip(int64_t decoder, int64_t dtype, const at::Tensor& z, const at::Tensor& mask,
                                  const at::Tensor& mu, int64_t n_timesteps, const std::optional<at::Tensor>& spk) {
   check_decoder_io(z, mask, mu, "z");
@@ -83,6 +97,7 @@ at::Tensor reverse_diffusion_hip(int64_t decoder, int64_t dtype, const at::Tenso
   if (spk.has_value()) s32 = f32c(*spk, dev);
   at::Tensor out = at::empty({B, 80, T}, z32.options());
   if (B == 0) return out.to(z.scalar_type());
+  check_binary_mask(m32, stream_of(dev));
   auto* d = reinterpret_cast<gt_decoder*>(decoder);
   const Api& A = api();
   const size_t nb = A.ws_bytes(d, (int)dtype, B, T, (int32_t)n_timesteps);
@@ -107,6 +122,7 @@ at::Tensor estimator_hip(int64_t decoder, int64_t dtype, const at::Tensor& x, co
   if (spk.has_value()) s32 = f32c(*spk, dev);
   at::Tensor out = at::empty({B, 80, T}, x32.options());
   if (B == 0) return out.to(x.scalar_type());
+  check_binary_mask(m32, stream_of(dev));
   auto* d = reinterpret_cast<gt_decoder*>(decoder);
   const Api& A = api();
   const size_t nb = A.ws_bytes(d, (int)dtype, B, T, 0);

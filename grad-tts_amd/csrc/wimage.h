@@ -21,57 +21,30 @@ inline __host__ __device__ constexpr int conv_nt(int act_bf16, int cout) { retur
 // (320 positions): every level's row count (80 >> l) divides by 5, and at B = 32 the level-2 grid becomes one
 // whole round of 2 workgroups per CU (512 tiles instead of 640). The GroupNorm-input variant keeps 4 rows (the
 // extra accumulators spill there), as do 128-output convs (256 tiles would leave half the slots empty).
-#ifndef GT_TF5
-#define GT_TF5 1
-#endif
-// 128-output convs without an operand transform on the 40-row level-1 grid on 5-row tiles too (1024 tiles at B = 32
-// instead of 1280). On since round 2 (same-box A/B: 97.5 -> 95.0 us and 65.4 -> 62.3 us for the two level-1 block1
-// convs); in round 1 it was tied to a gn_apply pass for the GroupNorm-input variant, which GT_L1_TF5_GN replaced.
-#ifndef GT_L1_TF5
-#define GT_L1_TF5 1
-#endif
-// The level-1 GroupNorm-input conv (128 -> 128, 40 rows) on 5-row tiles with the in-register GroupNorm transform:
-// 1024 tiles at B = 32 (two whole rounds of 512 slots) instead of 1280. On since round 2: with the interleaved
-// row blocks it fits 247 VGPRs without spilling (round 1: 51 VGPRs spilled, 196 vs 139 us); same-box A/B
-// +0.7-0.9 % end to end (tools/ab_variants_full.sh).
-#ifndef GT_L1_TF5_GN
-#define GT_L1_TF5_GN 1
-#endif
-// 128-wide 1x1 convs on 5-row tiles where that removes a partial round of workgroups (2 per CU): level 2 with 256
-// output channels (640 -> 512 tiles at B = 32) and level 1 (1280 -> 1024)
-#ifndef GT_TF5_1X1
-#define GT_TF5_1X1 1
-#endif
-// Identity-residual ResnetBlock outputs that feed an attention block are formed inside attn_kv_kernel (operand load)
-// instead of a separate gn_mish pass (6 of the 7 such blocks per U-Net evaluation; mid_block2 keeps the pass)
-#ifndef GT_RB_ATTN
-#define GT_RB_ATTN 1
-#endif
-// The 128-channel Upsample (level 2 -> 1, 20 coarse rows) on 5-row tiles: 1280 -> 1024 workgroups at B = 32 (two
-// whole rounds of 512 instead of 2.5)
-#ifndef GT_TF5_T
-#define GT_TF5_T 1
-#endif
+// Also on 5-row tiles (round-2 same-box A/Bs):
+//  * 128-output convs without an operand transform on the 40-row level-1 grid (1024 tiles at B = 32 instead of 1280;
+//    97.5 -> 95.0 us and 65.4 -> 62.3 us for the two level-1 block1 convs);
+//  * the level-1 GroupNorm-input conv (128 -> 128, 40 rows) with the in-register GroupNorm transform: two whole rounds
+//    of 512 slots instead of 1280 tiles; fits 247 VGPRs with the interleaved row blocks (+0.7-0.9 % end to end);
+//  * 128-wide 1x1 convs where that removes a partial round of workgroups (2 per CU): level 2 with 256 output channels
+//    (640 -> 512 tiles at B = 32) and level 1 (1280 -> 1024);
+//  * the 128-channel Upsample (level 2 -> 1, 20 coarse rows): 1280 -> 1024 workgroups at B = 32.
+// (conv3w, conv3w.hip, now runs most of these 3x3 convs on the bf16 throughput plan; conv_kernel keeps the rest.)
 // mel rows per 3x3 / 1x1 tile (kind/im: ConvKind/InMode values, nt: channel tile, cout: output channels, f: grid
 // rows, small: the small-batch plan). Small batches (decoder.cpp small_plan) take one-row tiles for 128-wide and
 // two-row tiles for 64-wide convs (64 positions per wave pair: 4-5x the workgroups of the throughput tiles, which at
 // B = 1 fill 16-40 of the 256 CUs).
 inline __host__ __device__ constexpr int conv_tf(int kind, int im, int nt, int cout, int f, int small = 0) {
   return (small && (kind == 0 /*CONV3*/ || kind == 2 /*CONV1*/)) ? (nt == 128 ? 1 : 2)
-         : (GT_TF5_1X1 && kind == 2 /*CONV1*/ && nt == 128 && (cout >= 256 || f == 40)) ? 5
-         : (GT_TF5_T && kind == 3 /*CONVT4*/ && nt == 128 && f == 40) ? 5
-         : (GT_TF5 && kind == 0 /*CONV3*/ && nt == 128 &&
-            ((im != 2 /*IN_GN*/ && (cout >= 256 || (GT_L1_TF5 && cout == 128 && f == 40))) ||
-             (im == 2 && (cout >= 256 || (GT_L1_TF5_GN && cout == 128 && f == 40))))) ? 5 : 4;
+         : (kind == 2 /*CONV1*/ && nt == 128 && (cout >= 256 || f == 40)) ? 5
+         : (kind == 3 /*CONVT4*/ && nt == 128 && f == 40) ? 5
+         : (kind == 0 /*CONV3*/ && nt == 128 && (cout >= 256 || (cout == 128 && f == 40))) ? 5 : 4;
 }
 // bytes of one position's channel chunk in LDS: 16 channels = one MFMA k-step (32 B bf16, 64 B fp32). bf16 1x1 convs
-// over activations (cin > 16) take GT_CKB_1X1 bytes (default 32 channels = two k-steps): a 1x1 chunk is one tap, so a
-// 16-channel chunk left one barrier + weight/patch round trip per 10 MFMAs per wave.
-#ifndef GT_CKB_1X1
-#define GT_CKB_1X1 64
-#endif
+// over activations (cin > 16) take 64 bytes (32 channels = two k-steps): a 1x1 chunk is one tap, so a 16-channel chunk
+// left one barrier + weight/patch round trip per 10 MFMAs per wave (64-channel chunks measured slower: registers).
 inline __host__ __device__ constexpr int conv_ckb(int act_bf16, int ntap = 9, int cin = 0) {
-  return act_bf16 ? ((ntap == 1 && cin > 16) ? GT_CKB_1X1 : 32) : 64;
+  return act_bf16 ? ((ntap == 1 && cin > 16) ? 64 : 32) : 64;
 }
 inline __host__ __device__ constexpr int conv_wrow(int ntap, int ckb) { return ntap * ckb + 16; }
 inline __host__ __device__ constexpr int round4k(int b) { return ((b + 4095) / 4096) * 4096; }

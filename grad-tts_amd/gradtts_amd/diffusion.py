@@ -125,6 +125,18 @@ def _f32c(t, device):
     return None if t is None else t.to(device=device, dtype=torch.float32).contiguous()
 
 
+def _check_binary_mask(mask):
+    """Masks are 0/1 (``sequence_mask``, model/utils.py:6-10). The library computes the reference's double masking
+    (``(Mish(GN(h)) * m + tb) * m``, model/diffusion.py:56-58, 74-77) as one multiply, exact only for 0/1 masks, so a
+    fractional mask is rejected rather than decoded wrongly. Same rule as the torch ops (csrc/torch_ops.cpp
+    check_binary_mask); skipped inside a graph capture, where the host cannot read the flag."""
+    if mask.is_cuda and torch.cuda.is_current_stream_capturing():
+        return
+    if bool(((mask != 0) & (mask != 1)).any()):
+        raise RuntimeError("gradtts: mask values must be 0 or 1 (sequence_mask); fractional masks are not supported "
+                           "by the fused decoder (the reference's double masking x*m*m is computed as x*m)")
+
+
 class GradLogPEstimator2d(torch.nn.Module):
     """Score network s_theta (model/diffusion.py:128-216) -- parameters here, compute in libgradtts.so."""
 
@@ -377,6 +389,7 @@ class Diffusion(torch.nn.Module):
             z = torch.randn(x0.shape, dtype=x0.dtype, device=x0.device, requires_grad=False)
         B, _, T = x0.shape
         x32, m32, mu32, z32 = (_f32c(a, device) for a in (x0, mask, mu, z))
+        _check_binary_mask(m32)
         t32 = _f32c(torch.as_tensor(t).reshape(-1), device)
         spk32 = est._spk(spk, B, device)
         if torch.is_grad_enabled() and (any(p.requires_grad for p in est.parameters()) or mu.requires_grad or

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ._lib import check, lib
+from .diffusion import _check_binary_mask
 
 
 class SPEECHSDE:
@@ -138,6 +139,7 @@ class _Evaluator:
             raise RuntimeError("gradtts_amd.likelihood needs a HIP (MI355X) device; there is no CPU path")
         self.mu = _f32(sde.mu, self.device)
         self.mask = _f32(sde.mask, self.device)
+        _check_binary_mask(self.mask)
         self.B, _, self.T = self.mu.shape
         spk = getattr(model, "spk", sde.speaker)
         self.spk = est._spk(spk, self.B, self.device)

@@ -107,7 +107,8 @@ int gt_decoder_set_graphs(gt_decoder* dec, int on);
 int64_t gt_decoder_graph_captures(const gt_decoder* dec);
 /* Small-batch tile plan: GT_BF16 and GT_BF16_W8 calls on at most max_b utterances (env GT_SMALL_B at creation)
  * use 1-/2-row conv tiles and (GT_BF16) one-tile conv64 segments, so a single utterance fills the GPU (latency). Default 4. Each plan
- * is batch-invariant on its own; across plans results agree to fp32 rounding of the GroupNorm sums. 0 disables. */
+ * is batch-invariant on its own; across plans results agree to fp32 rounding of the GroupNorm sums. 0 disables;
+ * max_b > 16 is rejected (GT_ERR_ARG: the workspace holds the small plan's attention partials up to 16 utterances). */
 int gt_decoder_set_small_batch(gt_decoder* dec, int64_t max_b);
 /* Wide-tile 3x3 convs (default on; env GT_CONV3W=0 at creation turns them off): GT_BF16 throughput-plan calls run the
  * level-1/2 Block convs (model/diffusion.py:52; Cout 64/128/256, Cin % 32 == 0) as one 8-wave workgroup per CU that owns
