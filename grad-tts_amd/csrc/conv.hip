@@ -81,6 +81,13 @@ struct ConvCfg {
   // 1x1 convs: two weight slabs, chunk c+1's DMA in flight during chunk c's MFMAs (a 1x1 chunk is one tap, too
   // short to hide a weight round trip behind; the slab is 4-8 KB)
   static constexpr bool DBW = (!SPLIT && KIND == CONV1) || SMALLDB;
+  // Split-K (small-batch plan, 128-wide bf16 3x3 tiles): p.ksplit workgroups per output tile each run a contiguous
+  // range of input-channel chunks and leave their fp32 accumulators in p.sk_part; the last to finish (a counter per
+  // tile, which it re-arms) adds the partials in split order -- a fixed order, so the result does not depend on which
+  // finished last -- and runs the epilogue. A single utterance's level-2 convs otherwise occupy 80 of the 256 CUs, each
+  // streaming 590 KB of weights through LDS.
+  static constexpr bool SK = KIND == CONV3 && OUT == OUT_STATS && NT == 128 && (TF_ == TF1_DBW || TF_ == 1) &&
+                             IN != IN_INPUT && !W8 && sizeof(A) == 2;
   static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
   static constexpr int CK = A8 ? 32 : CKB / (int)sizeof(A);   // input channels per chunk
   static constexpr int ICH = 16 / (int)sizeof(A);            // channels per item (one 16-B global load)
@@ -146,15 +153,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   // 1-D grid, XCD-aware (launch_t): workgroup ids go round robin over the 8 XCDs, so the ny output-channel tiles (x 4
   // sub-pixel parities for CONVT4) of one spatial tile -- which all read the same input patch -- get ids 8 apart: the
   // same XCD, dispatched together, the patch fetched into that XCD's L2 once instead of once per tile.
-  const int ny = p.Cout / NT, nyz = ny * (CONVT ? 4 : 1);
+  const int ksplit = C::SK && p.ksplit > 1 ? p.ksplit : 1;
+  const int ny = p.Cout / NT, nyz = ny * (CONVT ? 4 : ksplit);
   // XCD x walks the contiguous spatial range [x S, x S + S) in order (S = ceil(nsp / 8)), so the tiles one XCD runs
   // together are vertical neighbours whose halo rows its L2 already holds (round 2: -19 % fetched bytes per U-Net
   // evaluation against the 3-D grid, +0.9 % against an interleaved 1-D order)
   const int nsp = p.B * n_ft * n_tt, lin = blockIdx.x, j = lin >> 3, yz = j % nyz;
   int bid = (lin & 7) * ((nsp + 7) >> 3) + j / nyz;
   const int ntile = yz % ny;
-  const int par = yz / ny;
+  const int par = CONVT ? yz / ny : 0;
+  const int split = C::SK ? yz / ny : 0;
   if (bid >= nsp) return;   // grid padding: the whole workgroup, before any barrier
+  const int sp_id = bid;    // spatial tile (split-K: the counter / partial slot is per (spatial tile, ntile))
   const int tt = bid % n_tt; bid /= n_tt;
   const int ft = bid % n_ft;
   const int b = bid / n_ft;
@@ -212,12 +222,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(p.in1 ? p.in1 : p.in0), (short)0, npos * (p.in1 ? p.C1 : p.C0) * ES, 0x00020000);
   // byte offset of item j = pidx[j] * pos_bytes + sub * 16, formed per load (one VALU op; no offset registers)
-  int pos_bytes = p.C0 * ES;
+  // split-K: this workgroup's input-channel chunks [c_lo, c_lo + nchunk) of nchunk_all
+  const int nchunk_all = p.Cin_pad / C::CK;
+  const int c_lo = split * nchunk_all / ksplit;
+  const int nchunk = (split + 1) * nchunk_all / ksplit - c_lo;
+  const int cb0 = c_lo * C::CK;   // first input channel; load_patch / store_patch / issue_patch take offsets from it
+  int pos_bytes = (IN != IN_INPUT && p.C1 != 0 && cb0 >= p.C0 ? p.C1 : p.C0) * ES;
   auto set_offsets = [&](int Cs) { pos_bytes = Cs * ES; };
   auto voff = [&](int j) { return pidx[j] * pos_bytes + sub * 16; };
 
   u32x4 preg[C::PPT];
   auto load_patch = [&](int c0) {
+    c0 += cb0;
     if (IN == IN_INPUT) {   // channels {mu, x_t, spk} (diffusion.py:181/184) -- single chunk
 #pragma unroll
       for (int j = 0; j < C::PPT; ++j) {
@@ -268,6 +284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
     }
   };
   auto store_patch = [&](int c0) {
+    c0 += cb0;
     float sc[C::ICH], sh[C::ICH], tb[C::ICH];
     if (IN == IN_GN) {
 #pragma unroll
@@ -351,8 +368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
       for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
 
   const char* wimg = reinterpret_cast<const char*>(p.w) + (long)b * p.w_bstride;
-  const int nchunk = p.Cin_pad / C::CK;
-  wimg += ((long)(par * ny + ntile) * nchunk) * C::WBYTES;
+  wimg += ((long)(par * ny + ntile) * nchunk_all + c_lo) * C::WBYTES;
 
   auto dma_weights_to = [&](int ch, char* dst) {   // contiguous slab, 1 KiB per wave instruction, compile-time count
     const char* src = wimg + (long)ch * C::WBYTES + lane * 16;
@@ -542,7 +558,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   // patch loads of chunk k (channels k*CK..): switch to the second tensor's offsets at the concat boundary
   auto issue_patch = [&](int k) {
     const int ck0 = k * C::CK;
-    if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && ck0 == p.C0) set_offsets(p.C1);
+    if (IN != IN_INPUT && p.C1 != 0 && p.C1 != p.C0 && cb0 + ck0 == p.C0) set_offsets(p.C1);
     load_patch(ck0);
   };
 
@@ -619,6 +635,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
       cta_sync();
       if (ch + 1 < nchunk) issue_patch(ch + 1);        // in flight during this chunk's MFMAs
       mma_taps(0, C::NTAP);
+    }
+  }
+
+  if constexpr (C::SK) {
+    if (ksplit > 1) {   // split-K: publish this split's accumulators; the tile's last workgroup reduces and goes on
+      // The partials and the counter are accessed as agent-scope relaxed atomics (stores / loads at the device
+      // coherence point, past the XCDs' non-coherent L2s; vector memory instructions) and ordered by waiting for the
+      // stores' completion before the counter increment: a __threadfence() here (L2 write-back + invalidate per
+      // workgroup) measured slower than not splitting at all.
+      constexpr int PW = C::RBW * 2 * 16 * 256;   // floats per (tile, split), [rb][cb][k][thread]
+      const long slot = (long)sp_id * ny + ntile;
+      float* mine = p.sk_part + (slot * ksplit + split) * PW;
+#pragma unroll
+      for (int rb = 0; rb < C::RBW; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            __hip_atomic_store(mine + ((rb * 2 + cb) * 16 + k) * 256 + tid, acc[rb][cb][k], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores completed
+      __syncthreads();                                    // ... and every other wave's
+      int* s_flag = reinterpret_cast<int*>(s_mean);       // (s_mean / s_rstd are prologue-only)
+      if (tid == 0) s_flag[0] = __hip_atomic_fetch_add(p.sk_cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      if (s_flag[0] != ksplit - 1) return;                // workgroup-uniform: another split finishes the tile
+      const float* base = p.sk_part + slot * ksplit * PW;
+#pragma unroll
+      for (int rb = 0; rb < C::RBW; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          f32x16 sum = acc[rb][cb];
+          for (int sp = 0; sp < ksplit; ++sp) {           // fixed order: split 0 + split 1 + ...
+            f32x16 v = acc[rb][cb];
+            if (sp != split) {
+#pragma unroll
+              for (int k = 0; k < 16; ++k)
+                v[k] = __hip_atomic_load(base + sp * PW + ((rb * 2 + cb) * 16 + k) * 256 + tid, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (sp == 0) {
+              sum = v;
+            } else {
+#pragma unroll
+              for (int k = 0; k < 16; ++k) sum[k] += v[k];
+            }
+          }
+          acc[rb][cb] = sum;
+        }
+      if (tid == 0) __hip_atomic_store(p.sk_cnt + slot, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
     }
   }
 
@@ -785,7 +851,7 @@ template <class A, int IN, int NT, int W8>
 static hipError_t launch_c3(const ConvParams& p, hipStream_t s) {
   if constexpr (sizeof(A) == 2) {
     if constexpr (NT == 128 && !W8 && IN != IN_INPUT)
-      if (p.small && (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128) <= 256)   // <= one workgroup per CU
+      if (p.small && (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128) * (p.ksplit > 1 ? p.ksplit : 1) <= 256)
         return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, TF1_DBW>(p, s);
     if (p.small) return launch_t<A, CONV3, IN, OUT_STATS, NT, W8, NT == 128 ? 1 : 2>(p, s);
   }
@@ -818,7 +884,9 @@ static hipError_t launch_t(const ConvParams& p, hipStream_t s) {
   if ((long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * (long)sizeof(A) >= (1L << 31))
     return hipErrorInvalidValue;   // raw buffer ranges are 32-bit
   const long nsp = (long)p.B * (Fg / C::TF) * ((Tg + C::TT - 1) / C::TT);   // spatial tiles
-  const unsigned nyz = (unsigned)(p.Cout / NT) * (KIND == CONVT4 ? 4u : 1u);
+  const unsigned ks = C::SK && p.ksplit > 1 ? (unsigned)p.ksplit : 1u;
+  if (ks > 1 && (ks > (unsigned)(p.Cin_pad / C::CK) || !p.sk_part || !p.sk_cnt)) return hipErrorInvalidValue;
+  const unsigned nyz = (unsigned)(p.Cout / NT) * (KIND == CONVT4 ? 4u : ks);
   const dim3 grid((unsigned)(8 * nyz * ((nsp + 7) / 8)));
   if (W8 && !p.wscale) return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_kernel<A, KIND, IN, OUT, NT, W8, TF_>), grid, dim3(256), 0, s, p);
@@ -862,6 +930,15 @@ static hipError_t dispatch_a8(ConvKind kind, InMode im, OutMode om, const ConvPa
     if (im == IN_PLAIN) return launch_c3<bf16, IN_PLAIN, NT, 2>(p, s);
   }
   return hipErrorNotSupported;
+}
+
+int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target) {
+  if (Cout % 128 != 0 || target <= 0) return 1;
+  const long tiles = (long)F * ((T + 63) / 64) * (Cout / 128);   // 1-row 64-frame tiles of one utterance
+  const int nchunk = Cin_pad / (conv_ckb(1, 9, Cin_pad) / 2);    // bf16 chunks (ConvCfg::CK of these tiles)
+  long ks = target / tiles;
+  ks = std::min<long>(ks, std::min(4, nchunk / 2));              // at least two chunks per split
+  return ks > 1 ? (int)ks : 1;
 }
 
 int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small, int a8) {   // CONV3: TF rows x 64 frames x NT

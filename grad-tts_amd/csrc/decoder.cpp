@@ -146,6 +146,10 @@ constexpr int64_t kSmallBMax = 16;
 // box): 64 tiles + one merge workgroup per head 43.9 ms per decode, + 8 merge workgroups 42.9, 128 tiles 42.3, 256 42.0
 constexpr int kSmallTiles = 256;
 constexpr int kMergeDrSmall = 4;
+// small-batch plan split-K target: workgroups per utterance the 128-wide 3x3 convs aim for (conv_small_ksplit; 0 off).
+// Measured in round 4 (T = 512, N = 50, one box, ms per decode, off / 256): B = 1 42.4 / 37.8, B = 2 45.7 / 42.6, B = 4
+// 57.2 / 59.4; targets 384 and 512 38.4 at B = 1 (level-1 tiles split too: two workgroup rounds)
+constexpr int kSkTarget = 256;
 
 }  // namespace
 
@@ -195,6 +199,7 @@ struct gt_decoder {
   // (GT_MERGE_DR_SMALL: 4 spreads a head's merge over 8 workgroups; 32 is the throughput plan's single workgroup)
   int small_tiles = kSmallTiles;
   int merge_dr_small = kMergeDrSmall;
+  int sk_target = kSkTarget;   // GT_SK_TARGET (0: no split-K)
   // training path: every parameter in fp32, reference layout, contiguous in inventory order (the layout of the
   // flat gradient buffer too), plus the SinusoidalPosEmb frequencies at the end
   bool raw_dirty = true;
@@ -558,6 +563,7 @@ int prepare(gt_decoder* d, int code) {
 struct Layout {
   size_t act[3][5];        // per level: 4-5 activation buffers
   size_t stats, part, G, Mw, tb, spk, betas, step, total;
+  size_t skcnt, skpart; long skcnt_n, skpart_n;   // small plan split-K: counters, fp32 partials (0: not allocated)
   int pmax;
   int tile_pos[3], ntile[3];
 };
@@ -596,7 +602,7 @@ int max_gn_parts(int dt, int64_t T) {
   return m;
 }
 
-Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles) {
+Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles, int small) {
   Layout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = (o + bytes + 255) & ~size_t(255); return r; };
@@ -622,6 +628,12 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles) {
   L.spk = take((size_t)B * 80 * 4);
   L.betas = take((size_t)std::max<int32_t>(N, 1) * 4);
   L.step = take(4);
+  if (small && dt) {   // 128-wide 3x3 tiles of levels 1-2 (at most 2 x 128 output channels), up to 4 splits of 8192 floats
+    L.skcnt_n = (long)B * 40 * (((T >> 1) + 63) / 64) * 2;
+    L.skpart_n = L.skcnt_n * 4 * 8192;
+    L.skcnt = take((size_t)L.skcnt_n * 4);
+    L.skpart = take((size_t)L.skpart_n * 4);
+  }
   L.total = o;
   return L;
 }
@@ -708,6 +720,12 @@ struct Run {
     }
     const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
     if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
+    if (small && dt && !p.wscale && p.Cout % 128 == 0 && im != IN_INPUT && L.skcnt_n) {   // split-K (conv.hip ConvCfg::SK)
+      p.ksplit = conv_small_ksplit(p.Fout, p.Tout, p.Cout, p.Cin_pad, d->sk_target);
+      const long tiles = (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128);
+      if (p.ksplit > 1 && (tiles > L.skcnt_n || tiles * p.ksplit * 8192 > L.skpart_n)) { chk(hipErrorInvalidValue); return np; }
+      p.sk_part = (float*)(ws + L.skpart); p.sk_cnt = (int*)(ws + L.skcnt);
+    }
     conv(CONV3, im, OUT_STATS, p);
     return np;
   }
@@ -1082,6 +1100,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
+  if (const char* e = getenv("GT_SK_TARGET")) d->sk_target = std::max(0, atoi(e));
   *out = d;
   return GT_OK;
 }
@@ -1166,7 +1185,7 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int
   (void)d;
   if (B <= 0 || T <= 0) return 0;
   const int dt = dtype ? 1 : 0;
-  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps, d->small_tiles).total + 256;
+  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps, d->small_tiles, small_plan(d, dtype, B)).total + 256;
 }
 
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
@@ -1186,7 +1205,9 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = (hipStream_t)stream;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, 0, d->small_tiles);
+    R.L = layout(R.dt, nb, T, 0, d->small_tiles, R.small);
+    // split-K counters start at zero (every launch leaves them zeroed); a kernel node, not a memset, in captures
+    if (R.L.skcnt_n) R.chk(launch_fill_f32((float*)(R.ws + R.L.skcnt), R.L.skcnt_n, 0.f, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = x + fo; R.spk_s = nullptr;
     R.probe = probe; R.probe_out = probe_out;
     float* tbuf = (float*)(R.ws + R.L.tb);
@@ -1446,7 +1467,8 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = st;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, n_timesteps, d->small_tiles);
+    R.L = layout(R.dt, nb, T, n_timesteps, d->small_tiles, R.small);
+    if (R.L.skcnt_n) R.chk(launch_fill_f32((float*)(R.ws + R.L.skcnt), R.L.skcnt_n, 0.f, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = out + fo; R.spk_s = nullptr;
     float* xt = out + fo;
     R.chk(launch_mask_copy(z + fo, R.mask, (int)nb, 80, (int)T, xt, R.s));   // xt = z * mask  (diffusion.py:257)

@@ -42,7 +42,14 @@ struct ConvParams {
   void* out; float* out_part;                         // OUT_STATS: GroupNorm partials of the output (common.h)
   const void* pre; const float* pre_part; int pre_nparts; const float* pre_gamma; const float* pre_beta; long pre_count;  // OUT_RBOUT
   int small;                     // small-batch tile plan (wimage.h conv_tf; conv64 one-tile segments)
+  // split-K of the small plan's 128-wide bf16 3x3 tiles (conv.hip ConvCfg::SK; ignored elsewhere): ksplit <= 1 off;
+  // sk_part: fp32 partials [spatial tile][Cout/128][ksplit][8192]; sk_cnt: one zeroed counter per (spatial tile,
+  // Cout/128), left zeroed by every launch (the last workgroup of a tile re-arms it)
+  int ksplit; float* sk_part; int* sk_cnt;
 };
+// split count of the small plan's 128-wide 3x3 convs: a function of the utterance's grid and the input chunks only
+// (never of the batch, so a small-plan decode stays batch-invariant); 1 = no split
+int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target);
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid

@@ -9,7 +9,8 @@ segments, so that a single utterance fills the GPU. Checked here:
   * the throughput plan (forced on small batches with gt_decoder_set_small_batch(dec, 0)) still meets the
     reference-pinned bf16 gates on the golden fixtures (the default run of test_decoder_gpu.py now takes the
     small plan at those batch sizes);
-  * small-plan latency at B = 1, T = 512 is printed next to the throughput plan's (no timing gate).
+  * small-plan latency at B = 1, T = 512 is printed next to the throughput plan's (no timing gate);
+  * split-K of the small plan's 128-wide 3x3 convs is deterministic and agrees with the unsplit tiles.
 """
 import time
 
@@ -170,3 +171,20 @@ def test_latency_b1_report(mode):
     print(f"LATENCY {mode} B=1 T=512: small plan {ms_s:.3f} ms per step, throughput plan {ms_t:.3f} ms per step "
           f"({512 / (1000 * ms_s) * 1e3:.0f} vs {512 / (1000 * ms_t) * 1e3:.0f} mel-frames/s for 1000-step decodes)")
     assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
+
+
+def test_split_k_deterministic_and_agrees(monkeypatch):
+    """Split-K of the small plan's 128-wide 3x3 convs (conv.hip ConvCfg::SK: the last of a tile's workgroups adds the
+    fp32 partials in split order and re-arms the tile's counter): repeated decodes are bit-identical whichever workgroup
+    finishes last, a second decoder on the same workspace sizes sees zeroed counters, and the result agrees with the
+    unsplit tiles (GT_SK_TARGET=0) within the bf16 sampler gate. B = 1, T = 512: level-2 tiles split 3-4 ways."""
+    mu, z, mask, _ = _inputs(41, 1, 512, lengths=[480])
+    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    ya = dec(z, mask, mu, 4)
+    yb = dec(z, mask, mu, 4)
+    assert torch.isfinite(ya).all()
+    assert torch.equal(ya, yb), float((ya - yb).abs().max())
+    monkeypatch.setenv("GT_SK_TARGET", "0")
+    dec0, _ = make_decoder(1, 0, torch.bfloat16)
+    y0 = dec0(z, mask, mu, 4)
+    report("small plan split-K vs unsplit bf16 B=1 T=512 N=4", rel_err(ya.cpu().numpy(), y0.cpu().numpy()), BF16_REV_TOL)
