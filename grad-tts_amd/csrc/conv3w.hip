@@ -55,7 +55,7 @@ struct Cfg {
   static constexpr int TR = WM * RB;               // tile rows
   static constexpr int PR = TR + 2;                // patch rows
   static constexpr int PP = PR * PCOL;             // patch positions
-  static constexpr int PPAD = PP + ((2 - PP % 16) + 16) % 16;   // plane stride in 16-B entries, == 2 mod 16
+  static constexpr int PPAD = (PP + 15) & ~15;     // plane stride in 16-B entries, == 0 mod 16 (see the fragments)
   static constexpr int PLANE = PPAD * 16;
   static constexpr int PBUF = 4 * PLANE;           // one 32-channel patch buffer
   static constexpr int SLOT = BN * 64;             // one weight slot: BN channels x 32 input channels
@@ -66,7 +66,8 @@ struct Cfg {
   static constexpr int D = S - 1;                  // DMA issue distance in phases
   static constexpr int ITEMS = PP * 4;             // 16-B patch items per chunk
   static constexpr int NPT = (ITEMS + NTHR - 1) / NTHR;
-  static constexpr int NS = 2 * RB;                // MFMA steps per phase (k-step x row block)
+  static constexpr int NCB = 2 * CB;               // 16-channel blocks per wave
+  static constexpr int NS = 2 * RB;                // MFMA steps per phase (16-position blocks: row block x half)
   // phases between an item's load and its transform (item j: loaded at phase j, transformed at phase j + XD <= 7)
   static constexpr int XD = (8 - NPT) < 2 ? (8 - NPT) : 2;
   // phase of item j's transform (TP) and of its load (LP): XD phases apart, consecutive items in consecutive phases;
@@ -118,6 +119,16 @@ GT_DEV void asm_dma16(const void* gsrc, unsigned lds_addr) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
 }
+// v_mfma_f32_16x16x32_bf16 accumulating in place. hipcc does not tie the builtin's destination to its C operand (a third
+// of the builtin MFMAs of this loop wrote a fresh register set, the accumulators rotated through the register file and
+// the kernel spilled); the asm form keeps every accumulator in its registers. hipcc pads no hazards inside asm: the
+// accumulators are written by these MFMAs only, their A / B operands come from LDS reads (waited for by the compiler:
+// register inputs of the statement) and are overwritten no earlier than one MFMA group later, and the epilogue
+// (mfma_drain) waits out the last MFMAs before any other instruction reads an accumulator.
+GT_DEV void mfma16(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
+GT_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
 // raw buffer load hidden from hipcc's waitcnt bookkeeping (the s_nop covers an SGPR operand written just before)
 GT_DEV void asm_buffer_load(u32x4c_t& dst, int voff, __amdgpu_buffer_rsrc_t rs, int soff) {
   asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff) : "memory");
@@ -153,10 +164,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 #if GT_C3W_STAMP
   const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
 #endif
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  // v_mfma_f32_16x16x32_bf16 lanes: r = row of A (output channel) / column of B (position) in a 16 x 16 block, g = the
+  // 8-channel plane (k group) of both operands
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wv % C::WN, wm = wv / C::WN;
-  const int q16 = tid & 3;                       // this thread's 8-channel plane inside a chunk (fixed)
+  // patch items: a wave's 64 consecutive items are 16 consecutive positions x 4 planes, lanes 16q .. 16q + 15 on plane q
+  // (8 contiguous lanes store 128 contiguous bytes of one plane: conflict-free at any plane stride)
+  const int q16 = g;                             // this thread's 8-channel plane inside a chunk (fixed)
+  auto item_pos = [&](int j) { return (((tid + NTHR * j) >> 6) << 4) | r; };
 
   // ---- prologue loads: GroupNorm slots (IN_GN), per-channel coefficients, bias, masks
   GnLoad gl;
@@ -176,7 +192,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   bool frac = false;
 #pragma unroll
   for (int j = 0; j < C::NPT; ++j) {
-    const int pp = (tid + NTHR * j) >> 2;
+    const int pp = item_pos(j);
     const int pr = pp / PCOL, pc = pp - pr * PCOL;
     const int fi = f0 - 1 + pr, ti = t0 - 1 + pc;
     const bool ok = pp < C::PP && fi >= 0 && fi < F && ti >= 0 && ti < T;
@@ -229,8 +245,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // gn_mish_tb_l2), 4 channels at a time with their coefficients read from LDS right before (fewer registers live
   // across the MFMA stream than one coefficient set per chunk)
   auto put_item = [&](int j, int c, int buf) {
-    const int pp = (tid + NTHR * j) >> 2;
-    if (C::NPT * NTHR != C::ITEMS && pp >= C::PP) return;
+    const int pp = item_pos(j);
+    if (pp >= C::PP) return;
     u32x4c_t v4 = preg[j];
     if (IN == IN_GN) {
       float v[8];
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
   // DMA of their phase).
   constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
-  constexpr int NPRE = c3w::PF + CB;   // LDS reads of the next phase's first PF steps (top_wait)
+  constexpr int NPRE = c3w::PF + C::NCB;   // LDS reads of the next phase: its first PF steps' B and its A (top_wait)
   unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
   auto top_wait = [&](auto Tc, auto MOREc) {
@@ -321,25 +337,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (STAMP) st[2] += stamp() - a;
   };
 
-  // ---- fragments. A (weights): slot + plane (2s + h) x BN + channel; B (patch): buffer + plane (2s + h) + position.
-  const int a_lane = C::OFF_W + (h * BN + wn * 32 * CB + r) * 16;
-  const int b_lane = h * C::PLANE + (wm * RB * PCOL + r) * 16;
-  auto rd_a = [&](int slot, int s, int cb) {
-    return *reinterpret_cast<const bf16x8*>(smem + a_lane + slot * C::SLOT + (2 * s * BN + cb * 32) * 16);
+  // ---- fragments (v_mfma_f32_16x16x32_bf16: one 32-channel phase = one k of 32). A (weights): slot + plane g x BN +
+  // channel; B (patch): buffer + plane g + position. Each is 16 consecutive 16-B entries per plane: with plane strides
+  // == 0 mod 16 entries the four lane groups of a ds_read_b128 cover the 64 banks once.
+  const int a_lane = C::OFF_W + (g * BN + wn * 32 * CB + r) * 16;
+  const int b_lane = g * C::PLANE + (wm * RB * PCOL + r) * 16;
+  auto rd_a = [&](int slot, int cb) {
+    return *reinterpret_cast<const bf16x8*>(smem + a_lane + slot * C::SLOT + cb * 16 * 16);
   };
-  auto rd_b = [&](int buf, int t, int s, int rb) {
+  auto rd_b = [&](int buf, int t, int pb) {   // 16-position block pb = row block pb / 2, frames 16 (pb % 2) ..
     const int dr = t / 3, dc = t % 3;
-    return *reinterpret_cast<const bf16x8*>(smem + b_lane + buf * C::PBUF + 2 * s * C::PLANE +
-                                            ((rb + dr) * PCOL + dc) * 16);
+    return *reinterpret_cast<const bf16x8*>(smem + b_lane + buf * C::PBUF + ((pb / 2 + dr) * PCOL + (pb % 2) * 16 + dc) * 16);
   };
 
-  f32x16 acc[RB][CB];
+  f32x4 acc[C::NS][C::NCB];   // [16-position block][16-channel block]
 #pragma unroll
-  for (int i = 0; i < RB; ++i)
+  for (int i = 0; i < C::NS; ++i)
 #pragma unroll
-    for (int j = 0; j < CB; ++j)
+    for (int j = 0; j < C::NCB; ++j) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
+      for (int k = 0; k < 4; ++k) acc[i][j][k] = 0.f;
+      asm volatile("" : "+v"(acc[i][j]));   // the zeros are written here, ahead of the wait states below
+    }
+  asm volatile("s_nop 4" ::: "memory");   // VALU write -> MFMA C-operand read (mfma16 pads nothing)
 
   // ---- prologue: chunk 0 patch loads, then the first D weight slots, then the GroupNorm reduction
   load_patch(0);
@@ -349,9 +369,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   if (IN == IN_GN) {
     gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red);
     if (tid < p.Cin) {
-      const int g = tid / (p.Cin >> 3);
-      const float sc = c_g * s_rstd[g];
-      s_sc[tid] = sc * kLog2e; s_sh[tid] = (c_b - s_mean[g] * sc) * kLog2e; s_tb[tid] = c_t;
+      const int gi = tid / (p.Cin >> 3);
+      const float sc = c_g * s_rstd[gi];
+      s_sc[tid] = sc * kLog2e; s_sh[tid] = (c_b - s_mean[gi] * sc) * kLog2e; s_tb[tid] = c_t;
     }
   }
   if (tid < BN) { s_bias[tid] = c_bias; s_wsc[tid] = c_wsc; }
@@ -362,16 +382,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   vm_wait<(C::D - 2) * PW>();
   lds_barrier();
 
-  // MFMA steps i = s * RB + rb of a phase; fragments are read two steps ahead (B: ring of 3 by the chunk-global step
-  // index, a chunk being 90 steps; A: one register set per k-step s), across phase boundaries too: phase k+1's slot and
-  // patch are visible from the top of phase k.
-  constexpr int PF = c3w::PF, NB = PF + 1;   // fragment prefetch distance in steps; B ring of NB registers
-  static_assert(9 * C::NS % NB == 0 && PF <= RB, "B ring index chunk-periodic; A frags double-buffered by k-step");
-  bf16x8 fa[2][CB], fb[NB];
+  // MFMA steps i (16-position block i) of a phase, NCB MFMAs each; B fragments are read PF steps ahead (a ring of PF + 1
+  // by the chunk-global step index, a chunk being 90 steps), across phase boundaries too: phase k+1's slot and patch are
+  // visible from the top of phase k. The NCB A fragments of a phase are read after the previous phase's last MFMAs
+  // (into the same registers), so they land during the phase barrier.
+  constexpr int PF = c3w::PF, NB = PF + 1;
+  static_assert(9 * C::NS % NB == 0 && PF <= C::NS, "B ring index chunk-periodic");
+  bf16x8 fa[C::NCB], fb[NB];
 #pragma unroll
-  for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(0, 0, cb);
+  for (int cb = 0; cb < C::NCB; ++cb) fa[cb] = rd_a(0, cb);
 #pragma unroll
-  for (int n = 0; n < PF; ++n) fb[n] = rd_b(0, 0, 0, n);
+  for (int n = 0; n < PF; ++n) fb[n] = rd_b(0, 0, n);
 
   int slot = 0;   // weight slot of the current phase (k mod S)
   // MFMA steps of the item transforms: waves 0-3 at XS0, waves 4-7 at XS1
@@ -432,35 +453,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
       // (d) MFMAs of phase k
 #pragma unroll
       for (int i = 0; i < C::NS; ++i) {
-        const int s = i / RB, rb = i % RB;
-        const int g = t * C::NS + i;          // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
-        const int n = i + PF;                 // step whose fragments are read now
+        const int gi = t * C::NS + i;         // chunk-global step (90 per chunk: the B ring index is chunk-periodic)
+        const int n = i + PF;                 // step whose B fragment is read now
         int nrd = 0;
         if (n < C::NS) {
-          const int s1 = n / RB, rb1 = n % RB;
-          if (rb1 == 0) {
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb) fa[s1 & 1][cb] = rd_a(slot, s1, cb);
-            nrd += CB;
-          }
-          fb[(g + PF) % NB] = rd_b(cur, t, s1, rb1);
-          nrd += 1;
+          fb[(gi + PF) % NB] = rd_b(cur, t, n);
+          nrd = 1;
         } else if (MORE || t < 8) {           // phase k+1's steps 0 .. PF-1
-          const int rb1 = n - C::NS;
-          if (rb1 == 0) {
-#pragma unroll
-            for (int cb = 0; cb < CB; ++cb) fa[0][cb] = rd_a(nslot, 0, cb);
-            nrd += CB;
-          }
-          fb[(g + PF) % NB] = t < 8 ? rd_b(cur, t + 1, 0, rb1) : rd_b(nxt, 0, 0, rb1);
-          nrd += 1;
+          fb[(gi + PF) % NB] = t < 8 ? rd_b(cur, t + 1, n - C::NS) : rd_b(nxt, 0, n - C::NS);
+          nrd = 1;
         }
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb)
-          acc[rb][cb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][cb], fb[g % NB], acc[rb][cb], 0, 0, 0);
-        if (nrd == CB + 1) __builtin_amdgcn_sched_group_barrier(0x100, CB + 1, 0);
-        else if (nrd == 1) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, CB, 0);
+        for (int cb = 0; cb < C::NCB; ++cb) mfma16(acc[i][cb], fa[cb], fb[gi % NB]);
+        if (i == C::NS - 1 && (MORE || t < 8)) {   // phase k+1's A fragments, after this phase's last use
+#pragma unroll
+          for (int cb = 0; cb < C::NCB; ++cb) fa[cb] = rd_a(nslot, cb);
+        }
         // (e) one patch item of chunk c+1 per phase, phases 2 .. 1 + NPT, behind this phase's MFMAs
         // Staggered between the two waves of a SIMD (waves w and w + 4 share one; MI355X_MICROARCH.md, two waves per
         // SIMD, item 9): waves 0-3 at step XS0, waves 4-7 at step XS1, so one wave's transform VALU runs beside its
@@ -487,68 +495,66 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   if (STAMP) { st[4] = t_loop_end - t_loop; st[6] = t_loop - t_entry; }
 #endif
 
-  // ---- epilogue: bias, GroupNorm partial sums, 16-B stores (lane (r, h) of block (rb, cb) holds channels
-  // cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r; v_permlane32_swap leaves it 8 consecutive channels)
-  float gs[CB][2], gq[CB][2];
+  // ---- epilogue: bias, GroupNorm partial sums, 16-B stores. Lane (r, g) of 16 x 16 block (i, cb) holds channels
+  // cb*16 + 4g + 0..3 of position r of block i; one v_permlane16_swap per register of the block pair (2rb, 2rb+1) (the
+  // two 16-frame halves of row block rb) leaves lane (r, g) with channels cb*16 + 8 (g >> 1) + 0..7 of position
+  // 16 (g & 1) + r: one 16-B item and one GroupNorm 8-channel subgroup per lane and pair.
+  mfma_drain();
 #pragma unroll
-  for (int cb = 0; cb < CB; ++cb) { gs[cb][0] = gs[cb][1] = gq[cb][0] = gq[cb][1] = 0.f; }
+  for (int i = 0; i < C::NS; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NCB; ++j) asm volatile("" : "+v"(acc[i][j]));   // every read of acc stays after the drain
+  float gs[C::NCB], gq[C::NCB];
+#pragma unroll
+  for (int cb = 0; cb < C::NCB; ++cb) { gs[cb] = gq[cb] = 0.f; }
   bf16* out = reinterpret_cast<bf16*>(p.out);
-  const int tcol = t0 + r;
+  const int tcol = t0 + (g & 1) * 16 + r;
   const bool valid = tcol < T;
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int frow = f0 + wm * RB + rb;
     const long ob = (((long)b * F + frow) * T + tcol) * BN;
 #pragma unroll
-    for (int cb = 0; cb < CB; ++cb) {
-      float v[16];
+    for (int cb = 0; cb < C::NCB; ++cb) {
+      float v[8];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = acc[rb][cb][q];
+      for (int q = 0; q < 4; ++q) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[2 * rb][cb][q]),
+                                                         __float_as_uint(acc[2 * rb + 1][cb][q]), false, false);
+        v[q] = __uint_as_float(sw[0]);
+        v[4 + q] = __uint_as_float(sw[1]);
+      }
+      const int cl = wn * 32 * CB + cb * 16 + 8 * (g >> 1);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
+      float o[8];
+      if (w8) {   // wave-uniform
+        const f32x4 s0 = *reinterpret_cast<const f32x4*>(s_wsc + cl);
+        const f32x4 s1 = *reinterpret_cast<const f32x4*>(s_wsc + cl + 4);
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
+        for (int k = 0; k < 4; ++k) { o[k] = v[k] * s0[k] + b0[k]; o[4 + k] = v[4 + k] * s1[k] + b1[k]; }
+      } else {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]),
-                                                           __float_as_uint(v[8 * pr + 4 + q]), false, false);
-          v[8 * pr + q] = __uint_as_float(sw[0]);
-          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        for (int k = 0; k < 4; ++k) { o[k] = v[k] + b0[k]; o[4 + k] = v[4 + k] + b1[k]; }
+      }
+      if (valid) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          gs[cb] += o[k]; gq[cb] += o[k] * o[k];
+          asm volatile("" : "+v"(gs[cb]), "+v"(gq[cb]));   // scalar chains (conv.hip, packed-FP32 hazard)
         }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const int cl = wn * 32 * CB + cb * 32 + pr * 16 + 8 * h;
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
-        float o[8];
-        if (w8) {   // wave-uniform
-          const f32x4 s0 = *reinterpret_cast<const f32x4*>(s_wsc + cl);
-          const f32x4 s1 = *reinterpret_cast<const f32x4*>(s_wsc + cl + 4);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] * s0[k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] * s1[k] + b1[k]; }
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) { o[k] = v[8 * pr + k] + b0[k]; o[4 + k] = v[8 * pr + 4 + k] + b1[k]; }
-        }
-        if (valid) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            gs[cb][pr] += o[k]; gq[cb][pr] += o[k] * o[k];
-            asm volatile("" : "+v"(gs[cb][pr]), "+v"(gq[cb][pr]));   // scalar chains (conv.hip, packed-FP32 hazard)
-          }
-          *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(o, bf16());
-        }
+        *reinterpret_cast<uint4*>(out + ob + cl) = f_to_item(o, bf16());
       }
     }
   }
 #pragma unroll
-  for (int cb = 0; cb < CB; ++cb)
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const float s = half_sum32(gs[cb][pr]), q = half_sum32(gq[cb][pr]);
-      if (r == 0) {
-        s_sub[((wv * CB + cb) * 4 + pr * 2 + h) * 2 + 0] = s;
-        s_sub[((wv * CB + cb) * 4 + pr * 2 + h) * 2 + 1] = q;
-      }
+  for (int cb = 0; cb < C::NCB; ++cb) {   // over the 32 lanes of each lane half (the subgroup 8 (g >> 1) of block cb)
+    const float sm = half_sum32(gs[cb]), sq = half_sum32(gq[cb]);
+    if ((lane & 31) == 0) {
+      s_sub[((wv * C::NCB + cb) * 2 + (g >> 1)) * 2 + 0] = sm;
+      s_sub[((wv * C::NCB + cb) * 2 + (g >> 1)) * 2 + 1] = sq;
     }
+  }
   lds_barrier();
   if (tid < 8) {   // per GroupNorm group, over waves and 8-channel sub-groups in a fixed order: one slot per tile
     const int gshift = __builtin_ctz(BN >> 3);

@@ -931,7 +931,9 @@ struct Run {
     }
     const double npos = (double)B * a.n;
     // reference FLOPs of the attention block: qkv 1x1 (2*C*384) + two einsums (2 * 2*4*32*32) + to_out (2*128*C)
-    timed(std::string("attn_kv_kernel<") + (dt ? "bf16" : "float") + (rb ? ",rb>" : ">") + "@" + std::to_string(C) +
+    // label = the template instantiation (launch_attn_kv: all C channels resident in LDS for C <= 64, else chunked)
+    timed(std::string("attn_kv_kernel<") + (dt ? "bf16" : "float") + (C <= 64 ? ",res" : ",chunk") + (rb ? ",rb>" : ">") +
+              "@" + std::to_string(C) +
               "x" + std::to_string(Fl(lvl)), npos * (2.0 * C * 256 + 2.0 * 4 * 32 * 32),
           npos * C * esize(dt) * (rb ? 3.0 : 1.0), [&] { return launch_attn_kv(dt, a, s); });
     if (rb) tap(pend.name, lvl, in, C);
