@@ -38,12 +38,18 @@ def _deps_mtime():
     return max(os.path.getmtime(os.path.join(CSRC, f)) for f in os.listdir(CSRC) if f.endswith((".h", ".hip", ".cpp")))
 
 
+# per-source extra flags: conv64's pass loop (36 steps with the staging of 8 items, IN_RB0's ResnetBlock-output transform
+# the largest) must unroll fully -- past LLVM's default pragma-unroll size threshold the IN_RB0 loop stayed rolled and
+# indexed its register rings dynamically (thousands of v_cndmask)
+SRC_FLAGS = {"conv64.hip": ["-mllvm", "-pragma-unroll-threshold=1000000"]}
+
+
 def _compile(src, force):
     obj = os.path.join(OBJ, src + ".o")
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(_deps_mtime(), os.path.getmtime(os.path.join(REPO, "include", "gradtts.h"))):
         return obj, None
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
-    cmd = [HIPCC, *FLAGS, *lang, "-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC, *FLAGS, *SRC_FLAGS.get(src, []), *lang, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     return obj, (None if r.returncode == 0 else f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 

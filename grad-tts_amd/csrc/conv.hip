@@ -57,7 +57,7 @@ struct ConvCfg {
   static constexpr bool A8 = W8 == 2;
   static constexpr int CKB = A8 ? 32 : conv_ckb(sizeof(A) == 2, KIND == CONV1 ? 1 : 9, IN == IN_INPUT ? 3 : 64);
   static constexpr int SUBS = A8 ? 4 : CKB / 16;   // LDS items per position (A8: 8 e4m3 channels = 8 B per item)
-  static constexpr int POSB = CKB + 16;
+  static constexpr int POSB = CKB + 16;   // an odd number of 16-B slots per position: conflict-free fragment reads
   // weight slab: bf16/fp32 image (wimage.h: half A = taps [0, NA), half B = the rest) or the fp8 image
   // (conv8_wrow, W8: e4m3 weights, bf16 operands; conv_wimga8, A8)
   static constexpr int ABF = sizeof(A) == 2 ? 1 : 0;
@@ -93,7 +93,23 @@ struct ConvCfg {
   static constexpr int ICH = 16 / (int)sizeof(A);            // channels per item (one 16-B global load)
   static constexpr int KSTEP_B = 16 * (int)sizeof(A);
   static constexpr int KSTEPS = CKB / KSTEP_B;
-  static constexpr int PITEMS = PR * PC * SUBS;
+  // Patch items (16 B: sub-group `sub` of SUBS of a position). A ds_write_b128 serves lanes in groups of 8 with banks
+  // (a/4) mod 32 (8 slots of 16 B), while the conflict-free fragment reads need a position stride of an odd number of
+  // slots (P = POSB / 16): in position-major order (lanes 4i..4i+3 = one position, as A8 keeps for its DPP scale
+  // exchange) a group's two positions p, p + 1 share a bank. IMAP permutes the positions only, keeping each quad of
+  // lanes on one position (SUBS = 4: its 64 contiguous bytes, what the load coalesces) or two (SUBS = 2), so that a
+  // group's slots cover all 8 banks: SUBS = 4 (P = 5) pairs positions p and p + 4 in a group, SUBS = 2 (P = 3) takes
+  // positions {0, 2, 4, 6} or {1, 3, 5, 7} of a block of 8. Stride 2: positions in LDS (deinterleaved) order.
+  static constexpr bool IMAP = !A8 && (SUBS == 4 || SUBS == 2);
+  static constexpr int NPOS = PR * PC;
+  static constexpr int PITEMS = IMAP ? 8 * SUBS * ((NPOS + 7) / 8) : NPOS * SUBS;
+  static __host__ __device__ constexpr int ipos(int it) {
+    return !IMAP ? it / SUBS
+                 : 8 * (it / (8 * SUBS)) + (SUBS == 4 ? (((it >> 2) & 7) >> 1) + 4 * ((it >> 2) & 1)
+                                                      : 2 * ((it & 7) >> 1) + ((it >> 3) & 1));
+  }
+  static __host__ __device__ constexpr int isub(int it) { return it % SUBS; }
+  static __host__ __device__ constexpr int gcol(int lc) { return DEINT ? (lc < ODDC ? 2 * lc : 2 * (lc - ODDC) + 1) : lc; }
   static constexpr int PPT = (PITEMS + 255) / 256;
   static constexpr int A_BYTES = PR * PC * POSB;
   static constexpr int WBUF = DBW ? 2 * WBYTES : WBYTES;   // weight slab(s) in LDS
@@ -106,7 +122,7 @@ struct ConvCfg {
   static constexpr int SMEM = (CAP && SMEM0 <= 160 * 1024 / (CAP + 1)) ? 160 * 1024 / (CAP + 1) + 512 : SMEM0;
   static_assert(KSTEPS >= 1, "chunk smaller than one MFMA k-step");
   static_assert(TF * RBT % WM == 0, "row blocks split evenly over the waves");
-  static_assert(256 % SUBS == 0, "per-thread channel group must be fixed");
+  static_assert(256 % (IMAP ? 8 * SUBS : SUBS) == 0, "per-thread channel group must be fixed");
   static_assert(WBYTES % 1024 == 0, "whole DMA pieces");
   static_assert(!DBW || WPIECES_ALL % 4 == 0, "counted waits: every wave issues WPIECES weight pieces");
   static_assert(!SPLIT || (HA % 4096 == 0 && (WBYTES - HA) % 4096 == 0 && PB + PPT <= 63), "wave-even halves");
@@ -176,7 +192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar) wave index
   const int wm = wv % C::WM, wn = wv / C::WM;
   const int fi0 = f0 * C::S - C::PAD, ti0 = t0 * C::S - C::PAD;
-  const int sub = tid % C::SUBS;          // this thread's fixed 16-B channel group inside a chunk
+  const int sub = C::isub(tid);           // this thread's fixed 16-B channel group inside a chunk
 
   // ---- prologue, ordered so that its global round trips overlap: GroupNorm slot loads, the per-channel
   // coefficients and the mask are issued together; the first patch prefetch goes out before the fp64
@@ -202,10 +218,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
 #pragma unroll
   for (int j = 0; j < C::PPT; ++j) {
     const int it = tid + 256 * j;
-    const int pos = it / C::SUBS;
-    const int pr = pos / C::PC, pc = pos - pr * C::PC;
+    const int pos = C::ipos(it);   // LDS position
+    const int pr = pos / C::PC, pc = C::gcol(pos - pr * C::PC);
     const int fi = fi0 + pr, ti = ti0 + pc;
-    const bool ok = it < C::PITEMS && fi >= 0 && fi < p.Fin && ti >= 0 && ti < p.Tin;
+    const bool ok = pos < C::NPOS && fi >= 0 && fi < p.Fin && ti >= 0 && ti < p.Tin;
     const float m = ok ? mask_at(p.mask, p.T0, b, ti, p.lvl_in) : 0.f;
     int q = ok ? ((b * p.Fin + fi) * p.Tin + ti) : npos;
     if (IN == IN_MASK) {
@@ -316,9 +332,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
 #pragma unroll
     for (int j = 0; j < C::PPT; ++j) {
       const int it = tid + 256 * j;
-      if (it < C::PITEMS) {
-        const int ipos = it / C::SUBS, ipr = ipos / C::PC;
-        char* dst = sA + (ipr * C::PC + C::pcol(ipos - ipr * C::PC)) * C::POSB + sub * 16;
+      if (C::ipos(it) < C::NPOS) {
+        char* dst = sA + C::ipos(it) * C::POSB + sub * 16;
         const u32x4 u = preg[j];
         if (IN == IN_PLAIN || (IN == IN_MASK && !frac)) {   // zeros already came from the range check
           *reinterpret_cast<u32x4*>(dst) = u;

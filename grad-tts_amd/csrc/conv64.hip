@@ -53,16 +53,22 @@ constexpr int PPT = (NEW_ITEMS + NTHR - 1) / NTHR;        // 5 (the 5th only for
 constexpr int COLD_ITEMS = 6 * PC * 8;                    // first tile of a segment: all 6 rows
 constexpr int CPT = (COLD_ITEMS + NTHR - 1) / NTHR;       // 7
 constexpr int NCH = 4;                                    // 16-channel chunks
-constexpr int WLDS_MAX = 2;                               // taps whose weights live in LDS (the rest in registers)
+constexpr int WLDS_MAX = 3;                               // taps whose weights live in LDS (the rest in registers)
 constexpr int WTAP_B = 2 * NCH * 64 * 16;                 // one tap's fragments of both channel halves: 8 KB
-constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + NW * 8 + 16) * 4 + 272 * 8;
-// taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room
-constexpr int wreg_of(int in) { return in == IN_GN ? 7 : 8; }
+constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + 64 + NW * 8 + 16) * 4 + 272 * 8;
+// taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room; 6 for
+// IN_RB0 (the ResnetBlock-output transform plus each in-flight item's input channels)
+constexpr int wreg_of(int in) { return in == IN_RB0 ? 6 : in == IN_GN ? 7 : 8; }
+static_assert(9 - wreg_of(IN_RB0) <= WLDS_MAX && 9 - wreg_of(IN_GN) <= WLDS_MAX, "LDS weight taps");
 static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 }  // namespace c64
 
-// IN: IN_MASK / IN_GN / IN_PLAIN. Masks from sequence_mask are 0/1: x * m is then a select, decided per item on
-// the device (a fractional mask value takes a multiply in a branch that 0/1 masks never enter).
+// IN: IN_MASK / IN_GN / IN_PLAIN / IN_RB0. Masks from sequence_mask are 0/1: x * m is then a select, decided per item
+// on the device (a fractional mask value takes a multiply in a branch that 0/1 masks never enter).
+// IN_RB0 (downs.0.1's block1, diffusion.py:70-79, 192): the operand x * m with x = the first ResnetBlock's output
+// r0 = Mish(GN(h2)) * m + res_conv(in * m) (in = {mu, x_t, spk}, 2-3 channels) formed per staged item from h2, in the
+// same fp32 operations as gn_mish_kernel<RES = 1> (misc.hip, the pass it replaces), so r0 -- which this kernel also
+// writes once per position for the residual of downs.0.1 (attn_kv) -- is bit-identical to that pass's output.
 // One workgroup = one segment: L consecutive 4 x 32 tiles down the mel axis of one utterance's 32-frame column.
 // Two workgroups share a CU (one wave of each per SIMD) and drift out of phase, so one's staging/epilogue VALU
 // work overlaps the other's MFMAs.
@@ -83,7 +89,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
   float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB + WLDS_MAX * WTAP_B);   // [scale, shift, tb, unused][64]
   float* const s_wsc = s_coef + 2 * 4 * 64;                  // W8: per-output-channel weight scales
-  float* const s_sub = s_wsc + 64;                          // [wave][(pr, h) group][sum, sq]
+  float* const s_bias = s_wsc + 64;                         // the conv bias in accumulator layout, per (cb, h)
+  float* const s_sub = s_bias + 64;                         // [wave][(pr, h) group][sum, sq]
   float* const s_mean = s_sub + NW * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
@@ -121,11 +128,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   }
   const char* const wlp = sWL + (cb * NCH * 64 + lane) * 16;
-  f32x16 bias_acc;   // the conv bias in accumulator layout: register q of lane (r, h) is channel cb*32 + acc_row(q, h)
+  // the conv bias in accumulator layout: register q of lane (r, h) is channel cb*32 + acc_row(q, h). Held in registers
+  // across the loop, except for IN_RB0, which needs them for its operand transform: there it is re-read from LDS
+  // (s_bias[(cb * 2 + h) * 16 + q]) at the start of every pass
+  f32x16 bias_reg;
+  if (IN == IN_RB0) {
+    if (tid < 64) {
+      const int c = (tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1);
+      s_bias[tid] = p.bias[c];
+    }
+  } else {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int c = cb * 32 + acc_row(q, h);
-    bias_acc[q] = W8 ? p.bias[c] / p.wscale[c] : p.bias[c];
+    for (int q = 0; q < 16; ++q) {
+      const int c = cb * 32 + acc_row(q, h);
+      bias_reg[q] = W8 ? p.bias[c] / p.wscale[c] : p.bias[c];
+    }
   }
   if (W8 && tid < 64) s_wsc[tid] = p.wscale[tid];   // read by the epilogues, after the first tile's barrier
 
@@ -136,7 +153,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int t0 = tt * TT;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.in0, (short)0, npos * 128, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, npos * 128, 0x00020000);
-  auto load_item = [&](int it, int frow, u32x4_t& v, float& m) {
+  // IN_RB0: the U-Net input channels of an item's position (fp32 [B][F][T]; spk per mel row), 0 when out of range
+  // (raw buffer loads at 32-bit offsets: out-of-range positions read past the end, zeros)
+  const __amdgpu_buffer_rsrc_t rs_mu =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(IN == IN_RB0 ? p.mu : nullptr), (short)0, npos * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_xt =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(IN == IN_RB0 ? p.xt : nullptr), (short)0, npos * 4, 0x00020000);
+  auto load_in = [&](int frow, int ti, float* xi) {
+    const bool ok = frow >= 0 && frow < F && ti >= 0 && ti < T;
+    const int q = ok ? ((b * F + frow) * T + ti) * 4 : npos * 4;
+    xi[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_mu, q, 0, 0));   // (the builtin returns the bits)
+    xi[1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_xt, q, 0, 0));
+    xi[2] = 0.f;   // (spk: per mel row, read from LDS by the transform: s_coef + 384)
+  };
+  // IN_RB0: r0 is stored by the segment that owns the position (interior columns 1..32, rows of its tiles)
+  const __amdgpu_buffer_rsrc_t rs_rb =
+      __builtin_amdgcn_make_buffer_rsrc(IN == IN_RB0 ? p.rb_out : p.out, (short)0, npos * 128, 0x00020000);
+  auto rb_dst = [&](int frow, int c) {   // byte offset of the item's r0, or past the end (dropped)
+    const int ti = t0 - 1 + c;
+    const bool own = c >= 1 && c <= TT && ti < T && frow >= ft0 * TF && frow < (ft0 + L) * TF && frow < F;
+    return own ? ((b * F + frow) * T + ti) * 128 + sub * 16 : npos * 128;
+  };
+  auto load_item = [&](int it, int frow, u32x4_t& v, float& m, float* xi) {
     const int c = (it >> 3) % PC;
     const int ti = t0 - 1 + c;
     const bool ok = frow >= 0 && frow < F && ti >= 0 && ti < T;
@@ -146,8 +184,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const float mv = mask_at(p.mask, p.T0, b, ti < 0 ? 0 : (ti < T ? ti : T - 1), p.lvl_in);
       m = ok ? mv : 0.f;
     }
+    if (IN == IN_RB0) load_in(frow, ti, xi);
   };
-  auto put_item_at = [&](int lds_off, u32x4_t v4, float m) {
+  const bool spk3 = IN == IN_RB0 && p.cin_input == 3;   // IN_RB0: n_spks > 1 (a third U-Net input channel)
+  auto put_item_at = [&](int lds_off, u32x4_t v4, float m, float xi0, float xi1, int frow, int rbo)
+      __attribute__((always_inline)) {
     if (IN == IN_MASK) {
       if (__builtin_expect(m != 0.f && m != 1.f, 0)) {   // x * m, fractional mask value
         float v[8];
@@ -173,14 +214,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       }
       const uint4 o = f_to_item(v, bf16());
       v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
+    } else if (IN == IN_RB0) {   // r0 = Mish(GN(h2)) * m + res_conv(in * m), as gn_mish_kernel<RES = 1>
+      float v[8];
+      item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
+      const float x0 = xi0 * m, x1 = xi1 * m;
+#pragma unroll
+      for (int hq = 0; hq < 2; ++hq) {
+        const float* cf = s_coef + sub * 8 + hq * 4;
+        float r[4];
+        {
+          const f32x4 w0 = *reinterpret_cast<const f32x4*>(cf + 128);
+          const f32x4 w1 = *reinterpret_cast<const f32x4*>(cf + 192);
+          const f32x4 rbv = *reinterpret_cast<const f32x4*>(cf + 320);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) r[k] = fmaf(w1[k], x1, fmaf(w0[k], x0, rbv[k]));
+        }
+        if (spk3) {   // (wave-uniform) the third input channel: spk of this mel row, outermost as in the pass
+          const float x2 = ((frow >= 0 && frow < F) ? s_coef[384 + frow] : 0.f) * m;
+          const f32x4 w2 = *reinterpret_cast<const f32x4*>(cf + 256);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) r[k] = fmaf(w2[k], x2, r[k]);
+        }
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
+        const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_act<bf16>(v[4 * hq + k] * sc[k] + sh[k]) * m + r[k];
+      }
+      const uint4 o = f_to_item(v, bf16());
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, rs_rb, rbo, 0, 0);   // r0 (unmasked)
+      v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};                 // r0 * m
     }
     *reinterpret_cast<u32x4_t*>(sR + lds_off) = v4;
   };
-  auto put_item = [&](int it, int slot, u32x4_t v4, float m) {
-    put_item_at(slot * ROWB + ((it >> 3) % PC) * POSB + sub * 16, v4, m);
+  auto put_item = [&](int it, int slot, u32x4_t v4, float m, const float* xi, int frow) __attribute__((always_inline)) {
+    const int c = (it >> 3) % PC;
+    put_item_at(slot * ROWB + c * POSB + sub * 16, v4, m, xi[0], xi[1], frow, IN == IN_RB0 ? rb_dst(frow, c) : 0);
   };
 
   // GroupNorm scale/shift (and time bias) of the input channels of utterance b (IN_GN): once per segment
+  if (IN == IN_RB0) {   // GroupNorm affine of h2 (gn_affine, as gn_mish_kernel) and the res_conv weights, bias
+    static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
+    const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b, tid);
+    gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red, tid);
+    if (tid < 64) {
+      float sc, sh;
+      gn_affine(s_mean, s_rstd, 64, tid, p.gn_gamma, p.gn_beta, sc, sh);
+      s_coef[tid] = sc; s_coef[64 + tid] = sh;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) s_coef[128 + 64 * j + tid] = j < p.cin_input ? p.rb_w[tid * p.cin_input + j] : 0.f;
+      s_coef[320 + tid] = p.rb_b[tid];
+    }
+    for (int f = tid; f < F; f += NTHR) s_coef[384 + f] = p.cin_input == 3 ? p.spk_s[(long)b * F + f] : 0.f;
+    lds_barrier();
+  }
   if (IN == IN_GN) {
     const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
     static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
@@ -197,16 +283,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // ---- prologue: tile 0's 6 patch rows (mel rows 4 ft0 - 1 .. 4 ft0 + 4) into ring slots 0..5
   {
     u32x4_t cv[CPT];
-    float cm[CPT];
+    float cm[CPT], cx[IN == IN_RB0 ? CPT : 1][3];
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
       const int it = tid + NTHR * j;
-      load_item(it < COLD_ITEMS ? it : 0, ft0 * TF - 1 + (it < COLD_ITEMS ? it / (PC * 8) : 0), cv[j], cm[j]);
+      load_item(it < COLD_ITEMS ? it : 0, ft0 * TF - 1 + (it < COLD_ITEMS ? it / (PC * 8) : 0), cv[j], cm[j],
+                cx[IN == IN_RB0 ? j : 0]);
     }
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
       const int it = tid + NTHR * j;
-      if (CPT * NTHR == COLD_ITEMS || it < COLD_ITEMS) put_item(it, it / (PC * 8), cv[j], cm[j]);
+      if (CPT * NTHR == COLD_ITEMS || it < COLD_ITEMS)
+        put_item(it, it / (PC * 8), cv[j], cm[j], cx[IN == IN_RB0 ? j : 0], ft0 * TF - 1 + it / (PC * 8));
     }
   }
   // The next tiles' new rows (tile k: mel rows 4 (ft0+k) + 1 .. + 4). A thread's item j of every tile has the same
@@ -215,7 +303,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // compiler's vmcnt waits count only loads and stores. A masked (IN_MASK) or out-of-range item reads past the end
   // of the tensor (zeros from the range check, no traffic).
   const int oob = npos * 128;
-  int nrow[PPT], ncol[PPT], ngo[PPT];
+  int nrow[PPT], ncol[IN == IN_RB0 ? 1 : PPT], ngo[PPT], nti[IN == IN_RB0 ? PPT : 1];
   float nm[PPT];
 #pragma unroll
   for (int j = 0; j < PPT; ++j) {
@@ -226,21 +314,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     const float mv = mask_at(p.mask, p.T0, b, ti < 0 ? 0 : (ti < T ? ti : T - 1), p.lvl_in);
     nm[j] = (IN != IN_PLAIN && ok) ? mv : (IN == IN_PLAIN && ok ? 1.f : 0.f);
     nrow[j] = it / (PC * 8);
-    ncol[j] = c * POSB + sub * 16;
+    if (IN == IN_RB0) nti[j] = c;   // (IN_RB0: the column, for the r0 store; its LDS offset formed per use)
+    else ncol[j] = c * POSB + sub * 16;
     ngo[j] = (ok && !(IN == IN_MASK && nm[j] == 0.f)) ? ti * 128 + sub * 16 : -1;
   }
   u32x4_t preg[PPT];
-  auto issue_new = [&](int j, int k) {   // item j of tile k's new rows (rows past the mel axis read zeros)
+  float pin[IN == IN_RB0 ? PPT : 1][3];   // IN_RB0: mu, x_t of each in-flight item's position ([2] unused)
+  auto issue_new = [&](int j, int k) __attribute__((always_inline)) {   // item j of tile k's new rows (past the mel axis: zeros)
     const int frow = (ft0 + k) * TF + 1 + nrow[j];
     const int off = (ngo[j] >= 0 && frow < F) ? (b * F + frow) * T * 128 + ngo[j] : oob;
     preg[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    if (IN == IN_RB0) load_in(frow, t0 - 1 + nti[j], pin[j]);   // (nti: IN_RB0 only)
   };
-  auto put_new = [&](int j, int k) {     // store item j of tile k's new rows into ring slots 4k + 2 + i
+  auto put_new = [&](int j, int k) __attribute__((always_inline)) {   // item j of tile k's new rows -> ring slots 4k + 2 + i
     if (PPT * NTHR == NEW_ITEMS || tid + NTHR * j < NEW_ITEMS) {
       int slot = (4 * k + 2) % RING + nrow[j];
       slot = slot >= RING ? slot - RING : slot;
-      const bool inrow = (ft0 + k) * TF + 1 + nrow[j] < F;   // the zero padding row below the mel axis (IN_GN: no transform)
-      put_item_at(slot * ROWB + ncol[j], preg[j], inrow ? nm[j] : 0.f);
+      const int frow = (ft0 + k) * TF + 1 + nrow[j];
+      const bool inrow = frow < F;   // the zero padding row below the mel axis (IN_GN: no transform)
+      const float* xi = pin[IN == IN_RB0 ? j : 0];
+      const int col_off = IN == IN_RB0 ? nti[j] * POSB + sub * 16 : ncol[j];
+      put_item_at(slot * ROWB + col_off, preg[j], inrow ? nm[j] : 0.f, xi[0], xi[1], frow,
+                  IN == IN_RB0 ? rb_dst(frow, nti[j]) : 0);
     }
   };
 #pragma unroll
@@ -277,13 +372,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
                           : *reinterpret_cast<const bf16x8*>(wlp + (tap - WREG) * WTAP_B + ch * 1024);
       };
       constexpr int PF = 2, NB = PF + 1, NST = NCH * 9;   // (3, 4, 6 steps ahead: unchanged or spilling)
+      // the first MFMA of the pass accumulates onto the conv bias (the C operand: no epilogue adds)
+      const f32x16 bias_acc = IN == IN_RB0 ? *reinterpret_cast<const f32x16*>(s_bias + (cb * 2 + h) * 16) : bias_reg;
       bf16x8 xb[NB], wb[NB];
 #pragma unroll
       for (int st = 0; st < PF; ++st) { xb[st] = xread(st); wb[st] = wread(st); }
 #pragma unroll
       for (int st = 0; st < NST; ++st) {
         if (st + PF < NST) { xb[(st + PF) % NB] = xread(st + PF); wb[(st + PF) % NB] = wread(st + PF); }
-        // the first MFMA of the pass accumulates onto the conv bias (C operand = the bias registers, no epilogue adds)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[st % NB], xb[st % NB], st == 0 ? bias_acc : acc, 0, 0, 0);
         if (st + PF < NST) {   // pin: the reads of step st + PF ahead of step st's MFMA
           if ((st + PF) % 9 < WREG) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
@@ -380,7 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     unsigned long long v = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
-    if (lane < 8) gt_c64_stamps[((seg_raw & 511) * 4 + wv) * 8 + lane] = v;
+    if (lane < 8) gt_c64_stamps[((seg & 511) * 4 + wv) * 8 + lane] = v;
   }
 #endif
 }
@@ -427,6 +523,13 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
     else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, true>), dim3(grid), block, 0, s, p, L);
     else return hipErrorNotSupported;
   } else {
+    if (im == IN_RB0) {
+      if (!p.rb_out || !p.rb_w || !p.rb_b || !p.mu || !p.xt || p.cin_input < 2 || p.cin_input > 3 ||
+          (p.cin_input == 3 && !p.spk_s))
+        return hipErrorInvalidValue;
+      hipLaunchKernelGGL((conv64_kernel<IN_RB0, false>), dim3(grid), block, 0, s, p, L);
+      return hipGetLastError();
+    }
     if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, false>), dim3(grid), block, 0, s, p, L);
     else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, false>), dim3(grid), block, 0, s, p, L);
     else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, false>), dim3(grid), block, 0, s, p, L);

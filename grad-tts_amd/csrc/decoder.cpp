@@ -193,6 +193,9 @@ struct gt_decoder {
   bool wide = true;
   // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
   bool attn_ds = true;
+  // the first ResnetBlock's output formed by the next block's conv (conv64 IN_RB0) instead of its own pass
+  // (rbout_input); GT_RB0_FUSE=0 at creation: the pass
+  bool rb0_fuse = true;
   // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
   bool attn_us = true;
   // small-batch plan attention: tiles per utterance (GT_ATTN_TILES_SMALL) and the merge's rows per workgroup
@@ -693,6 +696,25 @@ struct Run {
   // utterance it wrote. bf16-operand 64 -> 64 convs (bf16 or fp8 weights; GT_FP8 too) take conv64 (weight-resident),
   // everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
+    if (pend0.on) {   // the first ResnetBlock's output is pending: formed here if this conv reads it, else by its pass
+      if (im == IN_MASK && p.in0 == pend0.out && !p.in1 && dt && wi == GT_BF16 && conv64_eligible(p) &&
+          d->dp[wi].count(wkey + ".w64")) {
+        p.w = W(wkey + ".w64");
+        p.in0 = pend0.pre;
+        p.gn_part = pend0.part; p.gn_nparts = pend0.nparts; p.gn_gamma = pend0.gamma; p.gn_beta = pend0.beta;
+        p.gn_count = pend0.count;
+        p.cin_input = pend0.cin; p.rb_w = pend0.rw; p.rb_b = pend0.rb; p.rb_out = pend0.out;
+        const double pos = (double)p.B * p.Fout * p.Tout;
+        const int np = conv64_nparts(p.Fout, p.Tout, p.small);
+        if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
+        pend0.on = false;
+        timed("conv64_kernel<4>@64x64x" + std::to_string(p.Fout), 2.0 * 64 * 64 * 9 * pos + 2.0 * pend0.cin * 64 * pos,
+              pos * (3 * 128.0 + 8.0) + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(IN_RB0, p, s); });
+        tap(pend0.name, pend0.lvl, pend0.out, 64);   // r0 is in place from here on
+        return np;
+      }
+      flush_rb0();
+    }
     if (dt && conv64_enabled() && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
         d->dp[wi].count(wkey + ".w64")) {
       p.w = W(wkey + ".w64");   // (fp8 weights: their e4m3 values; p.wscale stays the per-channel scale)
@@ -781,6 +803,29 @@ struct Run {
     const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
     const void* x; void* out;
   } pend;
+  // The first ResnetBlock's output r0 = Mish(GN(h2))*m + res_conv(x*m) held back for downs.0.1's block1 conv, which
+  // forms it in its operand load and writes it (conv64 IN_RB0, conv3_stats); any other next step runs its pass first
+  // (flush_rb0: rbout_input_kernel).
+  struct PendingRb0 {
+    bool on = false;
+    std::string name;
+    const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
+    void* out; const float* rw; const float* rb; int cin, lvl, C;
+  } pend0;
+  void flush_rb0() {
+    if (!pend0.on) return;
+    pend0.on = false;
+    const int lvl = pend0.lvl;
+    RbOutParams p{};
+    p.pre = pend0.pre; p.part = pend0.part; p.nparts = pend0.nparts; p.gamma = pend0.gamma; p.beta = pend0.beta;
+    p.count = pend0.count; p.out = pend0.out; p.mask = mask; p.B = B; p.F = Fl(lvl); p.T = Tl(lvl); p.C = pend0.C;
+    p.T0 = T; p.lvl = lvl; p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin = pend0.cin; p.rw = pend0.rw; p.rb = pend0.rb;
+    const double by = (2.0 * pend0.C * esize(dt) + 8.0) * B * Fl(lvl) * Tl(lvl);
+    timed(std::string("rbout_input_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(pend0.C) + "x" +
+              std::to_string(Fl(lvl)), 2.0 * pend0.cin * pend0.C * B * Fl(lvl) * Tl(lvl), by,
+          [&] { return launch_rbout_input(dt, p, s); });
+    tap(pend0.name, lvl, pend0.out, pend0.C);
+  }
 
   void resnet(const std::string& k, int lvl, const void* in0, int C0, const void* in1, int C1, int Cout, void* out,
               int tb_off, bool defer = false) {
@@ -823,18 +868,16 @@ struct Run {
       tap_part(stat_slot - 1);
     }
     if (d->index.count(k + "res_conv.weight") && input) {
-      // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m) as an elementwise pass (a 1x1 conv_kernel
-      // over 2-3 channels measured slower: 100.4 vs 86.3 us, round 3)
-      RbOutParams p{};
-      p.pre = pre2; p.part = st2; p.nparts = np2; p.gamma = Fp(k + "block2.block.1.weight");
-      p.beta = Fp(k + "block2.block.1.bias"); p.count = count; p.out = out; p.mask = mask; p.B = B; p.F = Fl(lvl);
-      p.T = Tl(lvl); p.C = Cout; p.T0 = T; p.lvl = lvl;
-      p.mu = mu; p.xt = xt; p.spk_s = spk_s; p.cin = cin; p.rw = Fp(k + "res_conv.weight.f32");
-      p.rb = Fp(k + "res_conv.bias");
-      const double by = (2.0 * Cout * esize(dt) + 8.0) * B * Fl(lvl) * Tl(lvl);
-      timed(std::string("rbout_input_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(Cout) + "x" +
-                std::to_string(Fl(lvl)), 2.0 * cin * Cout * B * Fl(lvl) * Tl(lvl), by,
-            [&] { return launch_rbout_input(dt, p, s); });
+      // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m), formed by the next block's conv
+      // (conv64 IN_RB0) on the bf16 path, else as an elementwise pass (flush_rb0; a 1x1 conv_kernel over 2-3 channels
+      // measured slower: 100.4 vs 86.3 us, round 3)
+      pend0.on = true; pend0.name = k.substr(0, k.size() - 1);
+      pend0.pre = pre2; pend0.part = st2; pend0.nparts = np2; pend0.gamma = Fp(k + "block2.block.1.weight");
+      pend0.beta = Fp(k + "block2.block.1.bias"); pend0.count = count; pend0.out = out;
+      pend0.rw = Fp(k + "res_conv.weight.f32"); pend0.rb = Fp(k + "res_conv.bias"); pend0.cin = cin; pend0.lvl = lvl;
+      pend0.C = Cout;
+      if (!(dt && wi == GT_BF16 && d->rb0_fuse && conv64_enabled() && Cout == 64)) flush_rb0();
+      return;
     } else if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);
       p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "res_conv.weight");
@@ -908,6 +951,7 @@ struct Run {
   }
 
   void attention_fold(const std::string& k, int lvl, const void* in, int C) {
+    flush_rb0();   // (defensive: only downs.0.1's block1 conv ever consumes the pending first-block output)
     float* part = (float*)(ws + L.part);
     float* G = (float*)(ws + L.G);
     void* Mw = ws + L.Mw;
@@ -1100,6 +1144,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
+  if (const char* e = getenv("GT_RB0_FUSE")) d->rb0_fuse = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
   if (const char* e = getenv("GT_SK_TARGET")) d->sk_target = std::max(0, atoi(e));

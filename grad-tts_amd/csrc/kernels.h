@@ -8,7 +8,8 @@
 
 namespace gt {
 
-enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3 };
+// IN_RB0 (conv64 only): the input is the first ResnetBlock's output formed in the operand load (ConvParams::rb_*)
+enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3, IN_RB0 = 4 };
 enum OutMode { OUT_STATS = 0, OUT_PLAIN = 1, OUT_RBOUT = 2, OUT_RESID = 3 };
 enum ConvKind { CONV3 = 0, CONV3_S2 = 1, CONV1 = 2, CONVT4 = 3 };
 
@@ -30,7 +31,11 @@ struct ConvParams {
   // ---- input
   const void* in0; const void* in1; int C0, C1;      // channels-last sources, concatenated on C
   const float* mu; const float* xt; const float* spk_s; int cin_input;   // IN_INPUT (level 0)
-  const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN
+  const float* gn_part; int gn_nparts; const float* gn_gamma; const float* gn_beta; long gn_count;  // IN_GN, IN_RB0
+  // IN_RB0 (conv64): in0 is the first ResnetBlock's block2 pre-activation h2 and gn_* its GroupNorm; the operand is
+  // its output r0 = Mish(GN(h2))*m + res_conv(x*m) over the U-Net input channels (mu, xt, spk_s; cin_input of them)
+  // with rb_w [64][cin] fp32 and rb_b [64]; r0 itself is also written to rb_out ([B][F][T][64] bf16, each position once)
+  const float* rb_w; const float* rb_b; void* rb_out;
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
   const int* stepp;                                   // IN_GN: device step index (tb_at), or null
   // ---- weights
