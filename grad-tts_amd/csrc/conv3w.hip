@@ -9,9 +9,11 @@
 //   * 8 waves (512 threads), ONE workgroup per CU. The workgroup owns ALL output channels of its spatial tile (BN = Cout:
 //     256, 128 or 64), so every input element of the tile is loaded and (IN_GN) GroupNorm + Mish + time-bias transformed
 //     exactly once per tile; halo rows add (TR + 2) / TR (1.2x at 10 rows, 1.1x at 20).
-//   * Tile = TR mel rows x 32 frames. Wave (wn, wm) computes CB x 32 output channels x RB = 5 rows (CB x 5 accumulators
-//     of 32 x 32, v_mfma_f32_32x32x16_bf16, weights as A, positions as B -> channel x position, as conv_kernel).
-//   * K loop = phases: one phase = one tap x 32 input channels (two MFMA k-steps). A weight slot (BN rows x 32 channels,
+//   * Tile = TR mel rows x 32 frames. Wave (wn, wm) computes CB x 32 output channels x RB = 5 rows: 2 RB x 2 CB blocks of
+//     16 positions x 16 channels on v_mfma_f32_16x16x32_bf16 (weights as A, positions as B), accumulated in place by
+//     inline asm (mfma16). The 16x16x32 shape holds a higher clock than 32x32x16 under this load (profiles/r05/
+//     mfma_shape_bench.txt).
+//   * K loop = phases: one phase = one tap x 32 input channels (one 16x16x32 k-step). A weight slot (BN rows x 32 channels,
 //     BN x 64 B) is staged by LDS DMA (global_load_lds, 1 KiB per wave instruction) into a ring of S slots, D = S - 1
 //     phases ahead; the counted `s_waitcnt vmcnt` at the top of phase k retires DMA(k+1), so each slot is visible one
 //     phase before it is read and the first fragments of phase k+1 are read during phase k (no MFMA bubble at the
@@ -26,7 +28,7 @@
 //     The weight image in HBM is pre-packed in exactly the slot layout (decoder.cpp pack_conv3w): a slot is one straight
 //     DMA.
 // Epilogue: bias, GroupNorm partial sums of the output (one slot per tile, fixed-order reduction), 16-B bf16 stores, from
-// the accumulators through v_permlane32_swap (as conv_kernel).
+// the accumulators through v_permlane16_swap.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
@@ -113,11 +115,12 @@ template <int N>
 GT_DEV void vm_wait_dep(u32x4c_t& x) { asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x) : "n"(N) : "memory"); }
 // LDS DMA (1 KiB per wave instruction) hidden from hipcc's waitcnt bookkeeping: hipcc models its builtin twin as an LDS
 // access too and then waits lgkmcnt(0) in front of the fragment reads that follow it. M0 is written and restored in the
-// same statement (guide §5.7).
-GT_DEV void asm_dma16(const void* gsrc, unsigned lds_addr) {
+// same statement (guide §5.7). Scalar base + one per-lane 32-bit offset register (the saddr form) for every DMA of the
+// kernel, where a 64-bit per-lane address per slot used to be held: 2-4 fewer VGPRs, no spill in the 256-wide GN form.
+GT_DEV void asm_dma16(const void* sbase, unsigned voff, unsigned lds_addr) {
   unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(gsrc), "s"(lds_addr) : "memory");
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
 }
 // v_mfma_f32_16x16x32_bf16 accumulating in place. hipcc does not tie the builtin's destination to its C operand (a third
 // of the builtin MFMAs of this loop wrote a fresh register set, the accumulators rotated through the register file and
@@ -288,12 +291,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const char* const wimg = reinterpret_cast<const char*>(p.w);
   const unsigned lds_base = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(smem));
+  const unsigned dma_voff = lane * 16;
   auto dma = [&](int k, int slot) {
-    const char* src = wimg + (long)k * C::SLOT + lane * 16;
+    const char* src = wimg + (long)k * C::SLOT;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int piece = C::PIECES >= c3w::NW ? wv + c3w::NW * i : wv % C::PIECES;
-      asm_dma16(src + piece * 1024, lds_base + C::OFF_W + slot * C::SLOT + piece * 1024);
+      asm_dma16(src + piece * 1024, dma_voff, lds_base + C::OFF_W + slot * C::SLOT + piece * 1024);
     }
   };
   // items of the next chunk loaded at phases in [lo, hi] (item j at phase LP(j))
