@@ -206,8 +206,13 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void
     for (int pr = 0; pr < 2; ++pr) {
       const int c0 = cb * 32 + pr * 16 + 8 * h;
       float o[8];
+      if (p.wsc) {   // fp8 weights (their e4m3 values in the image): conv_kernel W8's epilogue, acc * scale + bias
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] + p.bds[c0 + k];
+        for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] * p.wsc[c0 + k] + p.bds[c0 + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] + p.bds[c0 + k];
+      }
       *reinterpret_cast<uint4*>(out + c0) = f_to_item(o, bf16());
     }
   }
@@ -388,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           const int c0 = cb * 32 + pr * 16 + 8 * h;
           float o[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] + p.bup[c0 + k];
+          for (int k = 0; k < 8; ++k) o[k] = p.wsc ? v[8 * pr + k] * p.wsc[c0 + k] + p.bup[c0 + k] : v[8 * pr + k] + p.bup[c0 + k];
           *reinterpret_cast<uint4*>(out + c0) = f_to_item(o, bf16());
         }
       }

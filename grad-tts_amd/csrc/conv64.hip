@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   if (IN == IN_RB0) {
     if (tid < 64) {
       const int c = (tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1);
-      s_bias[tid] = p.bias[c];
+      s_bias[tid] = W8 ? p.bias[c] / p.wscale[c] : p.bias[c];
     }
   } else {
 #pragma unroll
@@ -517,16 +517,19 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   const long nseg = (long)p.B * ((p.Tout + 31) / 32) * (p.Fout / 4 / L);
   const unsigned grid = (unsigned)nseg;
   const dim3 block(256);
+  const bool rb_ok = p.rb_out && p.rb_w && p.rb_b && p.mu && p.xt && p.cin_input >= 2 && p.cin_input <= 3 &&
+                     (p.cin_input == 2 || p.spk_s);
   if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)
-    if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), block, 0, s, p, L);
+    if (im == IN_RB0) {
+      if (!rb_ok) return hipErrorInvalidValue;
+      hipLaunchKernelGGL((conv64_kernel<IN_RB0, true>), dim3(grid), block, 0, s, p, L);
+    } else if (im == IN_MASK) hipLaunchKernelGGL((conv64_kernel<IN_MASK, true>), dim3(grid), block, 0, s, p, L);
     else if (im == IN_GN) hipLaunchKernelGGL((conv64_kernel<IN_GN, true>), dim3(grid), block, 0, s, p, L);
     else if (im == IN_PLAIN) hipLaunchKernelGGL((conv64_kernel<IN_PLAIN, true>), dim3(grid), block, 0, s, p, L);
     else return hipErrorNotSupported;
   } else {
     if (im == IN_RB0) {
-      if (!p.rb_out || !p.rb_w || !p.rb_b || !p.mu || !p.xt || p.cin_input < 2 || p.cin_input > 3 ||
-          (p.cin_input == 3 && !p.spk_s))
-        return hipErrorInvalidValue;
+      if (!rb_ok) return hipErrorInvalidValue;
       hipLaunchKernelGGL((conv64_kernel<IN_RB0, false>), dim3(grid), block, 0, s, p, L);
       return hipGetLastError();
     }

@@ -458,6 +458,20 @@ std::vector<float> e4m3_values(const std::vector<float>& w, int rows) {
   return v;
 }
 
+// the same for a ConvTranspose2d [Cin][Cout][4][4] weight, quantized per output channel (dim 1) as pack_conv8's
+// transposed path does; returned in the weight's own layout
+std::vector<float> e4m3_values_t(const std::vector<float>& w, int cin, int cout) {
+  std::vector<float> rows((size_t)cout * cin * 16), v(w.size());
+  for (int co = 0; co < cout; ++co)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int k = 0; k < 16; ++k) rows[((size_t)co * cin + ci) * 16 + k] = w[((size_t)ci * cout + co) * 16 + k];
+  const std::vector<float> q = e4m3_values(rows, cout);
+  for (int co = 0; co < cout; ++co)
+    for (int ci = 0; ci < cin; ++ci)
+      for (int k = 0; k < 16; ++k) v[((size_t)ci * cout + co) * 16 + k] = q[((size_t)co * cin + ci) * 16 + k];
+  return v;
+}
+
 // a 3x3 [Cout][Cin][3][3] weight conv3w covers (Cin % 32 == 0, Cout 64 / 128 / 256; not the 64 -> 64 convs of conv64)
 static bool conv3w_shape(const std::vector<int64_t>& shp) {
   return shp.size() == 4 && shp[2] == 3 && shp[3] == 3 && shp[1] % 32 == 0 && (shp[0] == 64 || shp[0] == 128 || shp[0] == 256) &&
@@ -499,8 +513,11 @@ int prepare(gt_decoder* d, int code) {
       pack_conv8(blob, d, code, k, w, shp, false);
       if (code == GT_BF16_W8 && ends_with(k, ".block.0.weight") && conv3w_shape(shp))   // conv3w: the e4m3 values
         pack_conv3w(blob, k + ".w3w", e4m3_values(w, (int)shp[0]), (int)shp[0], (int)shp[1]);
+      if (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight") && shp[0] == 64 && shp[1] == 64)
+        pack_frag3x3(blob, k + ".wfr", e4m3_values(w, 64), 64, 64);   // attn_down_kernel: the e4m3 values
     } else if (w8 && starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv8(blob, d, code, k, w, shp, true);
+      if (shp[0] == 64 && shp[1] == 64) pack_fragT(blob, k + ".wfr", e4m3_values_t(w, 64, 64), 64, 64);   // attn_up_kernel
     } else if (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")) ||
         ends_with(k, "res_conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, false);
@@ -697,9 +714,9 @@ struct Run {
   // everything else conv_kernel.
   int conv3_stats(InMode im, ConvParams p, const std::string& wkey) {
     if (pend0.on) {   // the first ResnetBlock's output is pending: formed here if this conv reads it, else by its pass
-      if (im == IN_MASK && p.in0 == pend0.out && !p.in1 && dt && wi == GT_BF16 && conv64_eligible(p) &&
-          d->dp[wi].count(wkey + ".w64")) {
-        p.w = W(wkey + ".w64");
+      if (im == IN_MASK && p.in0 == pend0.out && !p.in1 && dt && conv64_eligible(p) && d->dp[wi].count(wkey + ".w64")) {
+        p.w = W(wkey + ".w64");   // (fp8 weights: their e4m3 values, p.wscale the per-channel scale; bf16 operands)
+        p.a8 = 0;
         p.in0 = pend0.pre;
         p.gn_part = pend0.part; p.gn_nparts = pend0.nparts; p.gn_gamma = pend0.gamma; p.gn_beta = pend0.beta;
         p.gn_count = pend0.count;
@@ -708,7 +725,7 @@ struct Run {
         const int np = conv64_nparts(p.Fout, p.Tout, p.small);
         if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
         pend0.on = false;
-        timed("conv64_kernel<4>@64x64x" + std::to_string(p.Fout), 2.0 * 64 * 64 * 9 * pos + 2.0 * pend0.cin * 64 * pos,
+        timed(std::string("conv64_kernel<4") + (p.wscale ? ",w8" : "") + ">@64x64x" + std::to_string(p.Fout), 2.0 * 64 * 64 * 9 * pos + 2.0 * pend0.cin * 64 * pos,
               pos * (3 * 128.0 + 8.0) + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(IN_RB0, p, s); });
         tap(pend0.name, pend0.lvl, pend0.out, 64);   // r0 is in place from here on
         return np;
@@ -876,7 +893,7 @@ struct Run {
       pend0.beta = Fp(k + "block2.block.1.bias"); pend0.count = count; pend0.out = out;
       pend0.rw = Fp(k + "res_conv.weight.f32"); pend0.rb = Fp(k + "res_conv.bias"); pend0.cin = cin; pend0.lvl = lvl;
       pend0.C = Cout;
-      if (!(dt && wi == GT_BF16 && d->rb0_fuse && conv64_enabled() && Cout == 64)) flush_rb0();
+      if (!(dt && d->rb0_fuse && conv64_enabled() && Cout == 64)) flush_rb0();
       return;
     } else if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);
@@ -916,16 +933,17 @@ struct Run {
   // never materialised). false (nothing launched) when not applicable: another dtype, the fused form disabled
   // (GT_ATTN_DS=0), or a probe of the attention output itself.
   bool attention_down(const std::string& ka, const std::string& kd, int lvl, const void* in, int C, void* out) {
-    if (!(dt && wi == GT_BF16 && d->attn_ds && lvl == 0 && d->dp[wi].count(kd + "conv.weight.wfr"))) return false;
+    if (!(dt && d->attn_ds && lvl == 0 && d->dp[wi].count(kd + "conv.weight.wfr"))) return false;
     if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
     AttnDownParams a{};
     a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
     a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
     a.wds = W(kd + "conv.weight.wfr"); a.bds = Fp(kd + "conv.bias"); a.out = out;
+    a.wsc = d->dp[wi].count(kd + "conv.weight.s") ? Fp(kd + "conv.weight.s") : nullptr;   // fp8 weights
     if (!attn_down_eligible(a)) return false;
     attention_fold(ka, lvl, in, C);
     const double pin = (double)B * a.F * a.T, pout = pin / 4;
-    timed("attn_down_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
+    timed(std::string("attn_down_kernel<bf16") + (a.wsc ? ",w8" : "") + ">@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
           2.0 * C * C * pin + 2.0 * C * C * 9 * pout, (pin + pout) * C * 2.0, [&] { return launch_attn_down(a, s); });
     tap(kd.substr(0, kd.size() - 1), lvl + 1, out, C);
     return true;
@@ -935,16 +953,17 @@ struct Run {
   // ups.1: the attention output and the Upsample after it as one pass (attn_up.hip); false (nothing launched) when not
   // applicable: another dtype, disabled (GT_ATTN_US=0), or a probe of the attention output
   bool attention_up(const std::string& ka, const std::string& ku, int lvl, const void* in, int C, void* out) {
-    if (!(dt && wi == GT_BF16 && d->attn_us && d->dp[wi].count(ku + "conv.weight.wfr"))) return false;
+    if (!(dt && d->attn_us && d->dp[wi].count(ku + "conv.weight.wfr"))) return false;
     if (probe && std::string(probe) == ka.substr(0, ka.size() - 1)) return false;
     AttnUpParams a{};
     a.x = in; a.B = B; a.F = Fl(lvl); a.T = Tl(lvl); a.C = C; a.T0 = T; a.mask = mask; a.lvl = lvl;
     a.mw = ws + L.Mw; a.mw_bstride = conv_wimg(dt, 1, C, C).total; a.gb = Fp(ka + "fn.fn.to_out.bias.g");
     a.wup = W(ku + "conv.weight.wfr"); a.bup = Fp(ku + "conv.bias"); a.out = out;
+    a.wsc = d->dp[wi].count(ku + "conv.weight.s") ? Fp(ku + "conv.weight.s") : nullptr;   // fp8 weights
     if (!attn_up_eligible(a)) return false;
     attention_fold(ka, lvl, in, C);
     const double pin = (double)B * a.F * a.T, pout = pin * 4;
-    timed("attn_up_kernel<bf16>@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
+    timed(std::string("attn_up_kernel<bf16") + (a.wsc ? ",w8" : "") + ">@" + std::to_string(C) + "x" + std::to_string(Fl(lvl)),
           2.0 * C * C * pin + 2.0 * C * C * 16 * pin, (pin + pout) * C * 2.0, [&] { return launch_attn_up(a, s); });
     tap(ku.substr(0, ku.size() - 1), lvl - 1, out, C);
     return true;

@@ -82,6 +82,7 @@ struct AttnDownParams {
   const float* gb;                  // g * b_out [C]
   const void* wds;                  // downsample weight in fragment order (decoder.cpp pack_frag3x3)
   const float* bds;                 // downsample bias [C]
+  const float* wsc;                 // fp8 weights: per-output-channel scale of the e4m3 values in wds (else null)
   void* out;                        // [B][F/2][T/2][C]
 };
 bool attn_down_eligible(const AttnDownParams& p);
@@ -96,6 +97,7 @@ struct AttnUpParams {
   const float* gb;                  // g * b_out [C]
   const void* wup;                  // upsample weight, four parities in fragment order (decoder.cpp pack_fragT)
   const float* bup;                 // upsample bias [C]
+  const float* wsc;                 // fp8 weights: per-output-channel scale of the e4m3 values in wup (else null)
   void* out;                        // [B][2F][2T][C]
 };
 bool attn_up_eligible(const AttnUpParams& p);

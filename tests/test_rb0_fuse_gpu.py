@@ -7,7 +7,8 @@ position for the residual of downs.0.1. So a decoder built with GT_RB0_FUSE=1 (t
 estimator outputs, samples and stage probes ("downs.0.0" = r0 as written by the conv, "downs.0.1.pre1" = the conv's
 own output, "downs.0.1") to one built with GT_RB0_FUSE=0, on ragged batches (masked frames carry r0 = res_conv bias:
 written, but staged as zeros), T not a multiple of 32 (partial column segments), 247 speakers (3 input channels) and
-on both tile plans (the small plan walks one-tile segments: the halo rows of a segment are not its own to write)."""
+on both tile plans (the small plan walks one-tile segments: the halo rows of a segment are not its own to write), and
+with fp8 weights (bf16_w8, fp8: the 64 -> 64 level-0 convs keep bf16 operands on conv64, accumulating from bias / scale)."""
 import numpy as np
 import pytest
 import torch
@@ -30,16 +31,20 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-@pytest.mark.parametrize("n_spks,B,T,lengths,small", [(1, 3, 132, [132, 100, 44], False), (247, 2, 96, [96, 61], False),
-                                                     (1, 2, 76, [76, 50], True), (247, 1, 132, None, True)])
-def test_rb0_fused_bit_identical(monkeypatch, n_spks, B, T, lengths, small):
+@pytest.mark.parametrize("n_spks,B,T,lengths,small,dtype", [(1, 3, 132, [132, 100, 44], False, torch.bfloat16),
+                                                           (247, 2, 96, [96, 61], False, torch.bfloat16),
+                                                           (1, 2, 76, [76, 50], True, torch.bfloat16),
+                                                           (247, 1, 132, None, True, torch.bfloat16),
+                                                           (1, 3, 132, [132, 100, 44], False, "bf16_w8"),
+                                                           (247, 2, 96, [96, 61], True, "fp8")])
+def test_rb0_fused_bit_identical(monkeypatch, n_spks, B, T, lengths, small, dtype):
     mu, z, mask, spk = synthetic_inputs(37, B, T, lengths=lengths)
     t = np.linspace(0.9, 0.2, B).astype(np.float32)
     args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), _cuda(spk) if n_spks > 1 else None)
     res = {}
     for fuse in (1, 0):
         monkeypatch.setenv("GT_RB0_FUSE", str(fuse))
-        dec, _ = make_decoder(n_spks, 17, torch.bfloat16)
+        dec, _ = make_decoder(n_spks, 17, dtype)
         _lib.check(_lib.lib().gt_decoder_set_small_batch(dec.estimator._native(), 16 if small else 0),
                    "gt_decoder_set_small_batch")
         z_, m_, mu_, t_, s_ = args
@@ -47,7 +52,7 @@ def test_rb0_fused_bit_identical(monkeypatch, n_spks, B, T, lengths, small):
         y = dec(z_, m_, mu_, 3, spk=s_)
         outs = [est.cpu(), y.cpu()]
         for st in ("downs.0.0", "downs.0.1.pre1", "downs.0.1"):
-            _, pr = probe(dec.estimator, torch.bfloat16, z_, m_, mu_, t_, s_, st, (B, 64, 80, T))
+            _, pr = probe(dec.estimator, dtype, z_, m_, mu_, t_, s_, st, (B, 64, 80, T))
             outs.append(pr.cpu())
         torch.cuda.synchronize()
         res[fuse] = outs

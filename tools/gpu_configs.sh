@@ -16,9 +16,11 @@ run() {   # run <name> <limit> <bench args...>
 run c2_bf16 300 --steps 5 --warmup 2
 run c2_fp32 300 --steps 2 --warmup 1 --dtype fp32
 run c3 400 --steps 2 --warmup 1 --batch 64 --n-spks 247 --n-timesteps 100
+run c5_bf16_b32 400 --steps 1 --warmup 1 --n-timesteps 1000
 run c5_w8_b32 400 --steps 1 --warmup 1 --n-timesteps 1000 --dtype bf16_w8
 run c5_fp8_b32 400 --steps 1 --warmup 1 --n-timesteps 1000 --dtype fp8
 run c5_w8_b1 300 --steps 1 --warmup 1 --n-timesteps 1000 --dtype bf16_w8 --batch 1
 run c5_fp8_b1 300 --steps 1 --warmup 1 --n-timesteps 1000 --dtype fp8 --batch 1
+run c5_bf16_b1 300 --steps 1 --warmup 1 --n-timesteps 1000 --batch 1
 run c2_b1 300 --steps 5 --warmup 2 --batch 1
 echo done

@@ -45,7 +45,7 @@ def _demangle(name: str) -> str:
 def norm(name: str) -> str:
     """rocprofv3 kernel name (mangled or demangled) -> the name decoder.cpp / bench.py use for the same kernel
     instantiation ("conv_kernel<bf16,KIND,IN,OUT,NT[,w8][,tf5]>", "conv64_kernel<IN>", "attn_kv_kernel<bf16>",
-    "rbout_identity_kernel<bf16>", "gn_apply_kernel<bf16>", ...). Kernels outside namespace gt (the runtime's
+    "rbout_identity_kernel<bf16>", "rbout_input_kernel<bf16>", ...). Kernels outside namespace gt (the runtime's
     copies / fills, torch's elementwise kernels) keep their base name; a gt:: kernel that does not parse raises."""
     d = _demangle(name)
     m = re.match(r"(?:void )?gt::(\w+)(?:<([^()]*)>)?\(", d)
@@ -62,8 +62,8 @@ def norm(name: str) -> str:
             return f"conv64_kernel<{args[0]}>"
         if base in ("conv3w_kernel", "attn_down_kernel"):   # <IN, COUT, CB> / <C, WY>
             return f"{base}<{','.join(args)}>"
-        if base == "gn_mish_kernel":         # <A, APPLY>: the ResnetBlock output or block2's in-place input
-            return ("gn_apply_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
+        if base == "gn_mish_kernel":         # <A, RES>: the ResnetBlock output, residual res_conv(input) or identity
+            return ("rbout_input_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
         if base in ("attn_kv_kernel", "final_kernel", "to_nchw_kernel"):
             return f"{base}<{ty(args[0])}>"
         if base == "attn_merge_kernel" and args:   # <DR>: rows per workgroup
