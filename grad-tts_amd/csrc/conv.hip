@@ -81,13 +81,13 @@ struct ConvCfg {
   // 1x1 convs: two weight slabs, chunk c+1's DMA in flight during chunk c's MFMAs (a 1x1 chunk is one tap, too
   // short to hide a weight round trip behind; the slab is 4-8 KB)
   static constexpr bool DBW = (!SPLIT && KIND == CONV1) || SMALLDB;
-  // Split-K (small-batch plan, 128-wide bf16 3x3 tiles): p.ksplit workgroups per output tile each run a contiguous
+  // Split-K (small-batch plan, 128-wide 3x3 tiles, bf16 activations): p.ksplit workgroups per output tile each run a contiguous
   // range of input-channel chunks and leave their fp32 accumulators in p.sk_part; the last to finish (a counter per
   // tile, which it re-arms) adds the partials in split order -- a fixed order, so the result does not depend on which
   // finished last -- and runs the epilogue. A single utterance's level-2 convs otherwise occupy 80 of the 256 CUs, each
   // streaming 590 KB of weights through LDS.
   static constexpr bool SK = KIND == CONV3 && OUT == OUT_STATS && NT == 128 && (TF_ == TF1_DBW || TF_ == 1) &&
-                             IN != IN_INPUT && !W8 && sizeof(A) == 2;
+                             IN != IN_INPUT && sizeof(A) == 2;   // (bf16, fp8-weight and fp8-operand tiles)
   static constexpr int PA = HA / 4096, PB = (WBYTES - HA) / 4096;
   static constexpr int CK = A8 ? 32 : CKB / (int)sizeof(A);   // input channels per chunk
   static constexpr int ICH = 16 / (int)sizeof(A);            // channels per item (one 16-B global load)
@@ -947,10 +947,10 @@ static hipError_t dispatch_a8(ConvKind kind, InMode im, OutMode om, const ConvPa
   return hipErrorNotSupported;
 }
 
-int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target) {
+int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target, int a8) {
   if (Cout % 128 != 0 || target <= 0) return 1;
   const long tiles = (long)F * ((T + 63) / 64) * (Cout / 128);   // 1-row 64-frame tiles of one utterance
-  const int nchunk = Cin_pad / (conv_ckb(1, 9, Cin_pad) / 2);    // bf16 chunks (ConvCfg::CK of these tiles)
+  const int nchunk = Cin_pad / (a8 ? 32 : conv_ckb(1, 9, Cin_pad) / 2);   // input chunks (ConvCfg::CK of these tiles)
   long ks = target / tiles;
   ks = std::min<long>(ks, std::min(4, nchunk / 2));              // at least two chunks per split
   return ks > 1 ? (int)ks : 1;

@@ -759,8 +759,8 @@ struct Run {
     }
     const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
     if (np > L.pmax) { chk(hipErrorInvalidValue); return np; }
-    if (small && dt && !p.wscale && p.Cout % 128 == 0 && im != IN_INPUT && L.skcnt_n) {   // split-K (conv.hip ConvCfg::SK)
-      p.ksplit = conv_small_ksplit(p.Fout, p.Tout, p.Cout, p.Cin_pad, d->sk_target);
+    if (small && dt && p.Cout % 128 == 0 && im != IN_INPUT && L.skcnt_n) {   // split-K (conv.hip ConvCfg::SK)
+      p.ksplit = conv_small_ksplit(p.Fout, p.Tout, p.Cout, p.Cin_pad, d->sk_target, p.a8);
       const long tiles = (long)p.B * p.Fout * ((p.Tout + 63) / 64) * (p.Cout / 128);
       if (p.ksplit > 1 && (tiles > L.skcnt_n || tiles * p.ksplit * 8192 > L.skpart_n)) { chk(hipErrorInvalidValue); return np; }
       p.sk_part = (float*)(ws + L.skpart); p.sk_cnt = (int*)(ws + L.skcnt);

@@ -54,7 +54,7 @@ struct ConvParams {
 };
 // split count of the small plan's 128-wide 3x3 convs: a function of the utterance's grid and the input chunks only
 // (never of the batch, so a small-plan decode stays batch-invariant); 1 = no split
-int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target);
+int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target, int a8);
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid

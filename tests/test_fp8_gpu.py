@@ -151,7 +151,14 @@ def test_fp8_sampler_N1000_matches_oracle():
 def test_fp8_sampler_T64_plus_matches_oracle(B, T, lengths):
     """The A8 sampler on the tile shapes the bench runs: B = 5 takes the throughput plan (4- and 5-row / 128-wide fp8
     tiles at levels 1-2, 64 frames wide), B = 2 the small plan; T >= 64 so every level has full-width tiles (the
-    N = 1000 check above uses T = 16). 50 Euler steps; gates as for N = 1000."""
+    N = 1000 check above uses T = 16). 50 Euler steps.
+
+    Gate against the fp8 oracle: half the quantization effect q (the fp8 oracle's distance to the fp32 oracle), not the
+    bf16 sampler's absolute 1e-2. The product stores activations in bf16 between kernels and projects attention with
+    bf16 weights; the oracle keeps fp32 there. Each such rounding moves some operands across an e4m3 rounding boundary
+    (a step of 1/8 relative), and over 50 steps these flips, not the arithmetic, set the distance between two fp8
+    realisations of the same sampler -- in units of what fp8 quantization does to the result (q), not of bf16 rounding.
+    Measured: 0.27-0.31 q (profiles/r05b/parity.jsonl); the absolute 1e-2 sat at 0.87-0.99 of its value."""
     from oracle import decoder as odec
     from gradtts_amd.params import synthetic_inputs
     dec, sd = make_decoder(1, 0, FP8)
@@ -164,7 +171,9 @@ def test_fp8_sampler_T64_plus_matches_oracle(B, T, lengths):
         ref32 = odec.reverse_diffusion(odec.to_torch_params(sd), *args, 50).numpy()
     y = dec(_cuda(z), _cuda(mask), _cuda(mu), 50).cpu().numpy()
     q = rel_err(ref8, ref32)
-    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle", rel_err(y, ref8), 1e-2, quant_effect=q)
+    e8 = rel_err(y, ref8)
+    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle", e8, 0.5 * q, quant_effect=q)
+    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle (absolute 1e-2, reported)", e8, 1e-2, gate=False, quant_effect=q)
     report(f"fp8 reverse N=50 B={B} T={T} vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
 
 

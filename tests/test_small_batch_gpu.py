@@ -173,18 +173,22 @@ def test_latency_b1_report(mode):
     assert torch.isfinite(y_s).all() and torch.isfinite(y_t).all()
 
 
-def test_split_k_deterministic_and_agrees(monkeypatch):
+@pytest.mark.parametrize("mode", [torch.bfloat16, "bf16_w8", "fp8"])
+def test_split_k_deterministic_and_agrees(monkeypatch, mode):
     """Split-K of the small plan's 128-wide 3x3 convs (conv.hip ConvCfg::SK: the last of a tile's workgroups adds the
-    fp32 partials in split order and re-arms the tile's counter): repeated decodes are bit-identical whichever workgroup
-    finishes last, a second decoder on the same workspace sizes sees zeroed counters, and the result agrees with the
-    unsplit tiles (GT_SK_TARGET=0) within the bf16 sampler gate. B = 1, T = 512: level-2 tiles split 3-4 ways."""
+    fp32 partials in split order and re-arms the tile's counter), for bf16, fp8-weight and fp8-operand tiles: repeated
+    decodes are bit-identical whichever workgroup finishes last, a second decoder on the same workspace sizes sees
+    zeroed counters, and the result agrees with the unsplit tiles (GT_SK_TARGET=0) within the bf16 sampler gate
+    (fp8 operands: the per-block scales are per position and chunk, so splitting K changes no quantization).
+    B = 1, T = 512: level-2 tiles split 3-4 ways."""
     mu, z, mask, _ = _inputs(41, 1, 512, lengths=[480])
-    dec, _ = make_decoder(1, 0, torch.bfloat16)
+    dec, _ = make_decoder(1, 0, mode)
     ya = dec(z, mask, mu, 4)
     yb = dec(z, mask, mu, 4)
     assert torch.isfinite(ya).all()
     assert torch.equal(ya, yb), float((ya - yb).abs().max())
     monkeypatch.setenv("GT_SK_TARGET", "0")
-    dec0, _ = make_decoder(1, 0, torch.bfloat16)
+    dec0, _ = make_decoder(1, 0, mode)
     y0 = dec0(z, mask, mu, 4)
-    report("small plan split-K vs unsplit bf16 B=1 T=512 N=4", rel_err(ya.cpu().numpy(), y0.cpu().numpy()), BF16_REV_TOL)
+    report(f"small plan split-K vs unsplit {mode} B=1 T=512 N=4", rel_err(ya.cpu().numpy(), y0.cpu().numpy()),
+           BF16_REV_TOL)
