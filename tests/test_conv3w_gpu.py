@@ -124,3 +124,23 @@ def test_wide_conv_deterministic_large_batch():
     assert torch.isfinite(y1).all()
     assert torch.equal(y1, y2), float((y1 - y2).abs().max())
     assert torch.equal(y1[30:], sub), float((y1[30:] - sub).abs().max())
+
+
+def test_fractional_mask_c_abi_paths_agree():
+    """A caller of the C ABI itself (no boundary check there) may still pass a fractional mask: conv3w's items then
+    read their mask values again (pm_of, the path 0/1 masks never take) and compute x * m as conv_kernel does. The
+    estimator through gt_estimator_probe with conv3w on and off agrees within the bf16 gate (both paths compute
+    (Mish(GN(h)) + tb) * m, the single-multiply form the boundary's 0/1 contract makes exact)."""
+    B, T = 3, 128
+    mu, z, mask, _ = synthetic_inputs(52, B, T, lengths=[128, 100, 60])
+    frac = (mask * np.random.default_rng(6).uniform(0.25, 1.0, mask.shape)).astype(np.float32)
+    t = np.linspace(0.9, 0.3, B).astype(np.float32)
+    args = [_cuda(a) for a in (z, frac, mu, t)]
+    outs = []
+    for wide in (True, False):
+        dec, _ = make_decoder(1, 0, torch.bfloat16)
+        _plan(dec, wide)
+        y, _ = probe(dec.estimator, torch.bfloat16, *args, None, "downs.1.1", (B, 128, 40, T // 2))
+        outs.append(y.cpu().numpy())
+    assert np.isfinite(outs[0]).all()
+    report("conv3w vs conv_kernel estimator, fractional mask (C ABI)", rel_err(outs[0], outs[1]), STAGE_TOL)
