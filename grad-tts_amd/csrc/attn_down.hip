@@ -40,7 +40,9 @@ template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   /
 typedef unsigned u32x4a_t __attribute__((ext_vector_type(4)));
 
 // 4 waves (the attention output itself is not needed at level 0).
-template <int C>
+// W8: fp8 weights (p.wsc): the stage-2 epilogue is conv_kernel W8's acc * scale + bias (a template parameter: a run-time
+// test in the epilogue cost attn_up 82 -> 119 us)
+template <int C, bool W8>
 __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void attn_down_kernel(AttnDownParams p) {
   using namespace ad;
   constexpr int NCB = C / 32;   // 32-channel blocks
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void
     for (int pr = 0; pr < 2; ++pr) {
       const int c0 = cb * 32 + pr * 16 + 8 * h;
       float o[8];
-      if (p.wsc) {   // fp8 weights (their e4m3 values in the image): conv_kernel W8's epilogue, acc * scale + bias
+      if (W8) {   // fp8 weights (their e4m3 values in the image): conv_kernel W8's epilogue, acc * scale + bias
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = v[8 * pr + k] * p.wsc[c0 + k] + p.bds[c0 + k];
       } else {
@@ -225,7 +227,8 @@ bool attn_down_eligible(const AttnDownParams& p) {
 hipError_t launch_attn_down(const AttnDownParams& p, hipStream_t s) {
   if (!attn_down_eligible(p)) return hipErrorInvalidValue;
   const long grid = (long)p.B * (p.F / 4) * ((p.T / 2 + 31) / 32);
-  hipLaunchKernelGGL((attn_down_kernel<64>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  if (p.wsc) hipLaunchKernelGGL((attn_down_kernel<64, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((attn_down_kernel<64, false>), dim3((unsigned)grid), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 
@@ -240,6 +243,7 @@ constexpr int PLANE = NPOS;                                                     
 constexpr int SMEM = 8 * PLANE * 16;                                                 // 26,112 B
 }  // namespace au
 
+template <bool W8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void attn_up_kernel(AttnUpParams p) {
   using namespace au;
   constexpr int C = 64;
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
           const int c0 = cb * 32 + pr * 16 + 8 * h;
           float o[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] = p.wsc ? v[8 * pr + k] * p.wsc[c0 + k] + p.bup[c0 + k] : v[8 * pr + k] + p.bup[c0 + k];
+          for (int k = 0; k < 8; ++k) o[k] = W8 ? v[8 * pr + k] * p.wsc[c0 + k] + p.bup[c0 + k] : v[8 * pr + k] + p.bup[c0 + k];
           *reinterpret_cast<uint4*>(out + c0) = f_to_item(o, bf16());
         }
       }
@@ -408,7 +412,8 @@ bool attn_up_eligible(const AttnUpParams& p) {
 hipError_t launch_attn_up(const AttnUpParams& p, hipStream_t s) {
   if (!attn_up_eligible(p)) return hipErrorInvalidValue;
   const long grid = (long)p.B * (p.F / 4) * ((p.T + 31) / 32);
-  hipLaunchKernelGGL(attn_up_kernel, dim3((unsigned)grid), dim3(256), 0, s, p);
+  if (p.wsc) hipLaunchKernelGGL(attn_up_kernel<true>, dim3((unsigned)grid), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(attn_up_kernel<false>, dim3((unsigned)grid), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -60,8 +60,12 @@ def norm(name: str) -> str:
                     ("" if tf == "4" else ",tf" + tf) + ">")
         if base == "conv64_kernel":          # <IN>
             return f"conv64_kernel<{args[0]}>"
-        if base in ("conv3w_kernel", "attn_down_kernel"):   # <IN, COUT, CB> / <C, WY>
+        if base == "conv3w_kernel":          # <IN, COUT, CB>
             return f"{base}<{','.join(args)}>"
+        if base == "attn_down_kernel":       # <C, W8>
+            return f"{base}<{args[0]}" + (",w8" if args[1] in ("true", "1") else "") + ">"
+        if base == "attn_up_kernel":         # <W8>
+            return base + ("<w8>" if args[0] in ("true", "1") else "")
         if base == "gn_mish_kernel":         # <A, RES>: the ResnetBlock output, residual res_conv(input) or identity
             return ("rbout_input_kernel" if args[1] in ("true", "1") else "rbout_identity_kernel") + f"<{ty(args[0])}>"
         if base in ("attn_kv_kernel", "final_kernel", "to_nchw_kernel"):
