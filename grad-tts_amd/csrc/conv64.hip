@@ -346,7 +346,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // pass in a fixed order; reduced across lanes and waves once, at the end
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
   const unsigned long long t_loop = stamp();
+  // The two workgroups sharing a CU start together, and the arbiter favours the older one's waves: the second-dispatched
+  // (upper half of the grid) used to run the last ~20 % of its segment alone. Its waves take priority 1 for the first
+  // two thirds of their tiles (measured: level-0 GN conv 112.7 -> 109.4 us, same box; switching at 1/4, 1/3, 1/2 of
+  // the tiles or never back: less).
+  const bool young = (int)blockIdx.x >= (int)(gridDim.x / 2);
+  if (young) __builtin_amdgcn_s_setprio(1);
   for (int k = 0; k < L; ++k) {
+    if (young && k == (2 * L) / 3) __builtin_amdgcn_s_setprio(0);
     const int ft = ft0 + k;
 #pragma unroll
     for (int ps = 0; ps < 2; ++ps) {
