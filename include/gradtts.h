@@ -85,7 +85,11 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* dec, int dtype, int64_t B, i
 
 /* One score evaluation: out[B,80,T] = s_theta(x, mask, mu, t, spk).
  * x, mu, out: [B,80,T] fp32; mask: [B,1,T] fp32 (0/1); t: [B] fp32; spk: [B,64] fp32 or NULL.
- * T must be a multiple of 4 (fix_len_compatibility, model/utils.py:13-17). */
+ * T must be a multiple of 4 (fix_len_compatibility, model/utils.py:13-17).
+ * Masks are sequence_mask outputs, 0 or 1: the kernels compute the reference's x * m * m as x * m, exact only then.
+ * The C ABI does not scan the mask (device memory, the caller's stream); the Python / torch.ops boundary rejects any
+ * other value (gradtts_amd.diffusion, csrc/torch_ops.cpp). A fractional mask here gives a consistent result on every
+ * kernel path, but not the reference's. */
 int gt_estimator_forward(gt_decoder* dec, int dtype, const float* x, const float* mask, const float* mu,
                          const float* t, const float* spk, int64_t B, int64_t T, float* out, void* workspace,
                          size_t workspace_bytes, void* stream);
