@@ -32,6 +32,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
+#include "c3w_asm.h"
 
 namespace gt {
 
@@ -100,28 +101,12 @@ struct Cfg {
 };
 }  // namespace c3w
 
-typedef unsigned u32x4c_t __attribute__((ext_vector_type(4)));
-
 #if GT_C3W_STAMP
 // [workgroup slot 0..511][wave 0..7][counter 0..7]: cycles in the DMA wait, the phase barrier, the item waits, the item
 // transforms + writes, the whole chunk loop, phases (the last launch of the stamped instantiation wins)
 __device__ unsigned long long gt_c3w_stamps[512 * 8 * 8];
 #endif
 
-template <int N>
-GT_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
-// counted wait that names the registers of an asm load (they are written when it retires)
-template <int N>
-GT_DEV void vm_wait_dep(u32x4c_t& x) { asm volatile("s_waitcnt vmcnt(%1)" : "+v"(x) : "n"(N) : "memory"); }
-// LDS DMA (1 KiB per wave instruction) hidden from hipcc's waitcnt bookkeeping: hipcc models its builtin twin as an LDS
-// access too and then waits lgkmcnt(0) in front of the fragment reads that follow it. M0 is written and restored in the
-// same statement (guide §5.7). Scalar base + one per-lane 32-bit offset register (the saddr form) for every DMA of the
-// kernel, where a 64-bit per-lane address per slot used to be held: 2-4 fewer VGPRs, no spill in the 256-wide GN form.
-GT_DEV void asm_dma16(const void* sbase, unsigned voff, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_addr) : "memory");
-}
 // v_mfma_f32_16x16x32_bf16 accumulating in place. hipcc does not tie the builtin's destination to its C operand (a third
 // of the builtin MFMAs of this loop wrote a fresh register set, the accumulators rotated through the register file and
 // the kernel spilled); the asm form keeps every accumulator in its registers. hipcc pads no hazards inside asm: the
@@ -130,11 +115,6 @@ GT_DEV void asm_dma16(const void* sbase, unsigned voff, unsigned lds_addr) {
 // (mfma_drain) waits out the last MFMAs before any other instruction reads an accumulator.
 GT_DEV void mfma16(f32x4& c, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
-}
-GT_DEV void mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-// raw buffer load hidden from hipcc's waitcnt bookkeeping (the s_nop covers an SGPR operand written just before)
-GT_DEV void asm_buffer_load(u32x4c_t& dst, int voff, __amdgpu_buffer_rsrc_t rs, int soff) {
-  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(dst) : "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
 
 // IN: IN_MASK (x * mask), IN_GN ((Mish(GN(h)) + tb) * mask), IN_PLAIN. OUT: OUT_STATS.
@@ -591,8 +571,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
 #endif
 }
 
-// (BN, CB) of a conv on an F-row grid with Cout outputs, or 0 if conv3w does not cover it
-static int c3w_cfg(int Cout, int F) {
+// (BN, CB) of a conv on an F-row grid with Cout outputs, or 0 if conv3w does not cover it (shared with conv3w_a8.hip)
+int conv3w_cfg(int Cout, int F) {
   if (Cout == 256 && F % 10 == 0) return 1;    // <256, 2>: 10-row tiles (level 2)
   if (Cout == 128 && F % 20 == 0 && F >= 40) return 2;   // <128, 2>: 20-row tiles (level 1)
   if (Cout == 128 && F % 10 == 0) return 3;    // <128, 1>: 10-row tiles (level 2)
@@ -601,17 +581,21 @@ static int c3w_cfg(int Cout, int F) {
 }
 static int c3w_rows(int cfg) { return (cfg == 1 || cfg == 3) ? 10 : 20; }
 
-bool conv3w_eligible(const ConvParams& p, InMode im) {
+// shapes and input modes either form (bf16 operands / fp8 operands) covers
+static bool c3w_shape_ok(const ConvParams& p, InMode im) {
   if (im != IN_MASK && im != IN_GN && im != IN_PLAIN) return false;
-  if (p.small || p.a8 || p.w_bstride || p.Fin != p.Fout || p.Tin != p.Tout) return false;
+  if (p.small || p.w_bstride || p.Fin != p.Fout || p.Tin != p.Tout) return false;
   if (p.Cin % 32 || p.C0 % 32 || (p.in1 && p.C1 % 32) || p.Cin_pad != p.Cin || p.Cin != p.C0 + (p.in1 ? p.C1 : 0)) return false;
   if (im == IN_GN && p.Cin > 256) return false;
-  if (!c3w_cfg(p.Cout, p.Fout)) return false;
+  if (!conv3w_cfg(p.Cout, p.Fout)) return false;
   return (long)p.B * p.Fin * p.Tin * (p.C0 > p.C1 ? p.C0 : p.C1) * 2 < (1L << 31);
 }
 
+bool conv3w_eligible(const ConvParams& p, InMode im) { return !p.a8 && c3w_shape_ok(p, im); }
+bool conv3w_a8_eligible(const ConvParams& p, InMode im) { return p.a8 && p.wscale && c3w_shape_ok(p, im); }
+
 int conv3w_nparts(int F, int T, int Cout) {
-  const int cfg = c3w_cfg(Cout, F);
+  const int cfg = conv3w_cfg(Cout, F);
   return cfg ? (F / c3w_rows(cfg)) * ((T + 31) / 32) : 0;
 }
 
@@ -633,7 +617,7 @@ static hipError_t launch_c3w_in(InMode im, const ConvParams& p, hipStream_t s) {
 
 hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s) {
   if (!conv3w_eligible(p, im)) return hipErrorInvalidValue;
-  switch (c3w_cfg(p.Cout, p.Fout)) {
+  switch (conv3w_cfg(p.Cout, p.Fout)) {
     case 1: return launch_c3w_in<256, 2>(im, p, s);
     case 2: return launch_c3w_in<128, 2>(im, p, s);
     case 3: return launch_c3w_in<128, 1>(im, p, s);

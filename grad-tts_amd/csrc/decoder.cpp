@@ -191,6 +191,9 @@ struct gt_decoder {
   // bf16 throughput-plan 3x3 convs at levels 1-2 on conv3w (one 8-wave workgroup per CU owning all output channels of
   // a tile); GT_CONV3W=0 at creation or gt_decoder_set_wide_conv(dec, 0) runs them on conv_kernel
   bool wide = true;
+  // fp8-operand convs (GT_FP8) of the same shapes on conv3w_a8 (conv3w_a8.hip) instead of conv_kernel's A8 form, when
+  // `wide` too; GT_CONV3W_A8=0 disables it (A/B)
+  bool wide_a8 = false;
   // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
   bool attn_ds = true;
   // the first ResnetBlock's output formed by the next block's conv (conv64 IN_RB0) instead of its own pass
@@ -442,6 +445,27 @@ void pack_conv3w(Blob& blob, const std::string& key, const std::vector<float>& w
   blob.put(key, img.data(), img.size() * 2);
 }
 
+// pack a 3x3 [Cout][Cin][3][3] weight (Cin % 32 == 0) for conv3w_a8 (conv3w_a8.hip): e4m3 codes quantized per output
+// channel exactly as pack_conva8 (its ".s" scale serves both), one slot per (32-channel chunk c, tap pair u) in phase
+// order k = 5 c + u, each [plane q = 2 v + h][co][16 channels 32 c + 16 h ..] of tap 2 u + v (tap 9: zero) -- the LDS
+// image of a weight slot
+void pack_conv3w_a8(Blob& blob, const std::string& key, const std::vector<float>& w, int cout, int cin) {
+  std::vector<uint8_t> q(w.size());
+  std::vector<float> sc(cout);
+  gt_quantize_e4m3(w.data(), cout, (int64_t)cin * 9, (int64_t)cin * 9, 1, q.data(), sc.data());
+  std::vector<uint8_t> img((size_t)(cin / 32) * 5 * cout * 64, 0);
+  size_t i = 0;
+  for (int c = 0; c < cin / 32; ++c)
+    for (int u = 0; u < 5; ++u)
+      for (int pl = 0; pl < 4; ++pl) {
+        const int t = 2 * u + (pl >> 1), hh = pl & 1;
+        for (int co = 0; co < cout; ++co)
+          for (int e = 0; e < 16; ++e, ++i)
+            if (t < 9) img[i] = q[((size_t)co * cin + 32 * c + 16 * hh + e) * 9 + t];
+      }
+  blob.put(key, img.data(), img.size());
+}
+
 // e4m3 values (codes decoded, without the scale) of a [rows][...] weight quantized per row as gt_quantize_e4m3 does:
 // exact in bf16, for the conv64 image of an fp8-weight conv (the scale is applied in conv64's epilogue)
 std::vector<float> e4m3_values(const std::vector<float>& w, int rows) {
@@ -509,6 +533,7 @@ int prepare(gt_decoder* d, int code) {
       pack_conv64(blob, k + ".w64", e4m3_values(w, 64));
     } else if (a8 && ends_with(k, ".block.0.weight") && shp[1] >= 32) {
       pack_conva8(blob, d, code, k, w, shp);
+      if (conv3w_shape(shp)) pack_conv3w_a8(blob, k + ".w3a", w, (int)shp[0], (int)shp[1]);   // conv3w_a8
     } else if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
       pack_conv8(blob, d, code, k, w, shp, false);
       if (code == GT_BF16_W8 && ends_with(k, ".block.0.weight") && conv3w_shape(shp))   // conv3w: the e4m3 values
@@ -755,6 +780,18 @@ struct Run {
                 "x" + std::to_string(p.Fout),
             2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + 9.0 * p.Cin * p.Cout * 2,
             [&] { return launch_conv3w(im, p, s); });
+      return np;
+    }
+    if (dt && wi == GT_FP8 && d->wide && d->wide_a8 && conv3w_a8_eligible(p, im) && d->dp[wi].count(wkey + ".w3a")) {
+      p.w = W(wkey + ".w3a");   // (p.wscale: the per-channel scale of the e4m3 codes, shared with conv_kernel's image)
+      const int np = conv3w_nparts(p.Fout, p.Tout, p.Cout);
+      if (np <= 0 || np > L.pmax) { chk(hipErrorInvalidValue); return np; }
+      const double pos = (double)p.B * p.Fout * p.Tout;
+      const int cb = (p.Cout == 256 || (p.Cout == 128 && p.Fout % 20 == 0 && p.Fout >= 40)) ? 2 : 1;
+      timed(std::string("conv3w_a8_kernel<") + std::to_string((int)im) + "," + std::to_string(p.Cout) + "," +
+                std::to_string(cb) + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" + std::to_string(p.Fout),
+            2.0 * p.Cin * p.Cout * 9 * pos, pos * (p.Cin + p.Cout) * 2.0 + 9.0 * p.Cin * p.Cout,
+            [&] { return launch_conv3w_a8(im, p, s); });
       return np;
     }
     const int np = conv_gn_nparts(dt, im, p.Fout, p.Tout, p.Cout, p.small, p.a8);
@@ -1161,6 +1198,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_MAX_CHUNK")) d->max_chunk = atoll(e);
   if (const char* e = getenv("GT_SMALL_B")) d->small_b = std::max<int64_t>(0, std::min<int64_t>(kSmallBMax, atoll(e)));
   if (const char* e = getenv("GT_CONV3W")) d->wide = atoi(e) != 0;
+  if (const char* e = getenv("GT_CONV3W_A8")) d->wide_a8 = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   if (const char* e = getenv("GT_RB0_FUSE")) d->rb0_fuse = atoi(e) != 0;

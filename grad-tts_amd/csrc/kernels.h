@@ -159,5 +159,10 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s);
 bool conv3w_eligible(const ConvParams& p, InMode im);
 int conv3w_nparts(int F, int T, int Cout);
 hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s);
+int conv3w_cfg(int Cout, int F);
+// fp8-operand form (conv3w_a8.hip; GT_FP8's throughput plan): the same tiles and partial slots as conv3w, the conv's
+// .w3a image (decoder.cpp pack_conv3w_a8) and its per-output-channel weight scale (p.wscale)
+bool conv3w_a8_eligible(const ConvParams& p, InMode im);
+hipError_t launch_conv3w_a8(InMode im, const ConvParams& p, hipStream_t s);
 
 }  // namespace gt

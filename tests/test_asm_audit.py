@@ -4,7 +4,7 @@ conv3w (csrc/conv3w.hip) loads the next chunk's patch items with inline-asm `buf
 drain the weight DMAs with a conservative `s_waitcnt vmcnt(0)`; the matching counted `s_waitcnt vmcnt(N)` is written by
 hand. If the compiler (or a source edit) lets an instruction read or overwrite a load's destination registers before
 the wait that retires it, the kernel reads stale data or -- as in round 4 -- faults the GPU with an illegal address.
-This test compiles every csrc/*.hip file whose inline asm issues buffer loads to a gfx950 listing (hipcc -S, device
+This test compiles every csrc/*.hip file whose inline asm (its own or c3w_asm.h's) issues buffer loads to a gfx950 listing (hipcc -S, device
 only) and runs the audit over each kernel: a hazard fails here, on the CPU, instead of on the GPU."""
 import os
 import re
@@ -20,17 +20,26 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ASM_LOAD = re.compile(r'asm\s+volatile\s*\(\s*"[^"]*buffer_load_dword', re.S)
 
 
+# headers whose inline asm issues buffer loads (c3w_asm.h: asm_buffer_load / asm_buffer_load2)
+ASM_HEADERS = [f for f in sorted(os.listdir(CSRC)) if f.endswith(".h") and ASM_LOAD.search(open(os.path.join(CSRC, f)).read())]
+
+
 def _sources():
     out = []
     for f in sorted(os.listdir(CSRC)):
-        if f.endswith(".hip") and ASM_LOAD.search(open(os.path.join(CSRC, f)).read()):
+        if not f.endswith(".hip"):
+            continue
+        text = open(os.path.join(CSRC, f)).read()
+        if ASM_LOAD.search(text) or any(f'#include "{h}"' in text and "asm_buffer_load" in text for h in ASM_HEADERS):
             out.append(f)
     return out
 
 
 def test_asm_load_sources_found():
-    # conv3w is the kernel family whose inline-asm loads the audit guards; if it stops using them, update this test
-    assert "conv3w.hip" in _sources()
+    # conv3w and its fp8-operand twin are the kernels whose inline-asm loads the audit guards (their loads live in
+    # c3w_asm.h); if they stop using them, update this test
+    assert "c3w_asm.h" in ASM_HEADERS
+    assert "conv3w.hip" in _sources() and "conv3w_a8.hip" in _sources()
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")

@@ -42,6 +42,15 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+def _throughput_plan(dec):
+    """Force the throughput plan (wide tiles: conv3w_a8 for the level-1/2 convs) at any batch."""
+    from gradtts_amd import _lib
+    L = _lib.lib()
+    h = dec.estimator._native()
+    _lib.check(L.gt_decoder_set_small_batch(h, 0), "gt_decoder_set_small_batch")
+    _lib.check(L.gt_decoder_set_wide_conv(h, 1), "gt_decoder_set_wide_conv")
+
+
 def _stage(dec, args, name, shape):
     _, pr = probe(dec.estimator, FP8, *args, None, name, shape)
     return pr.cpu()
@@ -58,11 +67,16 @@ MASK_LAYERS = [
 ]
 
 
+@pytest.mark.parametrize("plan", ["small", "wide"])
 @pytest.mark.parametrize("ins,out,lvl,cin,cout", MASK_LAYERS, ids=[m[1] for m in MASK_LAYERS])
-def test_fp8_mask_conv_matches_oracle_on_identical_inputs(ins, out, lvl, cin, cout):
+def test_fp8_mask_conv_matches_oracle_on_identical_inputs(ins, out, lvl, cin, cout, plan):
+    """plan "wide": the throughput plan forced at B = 1, so the level-1/2 convs run conv3w_a8 (conv3w_a8.hip; the
+    64 -> 64 conv stays on conv64) -- its quantization, tap pairs and scale bytes against the same oracle."""
     from oracle import decoder as odec
     g = load_golden("estimator_s1_T132.npz")
     dec, sd = make_decoder(1, 0, FP8)
+    if plan == "wide":
+        _throughput_plan(dec)
     args = [_cuda(g[k]) for k in ("x", "mask", "mu", "t")]
     B, _, T = g["x"].shape
     F_, T_ = 80 >> lvl, T >> lvl
@@ -79,16 +93,19 @@ def test_fp8_mask_conv_matches_oracle_on_identical_inputs(ins, out, lvl, cin, co
     xin = odec.quantize_act_e4m3(x * m) if odec.fp8_operand_conv(cin, cout) else x * m   # 64 -> 64: bf16 operands
     ref = F.conv2d(xin, p8[key + "weight"], p8[key + "bias"], padding=1).numpy()
     y = _stage(dec, args, out, ref.shape).numpy()
-    report(f"fp8 layer {out} ({cin}->{cout}, identical inputs)", rel_err(y, ref), LAYER_TOL)
+    report(f"fp8 layer {out} ({cin}->{cout}, identical inputs, {plan} plan)", rel_err(y, ref), LAYER_TOL)
 
 
-def test_fp8_gn_conv_close_to_oracle_on_gpu_inputs():
+@pytest.mark.parametrize("plan", ["small", "wide"])
+def test_fp8_gn_conv_close_to_oracle_on_gpu_inputs(plan):
     """block2 (GroupNorm + Mish + time bias in the operand load) from the GPU's own block1 output. The GroupNorm
     statistics come from the fp32 conv outputs on the GPU and from their bf16-stored copy here, so a few e4m3
     rounding decisions may flip: the gate is 2x the layer gate (measured 2.5-3.4e-3; an operand-layout error is O(1))."""
     from oracle import decoder as odec
     g = load_golden("estimator_s1_T132.npz")
     dec, sd = make_decoder(1, 0, FP8)
+    if plan == "wide":
+        _throughput_plan(dec)
     args = [_cuda(g[k]) for k in ("x", "mask", "mu", "t")]
     B, _, T = g["x"].shape
     p8 = odec.fp8_params(sd)
@@ -105,7 +122,7 @@ def test_fp8_gn_conv_close_to_oracle_on_gpu_inputs():
         ref = F.conv2d(odec.quantize_act_e4m3(h * m), p8[key + "block2.block.0.weight"],
                        p8[key + "block2.block.0.bias"], padding=1).numpy()
         y = _stage(dec, args, key + "pre2", ref.shape).numpy()
-        report(f"fp8 layer {key}pre2 (GroupNorm operand, GPU block1 output)", rel_err(y, ref), 2 * LAYER_TOL)
+        report(f"fp8 layer {key}pre2 (GroupNorm operand, GPU block1 output, {plan} plan)", rel_err(y, ref), 2 * LAYER_TOL)
 
 
 @pytest.mark.parametrize("name", EST)
