@@ -100,6 +100,9 @@ GT_DEV void mfma8s(f32x16& c, const v8i_t& a, const v8i_t& b, int sa, int sb) {
     asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
                  : "+v"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
+#ifndef GT_C3W8_GNPIPE
+#define GT_C3W8_GNPIPE 0
+#endif
 #ifndef GT_C3W8_AGR
 #define GT_C3W8_AGR 0
 #endif
@@ -206,6 +209,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     item_to_f(make_uint4(preg[j][1][0], preg[j][1][1], preg[j][1][2], preg[j][1][3]), v + 8, bf16());
     if (IN == IN_GN) {
       const int ch = c * 32 + h * 16;
+#if GT_C3W8_GNPIPE
+      // coefficient pairs read one pair ahead of their use: the LDS latency of pair u + 1 runs under pair u's math
+      f32x2_t sc0 = *reinterpret_cast<const f32x2_t*>(s_sc + ch), sh0 = *reinterpret_cast<const f32x2_t*>(s_sh + ch),
+              tb0 = *reinterpret_cast<const f32x2_t*>(s_tb + ch);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        f32x2_t sc1 = sc0, sh1 = sh0, tb1 = tb0;
+        if (u < 7) {
+          sc1 = *reinterpret_cast<const f32x2_t*>(s_sc + ch + 2 * u + 2);
+          sh1 = *reinterpret_cast<const f32x2_t*>(s_sh + ch + 2 * u + 2);
+          tb1 = *reinterpret_cast<const f32x2_t*>(s_tb + ch + 2 * u + 2);
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) v[2 * u + k] = gn_mish_tb_l2(v[2 * u + k], sc0[k], sh0[k], tb0[k]);
+        asm volatile("" ::: "memory");   // at most two coefficient pairs in registers (register budget)
+        sc0 = sc1; sh0 = sh1; tb0 = tb1;
+      }
+#else
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const f32x2_t sc = *reinterpret_cast<const f32x2_t*>(s_sc + ch + 2 * u);
@@ -213,8 +234,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         const f32x2_t tb = *reinterpret_cast<const f32x2_t*>(s_tb + ch + 2 * u);
 #pragma unroll
         for (int k = 0; k < 2; ++k) v[2 * u + k] = gn_mish_tb_l2(v[2 * u + k], sc[k], sh[k], tb[k]);
-        asm volatile("" ::: "memory");   // one coefficient group in registers at a time (register budget)
+        asm volatile("" ::: "memory");   // one coefficient pair in registers at a time (register budget)
       }
+#endif
     }
     if ((IN == IN_GN || IN == IN_MASK) && frac) {
 #pragma unroll

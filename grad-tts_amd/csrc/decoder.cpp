@@ -193,7 +193,7 @@ struct gt_decoder {
   bool wide = true;
   // fp8-operand convs (GT_FP8) of the same shapes on conv3w_a8 (conv3w_a8.hip) instead of conv_kernel's A8 form, when
   // `wide` too; GT_CONV3W_A8=0 disables it (A/B)
-  bool wide_a8 = false;
+  bool wide_a8 = true;
   // level-0 attention output + Downsample as one pass (attn_down_kernel); GT_ATTN_DS=0 at creation: two launches
   bool attn_ds = true;
   // the first ResnetBlock's output formed by the next block's conv (conv64 IN_RB0) instead of its own pass
