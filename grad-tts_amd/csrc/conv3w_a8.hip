@@ -31,14 +31,10 @@ namespace c3w8 {
 constexpr int NTHR = 512, NW = 8, RB = 5, PCOL = 34;
 constexpr int NPH = 5;            // phases per 32-channel chunk (tap pairs)
 constexpr int S = 6, D = S - 1;   // weight ring slots, DMA distance (D <= NPH: DMA(k + D) exists iff chunk c+1 does or t + D < NPH)
-#ifndef GT_C3W8_PF
-#define GT_C3W8_PF 1
-#endif
-#ifndef GT_C3W8_LAT
-#define GT_C3W8_LAT 1
-#endif
-constexpr int PF = GT_C3W8_PF;    // B fragment prefetch distance in steps (ring of RB by step: chunk-periodic)
-constexpr int LAT = GT_C3W8_LAT;  // phases from an item's load to its transform
+// B fragment prefetch distance in steps (ring of RB by step: chunk-periodic), and phases from an item's load to its
+// transform: 2 / 2 spilled 5-230 registers (the 160 accumulators leave about 90)
+constexpr int PF = 1;
+constexpr int LAT = 1;
 
 template <int BN, int CB>
 struct Cfg {
@@ -87,26 +83,15 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 struct FragP8 { v8i_t v; int s; };
 
 // v_mfma_scale_f32_32x32x64_f8f6f4 accumulating in place (weights A with E8M0 scale sa, patch B with scale sb; e4m3 both).
-// As conv3w's mfma16: the asm form keeps each accumulator in its registers -- here the ACCUMULATION registers (AGPRs:
-// the 160 accumulator registers beside 256 VGPRs of fragments, items and addresses; in VGPRs the 128-wide forms spilled
-// 34-231 registers); the operands come from LDS reads waited for by the compiler, and mfma_drain waits out the last
-// MFMAs before the epilogue reads an accumulator.
-template <bool AG>
+// As conv3w's mfma16: the asm form keeps each accumulator in its registers; the operands come from LDS reads waited for
+// by the compiler, and mfma_drain waits out the last MFMAs before the epilogue reads an accumulator. The 160 accumulator
+// registers stay VGPRs: with two waves per SIMD the unified 512-entry file gives a wave 256 registers in all, and hipcc
+// splits them 128 / 128 as soon as AGPRs are used (measured: 300-450 spilled); in VGPRs only the item words' move to
+// LDS (s_pidx / s_pm) and one-item-at-a-time transforms were needed.
 GT_DEV void mfma8s(f32x16& c, const v8i_t& a, const v8i_t& b, int sa, int sb) {
-  if constexpr (AG)
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
-                 : "+a"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
-  else
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
-                 : "+v"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+               : "+v"(c) : "v"(a), "v"(b), "v"(sa), "v"(sb));
 }
-#ifndef GT_C3W8_GNPIPE
-#define GT_C3W8_GNPIPE 0
-#endif
-#ifndef GT_C3W8_AGR
-#define GT_C3W8_AGR 0
-#endif
-constexpr int AGR = GT_C3W8_AGR;   // row blocks whose accumulators live in AGPRs
 
 // IN: IN_MASK (x * mask), IN_GN ((Mish(GN(h)) + tb) * mask), IN_PLAIN. OUT: OUT_STATS.
 template <int IN, int BN, int CB>
@@ -209,24 +194,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     item_to_f(make_uint4(preg[j][1][0], preg[j][1][1], preg[j][1][2], preg[j][1][3]), v + 8, bf16());
     if (IN == IN_GN) {
       const int ch = c * 32 + h * 16;
-#if GT_C3W8_GNPIPE
-      // coefficient pairs read one pair ahead of their use: the LDS latency of pair u + 1 runs under pair u's math
-      f32x2_t sc0 = *reinterpret_cast<const f32x2_t*>(s_sc + ch), sh0 = *reinterpret_cast<const f32x2_t*>(s_sh + ch),
-              tb0 = *reinterpret_cast<const f32x2_t*>(s_tb + ch);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        f32x2_t sc1 = sc0, sh1 = sh0, tb1 = tb0;
-        if (u < 7) {
-          sc1 = *reinterpret_cast<const f32x2_t*>(s_sc + ch + 2 * u + 2);
-          sh1 = *reinterpret_cast<const f32x2_t*>(s_sh + ch + 2 * u + 2);
-          tb1 = *reinterpret_cast<const f32x2_t*>(s_tb + ch + 2 * u + 2);
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) v[2 * u + k] = gn_mish_tb_l2(v[2 * u + k], sc0[k], sh0[k], tb0[k]);
-        asm volatile("" ::: "memory");   // at most two coefficient pairs in registers (register budget)
-        sc0 = sc1; sh0 = sh1; tb0 = tb1;
-      }
-#else
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const f32x2_t sc = *reinterpret_cast<const f32x2_t*>(s_sc + ch + 2 * u);
@@ -236,7 +203,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         for (int k = 0; k < 2; ++k) v[2 * u + k] = gn_mish_tb_l2(v[2 * u + k], sc[k], sh[k], tb[k]);
         asm volatile("" ::: "memory");   // one coefficient pair in registers at a time (register budget)
       }
-#endif
     }
     if ((IN == IN_GN || IN == IN_MASK) && frac) {
 #pragma unroll
@@ -359,8 +325,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int j = 0; j < CB; ++j) {
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][j][k] = 0.f;
-      if (i < AGR) asm volatile("" : "+a"(acc[i][j]));   // the zeros are written here (after the prologue: its registers are free), ahead of the wait states below
-      else asm volatile("" : "+v"(acc[i][j]));
+      asm volatile("" : "+v"(acc[i][j]));   // zeros written here, after the prologue, ahead of the wait states below
     }
   int scale_one = 127;   // the weight operand's E8M0 1.0 (its per-channel fp32 scale is applied in the epilogue)
   asm volatile("" : "+v"(scale_one));
@@ -417,10 +382,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         if (n < RB) fb[n] = rd_b(cur, t, n);
         else if (MORE || t < NPH - 1) fb[n - RB] = t < NPH - 1 ? rd_b(cur, t + 1, n - RB) : rd_b(nxt, 0, n - RB);
 #pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          if (i < AGR) mfma8s<true>(acc[i][cb], fa[cb], fb[i].v, scale_one, fb[i].s);
-          else mfma8s<false>(acc[i][cb], fa[cb], fb[i].v, scale_one, fb[i].s);
-        }
+        for (int cb = 0; cb < CB; ++cb) mfma8s(acc[i][cb], fa[cb], fb[i].v, scale_one, fb[i].s);
         if (i == RB - 1 && (MORE || t < NPH - 1)) {   // phase k+1's A fragments, after this phase's last use
 #pragma unroll
           for (int cb = 0; cb < CB; ++cb) fa[cb] = rd_a(nslot, cb);

@@ -60,7 +60,7 @@ def norm(name: str) -> str:
                     ("" if tf == "4" else ",tf" + tf) + ">")
         if base == "conv64_kernel":          # <IN>
             return f"conv64_kernel<{args[0]}>"
-        if base == "conv3w_kernel":          # <IN, COUT, CB>
+        if base in ("conv3w_kernel", "conv3w_a8_kernel"):   # <IN, COUT, CB>
             return f"{base}<{','.join(args)}>"
         if base == "attn_down_kernel":       # <C, W8>
             return f"{base}<{args[0]}" + (",w8" if args[1] in ("true", "1") else "") + ">"
