@@ -10,7 +10,9 @@ scale per position and 32 channels). Two kinds of checks:
   quantization decisions are identical and the only differences are fp32 summation order and the bf16 rounding of
   the stored conv output: gate 1.05 x 2^-8 of max|ref| (bf16's half-ulp is 2^-8 of a value in [2^e, 2^(e+1)), so at
   most 2^-8 of max|ref|; 5 % for the summation order). A wrong operand layout, scale block or tap pairing shows up as
-  an O(1) error here (measured: 2.2-3.3e-3);
+  an O(1) error here (measured: 2.2-3.3e-3). Each layer check runs on both tile plans: "small" (conv_kernel's A8 tiles,
+  what B <= 4 takes) and "wide" (the throughput plan forced at B = 1: conv3w_a8, csrc/conv3w_a8.hip, for the level-1/2
+  shapes; the 64 -> 64 conv stays on conv64);
 * end to end: one estimator call cannot be pinned tighter than the quantization's own effect -- GPU and oracle see
   inputs that differ by bf16 rounding, and every e4m3 rounding decision that flips moves an operand by 2^-4 of
   itself -- so the gates are relative to that effect: the GPU's distance to the fp8 oracle must stay below the fp8
