@@ -79,6 +79,24 @@ GT_DEV void sfor(F&& f) {   // f(integral_constant<I>) ... f(integral_constant<N
 }
 }  // namespace c3w8
 
+#ifndef GT_C3W8_STAMP
+#define GT_C3W8_STAMP 0   // diagnostic builds only: s_memtime stamps of the phase waits (gt_diag_conv3w_a8_stamps)
+#endif
+#ifndef GT_C3W8_STAMP_BN
+#define GT_C3W8_STAMP_BN 256
+#endif
+#ifndef GT_C3W8_STAMP_IN
+#define GT_C3W8_STAMP_IN 2
+#endif
+#ifndef GT_C3W8_STAMP_CB
+#define GT_C3W8_STAMP_CB 2
+#endif
+#if GT_C3W8_STAMP
+// [workgroup slot 0..511][wave 0..7][counter 0..7]: cycles in the DMA wait, the phase barrier, the item waits, the item
+// transforms + writes, the whole chunk loop, phases, prologue, epilogue (the last launch of the stamped instantiation)
+__device__ unsigned long long gt_c3w8_stamps[512 * 8 * 8];
+#endif
+
 typedef int v8i_t __attribute__((ext_vector_type(8)));
 struct FragP8 { v8i_t v; int s; };
 
@@ -123,6 +141,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int ft = bid % n_ft;
   const int b = bid / n_ft;
   const int f0 = ft * C::TR, t0 = tt * 32;
+  constexpr bool STAMP = GT_C3W8_STAMP && BN == GT_C3W8_STAMP_BN && IN == GT_C3W8_STAMP_IN && CB == GT_C3W8_STAMP_CB;
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
+  const unsigned long long t_entry = stamp();
 
   // v_mfma_*_32x32x64 lanes: r = row of A (output channel) / column of B (position), h = the 16-channel plane
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -354,8 +376,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         constexpr int ndma0 = MORE ? D - 2 : ((NPH - t - 2) < (D - 2) ? (NPH - t - 2) : (D - 2));
         constexpr int ndma = ndma0 > 0 ? ndma0 : 0;
         constexpr int npl = MORE ? 2 * n_lp(t + 1 - D, t - 1) : 0;
+        const unsigned long long s0 = stamp();
         vm_wait<ndma * PW + npl>();
+        const unsigned long long s1 = stamp();
         asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(npre(t)) : "memory");
+        if (STAMP) { const unsigned long long s2 = stamp(); st[0] += s1 - s0; st[1] += s2 - s1; st[5] += 1; }
       }
       int nslot = slot + 1;
       nslot = nslot == S ? 0 : nslot;
@@ -372,7 +397,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         });
         c3w8::sfor<0, C::NPT>([&](auto Jc) {
           constexpr int j = decltype(Jc)::value;
-          if constexpr (C::TP(j) == t) vm_wait_dep2<n_after(j)>(preg[j][0], preg[j][1]);
+          if constexpr (C::TP(j) == t) {
+            const unsigned long long s0 = stamp();
+            vm_wait_dep2<n_after(j)>(preg[j][0], preg[j][1]);
+            if (STAMP) st[2] += stamp() - s0;
+          }
         });
       }
       // (d) MFMAs of phase k: step i = row block i, CB MFMAs; B read PF steps ahead (into phase k+1 for the last PF)
@@ -394,8 +423,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             c3w8::sfor<0, C::NPT>([&](auto Jc) {
               constexpr int j = decltype(Jc)::value;
               if constexpr (C::TP(j) == t) {
+                const unsigned long long s0 = stamp();
                 put_item(j, c + 1, nxt);
                 asm volatile("" ::: "memory");
+                if (STAMP) st[3] += stamp() - s0;
               }
             });
           }
@@ -406,8 +437,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     });
   };
   int c = 0;
+  const unsigned long long t_loop = stamp();
   for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
   chunk(c, std::false_type{});
+  const unsigned long long t_loop_end = stamp();
 
   // ---- epilogue: lane (r, h) of block (rb, cb) holds channels cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r;
   // v_permlane32_swap leaves it 8 consecutive channels per 16-channel half
@@ -492,6 +525,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = Ssum;
     dst[1] = Qsum;
   }
+#if GT_C3W8_STAMP
+  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
+    st[4] = t_loop_end - t_loop; st[6] = t_loop - t_entry; st[7] = stamp() - t_loop_end;
+    unsigned long long v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
+    if (lane < 8) gt_c3w8_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
+  }
+#else
+  (void)t_entry; (void)t_loop; (void)t_loop_end; (void)st;
+#endif
 }
 
 template <int IN, int BN, int CB>
@@ -520,5 +564,12 @@ hipError_t launch_conv3w_a8(InMode im, const ConvParams& p, hipStream_t s) {
   }
   return hipErrorNotSupported;
 }
+
+#if GT_C3W8_STAMP
+extern "C" int gt_diag_conv3w_a8_stamps(unsigned long long* out, long n) {   // diagnostic builds only
+  if (n > 512 * 8 * 8) n = 512 * 8 * 8;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c3w8_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // namespace gt
