@@ -114,10 +114,12 @@ int64_t gt_decoder_graph_captures(const gt_decoder* dec);
  * is batch-invariant on its own; across plans results agree to fp32 rounding of the GroupNorm sums. 0 disables;
  * max_b > 16 is rejected (GT_ERR_ARG: the workspace holds the small plan's attention partials up to 16 utterances). */
 int gt_decoder_set_small_batch(gt_decoder* dec, int64_t max_b);
-/* Wide-tile 3x3 convs (default on; env GT_CONV3W=0 at creation turns them off): GT_BF16 throughput-plan calls run the
- * level-1/2 Block convs (model/diffusion.py:52; Cout 64/128/256, Cin % 32 == 0) as one 8-wave workgroup per CU that owns
- * every output channel of a 10- or 20-row x 32-frame tile (csrc/conv3w.hip). Off: the 128-wide conv_kernel tiles. The
- * two agree to fp32 accumulation order (different K order and GroupNorm partition). */
+/* Wide-tile 3x3 convs (default on; env GT_CONV3W=0 at creation turns them off): GT_BF16 / GT_BF16_W8 throughput-plan
+ * calls run the level-1/2 Block convs (model/diffusion.py:52; Cout 64/128/256, Cin % 32 == 0) as one 8-wave workgroup per
+ * CU that owns every output channel of a 10- or 20-row x 32-frame tile (csrc/conv3w.hip); GT_FP8 calls run the same
+ * convs on their fp8-operand twin (csrc/conv3w_a8.hip, same quantization as the conv_kernel A8 tiles; env
+ * GT_CONV3W_A8=0 keeps fp8 on conv_kernel). Off: the 128-wide conv_kernel tiles. The forms agree to fp32 accumulation
+ * order (different K order and GroupNorm partition). */
 int gt_decoder_set_wide_conv(gt_decoder* dec, int on);
 
 /* Batches of any size: a compute call runs the batch in chunks of at most
