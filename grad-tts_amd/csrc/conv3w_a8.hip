@@ -35,9 +35,12 @@ constexpr int NTHR = 512, NW = 8, RB = 5, PCOL = 34;
 constexpr int NPH = 5;            // phases per 32-channel chunk (tap pairs)
 constexpr int S = 6, D = S - 1;   // weight ring slots, DMA distance (D <= NPH: DMA(k + D) exists iff chunk c+1 does or t + D < NPH)
 // B fragment prefetch distance in steps (ring of RB by step: chunk-periodic), and phases from an item's load to its
-// transform: 2 / 2 spilled 5-230 registers (the 160 accumulators leave about 90)
-constexpr int PF = 1;
+// transform (2 / 2 spilled 5-230 registers: the 160 accumulators leave about 90). Two steps ahead only where it fits and
+// paid: the 256-wide mask / plain forms (level-2 mask conv 53.2 -> 52.2 us, same box; the 64/128-wide CB = 1 forms did
+// not move, the GroupNorm forms' split transform needs steps 0-3 before the first prefetch read)
 constexpr int LAT = 1;
+template <int IN, int BN, int CB>
+constexpr int pf() { return IN != IN_GN && BN == 256 ? 2 : 1; }
 
 template <int BN, int CB>
 struct Cfg {
@@ -67,7 +70,6 @@ struct Cfg {
   static_assert(WN * WM == NW && WN >= 1, "wave grid");
   static_assert(PIECES * 1024 == SLOT, "whole DMA pieces");
   static_assert(NPT >= 1 && NPT <= 3 && TP(0) >= 1, "items transformed in phases 1..3");
-  static_assert(PF >= 1 && PF < RB, "prefetch distance");
   static_assert(NTHR / 64 * 32 * NPT >= PP, "item map covers the patch");
   static_assert(SMEM <= 160 * 1024, "LDS budget: one workgroup per CU");
   static_assert(PBUF >= 272 * 8, "s_red aliases patch buffer 1");
@@ -307,7 +309,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   };
   // LDS reads of the next phase issued before its barrier: its first PF steps' B (2 x b128 + 1 byte each) and its A
   // (pair 4's second tap is its first again: one b128 fewer, rd_b)
-  constexpr auto npre = [](int pr) { return c3w8::PF * (pr == 4 ? 2 : 3) + 2 * CB; };
+  constexpr int PF = c3w8::pf<IN, BN, CB>();
+  static_assert(PF >= 1 && PF < RB, "prefetch distance");
+  constexpr auto npre = [](int pr) { return PF * (pr == 4 ? 2 : 3) + 2 * CB; };
 
   // ---- fragments. A (weights): plane q = 2u + h of the slot, row; B (patch): plane h, position; scale byte of tap t
   // (h = 0) or t' (h = 1): t' - t = +1 column, except pair 1 (tap 3 opens the next row) and pair 4 (t' = t = 8)
@@ -369,7 +373,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   asm volatile("" : "+v"(scale_one));
   asm volatile("s_nop 7" ::: "memory");   // VALU writes -> MFMA operand reads (mfma8s pads nothing)
 
-  constexpr int PF = c3w8::PF;
   v8i_t fa[CB];
   FragP8 fb[RB];   // B ring by step index (a phase is RB steps, so step i of every phase uses entry i)
 #pragma unroll
