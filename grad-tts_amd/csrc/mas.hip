@@ -6,188 +6,204 @@
 //              V[x, y] = ((v_prev > v_cur) ? v_prev : v_cur) + V[x, y]          (one fp32 max + one fp32 add)
 //   backtrack idx = t_x-1; for y = t_y-1..0: P[idx, y] = 1;
 //              if idx != 0 && (idx == y || V[idx, y-1] < V[idx-1, y-1]) idx -= 1
-// Column y depends only on column y-1, so the DP runs column-parallel: ONE wave per utterance, lane L
-// owns rows x = L*XPL .. L*XPL+XPL-1 in registers; the only cross-lane traffic per column is the
-// neighbour's last row (one shuffle). The backtrack needs only the comparison V[x,y-1] < V[x-1,y-1] that
-// the forward already evaluates for in-band cells, so the forward stores one "step down" bit per cell
-// (in LDS, XPL bits per lane per column) instead of the fp32 DP table. Both steps use exactly the
-// reference's fp32 operations in the same order -> bit-identical paths.
-// The {0,1} path tensor is then written by a separate full-bandwidth kernel from the per-column row
-// index (t_y ints per utterance).
+// Column y depends only on column y-1, so the DP runs column-parallel. One workgroup per utterance, NW waves
+// (one per SIMD up to 4, two per SIMD at 8), wave w owning rows [w*64*XPL, (w+1)*64*XPL), lane L rows
+// w*64*XPL + L*XPL + i in registers. Inside a wave the neighbour row arrives by a DPP wave_shr:1; across waves the
+// schedule is skewed: the columns go in blocks of 32 and wave w runs block j in step j + w, one workgroup barrier
+// per step, so the row above a wave's first row (the previous wave's last row, 32 columns of it) was written to LDS
+// one step earlier. The backtrack needs only the comparison V[x,y-1] < V[x-1,y-1], which the forward's max already
+// evaluates (for x != y, x != 0 it IS v_prev > v_cur), so the forward keeps one "step down" bit per cell -- shifted
+// into a per-row register word, one LDS word per row and 32-column block -- instead of the fp32 DP table; row 0
+// clears it, and the backtrack adds the diagonal's forced step. Both steps use exactly the reference's fp32 operations in the same order
+// -> bit-identical paths. Cells outside the band are updated too (unconditionally): in-band cells read only in-band
+// cells of the previous column (or the NEG / 0 constants), and the backtrack visits only in-band cells.
+// The value columns stream through a ring of register blocks, several 32-column blocks ahead of the column being
+// computed (one wave per utterance with a single block ahead had left the DP waiting on HBM latency), by temporal
+// loads (nontemporal ones, each 16 B of a different 128-B line per lane, re-fetched every line eight times), and the
+// {0,1} path tensor is written by a separate full-bandwidth kernel from the per-column row index.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 
 #include "gradtts.h"
 
+#define GT_MAS_DEV __device__ __forceinline__
+
 namespace {
 
-// MODE bits (A/B via GT_MAS_MODE; default 53 = 1|4|16|32, measured 1.9x (b=32, 200x800) and 2.2x (ragged
-// training batch) faster than MODE 0, the first version, on the same box; bench_mas.py):
-//   1  the neighbour row arrives by DPP wave_shr:1 (a VALU op) instead of ds_bpermute
-//   2  deeper register prefetch of the value columns (measured slower; kept for A/B only)
-//   4  windowed backtrack: 64 columns per LDS round trip instead of one dependent LDS read per column
-//  16  lean row update: every row updated unconditionally, one compare serves the max and the step bit
-//  32  16-byte value loads (4 columns of a row per load instruction)
-template <int XPL, int YCAP, int MODE>
-__global__ __launch_bounds__(64) void mas_dp_kernel(const float* __restrict__ values, const int32_t* t_xs,
-                                                    const int32_t* t_ys, int tx_max, int ty_max, float neg,
-                                                    int32_t* __restrict__ pidx) {
-  constexpr int kYB = (MODE & 32) ? (XPL >= 8 ? 4 : 8) : (MODE & 2) ? (XPL >= 16 ? 4 : (XPL >= 8 ? 8 : 16))
-                           : (XPL >= 16 ? 2 : (XPL >= 8 ? 4 : 8));   // value columns prefetched per block
-  __shared__ uint16_t bits[YCAP][64];
-  const int b = blockIdx.x, L = threadIdx.x;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kMasCols = 32;             // columns per block (= bits per LDS word)
+constexpr int kMasMaxBlk = 1024 / kMasCols;
+constexpr int kMasMaxRows = 1024;
+constexpr int kMasMaxWaves = 8;
+
+// value blocks held in registers per lane (the block being computed + RING-1 in flight)
+template <int XPL> struct MasRing { static constexpr int n = XPL == 1 ? 4 : 2; };
+
+// Value loads: 16-byte buffer loads, 8 per row and 32-column block. Rows at or past t_x, and blocks past the
+// utterance's last, carry an offset outside the buffer (num_records = the utterance's grid), so the range check
+// returns zeros without touching memory; a grid row's last block reads past the row end into the next row (columns
+// >= t_y_max: computed, never read) or out of the buffer (zeros). Every wave issues exactly the same loads in every
+// step, outside any branch, so hipcc's vmcnt bookkeeping sees the ring exactly and waits for a block only when its
+// first value is used (loads inside the compute branch, with an idle path beside it, had merged into vmcnt(0) waits
+// that drained the ring).
+GT_MAS_DEV void mas_ld(f32x4& dst, __amdgpu_buffer_rsrc_t rs, uint32_t voff) {
+  dst = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, 0));
+}
+
+// One 32-column block of one wave. DIAG: the block meets the diagonal x == y inside this wave's rows, where v_cur is
+// NEG (the diagonal's forced step is added by the backtrack).
+template <int XPL, int RING, bool DIAG>
+GT_MAS_DEV void mas_block(float (&V)[XPL], f32x4 (&val)[XPL][kMasCols / 4], const f32x4* bsrc, float& carry,
+                          f32x4* bdst, bool lane63, uint32_t (&wb)[XPL], int r0, int y0, float neg) {
+  int kd[XPL];   // column (within the block) of this lane's diagonal cell, per row
+#pragma unroll
+  for (int i = 0; i < XPL; ++i) kd[i] = r0 + i - y0;
+  // the row above this wave's first row (the previous wave's last row, or NEG for wave 0: x == 0 has v_prev = NEG for
+  // y > 0), 4 columns per LDS read, one read ahead; `old` = its column y-1
+  f32x4 ch = bsrc[0], chn = bsrc[1], bo4;
+  float old = carry;
+#pragma unroll
+  for (int k = 0; k < kMasCols; ++k) {
+    // V[r0-1, y-1] from lane L-1; lane 0 takes `old` (bound_ctrl off: an invalid source lane keeps the old value)
+    const float left = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(V[XPL - 1]),
+                                                                  0x138, 0xf, 0xf, false));
+#pragma unroll
+    for (int i = XPL - 1; i >= 0; --i) {
+      const float v_prev = i > 0 ? V[i - 1] : left;
+      float v_cur = V[i];
+      if constexpr (DIAG) v_cur = kd[i] == k ? neg : v_cur;
+      const bool gt = v_prev > v_cur;
+      V[i] = (gt ? v_prev : v_cur) + val[i][k >> 2][k & 3];
+      wb[i] = wb[i] + wb[i] + (gt ? 1u : 0u);   // bit (31 - k) <-> column y0 + k
+      asm volatile("" : "+v"(wb[i]));   // fold the bit in now: hipcc otherwise keeps 32 compare masks alive in SGPRs
+    }
+    bo4[k % 4] = V[XPL - 1];
+    old = ch[k % 4];
+    if (k % 4 == 3) {
+      if (lane63) bdst[k / 4] = bo4;   // this wave's last row, for the next wave (the last wave's goes unread)
+      ch = chn;
+      if (k / 4 + 2 < kMasCols / 4) chn = bsrc[k / 4 + 2];
+    }
+  }
+  carry = old;
+}
+
+// One backtrack column: SCC = bit f of the column's word (step down from row idx0 - f); D |= BIT if so; f += SCC.
+template <uint32_t BIT>
+GT_MAS_DEV void mas_walk_step(uint32_t& f, uint32_t& D, uint32_t cw) {
+  uint32_t t;
+  asm volatile("s_bitcmp1_b32 %3, %0\n\ts_cselect_b32 %2, %4, 0\n\ts_addc_u32 %0, %0, 0\n\ts_or_b32 %1, %1, %2"
+               : "+s"(f), "+s"(D), "=&s"(t) : "s"(cw), "n"(BIT) : "scc");
+}
+
+// Columns K and K-1 (one ballot), then the pair below, down to column 0.
+template <int K>
+GT_MAS_DEV void mas_walk(uint32_t& f, uint32_t& D, uint32_t word) {
+  if constexpr (K > 0) {
+    const uint64_t cw = __builtin_amdgcn_ballot_w64(((word >> (31 - K)) & 1u) != 0u);
+    mas_walk_step<(1u << K)>(f, D, (uint32_t)cw);
+    mas_walk_step<(1u << (K - 1))>(f, D, (uint32_t)(cw >> 32));
+    mas_walk<K - 2>(f, D, word);
+  }
+}
+
+template <int XPL>
+__global__ __launch_bounds__(kMasMaxWaves * 64) void mas_dp_kernel(const float* __restrict__ values,
+                                                                  const int32_t* t_xs, const int32_t* t_ys,
+                                                                  int tx_max, int ty_max, float neg,
+                                                                  int32_t* __restrict__ pidx) {
+  constexpr int RING = MasRing<XPL>::n;
+  constexpr int RW = 64 * XPL;                                  // rows per wave
+  __shared__ uint32_t bits[kMasMaxBlk * kMasMaxRows];           // [block][row]: step-down bits, bit 31-k = column 32j+k
+  __shared__ __attribute__((aligned(16))) float bnd[kMasMaxWaves][2][kMasCols];   // wave w's last row, by block parity
+  __shared__ f32x4 bneg[kMasCols / 4];   // wave 0's "row above": x == 0 has v_prev = NEG for y > 0
+  const int nw = blockDim.x >> 6, RP = nw * RW;
+  // w through readfirstlane: hipcc then knows it is wave-uniform, and the per-wave conditions (active, diagonal block,
+  // boundary writer) become scalar branches, not exec-masked both-sides code
+  const int b = blockIdx.x, L = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tx = t_xs[b], ty = t_ys[b];
   tx = tx > tx_max ? tx_max : tx;
   ty = ty > ty_max ? ty_max : ty;
   int32_t* P = pidx + (long)b * ty_max;
-  if (tx <= 0 || ty <= 0) {
-    for (int y = L; y < ty_max; y += 64) P[y] = -1;
-    return;
-  }
+  for (int y = (ty > 0 ? ty : 0) + (int)threadIdx.x; y < ty_max; y += blockDim.x) P[y] = -1;
+  if (tx <= 0 || ty <= 0) return;   // uniform over the workgroup: no barrier has run
+  if (threadIdx.x < kMasCols / 4) bneg[threadIdx.x] = f32x4{neg, neg, neg, neg};   // read by wave 0 only
   const float* V0 = values + (long)b * tx_max * ty_max;
-  float V[XPL];
-  float cur[XPL][kYB], nxt[XPL][kYB];
-#pragma unroll
-  for (int i = 0; i < XPL; ++i) V[i] = 0.f;
+  const int nblk = (ty + kMasCols - 1) / kMasCols;
+  const int r0 = w * RW + L * XPL;
 
-  // Unconditional loads at clamped indices (rows >= tx_max read the last row, columns >= ty the last
-  // column): those values never enter the band, so no per-load branch is needed; 32-bit offsets from the
-  // utterance's (uniform) grid base.
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)V0, (short)0, (int)((uint32_t)tx_max * ty_max * 4u), 0x00020000);
+  constexpr uint32_t kOut = 0x80000000u;   // an offset past any grid (at most 1024 x 1024 x 4 B)
   uint32_t roff[XPL];
 #pragma unroll
-  for (int i = 0; i < XPL; ++i) {
-    const int x = L * XPL + i;
-    roff[i] = (uint32_t)((x < tx_max ? x : tx_max - 1) * ty_max) * 4u;   // bytes
-  }
-  auto load_block = [&](float (&dst)[XPL][kYB], int y0) {
-    if constexpr ((MODE & 32) != 0) {
-      // 16-byte loads of 4 consecutive columns per row (rows are only 4-byte aligned: global loads need dword
-      // alignment only). The last block of a grid falls back to clamped dword loads (uniform branch), so no
-      // load reaches past the row end.
-      if (y0 + kYB <= ty_max) {
-        typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  for (int i = 0; i < XPL; ++i) roff[i] = r0 + i < tx ? (uint32_t)((r0 + i) * ty_max) * 4u : kOut;
+  auto boff = [&](int j) { return j < nblk ? (uint32_t)(j * kMasCols) * 4u : kOut; };
+  f32x4 vb[RING][XPL][kMasCols / 4];
 #pragma unroll
-        for (int q = 0; q < kYB / 4; ++q)
+  for (int s = 0; s < RING - 1; ++s)
 #pragma unroll
-          for (int i = 0; i < XPL; ++i) {
-            const f4u v = __builtin_nontemporal_load((const f4u*)((const char*)V0 + (roff[i] + (uint32_t)(y0 + 4 * q) * 4u)));
-            dst[i][4 * q] = v.x; dst[i][4 * q + 1] = v.y; dst[i][4 * q + 2] = v.z; dst[i][4 * q + 3] = v.w;
-          }
-        return;
-      }
-    }
+    for (int q = 0; q < kMasCols / 4; ++q)
 #pragma unroll
-    for (int k = 0; k < kYB; ++k) {
-      const uint32_t y4 = (uint32_t)(y0 + k < ty ? y0 + k : ty - 1) * 4u;
+      for (int i = 0; i < XPL; ++i) mas_ld(vb[s][i][q], rs, roff[i] + boff(s) + 16u * q);
+  float V[XPL];
 #pragma unroll
-      for (int i = 0; i < XPL; ++i)
-        dst[i][k] = __builtin_nontemporal_load((const float*)((const char*)V0 + (roff[i] + y4)));
-    }
-  };
-  load_block(cur, 0);
-  for (int y0 = 0; y0 < ty; y0 += kYB) {
-    if (y0 + kYB < ty) load_block(nxt, y0 + kYB);
+  for (int i = 0; i < XPL; ++i) V[i] = 0.f;
+  float carry = 0.f;   // row above, column 32j - 1 (column -1: the reference's y == 0 constant 0 for row 0)
+  for (int i = 0; i < w; ++i) __syncthreads();   // skew: wave w starts block 0 in step w
+  for (int j0 = 0; j0 < nblk; j0 += RING) {
 #pragma unroll
-    for (int k = 0; k < kYB; ++k) {
-      const int y = y0 + k;
-      if (y < ty) {   // wave-uniform
-        // V[L*XPL-1, y-1] from lane L-1 (lane 0's value is never used: its x = 0 row takes the constant)
-        const float left = (MODE & 1) ? __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(V[XPL - 1]), 0x138,
-                                                                             0xf, 0xf, false))
-                                : __shfl_up(V[XPL - 1], 1);
-        uint32_t w = 0;
-        if constexpr ((MODE & 16) != 0) {
-          // Lean update. Cells in the band (lo <= x < min(tx, y+1), lo = tx + y - ty) read only in-band cells
-          // of column y-1 (or the NEG / 0 constants), and the backtrack visits only in-band cells, so every
-          // row is updated unconditionally: out-of-band rows hold values nothing reads. For x != y, x != 0
-          // the backtrack's compare V[x,y-1] < V[x-1,y-1] is the max's own v_prev > v_cur, so one compare
-          // serves both; x == y forces the step (and takes NEG as v_cur), x == 0 never steps.
-          const int dy = y - L * XPL;   // x == y  <=>  i == dy
+    for (int s = 0; s < RING; ++s) {
+      const int j = j0 + s;
+      // the next ring block's loads, in one burst outside every branch (issued inside the column loop, the register
+      // allocator reused the slot's registers around them and hipcc's vmcnt waits drained the ring)
 #pragma unroll
-          for (int i = XPL - 1; i >= 0; --i) {
-            const bool diag = dy == i;
-            const float v_cur = diag ? neg : V[i];
-            float v_prev = (i > 0) ? V[i - 1] : left;
-            if (i == 0) v_prev = (L == 0) ? (y == 0 ? 0.f : neg) : v_prev;
-            const bool gt = v_prev > v_cur;
-            V[i] = (gt ? v_prev : v_cur) + cur[i][k];
-            const bool down = (i > 0 || L != 0) && (diag || gt);
-            w |= (down ? 1u : 0u) << i;
-          }
-          bits[y][L] = (uint16_t)w;
-          continue;
+      for (int q = 0; q < kMasCols / 4; ++q)
+#pragma unroll
+        for (int i = 0; i < XPL; ++i) mas_ld(vb[(s + RING - 1) % RING][i][q], rs, roff[i] + boff(j + RING - 1) + 16u * q);
+      if (j < nblk) {   // workgroup-uniform
+        if (w * RW < tx) {   // wave-uniform: a wave whose rows all lie past t_x only keeps the barrier count
+          uint32_t wb[XPL];
+#pragma unroll
+          for (int i = 0; i < XPL; ++i) wb[i] = 0u;
+          const int y0 = j * kMasCols;
+          f32x4* bdst = (f32x4*)bnd[w][j & 1];
+          const f32x4* bsrc = w > 0 ? (const f32x4*)bnd[w - 1][j & 1] : bneg;
+          if (y0 < w * RW + RW && y0 + kMasCols > w * RW)
+            mas_block<XPL, RING, true>(V, vb[s], bsrc, carry, bdst, L == 63, wb, r0, y0, neg);
+          else
+            mas_block<XPL, RING, false>(V, vb[s], bsrc, carry, bdst, L == 63, wb, r0, y0, neg);
+#pragma unroll
+          for (int i = 0; i < XPL; ++i) bits[j * RP + r0 + i] = r0 + i == 0 ? 0u : wb[i];   // row 0 never steps
         }
-        const int lo = tx + y - ty;                     // band: lo <= x < min(tx, y+1)
-        const int hi = min(tx, y + 1);
-#pragma unroll
-        for (int i = XPL - 1; i >= 0; --i) {
-          const int x = L * XPL + i;
-          const float vc_real = V[i];
-          const float vp_real = (i > 0) ? V[i - 1] : left;
-          const float v_cur = (x == y) ? neg : vc_real;
-          const float v_prev = (x == 0) ? (y == 0 ? 0.f : neg) : vp_real;
-          const float mx = (v_prev > v_cur) ? v_prev : v_cur;
-          const bool in_band = (x >= lo) && (x < hi);
-          const float val = cur[i][k];
-          V[i] = in_band ? (mx + val) : val;
-          const bool down = in_band && (x != 0) && ((x == y) || (vc_real < vp_real));
-          w |= (down ? 1u : 0u) << i;
-        }
-        bits[y][L] = (uint16_t)w;
+        __syncthreads();
       }
-    }
-#pragma unroll
-    for (int i = 0; i < XPL; ++i)
-#pragma unroll
-      for (int k = 0; k < kYB; ++k) cur[i][k] = nxt[i][k];
-  }
-  __syncthreads();
-  if constexpr ((MODE & 4) != 0) {
-    // Windowed backtrack. Within 64 steps idx falls by at most 63, so for the chunk of columns yc, yc-1, ...,
-    // yc-63 every row visited lies in [idx0-63, idx0]. Lane l gathers the "step down" bits of column yc-l for
-    // exactly those rows into a 64-bit window (parallel LDS reads); the serial walk then reads lane l's
-    // window with v_readlane (scalar registers, no memory latency) and records the falls as a 64-bit mask, from
-    // which every lane recovers its own idx (mbcnt), so the chunk's 64 path entries are one coalesced store.
-    int idx = tx - 1;
-    for (int yc = ty - 1; yc >= 0; yc -= 64) {
-      const int rb = idx - 63;   // window row 0
-      const int y = yc - L;
-      uint64_t win = 0;
-      if (y >= 0) {
-        const int w1 = idx / XPL;
-        for (int lw = (rb > 0 ? rb : 0) / XPL; lw <= w1; ++lw) {
-          const uint64_t w = bits[y][lw];
-          const int rel = lw * XPL - rb;
-          win |= rel >= 0 ? (w << rel) : (w >> (-rel));
-        }
-      }
-      const uint32_t lo = (uint32_t)win, hi = (uint32_t)(win >> 32);
-      const int n = yc + 1 < 64 ? yc + 1 : 64;
-      const int idx0 = idx;
-      uint64_t D = 0;   // bit l: idx fell at step l
-#pragma unroll
-      for (int l = 0; l < 64; ++l) {
-        if (l < n) {
-          const uint64_t sw = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane(lo, l);   // (readlane returns int)
-          const uint64_t d = (sw >> (idx - rb)) & 1u;
-          D |= d << l;
-          idx -= (int)d;
-        }
-      }
-      // lane L's entry = idx0 - (falls before step L) = idx0 - popcount(D below lane L)
-      if (y >= 0) P[y] = idx0 - (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(D >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)D, 0u));
-    }
-  } else if (L == 0) {
-    int idx = tx - 1;
-    for (int y = ty - 1; y >= 0; --y) {
-      P[y] = idx;
-      const uint32_t w = bits[y][idx / XPL];
-      if ((w >> (idx % XPL)) & 1u) idx -= 1;
     }
   }
-  for (int y = ty + L; y < ty_max; y += 64) P[y] = -1;
+  for (int i = w; i < nw - 1; ++i) __syncthreads();
+  if (w != 0) return;
+
+  // Backtrack, 32 columns per LDS round trip. Within a block idx falls by at most 31, so lane l < 32 holds the bits
+  // of row idx0 - l, and lane 32 + l the same word shifted by one column: one ballot gives column k's bits over those
+  // rows (low half) and column k-1's (high half). The walk is scalar: per column, SCC = bit f of the column word,
+  // f += SCC, and the fall recorded in D (s_bitcmp1 / s_cselect / s_addc / s_or).
+  int idx = tx - 1;
+  for (int j = nblk - 1; j >= 0; --j) {
+    const int y0 = j * kMasCols;
+    const int ncol = ty - y0 < kMasCols ? ty - y0 : kMasCols;   // uniform
+    const int row = idx - (L & 31);
+    uint32_t word = row >= 0 ? bits[j * RP + row] : 0u;
+    if (row > 0 && row >= y0 && row < y0 + kMasCols) word |= 1u << (31 - (row - y0));   // x == y: the step is forced
+    if (ncol < kMasCols) word &= ~((1u << (kMasCols - ncol)) - 1u);   // columns >= t_y: no step
+    word = L < 32 ? word : word >> 1;
+    uint32_t f = 0, D = 0;   // falls so far; bit k: idx fell at column y0 + k
+    mas_walk<kMasCols - 1>(f, D, word);
+    // column y0 + L: idx before its step = idx0 - (falls at columns > L)
+    if (L < ncol) P[y0 + L] = idx - (int)__builtin_popcountll((uint64_t)D >> (L + 1));
+    idx -= (int)f;
+  }
 }
 
 // Serial fallback for utterances beyond the register/LDS budget (t_x > 1024 or t_y > 1024): the
@@ -230,14 +246,6 @@ __global__ __launch_bounds__(256) void mas_fill_kernel(const int32_t* __restrict
   for (int y = threadIdx.x; y < ty_max; y += 256) out[y] = (P[y] == x) ? 1 : 0;
 }
 
-int mas_mode() {
-  static const int v = [] {
-    const char* e = getenv("GT_MAS_MODE");
-    return e ? atoi(e) : 53;
-  }();
-  return v;
-}
-
 // ty_max % 4 == 0: 16-byte stores, 4 columns per thread (rows are then 16-byte aligned)
 __global__ __launch_bounds__(256) void mas_fill4_kernel(const int32_t* __restrict__ pidx, int tx_max, int ty_max,
                                                         int32_t* __restrict__ paths) {
@@ -250,21 +258,10 @@ __global__ __launch_bounds__(256) void mas_fill4_kernel(const int32_t* __restric
   }
 }
 
-template <int XPL, int MODE>
-void launch_dp_v(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
-                 int ty_max, float neg, int32_t* pidx, hipStream_t s) {
-  if (ycap <= 256) hipLaunchKernelGGL((mas_dp_kernel<XPL, 256, MODE>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
-  else hipLaunchKernelGGL((mas_dp_kernel<XPL, 1024, MODE>), dim3(b), dim3(64), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
-}
-
 template <int XPL>
-hipError_t launch_dp(int ycap, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
+hipError_t launch_dp(int nw, const float* values, const int32_t* t_xs, const int32_t* t_ys, int b, int tx_max,
                      int ty_max, float neg, int32_t* pidx, hipStream_t s) {
-  switch (mas_mode()) {
-    case 0: launch_dp_v<XPL, 0>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
-    case 21: launch_dp_v<XPL, 21>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
-    default: launch_dp_v<XPL, 53>(ycap, values, t_xs, t_ys, b, tx_max, ty_max, neg, pidx, s); break;
-  }
+  hipLaunchKernelGGL(mas_dp_kernel<XPL>, dim3(b), dim3(64 * nw), 0, s, values, t_xs, t_ys, tx_max, ty_max, neg, pidx);
   return hipGetLastError();
 }
 
@@ -298,12 +295,9 @@ int gt_maximum_path(int32_t* paths, const float* values, const int32_t* t_xs, co
                        max_neg_val, pidx);
     e = hipGetLastError();
   } else {
-    const int xpl = (TX + 63) / 64;
-    if (xpl <= 1) e = launch_dp<1>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
-    else if (xpl <= 2) e = launch_dp<2>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
-    else if (xpl <= 4) e = launch_dp<4>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
-    else if (xpl <= 8) e = launch_dp<8>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
-    else e = launch_dp<16>(TY, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    // one wave per 64 rows up to 512 rows, then two rows per lane (8 waves, 1024 rows)
+    if (TX <= 64 * kMasMaxWaves) e = launch_dp<1>((TX + 63) / 64, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
+    else e = launch_dp<2>((TX + 127) / 128, values, t_xs, t_ys, B, TX, TY, max_neg_val, pidx, s);
   }
   if (e != hipSuccess) return GT_ERR_HIP;
   if (TY % 4 == 0 && ((uintptr_t)paths & 15) == 0) hipLaunchKernelGGL(mas_fill4_kernel, dim3(TX, B), dim3(256), 0, s, pidx, TX, TY, paths);
