@@ -182,10 +182,38 @@ def pmc_traffic(kernel, args, world):
     return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
 
 
+def host_cpus():
+    """(threads to use, host CPU count, CPU model). BASELINE.md §5 runs the restatement on os.cpu_count() threads; a
+    job whose CPU time is capped by its cgroup (cpu.max quota) or pinned to fewer CPUs gets that many instead, since
+    threads beyond the quota only queue behind it."""
+    n = os.cpu_count() or 1
+    usable = n
+    try:
+        usable = min(usable, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                usable = min(usable, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, n, model
+
+
 def cpu_baseline(args, sd):
     """Oracle restatement on the host cores, one Euler step of a bounded sample at the bench T."""
     from oracle import decoder as odec
-    threads = min(16, os.cpu_count() or 1)
+    threads, ncpu, model = host_cpus()
     torch.set_num_threads(threads)
     Bs = args.cpu_sample_batch
     mu, z, mask, spk = synthetic_inputs(99, Bs, args.frames)
@@ -200,6 +228,7 @@ def cpu_baseline(args, sd):
         dt = time.perf_counter() - t0
     frames_per_s = Bs * args.frames / (dt * args.n_timesteps)
     return {"value": frames_per_s, "unit": "mel-frames/s", "cores": threads, "kind": "port",
+            "host_cpus": ncpu, "cpu_model": model, "label": "build CPU restatement",
             "sample": f"oracle/decoder.py (torch CPU fp32), 1 of {args.n_timesteps} Euler steps, B={Bs}, "
                       f"T={args.frames}: {dt:.2f} s, projected x{args.n_timesteps}"}
 

@@ -162,8 +162,8 @@ int gt_forward_diffusion(gt_decoder* dec, const float* x0, const float* mask, co
                          const float* z, int64_t B, int64_t T, float* xt, float* zm, void* stream);
 /* Diffusion.loss_t (diffusion.py:274-281) forward value with the noise passed in: loss[0] (device fp32) =
  * sum((s_theta(xt) sqrt(1 - e^-cum) + z mask)^2) / (sum(mask) * 80), xt = the forward-diffused input (out,
- * [B,80,T]). Deterministic (fixed-order reductions). Parameter gradients are not implemented (the U-Net backward
- * is the next step of §8f row 1). */
+ * [B,80,T]). Deterministic (fixed-order reductions). Forward value only: the parameter gradients are
+ * gt_diffusion_loss_grad's, below. */
 size_t gt_diffusion_loss_workspace_bytes(const gt_decoder* dec, int dtype, int64_t B, int64_t T);
 int gt_diffusion_loss_t(gt_decoder* dec, int dtype, const float* x0, const float* mask, const float* mu,
                         const float* t, const float* z, const float* spk, int64_t B, int64_t T, float* loss,
