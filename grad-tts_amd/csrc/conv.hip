@@ -658,7 +658,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
       // The partials and the counter are accessed as agent-scope relaxed atomics (stores / loads at the device
       // coherence point, past the XCDs' non-coherent L2s; vector memory instructions) and ordered by waiting for the
       // stores' completion before the counter increment: a __threadfence() here (L2 write-back + invalidate per
-      // workgroup) measured slower than not splitting at all.
+      // workgroup) measured slower than not splitting at all. That lowering (sc1 on the partial stores and loads, the
+      // drain and barrier before the increment) is pinned by a CPU audit of the listing: tools/sk_order_audit.py,
+      // tests/test_asm_audit.py.
       constexpr int PW = C::RBW * 2 * 16 * 256;   // floats per (tile, split), [rb][cb][k][thread]
       const long slot = (long)sp_id * ny + ntile;
       float* mine = p.sk_part + (slot * ksplit + split) * PW;

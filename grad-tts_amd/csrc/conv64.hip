@@ -242,7 +242,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       }
       const uint4 o = f_to_item(v, bf16());
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, rs_rb, rbo, 0, 0);   // r0 (unmasked)
-      v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};                 // r0 * m
+      if (__builtin_expect(m != 0.f && m != 1.f, 0)) {   // r0 * m, fractional mask value: the unfused pass's
+        float rv[8];                                     // IN_MASK operand (bf16(r0) * m, rounded to bf16)
+        item_to_f(o, rv, bf16());
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rv[k] *= m;
+        const uint4 om = f_to_item(rv, bf16());
+        v4 = u32x4_t{om.x, om.y, om.z, om.w};
+      } else {
+        v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};   // r0 * m
+      }
     }
     *reinterpret_cast<u32x4_t*>(sR + lds_off) = v4;
   };

@@ -647,7 +647,7 @@ int max_gn_parts(int dt, int64_t T) {
   return m;
 }
 
-Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles, int small) {
+Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles, int small, int sk_target) {
   Layout L{};
   size_t o = 0;
   auto take = [&](size_t bytes) { size_t r = o; o = (o + bytes + 255) & ~size_t(255); return r; };
@@ -673,9 +673,14 @@ Layout layout(int dt, int64_t B, int64_t T, int32_t N, int small_tiles, int smal
   L.spk = take((size_t)B * 80 * 4);
   L.betas = take((size_t)std::max<int32_t>(N, 1) * 4);
   L.step = take(4);
-  if (small && dt) {   // 128-wide 3x3 tiles of levels 1-2 (at most 2 x 128 output channels), up to 4 splits of 8192 floats
-    L.skcnt_n = (long)B * 40 * (((T >> 1) + 63) / 64) * 2;
-    L.skpart_n = L.skcnt_n * 4 * 8192;
+  if (small && dt && sk_target > 0) {
+    // 128-wide 3x3 tiles of levels 1-2 (at most 2 x 128 output channels): one counter per tile; conv_small_ksplit
+    // splits an utterance's tiles only while tiles x splits <= sk_target (and at most 4 ways), so its fp32 partials
+    // (8192 floats per split tile) need B x min(sk_target, 4 x tiles) slabs, not 4 x every tile (Run::conv3_stats
+    // checks each launch against both sizes)
+    const long tiles = 40L * (((T >> 1) + 63) / 64) * 2;
+    L.skcnt_n = (long)B * tiles;
+    L.skpart_n = (long)B * std::min<long>(sk_target, 4 * tiles) * 8192;
     L.skcnt = take((size_t)L.skcnt_n * 4);
     L.skpart = take((size_t)L.skpart_n * 4);
   }
@@ -1289,7 +1294,7 @@ size_t gt_decoder_workspace_bytes(const gt_decoder* d, int dtype, int64_t B, int
   (void)d;
   if (B <= 0 || T <= 0) return 0;
   const int dt = dtype ? 1 : 0;
-  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps, d->small_tiles, small_plan(d, dtype, B)).total + 256;
+  return layout(dt, chunk_b(d, dt, B, T), T, n_timesteps, d->small_tiles, small_plan(d, dtype, B), d->sk_target).total + 256;
 }
 
 static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float* mask, const float* mu,
@@ -1309,7 +1314,7 @@ static int estimator_impl(gt_decoder* d, int dtype, const float* x, const float*
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = (hipStream_t)stream;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, 0, d->small_tiles, R.small);
+    R.L = layout(R.dt, nb, T, 0, d->small_tiles, R.small, d->sk_target);
     // split-K counters start at zero (every launch leaves them zeroed); a kernel node, not a memset, in captures
     if (R.L.skcnt_n) R.chk(launch_fill_f32((float*)(R.ws + R.L.skcnt), R.L.skcnt_n, 0.f, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = x + fo; R.spk_s = nullptr;
@@ -1571,7 +1576,7 @@ int gt_reverse_diffusion(gt_decoder* d, int dtype, const float* z, const float* 
     Run R;
     R.d = d; R.dt = dtype ? 1 : 0; R.wi = dtype; R.B = (int)nb; R.T = (int)T; R.small = small_plan(d, dtype, B); R.s = st;
     R.ws = align_ws(workspace);
-    R.L = layout(R.dt, nb, T, n_timesteps, d->small_tiles, R.small);
+    R.L = layout(R.dt, nb, T, n_timesteps, d->small_tiles, R.small, d->sk_target);
     if (R.L.skcnt_n) R.chk(launch_fill_f32((float*)(R.ws + R.L.skcnt), R.L.skcnt_n, 0.f, R.s));
     R.mask = mask + (size_t)b0 * T; R.mu = mu + fo; R.xt = out + fo; R.spk_s = nullptr;
     float* xt = out + fo;

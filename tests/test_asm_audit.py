@@ -90,3 +90,43 @@ def test_audit_flags_a_wait_only_some_waves_execute(tmp_path):
     ok = FAKE.replace("\ts_cmp_gt_i32", "\ts_waitcnt vmcnt(0)\n\ts_cmp_gt_i32").format(wait="s_nop 0")
     r = _run_audit(ok, tmp_path)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
+
+
+# ---- split-K ordering (tools/sk_order_audit.py): the small plan's split tiles hand fp32 partials between workgroups
+# through relaxed agent-scope atomics; the audit pins the lowering that makes that safe (sc1 stores and loads, the
+# stores drained and the workgroup past a barrier before the counter increment).
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_split_k_handoff_lowering(tmp_path):
+    listing = tmp_path / "conv.s"
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+           "-I", os.path.join(R, "include"), "-I", CSRC, "-Wno-unused-result",
+           "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
+           os.path.join(CSRC, "conv.hip"), "-o", str(listing)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    a = subprocess.run([sys.executable, os.path.join(R, "tools", "sk_order_audit.py"), str(listing)],
+                       capture_output=True, text=True)
+    print(a.stdout[-3000:])
+    assert a.returncode == 0 and a.stdout.strip().endswith("OK"), a.stdout[-3000:]
+
+
+SK_FAKE = """_Z2skv:
+\tglobal_store_dword v[2:3], v4, off {st}
+\t{wait}
+\ts_barrier
+\tglobal_atomic_add v5, v5, v6, s[0:1] sc0
+\ts_waitcnt vmcnt(0)
+\tglobal_load_dword v7, v[2:3], off sc1
+\ts_endpgm
+.Lfunc_end0:
+"""
+
+
+def test_split_k_audit_flags_missing_order(tmp_path):
+    f = tmp_path / "sk.s"
+    for st, wait, good in (("sc1", "s_waitcnt vmcnt(0)", True), ("", "s_waitcnt vmcnt(0)", False),
+                           ("sc1", "s_nop 0", False)):
+        f.write_text(SK_FAKE.format(st=st, wait=wait))
+        r = subprocess.run([sys.executable, os.path.join(R, "tools", "sk_order_audit.py"), str(f)],
+                           capture_output=True, text=True)
+        assert (r.returncode == 0) == good, r.stdout

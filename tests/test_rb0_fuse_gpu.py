@@ -59,3 +59,30 @@ def test_rb0_fused_bit_identical(monkeypatch, n_spks, B, T, lengths, small, dtyp
     for a, b_, name in zip(res[1], res[0], ("estimator", "sampler N=3", "downs.0.0", "downs.0.1.pre1", "downs.0.1")):
         assert torch.isfinite(a).all(), name
         assert torch.equal(a, b_), f"{name}: max |diff| {float((a - b_).abs().max())}"
+
+
+@pytest.mark.parametrize("small,dtype", [(False, torch.bfloat16), (True, torch.bfloat16), (False, "fp8")],
+                         ids=["bf16", "bf16-small", "fp8"])
+def test_rb0_fused_fractional_mask_c_abi(monkeypatch, small, dtype):
+    """A C-ABI caller (no boundary mask check) with a fractional mask: the fused IN_RB0 operand is bf16(r0) * m rounded
+    to bf16 -- the unfused IN_MASK conv's operand -- so both builds still give the same bits (gradtts.h: a consistent
+    result on every kernel path)."""
+    B, T = 3, 132
+    mu, z, mask, _ = synthetic_inputs(38, B, T, lengths=[132, 100, 44])
+    frac = (mask * np.random.default_rng(9).uniform(0.25, 1.0, mask.shape)).astype(np.float32)
+    t = np.linspace(0.9, 0.2, B).astype(np.float32)
+    args = (_cuda(z), _cuda(frac), _cuda(mu), _cuda(t), None)
+    res = {}
+    for fuse in (1, 0):
+        monkeypatch.setenv("GT_RB0_FUSE", str(fuse))
+        dec, _ = make_decoder(1, 17, dtype)
+        _lib.check(_lib.lib().gt_decoder_set_small_batch(dec.estimator._native(), 16 if small else 0),
+                   "gt_decoder_set_small_batch")
+        outs = []
+        for st in ("downs.0.1.pre1", "downs.0.1"):
+            y, pr = probe(dec.estimator, dtype, *args, st, (B, 64, 80, T))
+            outs += [pr.cpu(), y.cpu()]
+        res[fuse] = outs
+    for a, b_, name in zip(res[1], res[0], ("downs.0.1.pre1", "estimator", "downs.0.1", "estimator (2)")):
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, b_), f"{name}: max |diff| {float((a - b_).abs().max())}"
