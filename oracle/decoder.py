@@ -45,6 +45,8 @@ def linear(p, key, x):
 # on fp8 operands (fp8_operand_conv) is quantized by quantize_act_e4m3 before the conv (what csrc/conv.hip's A8 operand
 # load does)
 _ACT_Q = None
+# oracle.emulate.product_storage: the estimator with the library's bf16 / fp8 storage points (test infrastructure)
+_EMU = None
 
 
 def fp8_operand_conv(cin, cout):
@@ -102,7 +104,12 @@ def estimator(p, x, mask, mu, t, spk=None, n_spks=1, pe_scale=1000.0, dim=64, ta
     """``GradLogPEstimator2d.forward`` diffusion.py:174-216. x, mu: [B,80,T]; mask [B,1,T]; t [B].
 
     ``taps`` (optional dict) receives intermediate activations under the stage names the HIP library's
-    probe uses (include/gradtts.h gt_estimator_probe)."""
+    probe uses (include/gradtts.h gt_estimator_probe).
+
+    Inside ``oracle.emulate.product_storage(mode)`` this is the restatement with the HIP library's bf16 / fp8
+    storage points instead (oracle/emulate.py)."""
+    if _EMU is not None:
+        return _EMU(p, x, mask, mu, t, spk, n_spks, pe_scale, dim, taps)
     s = None
     if spk is not None:
         s = F.linear(mish(linear(p, "spk_mlp.0", spk)), p["spk_mlp.2.weight"], p["spk_mlp.2.bias"])

@@ -13,10 +13,13 @@ scale per position and 32 channels). Two kinds of checks:
   an O(1) error here (measured: 2.2-3.3e-3). Each layer check runs on both tile plans: "small" (conv_kernel's A8 tiles,
   what B <= 4 takes) and "wide" (the throughput plan forced at B = 1: conv3w_a8, csrc/conv3w_a8.hip, for the level-1/2
   shapes; the 64 -> 64 conv stays on conv64);
-* end to end: one estimator call cannot be pinned tighter than the quantization's own effect -- GPU and oracle see
-  inputs that differ by bf16 rounding, and every e4m3 rounding decision that flips moves an operand by 2^-4 of
-  itself -- so the gates are relative to that effect: the GPU's distance to the fp8 oracle must stay below the fp8
-  oracle's distance to the fp32 reference, and the GPU's distance to fp32 within 1.3x of it.
+* end to end, against the oracle with the library's storage points (oracle/emulate.py: bf16 activations between
+  kernels, GroupNorm statistics of the fp32 conv outputs, bf16 attention projections, e4m3 operands quantized from the
+  same fp32 values): absolute gates. One call cannot be pinned tighter than the arithmetic's own sensitivity -- a
+  quantized network turns an fp32 summation-order difference into e4m3 rounding flips (a 2^-3 step each) that
+  compound layer by layer -- so each estimator check also reports the emulating oracle's distance to itself summed in
+  fp64 (the floor) and gates the GPU at 1.5x it; the GPU's distance to fp32 stays within 1.3x of what fp8 does to
+  the call.
 Every check prints its achieved error (PARITY lines).
 """
 import numpy as np
@@ -127,8 +130,40 @@ def test_fp8_gn_conv_close_to_oracle_on_gpu_inputs(plan):
         report(f"fp8 layer {key}pre2 (GroupNorm operand, GPU block1 output, {plan} plan)", rel_err(y, ref), 2 * LAYER_TOL)
 
 
+def _floor_conv2d(x, w, b=None, *a, **k):
+    """conv2d summed in fp64: a second realisation of the same arithmetic that differs only in summation order."""
+    return _CONV2D(x.double(), w.double(), None if b is None else b.double(), *a, **k).float()
+
+
+_CONV2D = F.conv2d
+
+
+def _emulated(fn, mode, floor=False):
+    """fn() inside oracle.emulate.product_storage(mode); floor: with the convs summed in fp64 instead of fp32."""
+    from oracle import emulate
+    with torch.no_grad(), emulate.product_storage(mode):
+        if not floor:
+            return fn()
+        emulate.F.conv2d = _floor_conv2d
+        try:
+            return fn()
+        finally:
+            emulate.F.conv2d = _CONV2D
+
+
+# Absolute gates against the oracle with the library's storage points (oracle/emulate.py). A quantized network
+# amplifies rounding differences: an fp32 summation-order difference of 1e-7 flips an e4m3 rounding (a 2^-3 step) of a
+# few operands per layer, and the flips compound, so two realisations of the same fp8 arithmetic that differ only in
+# summation order sit 4-7e-2 apart after one estimator call (oracle vs the same oracle summing in fp64: the "floor"
+# printed beside each check) and 7.7e-3 after the N = 50 sampler. The GPU sits at that floor: the gates are absolute,
+# set just above it, plus 2x the floor measured in the test (a single draw of it scatters by tens of per cent).
+EST_GATE = 1.0e-1
+SAMPLER_GATE = 1.0e-2
+FLOOR_RATIO = 2.0
+
+
 @pytest.mark.parametrize("name", EST)
-def test_fp8_estimator_within_quantization_envelope(name):
+def test_fp8_estimator_vs_emulating_oracle(name):
     from oracle import decoder as odec
     g = load_golden(name)
     n_spks = int(g["n_spks"])
@@ -136,20 +171,23 @@ def test_fp8_estimator_within_quantization_envelope(name):
     spk = g["spk"] if n_spks != 1 else None
     args = [torch.from_numpy(g[k]) for k in ("x", "mask", "mu", "t")]
     spk_t = torch.from_numpy(spk) if spk is not None else None
-    with torch.no_grad():
-        with odec.fp8_activations():
-            ref8 = odec.estimator(odec.fp8_params(sd), *args, spk_t, n_spks).numpy()
+    p8 = odec.fp8_params(sd)
+    run = lambda: odec.estimator(p8, *args, spk_t, n_spks).numpy()
+    ref8 = _emulated(run, "fp8")
+    floor = rel_err(_emulated(run, "fp8", floor=True), ref8)
     ref32 = g["out"]   # the reference's own fp32 output (golden fixture)
     y = dec.estimator(*(a.cuda() for a in args), _cuda(spk) if spk is not None else None).cpu().numpy()
     assert np.isfinite(y).all()
     q = rel_err(ref8, ref32)   # what the fp8 quantization itself does to this call
-    report(f"fp8 estimator {name} vs fp8 oracle", rel_err(y, ref8), q, quant_effect=q)
+    report(f"fp8 estimator {name} vs emulating fp8 oracle", rel_err(y, ref8), EST_GATE, floor=floor, quant_effect=q)
+    report(f"fp8 estimator {name} vs emulating fp8 oracle, in units of its summation-order floor",
+           rel_err(y, ref8) / floor, FLOOR_RATIO)
     report(f"fp8 estimator {name} vs fp32 reference", rel_err(y, ref32), 1.3 * q, quant_effect=q)
 
 
 def test_fp8_sampler_N1000_matches_oracle():
     """Config 5's step count on a small ragged batch (the CPU oracle finishes it in about a minute): over 1000 Euler
-    steps the per-call quantization noise averages out; gate: within the bf16 sampler tolerance (1e-2) of the fp8
+    steps the per-call quantization noise averages out; gate: the absolute sampler gate against the emulating fp8
     oracle, and within the fp8 oracle's own distance to the fp32 oracle x 1.3 + 1e-2."""
     from oracle import decoder as odec
     from gradtts_amd.params import synthetic_inputs
@@ -157,12 +195,11 @@ def test_fp8_sampler_N1000_matches_oracle():
     mu, z, mask, _ = synthetic_inputs(11, 2, 16, lengths=[16, 12])
     torch.set_num_threads(min(16, torch.get_num_threads()))
     args = (torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu))
-    with odec.fp8_activations():
-        ref8 = odec.reverse_diffusion(odec.fp8_params(sd), *args, 1000).numpy()
+    ref8 = _emulated(lambda: odec.reverse_diffusion(odec.fp8_params(sd), *args, 1000).numpy(), "fp8")
     ref32 = odec.reverse_diffusion(odec.to_torch_params(sd), *args, 1000).numpy()
     y = dec(_cuda(z), _cuda(mask), _cuda(mu), 1000).cpu().numpy()
     q = rel_err(ref8, ref32)
-    report("fp8 reverse N=1000 vs fp8 oracle", rel_err(y, ref8), 1e-2, quant_effect=q)
+    report("fp8 reverse N=1000 vs emulating fp8 oracle", rel_err(y, ref8), SAMPLER_GATE, quant_effect=q)
     report("fp8 reverse N=1000 vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
 
 
@@ -170,29 +207,27 @@ def test_fp8_sampler_N1000_matches_oracle():
 def test_fp8_sampler_T64_plus_matches_oracle(B, T, lengths):
     """The A8 sampler on the tile shapes the bench runs: B = 5 takes the throughput plan (4- and 5-row / 128-wide fp8
     tiles at levels 1-2, 64 frames wide), B = 2 the small plan; T >= 64 so every level has full-width tiles (the
-    N = 1000 check above uses T = 16). 50 Euler steps.
-
-    Gate against the fp8 oracle: half the quantization effect q (the fp8 oracle's distance to the fp32 oracle), not the
-    bf16 sampler's absolute 1e-2. The product stores activations in bf16 between kernels and projects attention with
-    bf16 weights; the oracle keeps fp32 there. Each such rounding moves some operands across an e4m3 rounding boundary
-    (a step of 1/8 relative), and over 50 steps these flips, not the arithmetic, set the distance between two fp8
-    realisations of the same sampler -- in units of what fp8 quantization does to the result (q), not of bf16 rounding.
-    Measured: 0.27-0.31 q (profiles/r05b/parity.jsonl); the absolute 1e-2 sat at 0.87-0.99 of its value."""
+    N = 1000 check above uses T = 16). 50 Euler steps, against the oracle with the library's storage points
+    (oracle/emulate.py: bf16 activations between kernels, bf16 attention projections, e4m3 operands quantized from the
+    same fp32 values), absolute gate 1e-2; that oracle's own distance to itself summing in fp64 (7.7e-3 at B = 2,
+    T = 128) is the floor any fp8 realisation of this sampler sits at, measured here too: gate 2x it."""
     from oracle import decoder as odec
     from gradtts_amd.params import synthetic_inputs
     dec, sd = make_decoder(1, 0, FP8)
     mu, z, mask, _ = synthetic_inputs(13, B, T, lengths=lengths)
     torch.set_num_threads(min(16, torch.get_num_threads()))
     args = (torch.from_numpy(z), torch.from_numpy(mask), torch.from_numpy(mu))
+    run = lambda: odec.reverse_diffusion(odec.fp8_params(sd), *args, 50).numpy()
+    ref8 = _emulated(run, "fp8")
+    floor = rel_err(_emulated(run, "fp8", floor=True), ref8)
     with torch.no_grad():
-        with odec.fp8_activations():
-            ref8 = odec.reverse_diffusion(odec.fp8_params(sd), *args, 50).numpy()
         ref32 = odec.reverse_diffusion(odec.to_torch_params(sd), *args, 50).numpy()
     y = dec(_cuda(z), _cuda(mask), _cuda(mu), 50).cpu().numpy()
     q = rel_err(ref8, ref32)
     e8 = rel_err(y, ref8)
-    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle", e8, 0.5 * q, quant_effect=q)
-    report(f"fp8 reverse N=50 B={B} T={T} vs fp8 oracle (absolute 1e-2, reported)", e8, 1e-2, gate=False, quant_effect=q)
+    report(f"fp8 reverse N=50 B={B} T={T} vs emulating fp8 oracle", e8, SAMPLER_GATE, floor=floor, quant_effect=q)
+    report(f"fp8 reverse N=50 B={B} T={T} vs emulating fp8 oracle, in units of its summation-order floor", e8 / floor,
+           FLOOR_RATIO)
     report(f"fp8 reverse N=50 B={B} T={T} vs fp32 oracle", rel_err(y, ref32), 1.3 * q + 1e-2, quant_effect=q)
 
 
