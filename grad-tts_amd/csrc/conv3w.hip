@@ -33,6 +33,7 @@
 #include "kernels.h"
 #include "wimage.h"
 #include "c3w_asm.h"
+#include "stamps.h"
 
 namespace gt {
 
@@ -101,10 +102,13 @@ struct Cfg {
 };
 }  // namespace c3w
 
+// stamps.h counters: cycles in the DMA wait, the phase barrier, the item waits, the item transforms + writes, the whole
+// chunk loop, phases, prologue, epilogue (the last launch of the stamped instantiation wins)
 #if GT_C3W_STAMP
-// [workgroup slot 0..511][wave 0..7][counter 0..7]: cycles in the DMA wait, the phase barrier, the item waits, the item
-// transforms + writes, the whole chunk loop, phases (the last launch of the stamped instantiation wins)
-__device__ unsigned long long gt_c3w_stamps[512 * 8 * 8];
+GT_STAMP_BUFFER(gt_c3w_stamps, gt_diag_conv3w_stamps, 8)
+#define GT_C3W_STAMP_DST gt_c3w_stamps
+#else
+#define GT_C3W_STAMP_DST nullptr
 #endif
 
 // v_mfma_f32_16x16x32_bf16 accumulating in place. hipcc does not tie the builtin's destination to its C operand (a third
@@ -144,9 +148,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int b = bid / n_ft;
   const int f0 = ft * C::TR, t0 = tt * 32;
 
-#if GT_C3W_STAMP
-  const unsigned long long t_entry = __builtin_amdgcn_s_memtime();
-#endif
+  constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
+  Stamps<STAMP> ps;
+  const unsigned long long t_entry = ps.now();
   // v_mfma_f32_16x16x32_bf16 lanes: r = row of A (output channel) / column of B (position) in a 16 x 16 block, g = the
   // 8-channel plane (k group) of both operands
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, g = lane >> 4;
@@ -289,10 +293,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   // top of phase (t = tap, MORE: chunk c+1 exists): retire DMA(k+1). Younger VMEM ops of this wave: the DMAs of phases
   // k+2 .. k+D-1 that exist and the next chunk's items loaded at phases t+1-D .. t-1 of this chunk (issued after the
   // DMA of their phase).
-  constexpr bool STAMP = GT_C3W_STAMP && BN == GT_C3W_STAMP_BN && IN == GT_C3W_STAMP_IN;
   constexpr int NPRE = c3w::PF + C::NCB;   // LDS reads of the next phase: its first PF steps' B and its A (top_wait)
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
   auto top_wait = [&](auto Tc, auto MOREc) {
     constexpr int t = decltype(Tc)::value;
     constexpr bool MORE = decltype(MOREc)::value;
@@ -301,24 +302,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     constexpr int ndma = ndma0 > 0 ? ndma0 : 0;
     // items loaded in phases k + 1 - D .. k - 1 (each issued after the DMA of its phase)
     constexpr int npl = MORE ? n_lp(t + 1 - C::D, t - 1) : 0;
-    const unsigned long long a = stamp();
+    const unsigned long long a = ps.now();
     vm_wait<ndma * PW + npl>();
-    const unsigned long long b = stamp();
+    const unsigned long long b = ps.now();
     // LDS: every access of this wave but its last NPRE (the next phase's first fragments, read at the end of the
     // previous phase; they need no barrier, so their latency stays hidden) has completed -- the reads of the slot the
     // DMA below overwrites and the item writes of the next chunk's patch included (LDS ops complete in order)
     if (GT_C3W_STAMP) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(NPRE) : "memory");
-    if (STAMP) { const unsigned long long e = stamp(); st[0] += b - a; st[1] += e - b; st[5] += 1; }
+    ps.add(0, b - a); ps.add(1, ps.now() - b); ps.add(5, 1);
   };
   // before transforming item j at phase TP(j): younger VMEM ops are the items loaded at phases LP(j)+1 .. TP(j) and the
   // DMAs of those phases (each phase issues its DMA, then its item load, then this wait)
   auto item_wait = [&](auto Jc) {
     constexpr int j = decltype(Jc)::value;
     constexpr int n = n_lp(C::LP(j) + 1, C::TP(j)) + (C::TP(j) - C::LP(j)) * PW;
-    const unsigned long long a = stamp();
+    const unsigned long long a = ps.now();
     vm_wait_dep<n>(preg[j]);
-    if (STAMP) st[2] += stamp() - a;
+    ps.add(2, ps.now() - a);
   };
 
   // ---- fragments (v_mfma_f32_16x16x32_bf16: one 32-channel phase = one k of 32). A (weights): slot + plane g x BN +
@@ -459,10 +460,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         // partner's MFMAs instead of both leaving the matrix pipe idle at the same step.
         if (MORE && (i == XS0 || i == XS1) && C::jt(t) >= 0) {
           if ((i == XS0 && wv < c3w::NW / 2) || (i == XS1 && wv >= c3w::NW / 2)) {
-            const unsigned long long a = stamp();
+            const unsigned long long a = ps.now();
             put_item(C::jt(t), c + 1, nxt);
             asm volatile("" ::: "memory");   // the item's LDS write stays ahead of the phase-end fragment reads (NPRE)
-            if (STAMP) st[3] += stamp() - a;
+            ps.add(3, ps.now() - a);
           }
         }
       }
@@ -471,13 +472,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   };
   int c = 0;
-  const unsigned long long t_loop = stamp();
+  const unsigned long long t_loop = ps.now();
   for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
   chunk(c, std::false_type{});
-  const unsigned long long t_loop_end = stamp();
-#if GT_C3W_STAMP
-  if (STAMP) { st[4] = t_loop_end - t_loop; st[6] = t_loop - t_entry; }
-#endif
+  const unsigned long long t_loop_end = ps.now();
+  ps.set(4, t_loop_end - t_loop); ps.set(6, t_loop - t_entry);
 
   // ---- epilogue: bias, GroupNorm partial sums, 16-B stores. Lane (r, g) of 16 x 16 block (i, cb) holds channels
   // cb*16 + 4g + 0..3 of position r of block i; one v_permlane16_swap per register of the block pair (2rb, 2rb+1) (the
@@ -560,15 +559,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = S;
     dst[1] = Q;
   }
-#if GT_C3W_STAMP
-  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
-    st[7] = stamp() - t_loop_end;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
-    if (lane < 8) gt_c3w_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
-  }
-#endif
+  ps.set(7, ps.now() - t_loop_end);
+  ps.flush(GT_C3W_STAMP_DST, blockIdx.x & 511, 8, wv, lane);
 }
 
 // (BN, CB) of a conv on an F-row grid with Cout outputs, or 0 if conv3w does not cover it (shared with conv3w_a8.hip)
@@ -626,11 +618,5 @@ hipError_t launch_conv3w(InMode im, const ConvParams& p, hipStream_t s) {
   return hipErrorNotSupported;
 }
 
-#if GT_C3W_STAMP
-extern "C" int gt_diag_conv3w_stamps(unsigned long long* out, long n) {   // diagnostic builds only
-  if (n > 512 * 8 * 8) n = 512 * 8 * 8;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c3w_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 }  // namespace gt

@@ -27,6 +27,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "c3w_asm.h"
+#include "stamps.h"
 
 namespace gt {
 
@@ -96,10 +97,13 @@ GT_DEV void sfor(F&& f) {   // f(integral_constant<I>) ... f(integral_constant<N
 #ifndef GT_C3W8_STAMP_CB
 #define GT_C3W8_STAMP_CB 2
 #endif
+// stamps.h counters: cycles in the DMA wait, the phase barrier, the item waits, the item transforms + writes, the whole
+// chunk loop, phases, prologue, epilogue (the last launch of the stamped instantiation wins)
 #if GT_C3W8_STAMP
-// [workgroup slot 0..511][wave 0..7][counter 0..7]: cycles in the DMA wait, the phase barrier, the item waits, the item
-// transforms + writes, the whole chunk loop, phases, prologue, epilogue (the last launch of the stamped instantiation)
-__device__ unsigned long long gt_c3w8_stamps[512 * 8 * 8];
+GT_STAMP_BUFFER(gt_c3w8_stamps, gt_diag_conv3w_a8_stamps, 8)
+#define GT_C3W8_STAMP_DST gt_c3w8_stamps
+#else
+#define GT_C3W8_STAMP_DST nullptr
 #endif
 
 typedef int v8i_t __attribute__((ext_vector_type(8)));
@@ -147,9 +151,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
   const int b = bid / n_ft;
   const int f0 = ft * C::TR, t0 = tt * 32;
   constexpr bool STAMP = GT_C3W8_STAMP && BN == GT_C3W8_STAMP_BN && IN == GT_C3W8_STAMP_IN && CB == GT_C3W8_STAMP_CB;
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto stamp = [&]() -> unsigned long long { return STAMP ? __builtin_amdgcn_s_memtime() : 0ull; };
-  const unsigned long long t_entry = stamp();
+  Stamps<STAMP> ps;
+  const unsigned long long t_entry = ps.now();
 
   // v_mfma_*_32x32x64 lanes: r = row of A (output channel) / column of B (position), h = the 16-channel plane
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -400,11 +403,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         constexpr int ndma0 = MORE ? D - 2 : ((NPH - t - 2) < (D - 2) ? (NPH - t - 2) : (D - 2));
         constexpr int ndma = ndma0 > 0 ? ndma0 : 0;
         constexpr int npl = MORE ? 2 * n_lp(t + 1 - D, t - 1) : 0;
-        const unsigned long long s0 = stamp();
+        const unsigned long long s0 = ps.now();
         vm_wait<ndma * PW + npl>();
-        const unsigned long long s1 = stamp();
+        const unsigned long long s1 = ps.now();
         asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" :: "n"(npre(t)) : "memory");
-        if (STAMP) { const unsigned long long s2 = stamp(); st[0] += s1 - s0; st[1] += s2 - s1; st[5] += 1; }
+        ps.add(0, s1 - s0); ps.add(1, ps.now() - s1); ps.add(5, 1);
       }
       int nslot = slot + 1;
       nslot = nslot == S ? 0 : nslot;
@@ -422,9 +425,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
         c3w8::sfor<0, C::NPT>([&](auto Jc) {
           constexpr int j = decltype(Jc)::value;
           if constexpr (C::TP(j) == t) {
-            const unsigned long long s0 = stamp();
+            const unsigned long long s0 = ps.now();
             vm_wait_dep2<n_after(j)>(preg[j][0], preg[j][1]);
-            if (STAMP) st[2] += stamp() - s0;
+            ps.add(2, ps.now() - s0);
           }
         });
       }
@@ -450,11 +453,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
               c3w8::sfor<0, C::NPT>([&](auto Jc) {
                 constexpr int j = decltype(Jc)::value;
                 if constexpr (C::TP(j) == t) {
-                  const unsigned long long s0 = stamp();
+                  const unsigned long long s0 = ps.now();
                   gn_part(j, c + 1, i, vit);
                   if (i == 3) finish_item(j, nxt, vit);
                   asm volatile("" ::: "memory");
-                  if (STAMP) st[3] += stamp() - s0;
+                  ps.add(3, ps.now() - s0);
                 }
               });
             }
@@ -462,10 +465,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
             c3w8::sfor<0, C::NPT>([&](auto Jc) {
               constexpr int j = decltype(Jc)::value;
               if constexpr (C::TP(j) == t) {
-                const unsigned long long s0 = stamp();
+                const unsigned long long s0 = ps.now();
                 put_item(j, c + 1, nxt);
                 asm volatile("" ::: "memory");
-                if (STAMP) st[3] += stamp() - s0;
+                ps.add(3, ps.now() - s0);
               }
             });
           }
@@ -476,10 +479,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     });
   };
   int c = 0;
-  const unsigned long long t_loop = stamp();
+  const unsigned long long t_loop = ps.now();
   for (; c + 1 < nchunk; ++c) chunk(c, std::true_type{});
   chunk(c, std::false_type{});
-  const unsigned long long t_loop_end = stamp();
+  const unsigned long long t_loop_end = ps.now();
 
   // ---- epilogue: lane (r, h) of block (rb, cb) holds channels cb*32 + {0-3, 8-11, 16-19, 24-27} + 4h of position r;
   // v_permlane32_swap leaves it 8 consecutive channels per 16-channel half
@@ -564,17 +567,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = Ssum;
     dst[1] = Qsum;
   }
-#if GT_C3W8_STAMP
-  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
-    st[4] = t_loop_end - t_loop; st[6] = t_loop - t_entry; st[7] = stamp() - t_loop_end;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
-    if (lane < 8) gt_c3w8_stamps[((blockIdx.x & 511) * 8 + wv) * 8 + lane] = v;
-  }
-#else
-  (void)t_entry; (void)t_loop; (void)t_loop_end; (void)st;
-#endif
+  ps.set(4, t_loop_end - t_loop); ps.set(6, t_loop - t_entry); ps.set(7, ps.now() - t_loop_end);
+  ps.flush(GT_C3W8_STAMP_DST, blockIdx.x & 511, 8, wv, lane);
 }
 
 template <int IN, int BN, int CB>
@@ -604,11 +598,5 @@ hipError_t launch_conv3w_a8(InMode im, const ConvParams& p, hipStream_t s) {
   return hipErrorNotSupported;
 }
 
-#if GT_C3W8_STAMP
-extern "C" int gt_diag_conv3w_a8_stamps(unsigned long long* out, long n) {   // diagnostic builds only
-  if (n > 512 * 8 * 8) n = 512 * 8 * 8;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c3w8_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 }  // namespace gt

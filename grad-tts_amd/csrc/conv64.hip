@@ -30,6 +30,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
+#include "stamps.h"
 
 namespace gt {
 
@@ -74,10 +75,12 @@ static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
 // work overlaps the other's MFMAs.
 // W8: fp8 weights (GT_BF16_W8 / GT_FP8) -- the image holds the e4m3 values (exact in bf16) and p.wscale the
 // per-output-channel scale: the accumulator starts at bias / scale and the epilogue multiplies by the scale.
+// stamps.h counters (4 waves): prologue, loop, barrier wait, pass MFMA streams, pass epilogues, tiles, segment end, unused
 #if GT_C64_STAMP
-// [workgroup 0..511][wave 0..3][counter 0..7]: prologue, loop, barrier wait, pass MFMA streams, pass epilogues, tiles,
-// segment end, unused
-__device__ unsigned long long gt_c64_stamps[512 * 4 * 8];
+GT_STAMP_BUFFER(gt_c64_stamps, gt_diag_conv64_stamps, 4)
+#define GT_C64_STAMP_DST gt_c64_stamps
+#else
+#define GT_C64_STAMP_DST nullptr
 #endif
 
 template <int IN, bool W8>
@@ -95,10 +98,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
 
-  const bool STAMP = GT_C64_STAMP && IN == GT_C64_STAMP_IN && !W8 && p.Fout == 80;
-  auto stamp = [&]() -> unsigned long long { return (GT_C64_STAMP && STAMP) ? __builtin_amdgcn_s_memtime() : 0ull; };
-  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const unsigned long long t_entry = stamp();
+  Stamps<GT_C64_STAMP && IN == GT_C64_STAMP_IN && !W8> stp(p.Fout == 80);
+  const unsigned long long t_entry = stp.now();
   const int tid = threadIdx.x & 255, lane = tid & 63, r = lane & 31, h = lane >> 5;   // (range known: 256 threads)
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: ring-row addressing stays scalar
   const int cb = wv & 1, rp = wv >> 1;   // output channels cb*32.., mel rows 2 rp, 2 rp + 1 of the tile
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // per-lane GroupNorm partials of the whole segment (group cb*4 + pr*2 + h), accumulated tile by tile, pass by
   // pass in a fixed order; reduced across lanes and waves once, at the end
   float gs[2] = {0.f, 0.f}, gq[2] = {0.f, 0.f};
-  const unsigned long long t_loop = stamp();
+  const unsigned long long t_loop = stp.now();
   // The two workgroups sharing a CU start together, and the arbiter favours the older one's waves: the second-dispatched
   // (upper half of the grid) used to run the last ~20 % of its segment alone. Its waves take priority 1 for the first
   // two thirds of their tiles (measured: level-0 GN conv 112.7 -> 109.4 us, same box; switching at 1/4, 1/3, 1/2 of
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const char* rowp1 = sR + ((sbase + 1) % RING) * ROWB + r * POSB + h * 16;
       const char* rowp2 = sR + ((sbase + 2) % RING) * ROWB + r * POSB + h * 16;
       f32x16 acc;
-      const unsigned long long t_pass = stamp();
+      const unsigned long long t_pass = stp.now();
       // 36 MFMAs (4 chunks x 9 taps), fragment reads software-pipelined PF steps ahead (issued in the natural
       // order the compiler waited on each read right before its MFMA); behind each chunk's MFMAs one staging item of
       // tile k+1's new rows is stored and reloaded for tile k+2 (items spread over the 8 chunk slots of two passes)
@@ -417,12 +418,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       float v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) v[q] = acc[q];
-      unsigned long long t_epi = 0;
-      if (GT_C64_STAMP && STAMP) {   // the MFMA stream retired (the stamp would otherwise read the issue time)
-        asm volatile("" :: "v"(v[15]));
-        t_epi = stamp();
-        st[3] += t_epi - t_pass;
-      }
+      const unsigned long long t_epi = stp.now_after(v[15]);   // the MFMA stream retired
+      stp.add(3, t_epi - t_pass);
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr)
 #pragma unroll
@@ -456,13 +453,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         gs[pr] += valid ? s : 0.f;
         gq[pr] += valid ? q : 0.f;
       }
-      if (GT_C64_STAMP && STAMP) { asm volatile("" :: "v"(gs[1]), "v"(gq[1])); st[4] += stamp() - t_epi; }
+      stp.add(4, stp.now_after(gs[1], gq[1]) - t_epi);
     }
-    const unsigned long long t_bar = stamp();
+    const unsigned long long t_bar = stp.now();
     lds_barrier();   // tile k+1's rows complete
-    if (GT_C64_STAMP && STAMP) { st[2] += stamp() - t_bar; st[5] += 1; }
+    stp.add(2, stp.now() - t_bar); stp.add(5, 1);
   }
-  const unsigned long long t_loop_end = stamp();
+  const unsigned long long t_loop_end = stp.now();
   // segment done: this wave's groups over its positions, then the 2 waves of each channel half -> one slot
 #pragma unroll
   for (int pr = 0; pr < 2; ++pr) {
@@ -486,15 +483,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     dst[0] = S;
     dst[1] = Q;
   }
-#if GT_C64_STAMP
-  if (STAMP) {   // lanes 0..7 store one counter each (vector stores)
-    st[0] = t_loop - t_entry; st[1] = t_loop_end - t_loop; st[6] = stamp() - t_loop_end;
-    unsigned long long v = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v = lane == i ? st[i] : v;
-    if (lane < 8) gt_c64_stamps[((seg & 511) * 4 + wv) * 8 + lane] = v;
-  }
-#endif
+  stp.set(0, t_loop - t_entry); stp.set(1, t_loop_end - t_loop); stp.set(6, stp.now() - t_loop_end);
+  stp.flush(GT_C64_STAMP_DST, seg & 511, 4, wv, lane);
 }
 
 static int cu_count() {
@@ -557,11 +547,5 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-#if GT_C64_STAMP
-extern "C" int gt_diag_conv64_stamps(unsigned long long* out, long n) {   // diagnostic builds only
-  if (n > 512 * 4 * 8) n = 512 * 4 * 8;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gt_c64_stamps), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 }  // namespace gt
