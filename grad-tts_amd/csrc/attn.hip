@@ -359,35 +359,45 @@ __global__ __launch_bounds__(1024) void attn_merge_kernel(const float* part, int
 }
 
 // grid (B, C/64, C/64): M_b = A_b Wq  (C x 128 times 128 x C) with exact-fp32 MFMA (v_mfma_f32_32x32x2_f32),
-// 4 waves x one 32x32 block each, written straight into the packed 1x1 weight image (wimage.h).
+// 4 waves x one 32x32 block each, written straight into the packed 1x1 weight image (wimage.h). Both operands are staged
+// row-major from [row][128] fp32 (A_b rows co, W_q^T rows ci: the decoder packs W_q transposed), each row's 128 k
+// split by parity into two halves of 64 (row stride 132 floats): lane (r, h) of the MFMA then reads k + 2t + h,
+// t = 0..3, as one ds_read_b128 (16 lanes of a read group on 16 distinct 4-bank slots), and the float4 global loads
+// store as two ds_write_b64 of 16 consecutive lanes on 32 consecutive words: no bank conflicts either way (a 129-float
+// transposing stage had 2.67 conflict cycles per LDS instruction).
 template <class A>
-__global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const float* wq, int C, char* Mw, WImg W) {
-  __shared__ float s_a[64][129];    // A rows co0..co0+63, k = 0..127
-  __shared__ float s_q[64][129];    // Wq^T: [ci - ci0][k]
+__global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const float* wqt, int C, char* Mw, WImg W) {
+  constexpr int RS = 132;
+  __shared__ __attribute__((aligned(16))) float s_a[64 * RS];   // A rows co0..co0+63
+  __shared__ __attribute__((aligned(16))) float s_q[64 * RS];   // W_q^T rows ci0..ci0+63
   const int b = blockIdx.x, co0 = blockIdx.y * 64, ci0 = blockIdx.z * 64, tid = threadIdx.x;
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  auto stage = [&](float* dst, const float* src) __attribute__((always_inline)) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int i = tid + 256 * j, rr = i >> 5, k4 = (i & 31) * 4;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(Ain + ((long)b * C + co0 + rr) * 128 + k4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) s_a[rr][k4 + k] = v[k];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int i = tid + 256 * j, k = i >> 4, c4 = (i & 15) * 4;   // coalesced along ci
-    const f32x4 v = *reinterpret_cast<const f32x4*>(wq + (long)k * C + ci0 + c4);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s_q[c4 + c][k] = v[c];
-  }
+    for (int j = 0; j < 8; ++j) {
+      const int i = tid + 256 * j, rr = i >> 5, k4 = (i & 31) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(src + (long)rr * 128 + k4);
+      *reinterpret_cast<f32x2*>(dst + rr * RS + k4 / 2) = f32x2{v.x, v.z};        // even k
+      *reinterpret_cast<f32x2*>(dst + rr * RS + 64 + k4 / 2) = f32x2{v.y, v.w};   // odd k
+    }
+  };
+  stage(s_a, Ain + ((long)b * C + co0) * 128);
+  stage(s_q, wqt + (long)ci0 * 128);
   __syncthreads();
   const int lane = tid & 63, wv = tid >> 6, r = lane & 31, h = lane >> 5;
   const int bm = (wv >> 1) * 32, bn = (wv & 1) * 32;
+  const float* pa = s_a + (bm + r) * RS + h * 64;
+  const float* pq = s_q + (bn + r) * RS + h * 64;
   f32x16 acc;
 #pragma unroll
   for (int k = 0; k < 16; ++k) acc[k] = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < 128; k += 2)   // A[i = lane&31][k + h], B[k + h][j = lane&31]
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(s_a[bm + r][k + h], s_q[bn + r][k + h], acc, 0, 0, 0);
+#pragma unroll 4
+  for (int k = 0; k < 128; k += 8) {   // A[i = lane&31][k + 2t + h], B[k + 2t + h][j = lane&31]
+    const f32x4 a4 = *reinterpret_cast<const f32x4*>(pa + k / 2);
+    const f32x4 q4 = *reinterpret_cast<const f32x4*>(pq + k / 2);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[t], q4[t], acc, 0, 0, 0);
+  }
   char* img = Mw + (long)b * W.total;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
@@ -425,12 +435,12 @@ hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* w
   return hipGetLastError();
 }
 
-hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s) {
+hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wqt, int B, int C, void* Mw, hipStream_t s) {
   if (C % 64 != 0) return hipErrorInvalidValue;
   const WImg W = conv_wimg(act_bf16, 1, C, C);
   const dim3 grid(B, C / 64, C / 64);
-  if (act_bf16) hipLaunchKernelGGL(attn_fold_kernel<bf16>, grid, dim3(256), 0, s, Ain, wq, C, (char*)Mw, W);
-  else hipLaunchKernelGGL(attn_fold_kernel<float>, grid, dim3(256), 0, s, Ain, wq, C, (char*)Mw, W);
+  if (act_bf16) hipLaunchKernelGGL(attn_fold_kernel<bf16>, grid, dim3(256), 0, s, Ain, wqt, C, (char*)Mw, W);
+  else hipLaunchKernelGGL(attn_fold_kernel<float>, grid, dim3(256), 0, s, Ain, wqt, C, (char*)Mw, W);
   return hipGetLastError();
 }
 

@@ -20,9 +20,10 @@
 // (tests/test_attn_down_gpu.py) while the HBM traffic drops from read x + write y + read y + write out to read x (1.27x:
 // the 5 x 65 patch of a 2 x 32 output tile) + write out.
 //
-// LDS patch: C/8 planes (8 channels each) x 5 rows x 68 entries of 16 B, the 65 columns deinterleaved by parity (even
-// columns at entries 0..32, odd ones at 36..67): a stride-2 tap then reads 32 CONSECUTIVE entries (conflict-free
-// ds_read_b128), and the stage-1 item writes (even and odd columns alternating) land 16 banks apart.
+// LDS patch: C/8 planes (8 channels each) x 5 rows x 69 entries of 16 B, the 65 columns deinterleaved by parity (even
+// columns at entries 0..32, odd ones from entry 36 or 37: ad::odd_entry): a stride-2 tap then reads 32 CONSECUTIVE
+// entries (conflict-free ds_read_b128), and the stage-1 item writes (even and odd columns alternating) land 16 banks
+// apart.
 #include "common.h"
 #include "kernels.h"
 #include "wimage.h"
@@ -32,9 +33,15 @@ namespace gt {
 namespace ad {
 constexpr int PROWS = 5, PCOLS = 65, NPOS = PROWS * PCOLS;   // input patch of one 2 x 32 output tile
 constexpr int NPB = (NPOS + 31) / 32;                        // 11 position blocks of 32
-constexpr int ODD = 36, RS = 68;                             // odd-column offset and row stride (entries)
-constexpr int PLANE = PROWS * RS;                            // 340 entries
-template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   // 43,520 B (C = 64)
+// Odd columns of patch row r start at entry odd(r) = 36 + (r & 1). A group of 8 consecutive positions stored by one
+// ds_write_b128 lane group is 4 even and 4 odd columns; their two 16-bank ranges are disjoint when the odd entries
+// start 4 (mod 8) entries after the even ones -- odd(r) = 36 when the group starts at an even column, 37 when it starts
+// at an odd one, which in a 65-column patch enumerated row by row happens exactly in the odd rows (a single offset
+// of 36 left every odd-row group with a 2-way conflict: 0.77 conflict cycles per LDS instruction).
+constexpr int RS = 69;                                       // row stride (entries): odd entries reach 37 + 31 = 68
+GT_DEV int odd_entry(int prow) { return 36 + (prow & 1); }
+constexpr int PLANE = PROWS * RS;                            // 345 entries
+template <int C> constexpr int smem_bytes() { return (C / 8) * PLANE * 16; }   // 44,160 B (C = 64)
 }  // namespace ad
 
 typedef unsigned u32x4a_t __attribute__((ext_vector_type(4)));
@@ -75,7 +82,7 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
     for (int ks = 0; ks < C / 16; ++ks) xf[ks] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + ks * 32, 0, 0);
     m = inside ? mask_at(p.mask, p.T0, b, ti, p.lvl) : 0.f;
-    ent = pos < NPOS ? prow * RS + (pcol & 1) * ODD + (pcol >> 1) : -1;
+    ent = pos < NPOS ? prow * RS + ((pcol & 1) ? odd_entry(prow) : 0) + (pcol >> 1) : -1;
   };
   // the epilogue of one 32 x 32 stage-1 block (channels cb*32.., positions of one block): the accumulator (M_b x), the
   // bias g b_out, the residual (this lane's own x fragments of k-steps 2cb, 2cb+1) -> bf16 y -> LDS (masked)
@@ -169,7 +176,8 @@ __global__ __launch_bounds__(4 * C) __attribute__((amdgpu_waves_per_eu(3))) void
   auto aread = [&](int st) { return wsrc[st * 64]; };   // st = ch * 9 + tap
   auto bread = [&](int st) {
     const int ch = st / 9, tap = st % 9, dr = tap / 3, dc = tap - 3 * dr;
-    const int ent = (2 * orow + dr) * RS + (dc == 1 ? ODD : (dc >> 1)) + r;
+    const int prow = 2 * orow + dr;
+    const int ent = prow * RS + (dc == 1 ? odd_entry(prow) : (dc >> 1)) + r;
     return *reinterpret_cast<const bf16x8*>(smem + ((2 * ch + h) * PLANE + ent) * 16);
   };
   // weight fragments (L2) PFA steps ahead, patch fragments (LDS) PFB steps ahead

@@ -559,8 +559,10 @@ int prepare(gt_decoder* d, int code) {
         pack_fragT(blob, k + ".wfr", w, (int)shp[0], (int)shp[1]);   // the Upsample of attn_up_kernel
     } else if (ends_with(k, "to_qkv.weight")) {
       const int C = (int)shp[1];
-      std::vector<float> q(w.begin(), w.begin() + 128 * C);
-      blob.put(k + ".q", q.data(), q.size() * 4);
+      std::vector<float> qT((size_t)C * 128);   // W_q^T [C][128] for attn_fold (row-major staging like A_b)
+      for (int j = 0; j < 128; ++j)
+        for (int c = 0; c < C; ++c) qT[(size_t)c * 128 + j] = w[(size_t)j * C + c];
+      blob.put(k + ".qT", qT.data(), qT.size() * 4);
       std::vector<float> kv(w.begin() + 128 * C, w.end());   // [256][C], Cpad == C (multiple of 32)
       if (dt) {
         std::vector<uint16_t> hb(kv.size());
@@ -1047,7 +1049,7 @@ struct Run {
                                small ? d->merge_dr_small : 32, s);
     });
     timed(std::string("attn_fold_kernel<") + (dt ? "bf16>" : "float>") + "@" + std::to_string(C), 2.0 * B * C * 128.0 * C, 0.0,
-          [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.q"), B, C, Mw, s); });
+          [&] { return launch_attn_fold(dt, G, Fp(k + "fn.fn.to_qkv.weight.qT"), B, C, Mw, s); });
   }
 
   void attention_out(const std::string& k, int lvl, const void* in, int C, void* out) {   // y = x + M_b x + g b_out

@@ -105,7 +105,7 @@ hipError_t launch_attn_up(const AttnUpParams& p, hipStream_t s);
 // dr: rows d per workgroup, 32 (4 tile groups) or 4 (32 tile groups, 8 workgroups per head: small batches)
 hipError_t launch_attn_merge(const float* part, int B, int ntile, const float* wout, const float* g, int C, float* Aout,
                              int dr, hipStream_t s);
-hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wq, int B, int C, void* Mw, hipStream_t s);
+hipError_t launch_attn_fold(int act_bf16, const float* Ain, const float* wqt, int B, int C, void* Mw, hipStream_t s);   // wqt: W_q^T [C][128]
 
 struct FinalParams {
   const void* pre; const float* part; int nparts; const float* gamma; const float* beta; long count;
