@@ -59,9 +59,30 @@ constexpr int WTAP_B = 2 * NCH * 64 * 16;                 // one tap's fragments
 constexpr int SMEM = RING * ROWB + WLDS_MAX * WTAP_B + (2 * 4 * 64 + 64 + 64 + NW * 8 + 16) * 4 + 272 * 8;
 // taps in registers: 8 (128 VGPRs); 7 for the GroupNorm-input variant, whose operand transform needs the room; 6 for
 // IN_RB0 (the ResnetBlock-output transform plus each in-flight item's input channels)
-constexpr int wreg_of(int in) { return in == IN_RB0 ? 6 : in == IN_GN ? 7 : 8; }
+constexpr int wreg_of(int in) { return in == IN_RB0 ? 6 : (in == IN_GN || in == IN_X0) ? 7 : 8; }
 static_assert(9 - wreg_of(IN_RB0) <= WLDS_MAX && 9 - wreg_of(IN_GN) <= WLDS_MAX, "LDS weight taps");
-static_assert(SMEM <= 80 * 1024, "LDS budget: two workgroups per CU");
+// IN_X0: the U-Net input {mu, x_t} * m as bf16 pairs (one dword per position) in a window ring of XR rows x XC frames
+// (t0 - 2 .. t0 + 33: the 34 patch columns and their 3x3 neighbourhood)
+constexpr int XC = 36, XR = 12, XBYTES = XR * XC * 4;
+constexpr int smem_of(int in) { return in == IN_X0 ? SMEM + XBYTES : SMEM; }
+static_assert(SMEM <= 80 * 1024 && SMEM + XBYTES <= 80 * 1024, "LDS budget: two workgroups per CU");
+
+// The U-Net input conv (Block(2, 64).block[0], diffusion.py:52, 181: 3x3 over {mu, x_t} * m) for 32 positions x 32 output
+// channels as two v_mfma_f32_32x32x16_bf16 over K = taps x 2 channels: lane half h of k-step 0 holds taps (h, 0..2) and
+// (2, h), k-step 1 tap (2, 2) in half 0 (decoder.cpp pack_x0 orders the A fragments a0, a1 the same way). Lane (r, h)
+// supplies the B column of its position: window rows r1 (its row - 1 + h) and r2 (its row + 1), window column c = its
+// frame - (t0 - 2) - 1. Accumulates onto acc (the bias, in accumulator layout): register q = channel acc_row(q, h).
+GT_DEV f32x16 x0_mfma(const uint32_t* sX, int r1, int r2, int c, int h, const bf16x8& a0, const bf16x8& a1, f32x16 acc) {
+  const uint32_t* p1 = sX + r1 * XC + c;
+  const uint32_t* p2 = sX + r2 * XC + c;
+  const u32x4_t b0 = {p1[0], p1[1], p1[2], p2[h]};
+  const uint32_t t8 = p2[2];
+  const u32x4_t b1 = {h ? 0u : t8, 0u, 0u, 0u};
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, __builtin_bit_cast(bf16x8, b0), acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, __builtin_bit_cast(bf16x8, b1), acc, 0, 0, 0);
+}
+// x0 = bf16({mu, x_t} * m) of one position (the unfused input conv's operand rounding), 0 outside the grid
+GT_DEV uint32_t x0_pair(float mu, float xt, float m) { return pack_bf16x2(mu * m, xt * m); }
 }  // namespace c64
 
 // IN: IN_MASK / IN_GN / IN_PLAIN / IN_RB0. Masks from sequence_mask are 0/1: x * m is then a select, decided per item
@@ -86,17 +107,18 @@ GT_STAMP_BUFFER(gt_c64_stamps, gt_diag_conv64_stamps, 4)
 template <int IN, bool W8>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void conv64_kernel(ConvParams p, int L) {
   using namespace c64;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];   // one LDS object
+  __shared__ __attribute__((aligned(16))) char smem[smem_of(IN)];   // one LDS object
   char* const sR = smem;                                     // ring of RING patch rows
   constexpr int WREG = wreg_of(IN);
   char* const sWL = smem + RING * ROWB;                      // [tap - WREG][cb][chunk][lane] LDS-resident A fragments
-  float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB + WLDS_MAX * WTAP_B);   // [scale, shift, tb, unused][64]
+  float* const s_coef = reinterpret_cast<float*>(smem + RING * ROWB + WLDS_MAX * WTAP_B);   // [scale, shift, tb, x0 bias][64]
   float* const s_wsc = s_coef + 2 * 4 * 64;                  // W8: per-output-channel weight scales
   float* const s_bias = s_wsc + 64;                         // the conv bias in accumulator layout, per (cb, h)
   float* const s_sub = s_bias + 64;                         // [wave][(pr, h) group][sum, sq]
   float* const s_mean = s_sub + NW * 8;
   float* const s_rstd = s_mean + 8;
   double* const s_red = reinterpret_cast<double*>(s_rstd + 8);
+  uint32_t* const sX = reinterpret_cast<uint32_t*>(smem + SMEM);   // IN_X0: the {mu, x_t} window ring
 
   Stamps<GT_C64_STAMP && IN == GT_C64_STAMP_IN && !W8> stp(p.Fout == 80);
   const unsigned long long t_entry = stp.now();
@@ -129,11 +151,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     }
   }
   const char* const wlp = sWL + (cb * NCH * 64 + lane) * 16;
+  bf16x8 xa0, xa1;   // IN_X0: the input conv's A fragments of this wave's channel half (k-steps 0, 1)
+  if (IN == IN_X0) {
+    xa0 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 0) * 64 + lane];
+    xa1 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 1) * 64 + lane];
+  }
   // the conv bias in accumulator layout: register q of lane (r, h) is channel cb*32 + acc_row(q, h). Held in registers
-  // across the loop, except for IN_RB0, which needs them for its operand transform: there it is re-read from LDS
-  // (s_bias[(cb * 2 + h) * 16 + q]) at the start of every pass
+  // across the loop, except for IN_RB0 and IN_X0, which need them for their operand transforms: there it is re-read
+  // from LDS (s_bias[(cb * 2 + h) * 16 + q]) at the start of every pass
   f32x16 bias_reg;
-  if (IN == IN_RB0) {
+  if (IN == IN_RB0 || IN == IN_X0) {
     if (tid < 64) {
       const int c = (tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1);
       s_bias[tid] = W8 ? p.bias[c] / p.wscale[c] : p.bias[c];
@@ -157,9 +184,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   // IN_RB0: the U-Net input channels of an item's position (fp32 [B][F][T]; spk per mel row), 0 when out of range
   // (raw buffer loads at 32-bit offsets: out-of-range positions read past the end, zeros)
   const __amdgpu_buffer_rsrc_t rs_mu =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(IN == IN_RB0 ? p.mu : nullptr), (short)0, npos * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)((IN == IN_RB0 || IN == IN_X0) ? p.mu : nullptr), (short)0, npos * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_xt =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(IN == IN_RB0 ? p.xt : nullptr), (short)0, npos * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)((IN == IN_RB0 || IN == IN_X0) ? p.xt : nullptr), (short)0, npos * 4, 0x00020000);
   auto load_in = [&](int frow, int ti, float* xi) {
     const bool ok = frow >= 0 && frow < F && ti >= 0 && ti < T;
     const int q = ok ? ((b * F + frow) * T + ti) * 4 : npos * 4;
@@ -188,7 +215,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (IN == IN_RB0) load_in(frow, ti, xi);
   };
   const bool spk3 = IN == IN_RB0 && p.cin_input == 3;   // IN_RB0: n_spks > 1 (a third U-Net input channel)
-  auto put_item_at = [&](int lds_off, u32x4_t v4, float m, float xi0, float xi1, int frow, int rbo)
+  // (Mish(GN(h)) * m + tb) * m of the 8 channels of group g, m in {0,1} (diffusion.py:57-58, 76), as a bf16 item
+  auto gn_tb_item = [&](float* v, float m, int g) __attribute__((always_inline)) {
+#pragma unroll
+    for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
+      const float* cf = s_coef + g * 8 + hq * 4;
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
+      const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
+      const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[4 * hq + k] = gn_mish_tb_l2(v[4 * hq + k], sc[k], sh[k], tb[k]);
+    }
+    const uint4 o = f_to_item(v, bf16());
+    return m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
+  };
+  // g: the item's 8-channel group (the thread's `sub`)
+  auto put_item_at = [&](int lds_off, u32x4_t v4, float m, float xi0, float xi1, int frow, int rbo, int g)
       __attribute__((always_inline)) {
     if (IN == IN_MASK) {
       if (__builtin_expect(m != 0.f && m != 1.f, 0)) {   // x * m, fractional mask value
@@ -204,24 +246,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     } else if (IN == IN_GN) {   // (Mish(GN(h)) * m + tb) * m, m in {0,1}  (diffusion.py:57-58, 76)
       float v[8];
       item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
-#pragma unroll
-      for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
-        const float* cf = s_coef + sub * 8 + hq * 4;
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
-        const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
-        const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[4 * hq + k] = gn_mish_tb_l2(v[4 * hq + k], sc[k], sh[k], tb[k]);
-      }
-      const uint4 o = f_to_item(v, bf16());
-      v4 = m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};
+      v4 = gn_tb_item(v, m, g);
     } else if (IN == IN_RB0) {   // r0 = Mish(GN(h2)) * m + res_conv(in * m), as gn_mish_kernel<RES = 1>
       float v[8];
       item_to_f(make_uint4(v4[0], v4[1], v4[2], v4[3]), v, bf16());
       const float x0 = xi0 * m, x1 = xi1 * m;
 #pragma unroll
       for (int hq = 0; hq < 2; ++hq) {
-        const float* cf = s_coef + sub * 8 + hq * 4;
+        const float* cf = s_coef + g * 8 + hq * 4;
         float r[4];
         {
           const f32x4 w0 = *reinterpret_cast<const f32x4*>(cf + 128);
@@ -258,7 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   };
   auto put_item = [&](int it, int slot, u32x4_t v4, float m, const float* xi, int frow) __attribute__((always_inline)) {
     const int c = (it >> 3) % PC;
-    put_item_at(slot * ROWB + c * POSB + sub * 16, v4, m, xi[0], xi[1], frow, IN == IN_RB0 ? rb_dst(frow, c) : 0);
+    put_item_at(slot * ROWB + c * POSB + sub * 16, v4, m, xi[0], xi[1], frow, IN == IN_RB0 ? rb_dst(frow, c) : 0, sub);
   };
 
   // GroupNorm scale/shift (and time bias) of the input channels of utterance b (IN_GN): once per segment
@@ -277,8 +309,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     for (int f = tid; f < F; f += NTHR) s_coef[384 + f] = p.cin_input == 3 ? p.spk_s[(long)b * F + f] : 0.f;
     lds_barrier();
   }
-  if (IN == IN_GN) {
+  if (IN == IN_GN || IN == IN_X0) {
     const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
+    if (IN == IN_X0 && tid < 64)   // the input conv's bias in accumulator layout, per (cb, h): the C operand of x0_mfma
+      s_coef[192 + tid] = p.x0b[(tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1)];
     static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
     const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b, tid);
     const float tbv = tid < 64 ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid] : 0.f;
@@ -291,7 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
 
   // ---- prologue: tile 0's 6 patch rows (mel rows 4 ft0 - 1 .. 4 ft0 + 4) into ring slots 0..5
-  {
+  if (IN != IN_X0) {
     u32x4_t cv[CPT];
     float cm[CPT], cx[IN == IN_RB0 ? CPT : 1][3];
 #pragma unroll
@@ -316,7 +350,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   int nrow[PPT], ncol[IN == IN_RB0 ? 1 : PPT], ngo[PPT], nti[IN == IN_RB0 ? PPT : 1];
   float nm[PPT];
 #pragma unroll
-  for (int j = 0; j < PPT; ++j) {
+  for (int j = 0; j < (IN == IN_X0 ? 0 : PPT); ++j) {
     const int it = tid + NTHR * j;
     const bool have = PPT * NTHR == NEW_ITEMS || it < NEW_ITEMS;
     const int c = (it >> 3) % PC, ti = t0 - 1 + c;
@@ -345,11 +379,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const float* xi = pin[IN == IN_RB0 ? j : 0];
       const int col_off = IN == IN_RB0 ? nti[j] * POSB + sub * 16 : ncol[j];
       put_item_at(slot * ROWB + col_off, preg[j], inrow ? nm[j] : 0.f, xi[0], xi[1], frow,
-                  IN == IN_RB0 ? rb_dst(frow, nti[j]) : 0);
+                  IN == IN_RB0 ? rb_dst(frow, nti[j]) : 0, sub);
     }
   };
+  // IN_X0: h1 of patch row i_rel (mel row 4 ft0 - 1 + i_rel, ring slot i_rel % RING) at column c for this wave's 32
+  // channels, from the window (x0 frame row fr in window row (fr - (4 ft0 - 2)) % XR), GroupNorm + Mish + time-bias
+  // transformed straight from the fp32 accumulators (h1 is never stored, so it is never rounded to bf16: the
+  // statistics and the values they normalise are the same fp32 numbers). `valid`: lanes that store.
+  auto h1_block = [&](int i_rel, int c, float mc, bool valid) __attribute__((always_inline)) {
+    const f32x16 bias = *reinterpret_cast<const f32x16*>(s_coef + 192 + (cb * 2 + h) * 16);
+    const f32x16 acc = x0_mfma(sX, (i_rel + h) % XR, (i_rel + 2) % XR, c, h, xa0, xa1, bias);
+    float v[16];
 #pragma unroll
-  for (int j = 0; j < PPT; ++j) issue_new(j, 1);
+    for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)   // lane h: channels cb*32 + 16 pr + 8h + 0..7 (as the epilogue)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]), __float_as_uint(v[8 * pr + 4 + q]),
+                                                         false, false);
+        v[8 * pr + q] = __uint_as_float(sw[0]);
+        v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+      }
+    const int frow = 4 * ft0 - 1 + i_rel;
+    const float m = (frow >= 0 && frow < F) ? mc : 0.f;
+    const int base = (i_rel % RING) * ROWB + c * POSB;
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int g = cb * 4 + 2 * pr + h;
+      const u32x4_t item = gn_tb_item(v + 8 * pr, m, g);
+      if (valid) *reinterpret_cast<u32x4_t*>(sR + base + g * 16) = item;
+    }
+  };
+  // IN_X0 masks of this lane's columns: interior (c = r + 1, frame t0 + r) and halo (c = 0 / 33: frames t0 - 1, t0 + 32)
+  float m_int = 0.f, m_halo = 0.f;
+  // IN_X0 window loads: thread tid < 144 owns window column xc of new row xr (4 rows per tile), frame t0 - 2 + xc
+  const int xr = tid / XC, xc = tid - xr * XC, xt_ = t0 - 2 + xc;
+  float x_mk = 0.f, x_mu = 0.f, x_xt = 0.f;
+  auto x0_issue = [&](int fr) {   // x0 frame row fr of this thread's column (zeros outside the grid)
+    const bool ok = fr >= 0 && fr < F && xt_ >= 0 && xt_ < T;
+    const int q = ok ? ((b * F + fr) * T + xt_) * 4 : npos * 4;
+    x_mu = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_mu, q, 0, 0));
+    x_xt = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_xt, q, 0, 0));
+  };
+  if (IN == IN_X0) {
+    {
+      const int t = t0 + r;
+      m_int = t < T ? mask_at(p.mask, p.T0, b, t, p.lvl_in) : 0.f;
+      const int th = (r & 1) ? t0 + TT : t0 - 1;
+      m_halo = (th >= 0 && th < T) ? mask_at(p.mask, p.T0, b, th, p.lvl_in) : 0.f;
+      x_mk = (xt_ >= 0 && xt_ < T) ? mask_at(p.mask, p.T0, b, xt_, p.lvl_in) : 0.f;
+    }
+    // window rows 0..11 = x0 frame rows 4 ft0 - 2 .. 4 ft0 + 9 (tile 0's rows and tile 1's new rows)
+    float a[2], c2[2], mk[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int it = tid + NTHR * j;
+      const int wr = it / XC, wc = it - wr * XC, fr = 4 * ft0 - 2 + wr, t = t0 - 2 + wc;
+      const bool ok = it < XR * XC && fr >= 0 && fr < F && t >= 0 && t < T;
+      const int q = ok ? ((b * F + fr) * T + t) * 4 : npos * 4;
+      a[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_mu, q, 0, 0));
+      c2[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_xt, q, 0, 0));
+      mk[j] = (t >= 0 && t < T) ? mask_at(p.mask, p.T0, b, t < T ? t : T - 1, p.lvl_in) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int it = tid + NTHR * j;
+      if (it < XR * XC) sX[it] = x0_pair(a[j], c2[j], mk[j]);
+    }
+    lds_barrier();
+    // tile 0's 6 rows: interior rows rp, rp + 2, rp + 4 per wave; the 12 halo positions (row r >> 1) by the rp = 0 waves
+#pragma unroll
+    for (int i = 0; i < 3; ++i) h1_block(rp + 2 * i, r + 1, m_int, true);
+    if (rp == 0) h1_block(r < 12 ? r >> 1 : 5, (r & 1) * (TT + 1), m_halo, r < 12);
+    if (tid < 4 * XC) x0_issue(4 * ft0 + 10 + xr);   // tile 2's new window rows, stored at the end of tile 0
+  } else {
+#pragma unroll
+    for (int j = 0; j < PPT; ++j) issue_new(j, 1);
+  }
   lds_barrier();
 
   // per-lane GroupNorm partials of the whole segment (group cb*4 + pr*2 + h), accumulated tile by tile, pass by
@@ -390,7 +497,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       };
       constexpr int PF = 2, NB = PF + 1, NST = NCH * 9;   // (3, 4, 6 steps ahead: unchanged or spilling)
       // the first MFMA of the pass accumulates onto the conv bias (the C operand: no epilogue adds)
-      const f32x16 bias_acc = IN == IN_RB0 ? *reinterpret_cast<const f32x16*>(s_bias + (cb * 2 + h) * 16) : bias_reg;
+      const f32x16 bias_acc = (IN == IN_RB0 || IN == IN_X0) ? *reinterpret_cast<const f32x16*>(s_bias + (cb * 2 + h) * 16) : bias_reg;
       bf16x8 xb[NB], wb[NB];
 #pragma unroll
       for (int st = 0; st < PF; ++st) { xb[st] = xread(st); wb[st] = wread(st); }
@@ -405,7 +512,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         }
         if (st % 9 == 8) {
           const int j = ps * NCH + st / 9;
-          if (j < PPT) {
+          if (IN == IN_X0) {   // tile k+1's new rows (rel 4k + 6 ..): interior rows 2 rp, 2 rp + 1; halo every other tile
+            if (j == 1) h1_block(4 * k + 6 + 2 * rp, r + 1, m_int, true);
+            if (j == 3 && (k & 1) == rp) h1_block(4 * k + 6 + (r < 8 ? r >> 1 : 3), (r & 1) * (TT + 1), m_halo, r < 8);
+            if (j == 5) h1_block(4 * k + 7 + 2 * rp, r + 1, m_int, true);
+            if (j == 7 && tid < 4 * XC) {   // tile k+2's window rows (rel 4k + 12 + xr), then tile k+3's loads
+              sX[((4 * k + xr) % XR) * XC + xc] = x0_pair(x_mu, x_xt, x_mk);
+              x0_issue(4 * (ft0 + k) + 14 + xr);
+            }
+          } else if (j < PPT) {
             put_new(j, k + 1);
             issue_new(j, k + 2);
           }
@@ -487,6 +602,134 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   stp.flush(GT_C64_STAMP_DST, seg & 511, 4, wv, lane);
 }
 
+// GroupNorm statistics of the U-Net input conv's output h1 (block1 of downs.0.0, diffusion.py:52-58, 181), which the
+// consumer conv64<IN_X0> recomputes instead of reading: one workgroup per utterance x 32-frame column x 20 mel rows,
+// the {mu, x_t} * m window (22 x 36) in LDS, h1 per 32 positions x 32 channels by c64::x0_mfma (the same instructions
+// on the same operands as the consumer, so the statistics are those of the values it transforms), fp32 sums of h1 and
+// h1^2 per 8-channel group over the valid positions in a fixed order, one partial slot per workgroup (common.h
+// layout). Optionally stores bf16(h1) (p.out: the "pre1" probe of the unfused path's storage point).
+namespace x0s {
+constexpr int RG = 20, WR = RG + 2;   // mel rows per workgroup; window rows
+}
+__global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
+  using namespace c64;
+  __shared__ __attribute__((aligned(16))) uint32_t sX[x0s::WR * XC];
+  __shared__ __attribute__((aligned(16))) float s_xb[64];
+  __shared__ float s_sub[4 * 16];   // [wave][group g][h][sum, sq]
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), cb = wv & 1, rsel = wv >> 1;
+  const int F = p.Fout, T = p.Tout, n_tt = (T + 31) / 32, nrg = F / x0s::RG;
+  int wg = blockIdx.x;
+  const int rg = wg % nrg; wg /= nrg;
+  const int tt = wg % n_tt, b = wg / n_tt;
+  const int fr0 = rg * x0s::RG, t0 = tt * 32;
+  const int npos = p.B * F * T;
+  const __amdgpu_buffer_rsrc_t rs_mu = __builtin_amdgcn_make_buffer_rsrc((void*)p.mu, (short)0, npos * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_xt = __builtin_amdgcn_make_buffer_rsrc((void*)p.xt, (short)0, npos * 4, 0x00020000);
+  constexpr int NWIN = x0s::WR * XC, NJ = (NWIN + 255) / 256;
+  float a[NJ], c2[NJ], mk[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {   // window row w = x0 frame row fr0 - 1 + w, column = frame t0 - 2 + column
+    const int it = tid + 256 * j;
+    const int wr = it / XC, wc = it - wr * XC, fr = fr0 - 1 + wr, t = t0 - 2 + wc;
+    const bool ok = it < NWIN && fr >= 0 && fr < F && t >= 0 && t < T;
+    const int q = ok ? ((b * F + fr) * T + t) * 4 : npos * 4;
+    a[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_mu, q, 0, 0));
+    c2[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_xt, q, 0, 0));
+    mk[j] = (t >= 0 && t < T) ? mask_at(p.mask, p.T0, b, t, p.lvl_in) : 0.f;
+  }
+  if (tid < 64) s_xb[tid] = p.x0b[(tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1)];
+  const bf16x8 xa0 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 0) * 64 + lane];
+  const bf16x8 xa1 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 1) * 64 + lane];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int it = tid + 256 * j;
+    if (it < NWIN) sX[it] = x0_pair(a[j], c2[j], mk[j]);
+  }
+  lds_barrier();
+  const f32x16 bias = *reinterpret_cast<const f32x16*>(s_xb + (cb * 2 + h) * 16);
+  const int t = t0 + r;
+  const bool valid = t < T;
+  float gs[4] = {0.f, 0.f, 0.f, 0.f}, gq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+  for (int i = rsel; i < x0s::RG; i += 2) {   // output row fr0 + i (window rows i + h, i + 2), interior column r + 1
+    const f32x16 acc = x0_mfma(sX, i + h, i + 2, r + 1, h, xa0, xa1, bias);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {   // register q = channel cb*32 + acc_row(q, h): group cb*4 + (q >> 2)
+      float s = 0.f, q2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v = acc[4 * g + e];
+        s += v;
+        q2 += v * v;
+        asm volatile("" : "+v"(s), "+v"(q2));   // scalar chains (conv.hip: packed-FP32 op_sel hazard)
+      }
+      gs[g] += valid ? s : 0.f;
+      gq[g] += valid ? q2 : 0.f;
+    }
+    if (p.out) {   // diagnostics: bf16(h1), 8 consecutive channels per lane after the half-wave swap
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = acc[q];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * pr + q]), __float_as_uint(v[8 * pr + 4 + q]),
+                                                           false, false);
+          v[8 * pr + q] = __uint_as_float(sw[0]);
+          v[8 * pr + 4 + q] = __uint_as_float(sw[1]);
+        }
+      if (valid) {
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const uint4 o = f_to_item(v + 8 * pr, bf16());
+          *reinterpret_cast<uint4*>(reinterpret_cast<char*>(p.out) + (((long)(b * F + fr0 + i) * T + t) * 64 +
+                                                                      cb * 32 + 16 * pr + 8 * h) * 2) = o;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float s = half_sum32(gs[g]), q2 = half_sum32(gq[g]);
+    if (r == 0) {
+      s_sub[wv * 16 + (g * 2 + h) * 2 + 0] = s;
+      s_sub[wv * 16 + (g * 2 + h) * 2 + 1] = q2;
+    }
+  }
+  lds_barrier();
+  if (tid < 8) {   // group G = cb*4 + g: fixed-order sum over the two waves of channel half cb and both lane halves
+    const int gcb = tid >> 2, g = tid & 3;
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < 2; ++w2)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const float* q = s_sub + (w2 * 2 + gcb) * 16 + (g * 2 + hh) * 2;
+        S += q[0];
+        Q += q[1];
+      }
+    float* dst = p.out_part + ((long)b * (n_tt * nrg) + tt * nrg + rg) * 16 + tid * 2;
+    dst[0] = S;
+    dst[1] = Q;
+  }
+}
+
+int x0_stats_nparts(int F, int T) { return ((T + 31) / 32) * (F / x0s::RG); }
+
+bool x0_eligible(const ConvParams& p) {
+  return p.cin_input == 2 && p.Cout == 64 && p.Fout == p.Fin && p.Tout == p.Tin && p.Fout % x0s::RG == 0 && p.mu &&
+         p.xt && p.x0w && p.x0b && p.mask && (long)p.B * p.Fout * p.Tout * 128 < (1L << 31);
+}
+
+hipError_t launch_x0_stats(const ConvParams& p, hipStream_t s) {
+  if (!x0_eligible(p) || !p.out_part) return hipErrorInvalidValue;
+  const long nwg = (long)p.B * ((p.Tout + 31) / 32) * (p.Fout / x0s::RG);
+  hipLaunchKernelGGL(x0_stats_kernel, dim3((unsigned)nwg), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 static int cu_count() {
   static int n = [] {
     int dev = 0, v = 0;
@@ -525,6 +768,11 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   const dim3 block(256);
   const bool rb_ok = p.rb_out && p.rb_w && p.rb_b && p.mu && p.xt && p.cin_input >= 2 && p.cin_input <= 3 &&
                      (p.cin_input == 2 || p.spk_s);
+  if (im == IN_X0) {   // bf16 weights only (the fp8 modes keep the input conv's fp8 image: unfused)
+    if (p.wscale || !x0_eligible(p) || !p.gn_part) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv64_kernel<IN_X0, false>), dim3(grid), block, 0, s, p, L);
+    return hipGetLastError();
+  }
   if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)
     if (im == IN_RB0) {
       if (!rb_ok) return hipErrorInvalidValue;

@@ -199,6 +199,10 @@ struct gt_decoder {
   // the first ResnetBlock's output formed by the next block's conv (conv64 IN_RB0) instead of its own pass
   // (rbout_input); GT_RB0_FUSE=0 at creation: the pass
   bool rb0_fuse = true;
+  // the U-Net input conv (downs.0.0's block1, 2 -> 64 channels) recomputed inside the next conv (conv64 IN_X0) from
+  // {mu, x_t}, with a statistics-only pass for its GroupNorm, instead of written and read back (bf16 compute dtype,
+  // single speaker); GT_X0_FUSE=0 at creation: the input conv
+  bool x0_fuse = true;
   // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
   bool attn_us = true;
   // small-batch plan attention: tiles per utterance (GT_ATTN_TILES_SMALL) and the merge's rows per workgroup
@@ -380,6 +384,25 @@ void pack_conva8(Blob& blob, gt_decoder* d, int code, const std::string& key, co
 
 // pack a 64->64 3x3 [Cout][Cin][3][3] weight in conv64's register-fragment order (conv64.hip), bf16:
 // [cb 2][chunk 4][tap 9][lane 64][8 ci]: lane (r, h) = output channel cb*32 + r, input channels 16 chunk + 8h .. +7
+// The U-Net input conv [64][2][3][3] as the A fragments of conv64.hip c64::x0_mfma: [cb][k-step][lane][8] bf16, lane (r, h)
+// = output channel cb*32 + r; element j of k-step 0 is channel j & 1 of tap (h, j >> 1) for j < 6 and of tap (2, h) for
+// j = 6, 7; k-step 1 holds tap (2, 2) in elements 0, 1 of half 0, zeros elsewhere
+void pack_x0(Blob& blob, const std::string& key, const std::vector<float>& w) {
+  std::vector<uint16_t> img(2 * 2 * 64 * 8, 0);
+  for (int cb = 0; cb < 2; ++cb)
+    for (int ks = 0; ks < 2; ++ks)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int r = lane & 31, h = lane >> 5, co = cb * 32 + r, ch = j & 1, t = j >> 1;
+          int dr = -1, dc = -1;
+          if (ks == 0) { dr = t < 3 ? h : 2; dc = t < 3 ? t : h; }
+          else if (h == 0 && t == 0) { dr = 2; dc = 2; }
+          if (dr < 0) continue;
+          img[((cb * 2 + ks) * 64 + lane) * 8 + j] = f2bf(w[((co * 2 + ch) * 3 + dr) * 3 + dc]);
+        }
+  blob.put(key, img.data(), img.size() * 2);
+}
+
 void pack_conv64(Blob& blob, const std::string& key, const std::vector<float>& w) {
   std::vector<uint16_t> img((size_t)2 * 4 * 9 * 64 * 8);
   size_t i = 0;
@@ -553,6 +576,8 @@ int prepare(gt_decoder* d, int code) {
           (shp[0] == 64 || shp[0] == 128))
         pack_frag3x3(blob, k + ".wfr", w, (int)shp[0], (int)shp[1]);   // the Downsample of attn_down_kernel
       if (ends_with(k, "res_conv.weight") && shp[1] <= 3) blob.put(k + ".f32", w.data(), w.size() * 4);   // rbout_input
+      if (code == GT_BF16 && ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 2 && shp[2] == 3 && shp[3] == 3)
+        pack_x0(blob, k + ".x0", w);   // the input conv recomputed by conv64 IN_X0 / x0_stats
     } else if (starts_with(k, "ups.") && ends_with(k, ".3.conv.weight")) {
       pack_conv(blob, d, dt, code, k, w, shp, true);
       if (code == GT_BF16 && shp[0] == 64 && shp[1] == 64)
@@ -640,6 +665,7 @@ int max_gn_parts(int dt, int64_t T) {
     for (int small = 0; small < 2; ++small) {
       if (small && !dt) continue;
       m = std::max(m, conv64_nparts(80 >> l, (int)(T >> l), small));
+      m = std::max(m, x0_stats_nparts(80 >> l, (int)(T >> l)));
       for (int cout : {64, 128, 256}) m = std::max(m, conv3w_nparts(80 >> l, (int)(T >> l), cout));
       for (int cout : {64, 128, 256})
         for (int im : {IN_INPUT, IN_MASK, IN_GN, IN_PLAIN})
@@ -830,6 +856,16 @@ struct Run {
     }
   }
 
+  // downs.0.0 on the fused input-conv path (conv64 IN_X0 + x0_stats): bf16 weights and activations, two input channels
+  bool x0_fused(const std::string& k, int lvl, int cin, int Cout) {
+    if (!(d->x0_fuse && dt && wi == GT_BF16 && conv64_enabled() && cin == 2 && Cout == 64 && Fl(lvl) % 20 == 0 &&
+          d->dp[wi].count(k + "block1.block.0.weight.x0") && d->dp[wi].count(k + "block2.block.0.weight.w64")))
+      return false;
+    ConvParams p = base(lvl, lvl);
+    p.Cin = p.C0 = p.Cin_pad = Cout; p.Cout = Cout; p.cin_input = cin; p.mu = mu; p.xt = xt;
+    p.x0w = W(k + "block1.block.0.weight.x0"); p.x0b = Fp(k + "block1.block.0.bias");
+    return x0_eligible(p) && conv64_eligible(p);
+  }
   void* W(const std::string& k) { return d->dp[wi].at(k); }
   const float* Fp(const std::string& k) { return (const float*)d->dp[wi].at(k); }
   // weight image of a conv: its fp8 scales too when the image is fp8 (GT_BF16_W8, GT_FP8), and the fp8-operand flag
@@ -898,6 +934,37 @@ struct Run {
     float* st2 = stats();
     int np1 = 0, np2 = 0;                         // GroupNorm partial slots written by block1 / block2
     const long count = (long)(Cout / 8) * Fl(lvl) * Tl(lvl);
+    if (input && x0_fused(k, lvl, cin, Cout)) {
+      // block1's output h1 is never written: its GroupNorm statistics come from a statistics-only recompute (x0_stats)
+      // and block2's conv recomputes h1 itself in its operand load (conv64 IN_X0) -- the same MFMA instructions on the
+      // same operands, so the statistics are those of the values it transforms
+      ConvParams p = base(lvl, lvl);
+      p.Cin = cin; p.Cout = Cout; p.cin_input = cin; p.mu = mu; p.xt = xt;
+      p.x0w = W(k + "block1.block.0.weight.x0"); p.x0b = Fp(k + "block1.block.0.bias");
+      p.out_part = st1;
+      p.out = (probe && std::string(probe) == k + "pre1") ? pre1 : nullptr;   // diagnostics: bf16(h1)
+      np1 = x0_stats_nparts(Fl(lvl), Tl(lvl));
+      if (np1 > L.pmax) { chk(hipErrorInvalidValue); return; }
+      const double pos = (double)B * Fl(lvl) * Tl(lvl);
+      timed("x0_stats_kernel@2x64x" + std::to_string(Fl(lvl)), 2.0 * cin * Cout * 9 * pos, pos * (2 * 4.0 + 4.0),
+            [&] { return launch_x0_stats(p, s); });
+      tap(k + "pre1", lvl, pre1, Cout);
+      tap_part(stat_slot - 2);
+      ConvParams q = base(lvl, lvl);
+      q.Cin = Cout; q.Cout = Cout; q.Cin_pad = 64; q.C0 = Cout; q.in0 = nullptr;
+      q.cin_input = cin; q.mu = mu; q.xt = xt; q.x0w = p.x0w; q.x0b = p.x0b;
+      q.gn_part = st1; q.gn_nparts = np1; q.gn_gamma = Fp(k + "block1.block.1.weight"); q.gn_beta = Fp(k + "block1.block.1.bias");
+      q.gn_count = count; q.tb = tb + tb_off; q.tb_bstride = tb_bstride;
+      setw(q, k + "block2.block.0.weight"); q.bias = Fp(k + "block2.block.0.bias");
+      q.w = W(k + "block2.block.0.weight.w64");
+      q.out = pre2; q.out_part = st2;
+      np2 = conv64_nparts(q.Fout, q.Tout, q.small);
+      if (np2 > L.pmax) { chk(hipErrorInvalidValue); return; }
+      timed("conv64_kernel<5>@64x64x" + std::to_string(Fl(lvl)), 2.0 * 64 * 64 * 9 * pos + 2.0 * cin * Cout * 9 * pos,
+            pos * (2 * 4.0 + 4.0 + 128.0) + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(IN_X0, q, s); });
+      tap(k + "pre2", lvl, pre2, Cout);
+      tap_part(stat_slot - 1);
+    } else {
     {   // block1 conv on x*mask
       ConvParams p = base(lvl, lvl);
       p.Cin = cin; p.Cout = Cout; p.Cin_pad = d->cinpad[wi].at(k + "block1.block.0.weight");
@@ -927,6 +994,7 @@ struct Run {
       np2 = conv3_stats(IN_GN, p, k + "block2.block.0.weight");
       tap(k + "pre2", lvl, pre2, Cout);
       tap_part(stat_slot - 1);
+    }
     }
     if (d->index.count(k + "res_conv.weight") && input) {
       // the first block (2-3 input channels): Mish(GN(h2))*m + res_conv(x*m), formed by the next block's conv
@@ -1209,6 +1277,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   if (const char* e = getenv("GT_RB0_FUSE")) d->rb0_fuse = atoi(e) != 0;
+  if (const char* e = getenv("GT_X0_FUSE")) d->x0_fuse = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
   if (const char* e = getenv("GT_SK_TARGET")) d->sk_target = std::max(0, atoi(e));

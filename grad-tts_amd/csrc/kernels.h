@@ -9,7 +9,9 @@
 namespace gt {
 
 // IN_RB0 (conv64 only): the input is the first ResnetBlock's output formed in the operand load (ConvParams::rb_*)
-enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3, IN_RB0 = 4 };
+// IN_X0 (conv64 only): the input is the first ResnetBlock's block1 output h1, recomputed from {mu, x_t} on the MFMA in the
+// operand load (ConvParams::x0w / x0b) and GroupNorm-transformed as IN_GN; its statistics come from launch_x0_stats
+enum InMode { IN_INPUT = 0, IN_MASK = 1, IN_GN = 2, IN_PLAIN = 3, IN_RB0 = 4, IN_X0 = 5 };
 enum OutMode { OUT_STATS = 0, OUT_PLAIN = 1, OUT_RBOUT = 2, OUT_RESID = 3 };
 enum ConvKind { CONV3 = 0, CONV3_S2 = 1, CONV1 = 2, CONVT4 = 3 };
 
@@ -36,6 +38,9 @@ struct ConvParams {
   // its output r0 = Mish(GN(h2))*m + res_conv(x*m) over the U-Net input channels (mu, xt, spk_s; cin_input of them)
   // with rb_w [64][cin] fp32 and rb_b [64]; r0 itself is also written to rb_out ([B][F][T][64] bf16, each position once)
   const float* rb_w; const float* rb_b; void* rb_out;
+  // IN_X0 (conv64) and launch_x0_stats: the U-Net input conv (2 channels -> 64) as MFMA A fragments (decoder.cpp pack_x0)
+  // and its bias
+  const void* x0w; const float* x0b;
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
   const int* stepp;                                   // IN_GN: device step index (tb_at), or null
   // ---- weights
@@ -152,6 +157,13 @@ hipError_t launch_to_nchw(int act_bf16, const void* src, int B, int F, int T, in
 int conv64_nparts(int F, int T, int small);
 bool conv64_eligible(const ConvParams& p);
 hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s);
+// The U-Net input conv's GroupNorm statistics without its output (conv64.hip): h1 = conv3x3({mu, x_t} * m) + b over
+// every position, recomputed on the MFMA exactly as conv64<IN_X0> recomputes it, summed per 8-channel group into
+// x0_stats_nparts slots per utterance (p.out_part); p.out non-null also stores bf16(h1) ([B][F][T][64], diagnostics).
+// Preconditions (x0_eligible): 2 input channels, 64 outputs, F % 20 == 0.
+int x0_stats_nparts(int F, int T);
+bool x0_eligible(const ConvParams& p);
+hipError_t launch_x0_stats(const ConvParams& p, hipStream_t s);
 
 // wide-tile 3x3 conv for the 64/128/256-output convs of levels 1-2, bf16, throughput plan (conv3w.hip): one 8-wave
 // workgroup per CU owns all output channels of a tile; weight image decoder.cpp pack_conv3w (key ".w3w"). GroupNorm

@@ -13,7 +13,9 @@ library rounds, so the GPU can be pinned against it at fp32-summation-order dist
 * every stored activation -- a Block conv's output (csrc/conv3w.hip / conv64.hip / conv.hip epilogues), a ResnetBlock
   output (rbout passes, attn_kv's RB form, conv64 IN_RB0), an attention output (conv_kernel OUT_RESID), a
   Down/Upsample output -- is bf16 (round to nearest even); the GroupNorm statistics of a conv output are those of its
-  fp32 values (the epilogues sum before rounding), applied to the stored bf16 copy;
+  fp32 values (the epilogues sum before rounding), applied to the stored bf16 copy -- except the bf16 mode's
+  single-speaker U-Net input conv, whose output block2's conv recomputes instead of reading (conv64 IN_X0), so its
+  GroupNorm normalises the fp32 values;
 * a bf16 conv's operand is the bf16 rounding of its fp32 operand value (masked input, or (Mish(GN(h)) + tb) * m); an
   fp8-operand conv (GT_FP8, ``decoder.fp8_operand_conv``) quantizes that fp32 value straight to e4m3
   (``decoder.quantize_act_e4m3``: conv3w_a8.hip finish_item / conv.hip store_item_a8);
@@ -84,35 +86,41 @@ def _conv_w(p, key):
     return r16(w)
 
 
-def _gn_stored(y, gamma, beta):
+def _gn_stored(y, gamma, beta, stored=True):
     """GroupNorm(8) of the bf16-stored y with the statistics of the fp32 y (conv epilogue partial sums, reduced in
-    fp64: csrc/common.h gn_reduce)."""
+    fp64: csrc/common.h gn_reduce). stored=False: y is never stored (the U-Net input conv recomputed by its consumer,
+    conv64 IN_X0), so the normalised values are the fp32 ones."""
     B = y.shape[0]
     yg = y.reshape(B, D.GROUPS, -1).double()
     mean = yg.mean(-1)
     var = (yg * yg).mean(-1) - mean * mean
     rstd = 1.0 / torch.sqrt(var + 1e-5)
-    ys = r16(y).reshape(B, D.GROUPS, -1).double()
+    ys = (r16(y) if stored else y).reshape(B, D.GROUPS, -1).double()
     n = ((ys - mean[..., None]) * rstd[..., None]).reshape(y.shape)
     shp = (1, -1, 1, 1)
     return (n * gamma.double().reshape(shp) + beta.double().reshape(shp)).to(y.dtype)
 
 
-def _block(p, key, xop, mask, taps, tap_name, a8):
+def _block(p, key, xop, mask, taps, tap_name, a8, stored=True):
     """``Block`` (diffusion.py:49-58) on the fp32 operand value xop (already masked): bf16 operand or e4m3 (a8); the
-    conv output stored in bf16 (tap), GroupNorm with the fp32 statistics, Mish, mask."""
+    conv output stored in bf16 (tap), GroupNorm with the fp32 statistics, Mish, mask. stored=False: the output is
+    recomputed by its consumer instead of stored (GroupNorm + Mish of the fp32 values; the tap is still bf16, as the
+    library's diagnostic probe writes it)."""
     xin = D.quantize_act_e4m3(xop) if a8 else r16(xop)
     y = F.conv2d(xin, _conv_w(p, key + ".block.0.weight"), p[key + ".block.0.bias"], padding=1)
     if taps is not None and tap_name:
         taps[tap_name] = r16(y)
-    return D.mish(_gn_stored(y, p[key + ".block.1.weight"], p[key + ".block.1.bias"])) * mask
+    return D.mish(_gn_stored(y, p[key + ".block.1.weight"], p[key + ".block.1.bias"], stored)) * mask
 
 
 def _resnet(p, key, x, mask, t_emb, taps, first):
     """``ResnetBlock`` (diffusion.py:61-79); x is stored (bf16) except for the input block (fp32 mu, x_t, spk)."""
     cin, cout = x.shape[1], p[key + ".block1.block.0.weight"].shape[0]
     fp8 = _Cfg.mode == "fp8"
-    h = _block(p, key + ".block1", x * mask, mask, taps, key + ".pre1", fp8 and D.fp8_operand_conv(cin, cout))
+    # the bf16 mode's single-speaker input block recomputes h1 inside block2's conv (decoder.cpp x0_fused): never stored
+    fused_x0 = first and _Cfg.mode == "bf16" and cin == 2 and cout == 64 and x.shape[2] % 20 == 0
+    h = _block(p, key + ".block1", x * mask, mask, taps, key + ".pre1", fp8 and D.fp8_operand_conv(cin, cout),
+               stored=not fused_x0)
     tb = F.linear(D.mish(t_emb), p[key + ".mlp.1.weight"], p[key + ".mlp.1.bias"])
     h = (h + tb.unsqueeze(-1).unsqueeze(-1)) * mask
     h = _block(p, key + ".block2", h, mask, taps, key + ".pre2", fp8 and D.fp8_operand_conv(cout, cout))

@@ -6,7 +6,8 @@ e4m3 operands quantized from the same fp32 values in GT_FP8, the attention's til
 Two kinds of checks:
 
 * bit level, where the two computations still see identical inputs: the U-Net's first stages. The input conv's bf16
-  output must be bit-identical; after it only fp32 summation order and the library's exp2 / rcp forms of Mish and
+  output must be bit-identical but for the rare element whose bf16 rounding the MFMA's summation order flips (the bf16
+  mode recomputes it on the MFMA, conv64.hip IN_X0); after it only fp32 summation order and the library's exp2 / rcp forms of Mish and
   GroupNorm differ, which flip a bf16 rounding for the rare value within ~1e-6 of a rounding boundary: gates on the
   fraction of elements that are not bit-identical and on the rms error.
 * end to end: a bf16 / fp8 network amplifies such flips layer by layer (a bf16 flip moves a value 2^-9, an e4m3 flip
@@ -68,7 +69,9 @@ def _mismatch(a, b):
 
 # (stage, max fraction of elements not bit-identical, max rms relative error)
 FIRST_STAGES = {
-    "bf16": [("downs.0.0.pre1", 0.0, 0.0), ("downs.0.0.pre2", 2e-3, 3e-4), ("downs.0.0", 2e-3, 3e-4)],
+    # (bf16 pre1: the statistics pass's diagnostic copy of the recomputed input conv, conv64.hip x0_stats_kernel -- its
+    # 18 products summed in one MFMA pair, so a rare bf16 rounding differs from the oracle's fp32 conv)
+    "bf16": [("downs.0.0.pre1", 2e-4, 3e-5), ("downs.0.0.pre2", 2e-3, 3e-4), ("downs.0.0", 2e-3, 3e-4)],
     "fp8": [("downs.0.0.pre1", 1e-3, 1e-4), ("downs.0.0.pre2", 1e-2, 1e-3), ("downs.0.0", 1e-2, 1e-3)],
 }
 

@@ -1,0 +1,109 @@
+"""The U-Net input conv recomputed inside the next conv (csrc/conv64.hip IN_X0 + x0_stats_kernel, decoder.cpp resnet).
+
+downs.0.0's block1 conv (3x3 over {mu, x_t} * m, 2 -> 64 channels; model/diffusion.py:52-58, 181) used to write its
+output h1 ([B][80][T][64] bf16, 168 MB at B = 32, T = 512) for block2's conv to read straight back. On the fused path
+(bf16, single speaker) a statistics-only pass recomputes h1 on the MFMA for its GroupNorm sums and block2's conv
+(conv64 IN_X0) recomputes it per staged patch row from an LDS window of {mu, x_t} * m -- the same two MFMAs on the same
+operands in both, so the statistics are those of the values transformed; GroupNorm + Mish + time bias then apply to
+the fp32 h1 (never stored, so never rounded to bf16: oracle/emulate.py models this).
+
+The recompute sums the 18 products of a position in one MFMA k-step pair where the input conv summed them tap by tap,
+so h1 (read back as bf16 through the diagnostic probe) may differ from the unfused h1 in the bf16 rounding of a few
+elements, and the transform sees h1 unrounded: the checks
+bound the fraction of pre1 elements that differ and the size of the difference (one bf16 ulp of the value; near-zero
+values from cancellation may differ by more ulps of their own, so those are bounded against the largest |h1|), and take pre2 and the
+estimator through the bf16 agreement gates. The path must actually run: the test reads the launch list."""
+import ctypes
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+from gpu_util import make_decoder, probe, rel_err, report
+from gradtts_amd import _lib
+from gradtts_amd.params import synthetic_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not gpu_available():
+        pytest.skip("no HIP device")
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _launches(dec, args):
+    """Kernel names ("<kernel>@<shape>") of one estimator call."""
+    L = _lib.lib()
+    h = dec.estimator._native()
+    _lib.check(L.gt_decoder_profile_enable(h, 1), "gt_decoder_profile_enable")
+    dec.estimator(*args)
+    torch.cuda.synchronize()
+    buf = ctypes.create_string_buffer(1 << 20)
+    _lib.check(L.gt_decoder_profile_read(h, buf, len(buf)), "gt_decoder_profile_read")
+    _lib.check(L.gt_decoder_profile_enable(h, 0), "gt_decoder_profile_enable")
+    return [r["kernel"] for r in json.loads(buf.value.decode())]
+
+
+def _bf16_ulps(a, b):
+    """|a - b| in units of the bf16 ulp of max(|a|, |b|) (both bf16 values)."""
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    m = np.maximum(np.abs(a), np.abs(b))
+    ulp = np.where(m > 0, np.exp2(np.floor(np.log2(np.maximum(m, 1e-38))) - 7), 1.0)
+    return np.abs(a - b) / ulp
+
+
+@pytest.mark.parametrize("B,T,lengths,small", [(3, 132, [132, 100, 44], False), (2, 96, [96, 61], False),
+                                               (1, 76, None, True), (2, 132, [132, 70], True)])
+def test_x0_fused_matches_unfused(monkeypatch, B, T, lengths, small):
+    mu, z, mask, _ = synthetic_inputs(41, B, T, lengths=lengths)
+    t = np.linspace(0.9, 0.2, B).astype(np.float32)
+    args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), None)
+    res = {}
+    for fuse in (1, 0):
+        monkeypatch.setenv("GT_X0_FUSE", str(fuse))
+        dec, _ = make_decoder(1, 23, torch.bfloat16)
+        _lib.check(_lib.lib().gt_decoder_set_small_batch(dec.estimator._native(), 16 if small else 0),
+                   "gt_decoder_set_small_batch")
+        names = _launches(dec, args)
+        fused = any(n.startswith("x0_stats_kernel@") for n in names)
+        assert fused == bool(fuse), names
+        assert any(n.startswith("conv64_kernel<5>@") for n in names) == bool(fuse)
+        assert any(n.startswith("conv_kernel<bf16,0,0,") for n in names) == (not fuse)   # the input conv
+        outs = {"estimator": dec.estimator(*args).cpu().numpy(), "sampler N=3": dec(args[0], args[1], args[2], 3).cpu().numpy()}
+        for st in ("downs.0.0.pre1", "downs.0.0.pre2", "downs.0.0"):
+            _, pr = probe(dec.estimator, torch.bfloat16, *args, st, (B, 64, 80, T))
+            outs[st] = pr.cpu().numpy()
+        res[fuse] = outs
+    for name in res[1]:
+        assert np.isfinite(res[1][name]).all(), name
+    ulps = _bf16_ulps(res[1]["downs.0.0.pre1"], res[0]["downs.0.0.pre1"])
+    report(f"x0 fused pre1 B={B} T={T} small={small}: elements not bit-identical to the input conv's",
+           float(np.mean(ulps > 0)), 2e-3)
+    big = np.abs(res[0]["downs.0.0.pre1"]) >= 1e-2 * np.abs(res[0]["downs.0.0.pre1"]).max()   # (cancellation aside)
+    report(f"x0 fused pre1 B={B} T={T} small={small}: largest difference in bf16 ulps (|h1| >= 1e-2 max)",
+           float(ulps[big].max()), 1.0)
+    report(f"x0 fused pre1 B={B} T={T} small={small}: largest difference / max |h1|",
+           rel_err(res[1]["downs.0.0.pre1"], res[0]["downs.0.0.pre1"]), 2.0 ** -8)
+    # (the fused path's transform sees h1 unrounded, the unfused one its bf16 copy: two bf16 realisations of the network,
+    # so the end-to-end gates are the bf16 estimator's against its oracle, test_emulate_gpu.py)
+    for name, tol in (("downs.0.0.pre2", 1e-2), ("downs.0.0", 1e-2), ("estimator", 2e-2), ("sampler N=3", 2e-2)):
+        report(f"x0 fused {name} B={B} T={T} small={small} vs unfused", rel_err(res[1][name], res[0][name]), tol)
+
+
+def test_x0_fused_batch_invariant(monkeypatch):
+    """An utterance decodes to the same bits alone or inside a batch (per-utterance statistics slots, fixed order)."""
+    monkeypatch.setenv("GT_X0_FUSE", "1")
+    B, T = 3, 132
+    mu, z, mask, _ = synthetic_inputs(42, B, T, lengths=[132, 100, 44])
+    t = np.linspace(0.9, 0.2, B).astype(np.float32)
+    dec, _ = make_decoder(1, 23, torch.bfloat16)
+    full = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), None).cpu()
+    one = dec.estimator(_cuda(z[1:2]), _cuda(mask[1:2]), _cuda(mu[1:2]), _cuda(t[1:2]), None).cpu()
+    assert torch.equal(full[1:2], one)
