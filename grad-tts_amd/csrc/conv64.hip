@@ -608,8 +608,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
 // on the same operands as the consumer, so the statistics are those of the values it transforms), fp32 sums of h1 and
 // h1^2 per 8-channel group over the valid positions in a fixed order, one partial slot per workgroup (common.h
 // layout). Optionally stores bf16(h1) (p.out: the "pre1" probe of the unfused path's storage point).
+#ifndef GT_X0_RG
+#define GT_X0_RG 20
+#endif
 namespace x0s {
-constexpr int RG = 20, WR = RG + 2;   // mel rows per workgroup; window rows
+constexpr int RG = GT_X0_RG, WR = RG + 2;   // mel rows per workgroup; window rows
 }
 __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
   using namespace c64;
@@ -652,7 +655,8 @@ __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
   const bool valid = t < T;
   float gs[4] = {0.f, 0.f, 0.f, 0.f}, gq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 5
-  for (int i = rsel; i < x0s::RG; i += 2) {   // output row fr0 + i (window rows i + h, i + 2), interior column r + 1
+  for (int ii = 0; ii < x0s::RG / 2; ++ii) {   // output row fr0 + i (window rows i + h, i + 2), interior column r + 1
+    const int i = rsel + 2 * ii;
     const f32x16 acc = x0_mfma(sX, i + h, i + 2, r + 1, h, xa0, xa1, bias);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {   // register q = channel cb*32 + acc_row(q, h): group cb*4 + (q >> 2)
