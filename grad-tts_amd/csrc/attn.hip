@@ -79,18 +79,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const int tend = min(p.n, tbeg + p.tile_pos);
   uint4 xr[XIT], xq[RB ? XIT : 1];   // RB: xr = block2 pre-activation, xq = residual input
   float mk[RB ? XIT : 1];
+  // raw buffer access over this utterance's rows (byte offsets < 2^31: launch_attn_kv checks n * C): a position past the
+  // tile's end takes an offset outside the buffer, so its loads return zeros and its rb_out stores are dropped
+  const unsigned nbytes = (unsigned)(p.n * p.C * (int)sizeof(A));
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_pre = __builtin_amdgcn_make_buffer_rsrc((void*)(RB ? pre : x), (short)0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_rb = __builtin_amdgcn_make_buffer_rsrc((void*)(RB ? rb_out : x), (short)0, nbytes, 0x00020000);
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  auto ld16 = [](__amdgpu_buffer_rsrc_t rs, int off) {
+    const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
+  auto xoff = [&](int pos, int c) { return pos < tend ? (pos * p.C + c) * (int)sizeof(A) : (int)0x80000000; };
   auto load_x = [&](int pos0, int c0) {
 #pragma unroll
     for (int j = 0; j < XIT; ++j) {
       const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
       const int pos = pos0 + row;
-      const long e = (long)pos * p.C + c0 + sub * ICH;
+      const int off = xoff(pos, c0 + sub * ICH);
       if (RB) {
-        xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(pre + e) : make_uint4(0, 0, 0, 0);
-        xq[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + e) : make_uint4(0, 0, 0, 0);
-        mk[j] = pos < tend ? mask_at(p.mask, p.T0, b, pos % p.T, p.lvl) : 0.f;
+        xr[j] = ld16(rs_pre, off);
+        xq[j] = ld16(rs_x, off);
+        // the mask depends on the position only: once per sub-block (chunk 0), kept for its other chunks
+        if (c0 == 0) mk[j] = pos < tend ? mask_at(p.mask, p.T0, b, pos % p.T, p.lvl) : 0.f;
       } else {
-        xr[j] = pos < tend ? *reinterpret_cast<const uint4*>(x + e) : make_uint4(0, 0, 0, 0);
+        xr[j] = ld16(rs_x, off);
       }
     }
   };
@@ -99,18 +112,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
     for (int j = 0; j < XIT; ++j) {
       const int it = tid + 256 * j, row = it / IPR, sub = it - row * IPR;
       uint4 u = xr[j];
-      if (RB) {   // x_in = Mish(GN(pre))*m + x*m, as gn_mish_kernel<A, false>
+      if (RB) {   // x_in = (Mish(GN(pre)) + x) * m, as gn_mish_kernel<A, false>; positions past the tile: zeros, dropped
         const int pos = pos0 + row, c = c0 + sub * ICH;
-        if (pos < tend) {
-          float v[ICH], xv[ICH];
-          item_to_f(xr[j], v, A());
-          item_to_f(xq[j], xv, A());
-          const float m = mk[j];
+        float v[ICH], xv[ICH];
+        item_to_f(xr[j], v, A());
+        item_to_f(xq[j], xv, A());
+        const float m = mk[j];
 #pragma unroll
-          for (int k = 0; k < ICH; ++k) v[k] = mish_act<A>(v[k] * s_sc[c + k] + s_sh[c + k]) * m + xv[k] * m;
-          u = f_to_item(v, A());
-          *reinterpret_cast<uint4*>(rb_out + (long)pos * p.C + c) = u;
-        }
+        for (int k = 0; k < ICH; ++k) v[k] = gn_mish_res<A>(v[k], s_sc[c + k], s_sh[c + k], xv[k], m);
+        u = f_to_item(v, A());
+        const u32x4_t o = {u.x, u.y, u.z, u.w};
+        __builtin_amdgcn_raw_buffer_store_b128(o, rs_rb, xoff(pos, c), 0, 0);
       }
       *reinterpret_cast<uint4*>(sX + row * ROWB + sub * 16) = u;
     }
@@ -120,7 +132,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   load_x(tbeg, 0);
   if (RB) {
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
-    for (int c = tid; c < p.C; c += 256) gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
+    for (int c = tid; c < p.C; c += 256) {
+      gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
+      gn_res_coef<A>(s_sc[c], s_sh[c]);
+    }
   }
   // chunked path: the next k/v weight slice (item i of thread tid: row tid / IPR + (256 / IPR) i, 16 B at
   // (tid % IPR) * 16) is loaded into registers during the current chunk (level 1: 94.5 -> 82.4 us)
@@ -409,6 +424,7 @@ __global__ __launch_bounds__(256) void attn_fold_kernel(const float* Ain, const 
 hipError_t launch_attn_kv(int act_bf16, const AttnKVParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(p.B * p.ntile));
   if (p.rb_pre && (p.C > 256 || p.C != p.Cpad)) return hipErrorInvalidValue;   // s_sc / s_sh hold 256 channels
+  if ((long)p.n * p.C * (act_bf16 ? 2 : 4) >= (1L << 31)) return hipErrorInvalidValue;   // 32-bit buffer offsets
   if (p.Cpad > 64 && p.Cpad % (act_bf16 ? kKvCkb / 2 : 16) != 0) return hipErrorInvalidValue;   // whole chunks
   // resident k/v weights only for C = 64; wider inputs stream 64-channel chunks (bf16; 3 workgroups/CU,
   // measured faster at C = 128 than the 87 KB resident variant at 1 workgroup/CU)

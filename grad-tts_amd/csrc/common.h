@@ -51,6 +51,19 @@ GT_DEV float gn_mish_tb_l2(float h, float sc_l2, float sh_l2, float tb) {
   return __builtin_fmaf(yl, __builtin_fmaf(-2.f * kLn2, r, kLn2), tb);
 }
 
+// ResnetBlock output with identity residual (diffusion.py:57-58, 77-79), Mish(GN(h)) * m + x * m = (Mish(GN(h)) + x) * m.
+// The bf16 paths take the base-2 form of gn_mish_tb_l2 with the residual as its addend (GroupNorm coefficients
+// pre-scaled by log2 e, gn_res_coef): 5 FMA-class ops, exp2, rcp and the mask multiply per element, where the mish_act
+// form took 9 and the two transcendentals. fp32 keeps the reference formula.
+template <class A> GT_DEV void gn_res_coef(float&, float&) {}
+template <> GT_DEV void gn_res_coef<bf16>(float& sc, float& sh) { sc *= kLog2e; sh *= kLog2e; }
+template <class A> GT_DEV float gn_mish_res(float h, float sc, float sh, float x, float m) {
+  return mish_act<A>(h * sc + sh) * m + x * m;
+}
+template <> GT_DEV float gn_mish_res<bf16>(float h, float sc_l2, float sh_l2, float x, float m) {
+  return gn_mish_tb_l2(h, sc_l2, sh_l2, x) * m;
+}
+
 // ---------------------------------------------------------------- storage
 template <class A> struct Act;
 template <> struct Act<float> {

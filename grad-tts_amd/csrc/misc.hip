@@ -124,7 +124,10 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
   float sc[ICH], sh[ICH];
 #pragma unroll
-  for (int k = 0; k < ICH; ++k) gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
+  for (int k = 0; k < ICH; ++k) {
+    gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
+    if (!RES) gn_res_coef<A>(sc[k], sh[k]);   // (the identity-residual form, as attn_kv's RB operand load)
+  }
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
     const int e = e0 + i * 256 * ICH;
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
         float x[ICH];
         item_to_f(vx[i], x, A());
 #pragma unroll
-        for (int k = 0; k < ICH; ++k) v[k] = mish_act<A>(v[k] * sc[k] + sh[k]) * m + x[k] * m;
+        for (int k = 0; k < ICH; ++k) v[k] = gn_mish_res<A>(v[k], sc[k], sh[k], x[k], m);
       }
       *reinterpret_cast<uint4*>(out + e) = f_to_item(v, A());
     }
