@@ -652,24 +652,36 @@ __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
   lds_barrier();
   const f32x16 bias = *reinterpret_cast<const f32x16*>(s_xb + (cb * 2 + h) * 16);
   const int t = t0 + r;
-  const bool valid = t < T;
+  const bool valid = t < T, full = t0 + 32 <= T;
   float gs[4] = {0.f, 0.f, 0.f, 0.f}, gq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 5
   for (int ii = 0; ii < x0s::RG / 2; ++ii) {   // output row fr0 + i (window rows i + h, i + 2), interior column r + 1
     const int i = rsel + 2 * ii;
     const f32x16 acc = x0_mfma(sX, i + h, i + 2, r + 1, h, xa0, xa1, bias);
+    if (full) {   // (wave-uniform) every position of the column valid: straight into the running sums
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {   // register q = channel cb*32 + acc_row(q, h): group cb*4 + (q >> 2)
-      float s = 0.f, q2 = 0.f;
+      for (int g = 0; g < 4; ++g)   // register q = channel cb*32 + acc_row(q, h): group cb*4 + (q >> 2)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float v = acc[4 * g + e];
-        s += v;
-        q2 += v * v;
-        asm volatile("" : "+v"(s), "+v"(q2));   // scalar chains (conv.hip: packed-FP32 op_sel hazard)
+        for (int e = 0; e < 4; ++e) {
+          const float v = acc[4 * g + e];
+          gs[g] += v;
+          gq[g] = __builtin_fmaf(v, v, gq[g]);
+          asm volatile("" : "+v"(gs[g]), "+v"(gq[g]));   // scalar chains (conv.hip: packed-FP32 op_sel hazard)
+        }
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float s = 0.f, q2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = acc[4 * g + e];
+          s += v;
+          q2 = __builtin_fmaf(v, v, q2);
+          asm volatile("" : "+v"(s), "+v"(q2));
+        }
+        gs[g] += valid ? s : 0.f;
+        gq[g] += valid ? q2 : 0.f;
       }
-      gs[g] += valid ? s : 0.f;
-      gq[g] += valid ? q2 : 0.f;
     }
     if (p.out) {   // diagnostics: bf16(h1), 8 consecutive channels per lane after the half-wave swap
       float v[16];

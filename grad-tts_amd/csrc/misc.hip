@@ -38,14 +38,17 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
     if (p.euler) { x = p.xt[o]; mu = p.mu[o]; }
   }
   gn_reduce(p.part, p.nparts, b, p.count, s_mean, s_rstd, s_red);
+  constexpr bool L2 = sizeof(A) == 2;   // bf16: the base-2 Mish of gn_mish_tb_l2 with the final_conv weight folded in
   if (tid < 64) {
     float sc, sh;
     gn_affine(s_mean, s_rstd, 64, tid, p.gamma, p.beta, sc, sh);
-    s_sc[tid] = sc; s_sh[tid] = sh; s_w[tid] = p.wf[tid];
+    s_sc[tid] = L2 ? sc * kLog2e : sc; s_sh[tid] = L2 ? sh * kLog2e : sh; s_w[tid] = L2 ? p.wf[tid] * kLn2 : p.wf[tid];
   }
   __syncthreads();
   {
     if (!live) return;
+    // final_conv(y * m) with y = Mish(GN(h)) * m (final_block, Block: * mask): the mask is constant over the channels,
+    // so acc = sum_c w_c Mish(GN(h))_c and the output is (acc m^2 + b) m (diffusion.py:215-216)
     float acc = 0.f;
 #pragma unroll
     for (int it = 0; it < 64 / ICH; ++it) {
@@ -54,11 +57,17 @@ __global__ __launch_bounds__(256) void final_kernel(FinalParams p) {
 #pragma unroll
       for (int k = 0; k < ICH; ++k) {
         const int c = it * ICH + k;
-        const float y = mish_act<A>(v[k] * s_sc[c] + s_sh[c]) * m;   // final_block output (Block: * mask)
-        acc += s_w[c] * (y * m);                               // final_conv(x * mask)
+        if (L2) {   // w Mish(y) = (w ln2) yl (1 - 2 / ((1 + 2^yl)^2 + 1)), yl = log2(e) y
+          const float yl = __builtin_fmaf(v[k], s_sc[c], s_sh[c]);
+          const float t = __builtin_amdgcn_exp2f(yl) + 1.f;
+          const float g = __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_fmaf(t, t, 1.f)), 1.f);
+          acc = __builtin_fmaf(yl * s_w[c], g, acc);
+        } else {
+          acc += s_w[c] * mish_act<A>(v[k] * s_sc[c] + s_sh[c]);
+        }
       }
     }
-    const float s = (acc + p.bf[0]) * m;                       // (output * mask).squeeze(1)
+    const float s = (acc * (m * m) + p.bf[0]) * m;             // (output * mask).squeeze(1)
     if (!p.euler) {
       p.out[o] = s;
     } else {
