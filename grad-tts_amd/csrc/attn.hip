@@ -56,7 +56,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   const A* wkv = reinterpret_cast<const A*>(p.wkv);
   const A* pre = RB ? reinterpret_cast<const A*>(p.rb_pre) + (long)b * p.n * p.C : nullptr;
   A* rb_out = RB ? reinterpret_cast<A*>(p.rb_out) + (long)b * p.n * p.C : nullptr;
-  __shared__ float s_sc[RB ? 256 : 1], s_sh[RB ? 256 : 1], s_mean[8], s_rstd[8];
+  // GroupNorm coefficients of channel c at c + c / 8: the operand loads read 8 consecutive channels at 8 different
+  // 8-channel groups per half-wave (ds_read2_b32, banks (a/4) mod 32), which unskewed put groups g and g + 4 on one bank
+  __shared__ float s_sc[RB ? 288 : 1], s_sh[RB ? 288 : 1], s_mean[8], s_rstd[8];
+  auto cix = [](int c) { return c + (c >> 3); };
   __shared__ double s_red[RB ? 272 : 1];
   GnLoad gl;
   if (RB) gl = gn_load(p.rb_part, p.rb_nparts, b);   // slot loads in flight with the weight / first x loads
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
         item_to_f(xq[j], xv, A());
         const float m = mk[j];
 #pragma unroll
-        for (int k = 0; k < ICH; ++k) v[k] = gn_mish_res<A>(v[k], s_sc[c + k], s_sh[c + k], xv[k], m);
+        for (int k = 0; k < ICH; ++k) v[k] = gn_mish_res<A>(v[k], s_sc[cix(c) + k], s_sh[cix(c) + k], xv[k], m);
         u = f_to_item(v, A());
         const u32x4_t o = {u.x, u.y, u.z, u.w};
         __builtin_amdgcn_raw_buffer_store_b128(o, rs_rb, xoff(pos, c), 0, 0);
@@ -133,8 +136,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void a
   if (RB) {
     gn_finish(gl, p.rb_part, p.rb_nparts, b, p.rb_count, s_mean, s_rstd, s_red);
     for (int c = tid; c < p.C; c += 256) {
-      gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[c], s_sh[c]);
-      gn_res_coef<A>(s_sc[c], s_sh[c]);
+      gn_affine(s_mean, s_rstd, p.C, c, p.rb_gamma, p.rb_beta, s_sc[cix(c)], s_sh[cix(c)]);
+      gn_res_coef<A>(s_sc[cix(c)], s_sh[cix(c)]);
     }
   }
   // chunked path: the next k/v weight slice (item i of thread tid: row tid / IPR + (256 / IPR) i, 16 B at

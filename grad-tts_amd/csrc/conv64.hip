@@ -311,15 +311,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
   }
   if (IN == IN_GN || IN == IN_X0) {
     const float c_g = tid < 64 ? p.gn_gamma[tid] : 0.f, c_b = tid < 64 ? p.gn_beta[tid] : 0.f;
-    if (IN == IN_X0 && tid < 64)   // the input conv's bias in accumulator layout, per (cb, h): the C operand of x0_mfma
-      s_coef[192 + tid] = p.x0b[(tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1)];
+    if (IN == IN_X0 && tid < 64) {   // the input conv's bias in accumulator layout, per (cb, h): the C operand of x0_mfma
+      const int c = (tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1);
+      s_coef[192 + tid] = p.x0s ? p.x0b[c] / p.x0s[c] : p.x0b[c];
+    }
     static_assert(NTHR >= 256, "gn_load / gn_finish use 256 threads");
     const GnLoad gl = gn_load(p.gn_part, p.gn_nparts, b, tid);
     const float tbv = tid < 64 ? tb_at(p.tb, p.stepp)[(long)b * p.tb_bstride + tid] : 0.f;
     gn_finish(gl, p.gn_part, p.gn_nparts, b, p.gn_count, s_mean, s_rstd, s_red, tid);
     if (tid < 64) {
       const float sc = c_g * s_rstd[tid >> 3];   // the affine in base 2 (common.h gn_mish_tb_l2)
-      s_coef[tid] = sc * kLog2e; s_coef[64 + tid] = (c_b - s_mean[tid >> 3] * sc) * kLog2e; s_coef[128 + tid] = tbv;
+      // (IN_X0 with fp8 weights: the accumulators hold h1 / scale, so the scale joins the GroupNorm multiplier)
+      const float xs = (IN == IN_X0 && p.x0s) ? p.x0s[tid] : 1.f;
+      s_coef[tid] = sc * kLog2e * xs; s_coef[64 + tid] = (c_b - s_mean[tid >> 3] * sc) * kLog2e; s_coef[128 + tid] = tbv;
     }
     lds_barrier();
   }
@@ -617,7 +621,7 @@ constexpr int RG = GT_X0_RG, WR = RG + 2;   // mel rows per workgroup; window ro
 __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
   using namespace c64;
   __shared__ __attribute__((aligned(16))) uint32_t sX[x0s::WR * XC];
-  __shared__ __attribute__((aligned(16))) float s_xb[64];
+  __shared__ __attribute__((aligned(16))) float s_xb[64], s_xs[64];   // bias (/ scale), scale: accumulator layout
   __shared__ float s_sub[4 * 16];   // [wave][group g][h][sum, sq]
   const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), cb = wv & 1, rsel = wv >> 1;
@@ -641,7 +645,11 @@ __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
     c2[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_xt, q, 0, 0));
     mk[j] = (t >= 0 && t < T) ? mask_at(p.mask, p.T0, b, t, p.lvl_in) : 0.f;
   }
-  if (tid < 64) s_xb[tid] = p.x0b[(tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1)];
+  if (tid < 64) {
+    const int c = (tid >> 5) * 32 + acc_row(tid & 15, (tid >> 4) & 1);
+    s_xs[tid] = p.x0s ? p.x0s[c] : 1.f;
+    s_xb[tid] = p.x0s ? p.x0b[c] / p.x0s[c] : p.x0b[c];
+  }
   const bf16x8 xa0 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 0) * 64 + lane];
   const bf16x8 xa1 = reinterpret_cast<const bf16x8*>(p.x0w)[(cb * 2 + 1) * 64 + lane];
 #pragma unroll
@@ -657,7 +665,12 @@ __global__ __launch_bounds__(256) void x0_stats_kernel(ConvParams p) {
 #pragma unroll 5
   for (int ii = 0; ii < x0s::RG / 2; ++ii) {   // output row fr0 + i (window rows i + h, i + 2), interior column r + 1
     const int i = rsel + 2 * ii;
-    const f32x16 acc = x0_mfma(sX, i + h, i + 2, r + 1, h, xa0, xa1, bias);
+    f32x16 acc = x0_mfma(sX, i + h, i + 2, r + 1, h, xa0, xa1, bias);
+    if (p.x0s) {   // (uniform) fp8 weights: h1 = accumulator * scale
+      const f32x16 xs = *reinterpret_cast<const f32x16*>(s_xs + (cb * 2 + h) * 16);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] *= xs[q];
+    }
     if (full) {   // (wave-uniform) every position of the column valid: straight into the running sums
 #pragma unroll
       for (int g = 0; g < 4; ++g)   // register q = channel cb*32 + acc_row(q, h): group cb*4 + (q >> 2)
@@ -784,9 +797,10 @@ hipError_t launch_conv64(InMode im, const ConvParams& p, hipStream_t s) {
   const dim3 block(256);
   const bool rb_ok = p.rb_out && p.rb_w && p.rb_b && p.mu && p.xt && p.cin_input >= 2 && p.cin_input <= 3 &&
                      (p.cin_input == 2 || p.spk_s);
-  if (im == IN_X0) {   // bf16 weights only (the fp8 modes keep the input conv's fp8 image: unfused)
-    if (p.wscale || !x0_eligible(p) || !p.gn_part) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv64_kernel<IN_X0, false>), dim3(grid), block, 0, s, p, L);
+  if (im == IN_X0) {   // (p.wscale: block2's fp8 weights; p.x0s: the input conv's)
+    if (!x0_eligible(p) || !p.gn_part) return hipErrorInvalidValue;
+    if (p.wscale) hipLaunchKernelGGL((conv64_kernel<IN_X0, true>), dim3(grid), block, 0, s, p, L);
+    else hipLaunchKernelGGL((conv64_kernel<IN_X0, false>), dim3(grid), block, 0, s, p, L);
     return hipGetLastError();
   }
   if (p.wscale) {   // fp8 weights (the conv64-layout image of their e4m3 values)

@@ -559,6 +559,8 @@ int prepare(gt_decoder* d, int code) {
       if (conv3w_shape(shp)) pack_conv3w_a8(blob, k + ".w3a", w, (int)shp[0], (int)shp[1]);   // conv3w_a8
     } else if (w8 && (ends_with(k, ".block.0.weight") || (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight")))) {
       pack_conv8(blob, d, code, k, w, shp, false);
+      if (ends_with(k, ".block.0.weight") && shp[0] == 64 && shp[1] == 2 && shp[2] == 3 && shp[3] == 3)
+        pack_x0(blob, k + ".x0", e4m3_values(w, 64));   // the input conv recomputed by conv64 IN_X0: e4m3 values
       if (code == GT_BF16_W8 && ends_with(k, ".block.0.weight") && conv3w_shape(shp))   // conv3w: the e4m3 values
         pack_conv3w(blob, k + ".w3w", e4m3_values(w, (int)shp[0]), (int)shp[0], (int)shp[1]);
       if (starts_with(k, "downs.") && ends_with(k, ".3.conv.weight") && shp[0] == 64 && shp[1] == 64)
@@ -858,13 +860,17 @@ struct Run {
 
   // downs.0.0 on the fused input-conv path (conv64 IN_X0 + x0_stats): bf16 weights and activations, two input channels
   bool x0_fused(const std::string& k, int lvl, int cin, int Cout) {
-    if (!(d->x0_fuse && dt && wi == GT_BF16 && conv64_enabled() && cin == 2 && Cout == 64 && Fl(lvl) % 20 == 0 &&
+    if (!(d->x0_fuse && dt && (wi == GT_BF16 || wi == GT_BF16_W8 || wi == GT_FP8) && conv64_enabled() && cin == 2 && Cout == 64 && Fl(lvl) % 20 == 0 &&
           d->dp[wi].count(k + "block1.block.0.weight.x0") && d->dp[wi].count(k + "block2.block.0.weight.w64")))
       return false;
     ConvParams p = base(lvl, lvl);
     p.Cin = p.C0 = p.Cin_pad = Cout; p.Cout = Cout; p.cin_input = cin; p.mu = mu; p.xt = xt;
     p.x0w = W(k + "block1.block.0.weight.x0"); p.x0b = Fp(k + "block1.block.0.bias");
     return x0_eligible(p) && conv64_eligible(p);
+  }
+  const float* x0_scale(const std::string& k) {   // the input conv's fp8 scale (fp8-weight modes), else null
+    const auto it = d->dp[wi].find(k + "block1.block.0.weight.s");
+    return it != d->dp[wi].end() ? (const float*)it->second : nullptr;
   }
   void* W(const std::string& k) { return d->dp[wi].at(k); }
   const float* Fp(const std::string& k) { return (const float*)d->dp[wi].at(k); }
@@ -940,7 +946,7 @@ struct Run {
       // same operands, so the statistics are those of the values it transforms
       ConvParams p = base(lvl, lvl);
       p.Cin = cin; p.Cout = Cout; p.cin_input = cin; p.mu = mu; p.xt = xt;
-      p.x0w = W(k + "block1.block.0.weight.x0"); p.x0b = Fp(k + "block1.block.0.bias");
+      p.x0w = W(k + "block1.block.0.weight.x0"); p.x0b = Fp(k + "block1.block.0.bias"); p.x0s = x0_scale(k);
       p.out_part = st1;
       p.out = (probe && std::string(probe) == k + "pre1") ? pre1 : nullptr;   // diagnostics: bf16(h1)
       np1 = x0_stats_nparts(Fl(lvl), Tl(lvl));
@@ -952,7 +958,7 @@ struct Run {
       tap_part(stat_slot - 2);
       ConvParams q = base(lvl, lvl);
       q.Cin = Cout; q.Cout = Cout; q.Cin_pad = 64; q.C0 = Cout; q.in0 = nullptr;
-      q.cin_input = cin; q.mu = mu; q.xt = xt; q.x0w = p.x0w; q.x0b = p.x0b;
+      q.cin_input = cin; q.mu = mu; q.xt = xt; q.x0w = p.x0w; q.x0b = p.x0b; q.x0s = p.x0s;
       q.gn_part = st1; q.gn_nparts = np1; q.gn_gamma = Fp(k + "block1.block.1.weight"); q.gn_beta = Fp(k + "block1.block.1.bias");
       q.gn_count = count; q.tb = tb + tb_off; q.tb_bstride = tb_bstride;
       setw(q, k + "block2.block.0.weight"); q.bias = Fp(k + "block2.block.0.bias");
@@ -960,7 +966,7 @@ struct Run {
       q.out = pre2; q.out_part = st2;
       np2 = conv64_nparts(q.Fout, q.Tout, q.small);
       if (np2 > L.pmax) { chk(hipErrorInvalidValue); return; }
-      timed("conv64_kernel<5>@64x64x" + std::to_string(Fl(lvl)), 2.0 * 64 * 64 * 9 * pos + 2.0 * cin * Cout * 9 * pos,
+      timed(std::string("conv64_kernel<5") + (q.wscale ? ",w8" : "") + ">@64x64x" + std::to_string(Fl(lvl)), 2.0 * 64 * 64 * 9 * pos + 2.0 * cin * Cout * 9 * pos,
             pos * (2 * 4.0 + 4.0 + 128.0) + 64.0 * 9 * 64 * 2, [&] { return launch_conv64(IN_X0, q, s); });
       tap(k + "pre2", lvl, pre2, Cout);
       tap_part(stat_slot - 1);

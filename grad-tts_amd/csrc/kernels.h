@@ -39,8 +39,9 @@ struct ConvParams {
   // with rb_w [64][cin] fp32 and rb_b [64]; r0 itself is also written to rb_out ([B][F][T][64] bf16, each position once)
   const float* rb_w; const float* rb_b; void* rb_out;
   // IN_X0 (conv64) and launch_x0_stats: the U-Net input conv (2 channels -> 64) as MFMA A fragments (decoder.cpp pack_x0)
-  // and its bias
-  const void* x0w; const float* x0b;
+  // and its bias; x0s non-null: the fragments hold e4m3 weight values and x0s the per-output-channel scale
+  // (the fp8-weight modes: h1 = (bias / scale + sum) * scale)
+  const void* x0w; const float* x0b; const float* x0s;
   const float* tb; long tb_bstride;                   // IN_GN: time bias [.., Cin]; row b*tb_bstride
   const int* stepp;                                   // IN_GN: device step index (tb_at), or null
   // ---- weights

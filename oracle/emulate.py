@@ -13,9 +13,9 @@ library rounds, so the GPU can be pinned against it at fp32-summation-order dist
 * every stored activation -- a Block conv's output (csrc/conv3w.hip / conv64.hip / conv.hip epilogues), a ResnetBlock
   output (rbout passes, attn_kv's RB form, conv64 IN_RB0), an attention output (conv_kernel OUT_RESID), a
   Down/Upsample output -- is bf16 (round to nearest even); the GroupNorm statistics of a conv output are those of its
-  fp32 values (the epilogues sum before rounding), applied to the stored bf16 copy -- except the bf16 mode's
-  single-speaker U-Net input conv, whose output block2's conv recomputes instead of reading (conv64 IN_X0), so its
-  GroupNorm normalises the fp32 values;
+  fp32 values (the epilogues sum before rounding), applied to the stored bf16 copy -- except the single-speaker
+  U-Net input conv, whose output block2's conv recomputes instead of reading (conv64 IN_X0), so its GroupNorm
+  normalises the fp32 values;
 * a bf16 conv's operand is the bf16 rounding of its fp32 operand value (masked input, or (Mish(GN(h)) + tb) * m); an
   fp8-operand conv (GT_FP8, ``decoder.fp8_operand_conv``) quantizes that fp32 value straight to e4m3
   (``decoder.quantize_act_e4m3``: conv3w_a8.hip finish_item / conv.hip store_item_a8);
@@ -117,8 +117,8 @@ def _resnet(p, key, x, mask, t_emb, taps, first):
     """``ResnetBlock`` (diffusion.py:61-79); x is stored (bf16) except for the input block (fp32 mu, x_t, spk)."""
     cin, cout = x.shape[1], p[key + ".block1.block.0.weight"].shape[0]
     fp8 = _Cfg.mode == "fp8"
-    # the bf16 mode's single-speaker input block recomputes h1 inside block2's conv (decoder.cpp x0_fused): never stored
-    fused_x0 = first and _Cfg.mode == "bf16" and cin == 2 and cout == 64 and x.shape[2] % 20 == 0
+    # the single-speaker input block recomputes h1 inside block2's conv (decoder.cpp x0_fused): never stored
+    fused_x0 = first and cin == 2 and cout == 64 and x.shape[2] % 20 == 0
     h = _block(p, key + ".block1", x * mask, mask, taps, key + ".pre1", fp8 and D.fp8_operand_conv(cin, cout),
                stored=not fused_x0)
     tb = F.linear(D.mish(t_emb), p[key + ".mlp.1.weight"], p[key + ".mlp.1.bias"])
