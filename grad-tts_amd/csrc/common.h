@@ -63,6 +63,14 @@ template <class A> GT_DEV float gn_mish_res(float h, float sc, float sh, float x
 template <> GT_DEV float gn_mish_res<bf16>(float h, float sc_l2, float sh_l2, float x, float m) {
   return gn_mish_tb_l2(h, sc_l2, sh_l2, x) * m;
 }
+// ResnetBlock output with a res_conv residual r (unmasked: res_conv(x * m)), Mish(GN(h)) * m + r (diffusion.py:78);
+// bf16: the base-2 Mish (coefficients from gn_res_coef), then one FMA
+template <class A> GT_DEV float gn_mish_add(float h, float sc, float sh, float r, float m) {
+  return mish_act<A>(h * sc + sh) * m + r;
+}
+template <> GT_DEV float gn_mish_add<bf16>(float h, float sc_l2, float sh_l2, float r, float m) {
+  return __builtin_fmaf(gn_mish_tb_l2(h, sc_l2, sh_l2, 0.f), m, r);
+}
 
 // ---------------------------------------------------------------- storage
 template <class A> struct Act;

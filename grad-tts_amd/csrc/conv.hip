@@ -414,8 +414,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
     }
     if (OUT == OUT_RBOUT && tid < NT) {
       const int g = (cout0 + tid) / (p.Cout >> 3);
-      const float sc = c_g * s_rstd[g];
-      s_sc[tid] = sc; s_sh[tid] = c_b - s_mean[g] * sc;
+      float sc = c_g * s_rstd[g], sh = c_b - s_mean[g] * sc;
+      gn_res_coef<A>(sc, sh);   // bf16: base 2 (gn_mish_add)
+      s_sc[tid] = sc; s_sh[tid] = sh;
     }
   }
   if (tid < NT) s_bias[tid] = c_bias;                 // all visible after the first chunk barrier
@@ -805,7 +806,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NT == 64 &&
               // ResnetBlock output: Mish(GN(h2)) * mask + res_conv(x * mask)   (diffusion.py:57-58, 77-78)
               const float m = om[rb];
 #pragma unroll
-              for (int k = 0; k < 8; ++k) o[k] = mish_act<A>(e[k] * s_sc[cl + k] + s_sh[cl + k]) * m + o[k];
+              for (int k = 0; k < 8; ++k) o[k] = gn_mish_add<A>(e[k], s_sc[cl + k], s_sh[cl + k], o[k], m);
             } else {                                   // Residual: fn(x) + x   (diffusion.py:108)
 #pragma unroll
               for (int k = 0; k < 8; ++k) o[k] += e[k];

@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
         const f32x4 sc = *reinterpret_cast<const f32x4*>(cf);
         const f32x4 sh = *reinterpret_cast<const f32x4*>(cf + 64);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[4 * hq + k] = mish_act<bf16>(v[4 * hq + k] * sc[k] + sh[k]) * m + r[k];
+        for (int k = 0; k < 4; ++k) v[4 * hq + k] = gn_mish_add<bf16>(v[4 * hq + k], sc[k], sh[k], r[k], m);
       }
       const uint4 o = f_to_item(v, bf16());
       __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, rs_rb, rbo, 0, 0);   // r0 (unmasked)
@@ -301,6 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (tid < 64) {
       float sc, sh;
       gn_affine(s_mean, s_rstd, 64, tid, p.gn_gamma, p.gn_beta, sc, sh);
+      gn_res_coef<bf16>(sc, sh);   // (base 2: gn_mish_add, as rbout_input)
       s_coef[tid] = sc; s_coef[64 + tid] = sh;
 #pragma unroll
       for (int j = 0; j < 3; ++j) s_coef[128 + 64 * j + tid] = j < p.cin_input ? p.rb_w[tid * p.cin_input + j] : 0.f;

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
 #pragma unroll
   for (int k = 0; k < ICH; ++k) {
     gn_affine(s_mean, s_rstd, p.C, c0 + k, p.gamma, p.beta, sc[k], sh[k]);
-    if (!RES) gn_res_coef<A>(sc[k], sh[k]);   // (the identity-residual form, as attn_kv's RB operand load)
+    gn_res_coef<A>(sc[k], sh[k]);   // (the base-2 forms gn_mish_res / gn_mish_add, as attn_kv / conv64 IN_RB0)
   }
 #pragma unroll
   for (int i = 0; i < RB_IPT; ++i) {
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void gn_mish_kernel(RbOutParams p) {
 #pragma unroll
         for (int k = 0; k < ICH; ++k) {
           const float r = fmaf(rw[k][2], x2, fmaf(rw[k][1], x1, fmaf(rw[k][0], x0, rbias[k])));
-          v[k] = mish_act<A>(v[k] * sc[k] + sh[k]) * m + r;
+          v[k] = gn_mish_add<A>(v[k], sc[k], sh[k], r, m);
         }
       } else {
         float x[ICH];
