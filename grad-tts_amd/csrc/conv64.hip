@@ -215,7 +215,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
     if (IN == IN_RB0) load_in(frow, ti, xi);
   };
   const bool spk3 = IN == IN_RB0 && p.cin_input == 3;   // IN_RB0: n_spks > 1 (a third U-Net input channel)
-  // (Mish(GN(h)) * m + tb) * m of the 8 channels of group g, m in {0,1} (diffusion.py:57-58, 76), as a bf16 item
+  // (Mish(GN(h)) * m + tb) * m of the 8 channels of group g (diffusion.py:57-58, 76) as a bf16 item: a select for the
+  // 0/1 masks of sequence_mask; a fractional mask value (C-ABI callers: the boundary rejects them) takes the multiply in
+  // a branch 0/1 masks never enter, so the result is conv_kernel IN_GN's (Mish(GN(h)) + tb) * m on every path
   auto gn_tb_item = [&](float* v, float m, int g) __attribute__((always_inline)) {
 #pragma unroll
     for (int hq = 0; hq < 2; ++hq) {   // 4 channels at a time: fewer coefficient registers live
@@ -225,6 +227,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void c
       const f32x4 tb = *reinterpret_cast<const f32x4*>(cf + 128);
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[4 * hq + k] = gn_mish_tb_l2(v[4 * hq + k], sc[k], sh[k], tb[k]);
+    }
+    if (__builtin_expect(m != 0.f && m != 1.f, 0)) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] *= m;
     }
     const uint4 o = f_to_item(v, bf16());
     return m != 0.f ? u32x4_t{o.x, o.y, o.z, o.w} : u32x4_t{0u, 0u, 0u, 0u};

@@ -199,6 +199,9 @@ struct gt_decoder {
   // the first ResnetBlock's output formed by the next block's conv (conv64 IN_RB0) instead of its own pass
   // (rbout_input); GT_RB0_FUSE=0 at creation: the pass
   bool rb0_fuse = true;
+  // the 64 -> 64 3x3 convs on conv64 (persistent weight-resident, conv64.hip) for bf16 / fp8-weight calls; GT_CONV64=0
+  // at creation: conv_kernel (A/B, and the fractional-mask path agreement test)
+  bool conv64 = true;
   // the U-Net input conv (downs.0.0's block1, 2 -> 64 channels) recomputed inside the next conv (conv64 IN_X0) from
   // {mu, x_t}, with a statistics-only pass for its GroupNorm, instead of written and read back (bf16 compute dtype,
   // single speaker); GT_X0_FUSE=0 at creation: the input conv
@@ -525,17 +528,6 @@ static bool conv3w_shape(const std::vector<int64_t>& shp) {
          !(shp[0] == 64 && shp[1] == 64);
 }
 
-// conv64 (persistent weight-resident 64-channel 3x3 conv, conv64.hip) for bf16; GT_CONV64=0 disables it (A/B)
-static bool conv64_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("GT_CONV64");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
-
-
-
 int prepare(gt_decoder* d, int code) {
   if (!d->dirty[code]) return GT_OK;
   if (int rc = gt_internal_refresh_host(d)) return rc;
@@ -792,7 +784,7 @@ struct Run {
       }
       flush_rb0();
     }
-    if (dt && conv64_enabled() && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
+    if (dt && d->conv64 && (im == IN_MASK || im == IN_GN || im == IN_PLAIN) && conv64_eligible(p) &&
         d->dp[wi].count(wkey + ".w64")) {
       p.w = W(wkey + ".w64");   // (fp8 weights: their e4m3 values; p.wscale stays the per-channel scale)
       p.a8 = 0;
@@ -860,7 +852,7 @@ struct Run {
 
   // downs.0.0 on the fused input-conv path (conv64 IN_X0 + x0_stats): bf16 weights and activations, two input channels
   bool x0_fused(const std::string& k, int lvl, int cin, int Cout) {
-    if (!(d->x0_fuse && dt && (wi == GT_BF16 || wi == GT_BF16_W8 || wi == GT_FP8) && conv64_enabled() && cin == 2 && Cout == 64 && Fl(lvl) % 20 == 0 &&
+    if (!(d->x0_fuse && dt && (wi == GT_BF16 || wi == GT_BF16_W8 || wi == GT_FP8) && d->conv64 && cin == 2 && Cout == 64 && Fl(lvl) % 20 == 0 &&
           d->dp[wi].count(k + "block1.block.0.weight.x0") && d->dp[wi].count(k + "block2.block.0.weight.w64")))
       return false;
     ConvParams p = base(lvl, lvl);
@@ -1011,7 +1003,7 @@ struct Run {
       pend0.beta = Fp(k + "block2.block.1.bias"); pend0.count = count; pend0.out = out;
       pend0.rw = Fp(k + "res_conv.weight.f32"); pend0.rb = Fp(k + "res_conv.bias"); pend0.cin = cin; pend0.lvl = lvl;
       pend0.C = Cout;
-      if (!(dt && d->rb0_fuse && conv64_enabled() && Cout == 64)) flush_rb0();
+      if (!(dt && d->rb0_fuse && d->conv64 && Cout == 64)) flush_rb0();
       return;
     } else if (d->index.count(k + "res_conv.weight")) {   // Mish(GN(h2))*m + res_conv(x*m)
       ConvParams p = base(lvl, lvl);
@@ -1283,6 +1275,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_ATTN_DS")) d->attn_ds = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_US")) d->attn_us = atoi(e) != 0;
   if (const char* e = getenv("GT_RB0_FUSE")) d->rb0_fuse = atoi(e) != 0;
+  if (const char* e = getenv("GT_CONV64")) d->conv64 = atoi(e) != 0;
   if (const char* e = getenv("GT_X0_FUSE")) d->x0_fuse = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;

@@ -51,6 +51,18 @@ def _launches(dec, args):
     return [r["kernel"] for r in json.loads(buf.value.decode())]
 
 
+def _probe_launches(dec, dtype, args, stage, shape):
+    """(stage activation, kernel names) of one C-ABI estimator call (gt_estimator_probe: no boundary mask check)."""
+    L = _lib.lib()
+    h = dec.estimator._native()
+    _lib.check(L.gt_decoder_profile_enable(h, 1), "gt_decoder_profile_enable")
+    _, pr = probe(dec.estimator, dtype, *args, stage, shape)
+    buf = ctypes.create_string_buffer(1 << 20)
+    _lib.check(L.gt_decoder_profile_read(h, buf, len(buf)), "gt_decoder_profile_read")
+    _lib.check(L.gt_decoder_profile_enable(h, 0), "gt_decoder_profile_enable")
+    return pr, [r["kernel"] for r in json.loads(buf.value.decode())]
+
+
 def _bf16_ulps(a, b):
     """|a - b| in units of the bf16 ulp of max(|a|, |b|) (both bf16 values)."""
     a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
@@ -114,3 +126,29 @@ def test_x0_fused_batch_invariant(monkeypatch):
     full = dec.estimator(_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), None).cpu()
     one = dec.estimator(_cuda(z[1:2]), _cuda(mask[1:2]), _cuda(mu[1:2]), _cuda(t[1:2]), None).cpu()
     assert torch.equal(full[1:2], one)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, "fp8"], ids=["bf16", "fp8"])
+def test_fractional_mask_conv64_matches_conv_kernel(monkeypatch, dtype):
+    """A C-ABI caller (no boundary mask check) with a fractional mask: the level-0 64 -> 64 convs on conv64 (with the
+    fused input conv, IN_X0, and the GroupNorm-operand form) compute their operand as conv_kernel IN_GN does,
+    (Mish(GN(h)) + tb) * m -- the multiply taken in the branch 0/1 masks never enter -- so a decoder built with
+    GT_CONV64=0 (conv_kernel, unfused input conv) agrees within the plan-agreement gate, as for the 0/1 mask."""
+    B, T = 3, 128
+    mu, z, mask, _ = synthetic_inputs(53, B, T, lengths=[128, 100, 60])
+    frac = (mask * np.random.default_rng(7).uniform(0.25, 1.0, mask.shape)).astype(np.float32)
+    t = np.linspace(0.9, 0.3, B).astype(np.float32)
+    name = "bf16" if dtype is torch.bfloat16 else dtype
+    for label, m in (("fractional", frac), ("0/1", mask)):
+        args = (_cuda(z), _cuda(m), _cuda(mu), _cuda(t), None)
+        outs = []
+        for c64 in (1, 0):
+            monkeypatch.setenv("GT_CONV64", str(c64))
+            dec, _ = make_decoder(1, 0, dtype)
+            _lib.check(_lib.lib().gt_decoder_set_small_batch(dec.estimator._native(), 0), "gt_decoder_set_small_batch")
+            y, names = _probe_launches(dec, dtype, args, "downs.0.1", (B, 64, 80, T))
+            assert any(n.startswith("conv64_kernel<") for n in names) == bool(c64)
+            outs.append(y.cpu().numpy())
+        assert np.isfinite(outs[0]).all()
+        report(f"conv64 vs conv_kernel estimator, {label} mask (C ABI, {name})", rel_err(outs[0], outs[1]),
+               2e-2 if name == "bf16" else 5e-2)
