@@ -341,7 +341,9 @@ def main():
         flop_step = N * estimator_flops(B, T, args.n_spks)
         dom = next(p for p in timed if p["kernel"] == dom_name)   # events inside the timed region
         avg_s = dom["ms"] / dom["launches"] / 1e3
-        kpeak = PEAK["fp8"] if ",a8" in dom["kernel"] else PEAK["bf16" if args.dtype in ("bf16_w8", "fp8") else args.dtype]
+        # (fp8-operand kernels: conv_kernel's ",a8" instantiations and conv3w_a8_kernel issue the block-scaled fp8 MFMA)
+        fp8_mfma = ",a8" in dom["kernel"] or dom["kernel"].startswith("conv3w_a8_kernel")
+        kpeak = PEAK["fp8"] if fp8_mfma else PEAK["bf16" if args.dtype in ("bf16_w8", "fp8") else args.dtype]
         # bound: MFMA when the kernel's algorithmic FLOP per byte is past the ridge point (peak FLOP/s / 8 TB/s),
         # else HBM (achieved = algorithmic bytes per launch / launch time against 8 TB/s)
         mfma_bound = dom["flop"] > 0 and (dom["bytes"] <= 0 or dom["flop"] / dom["bytes"] >= kpeak / HBM_PEAK)
