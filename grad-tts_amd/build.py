@@ -22,7 +22,7 @@ OUT = os.path.join(HERE, "gradtts_amd", "libgradtts.so")
 OPS_OUT = os.path.join(HERE, "gradtts_amd", "libgradtts_ops.so")   # torch.ops.gradtts.* (csrc/torch_ops.cpp)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GRADTTS_ARCH", "gfx950")
-SOURCES = ["conv.hip", "conv64.hip", "conv3w.hip", "conv3w_a8.hip", "attn.hip", "attn_down.hip", "misc.hip", "mas.hip", "train.hip", "bwd.hip", "textenc.hip", "textenc_train.hip",
+SOURCES = ["conv.hip", "conv1s.hip", "conv64.hip", "conv3w.hip", "conv3w_a8.hip", "attn.hip", "attn_down.hip", "misc.hip", "mas.hip", "train.hip", "bwd.hip", "textenc.hip", "textenc_train.hip",
            "decoder.cpp", "train_bwd.cpp", "textenc.cpp", "vocoder.cpp"]
 # -packed-fp32-ops: keep the compiler from emitting v_pk_{fma,add,mul}_f32. Rounds 1-2 saw run-to-run differences
 # with them (GroupNorm sum-of-squares partials, W8 decodes); round 3 found the cause -- the compiler paired the

@@ -206,6 +206,9 @@ struct gt_decoder {
   // {mu, x_t}, with a statistics-only pass for its GroupNorm, instead of written and read back (bf16 compute dtype,
   // single speaker); GT_X0_FUSE=0 at creation: the input conv
   bool x0_fuse = true;
+  // the throughput plan's bf16 1x1 convs (res_conv + block output, attention output + residual) on conv1s (LDS-DMA
+  // ring, conv1s.hip); GT_CONV1S=0 at creation: conv_kernel
+  bool conv1s = true;
   // ups.1's attention output + Upsample as one pass (attn_up_kernel); GT_ATTN_US=0 at creation: two launches
   bool attn_us = true;
   // small-batch plan attention: tiles per utterance (GT_ATTN_TILES_SMALL) and the merge's rows per workgroup
@@ -754,6 +757,13 @@ struct Run {
     if (om == OUT_RBOUT || om == OUT_RESID) bytes += pout * p.Cout * es;
     // "<instantiation as rocprof names it>@<shape>": bench.py aggregates per instantiation
     const int nt = dt ? conv_nt(1, p.Cout) : 64;
+    if (kind == CONV1 && dt && d->conv1s && conv1s_eligible(im, om, p)) {
+      const std::string name = "conv1s_kernel<" + std::to_string((int)im) + "," + std::to_string((int)om) + "," +
+                               std::to_string(nt) + ">@" + std::to_string(p.Cin) + "x" + std::to_string(p.Cout) + "x" +
+                               std::to_string(p.Fout);
+      timed(name, flop, bytes, [&] { return launch_conv1s(im, om, p, s); });
+      return;
+    }
     const int tf = (dt && !(p.a8 && !p.small)) ? conv_tf(kind, im, nt, p.Cout, p.Fout, p.small) : 4;
     const std::string name = std::string("conv_kernel<") + (dt ? "bf16" : "float") + "," + std::to_string((int)kind) +
                              "," + std::to_string((int)im) + "," + std::to_string((int)om) + "," + std::to_string(nt) +
@@ -1277,6 +1287,7 @@ int gt_decoder_create(int n_feats, int dim, int n_spks, int spk_emb_dim, float b
   if (const char* e = getenv("GT_RB0_FUSE")) d->rb0_fuse = atoi(e) != 0;
   if (const char* e = getenv("GT_CONV64")) d->conv64 = atoi(e) != 0;
   if (const char* e = getenv("GT_X0_FUSE")) d->x0_fuse = atoi(e) != 0;
+  if (const char* e = getenv("GT_CONV1S")) d->conv1s = atoi(e) != 0;
   if (const char* e = getenv("GT_ATTN_TILES_SMALL")) d->small_tiles = std::max(1, std::min(256, atoi(e)));
   if (const char* e = getenv("GT_MERGE_DR_SMALL")) d->merge_dr_small = atoi(e) == 32 ? 32 : 4;
   if (const char* e = getenv("GT_SK_TARGET")) d->sk_target = std::max(0, atoi(e));

@@ -63,6 +63,10 @@ struct ConvParams {
 int conv_small_ksplit(int F, int T, int Cout, int Cin_pad, int target, int a8);
 
 hipError_t launch_conv(int act_bf16, ConvKind kind, InMode im, OutMode om, const ConvParams& p, hipStream_t s);
+// bf16 1x1 convs of the throughput plan (res_conv + ResnetBlock output: IN_MASK/OUT_RBOUT; attention output + residual:
+// IN_PLAIN/OUT_RESID) streamed through an LDS-DMA ring (conv1s.hip); same results as launch_conv for 0/1 masks
+bool conv1s_eligible(InMode im, OutMode om, const ConvParams& p);
+hipError_t launch_conv1s(InMode im, OutMode om, const ConvParams& p, hipStream_t s);
 // number of GroupNorm partial slots per utterance written by a CONV3/OUT_STATS launch on an F x T grid
 int conv_gn_nparts(int act_bf16, InMode im, int F, int T, int Cout, int small, int a8 = 0);
 
