@@ -58,8 +58,13 @@ def _launches(dec, fn):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, "fp8"], ids=["bf16", "fp8"])
-@pytest.mark.parametrize("B,T,lengths", [(3, 132, [132, 97, 40]), (2, 256, None)])
-def test_conv1s_bit_identical_to_conv_kernel(monkeypatch, dtype, B, T, lengths):
+@pytest.mark.parametrize("B,T,lengths,parts", [(3, 132, [132, 97, 40], 0), (2, 256, None, 0), (2, 256, [256, 170], 1),
+                                               (3, 132, [132, 97, 40], 3)])
+def test_conv1s_bit_identical_to_conv_kernel(monkeypatch, dtype, B, T, lengths, parts):
+    """parts: workgroups per (utterance, channel tile) (GT_CONV1S_PARTS; 0 = the launch's own choice, which at these
+    batch sizes gives every workgroup one or two stages): 1 and 3 run the stage ring through many wraps, as B = 32 does."""
+    if parts:
+        monkeypatch.setenv("GT_CONV1S_PARTS", str(parts))
     mu, z, mask, _ = synthetic_inputs(61, B, T, lengths=lengths)
     t = np.linspace(0.85, 0.15, B).astype(np.float32)
     args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(t), None)
@@ -79,8 +84,8 @@ def test_conv1s_bit_identical_to_conv_kernel(monkeypatch, dtype, B, T, lengths):
         a, b = res[1][name], res[0][name]
         assert np.isfinite(a).all(), name
         diff = float(np.mean(a != b))
-        report(f"conv1s vs conv_kernel {name} ({'bf16' if dtype is torch.bfloat16 else dtype}, B={B}, T={T}): "
-               "fraction of elements not bit-identical", diff, 0.0)
+        report(f"conv1s vs conv_kernel {name} ({'bf16' if dtype is torch.bfloat16 else dtype}, B={B}, T={T}, "
+               f"parts={parts}): fraction of elements not bit-identical", diff, 0.0)
 
 
 def test_conv1s_fractional_mask(monkeypatch):
