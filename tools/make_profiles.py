@@ -58,6 +58,8 @@ def norm(name: str) -> str:
             A, kind, im, om, nt, w8, tf = args
             return (f"conv_kernel<{ty(A)},{kind},{im},{om},{nt}" + (",w8" if w8 in ("1", "true") else "") +
                     ("" if tf == "4" else ",tf" + tf) + ">")
+        if base == "conv1s_kernel":          # <IN, OUT, NT, CIN>: the bench names it without CIN (in its shape)
+            return f"{base}<{args[0]},{args[1]},{args[2]}>"
         if base == "conv64_kernel":          # <IN>
             return f"conv64_kernel<{args[0]}>"
         if base in ("conv3w_kernel", "conv3w_a8_kernel"):   # <IN, COUT, CB>
