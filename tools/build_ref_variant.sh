@@ -10,7 +10,7 @@ D=$R/ab/$NAME; mkdir -p $D
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $SRC/include -I $SRC/grad-tts_amd/csrc -Wno-unused-result -Xclang -target-feature -Xclang -packed-fp32-ops"
 SRCS=$(cd $SRC/grad-tts_amd/csrc && ls *.hip *.cpp | grep -v torch_ops)
 for s in $SRCS; do
-  L=""; case $s in *.cpp) L="-x hip";; esac
+  L=""; case $s in *.cpp) L="-x hip";; conv64.hip) L="-mllvm -pragma-unroll-threshold=1000000";; esac   # (build.py SRC_FLAGS)
   /opt/rocm/bin/hipcc $F "$@" $L -c $SRC/grad-tts_amd/csrc/$s -o $D/$s.o 2>&1 | grep -v "packed-fp32-ops\|warning" || true &
 done
 wait

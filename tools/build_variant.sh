@@ -8,9 +8,9 @@ D=$R/ab/$NAME; mkdir -p $D
 # PK="" builds with the compiler's packed-fp32 instructions (the product build disables them, build.py)
 PK=${PK--Xclang -target-feature -Xclang -packed-fp32-ops}
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I $R/include -I $R/grad-tts_amd/csrc -Wno-unused-result $PK"
-SRCS="conv.hip conv64.hip conv3w.hip attn.hip attn_down.hip misc.hip mas.hip train.hip bwd.hip textenc.hip textenc_train.hip decoder.cpp train_bwd.cpp textenc.cpp vocoder.cpp"
+SRCS=$(cd $R/grad-tts_amd/csrc && ls *.hip *.cpp | grep -v torch_ops)   # (every library source, as build.py)
 for s in $SRCS; do
-  L=""; case $s in *.cpp) L="-x hip";; esac
+  L=""; case $s in *.cpp) L="-x hip";; conv64.hip) L="-mllvm -pragma-unroll-threshold=1000000";; esac   # (build.py SRC_FLAGS)
   /opt/rocm/bin/hipcc $F "$@" $L -c $R/grad-tts_amd/csrc/$s -o $D/$s.o 2>&1 | grep -v "packed-fp32-ops" || true &
 done
 wait
