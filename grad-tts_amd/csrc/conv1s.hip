@@ -31,6 +31,9 @@
 namespace gt {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 namespace c1s {
+#ifndef GT_C1S_AUX
+#define GT_C1S_AUX 0   // cache policy of the stage DMAs (experiment builds: 2 = nt)
+#endif
 constexpr int TMAX = 1024;   // frames per row at the conv's level (the mask row kept in LDS)
 template <int OUT, int NT, int CIN>
 struct Cfg {
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
       const int c = scode[j];
       const char* src = (c == 0 ? base[0] : c == 1 ? base[1] : base[2]) + gp * (c == 0 ? rowb[0] : c == 1 ? rowb[1] : rowb[2]) + soff[j];
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + (wv + 4 * j) * 1024),
-                                       16, 0, 0);
+                                       16, 0, GT_C1S_AUX);
     }
   };
   // Output: raw buffer stores, lanes past the utterance at an offset past the buffer (dropped; no branch around them).
