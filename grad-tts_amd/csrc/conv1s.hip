@@ -303,7 +303,7 @@ bool conv1s_eligible(InMode im, OutMode om, const ConvParams& p) {
   const int nt = conv_nt(1, p.Cout);
   const bool mode = (im == IN_MASK && om == OUT_RBOUT && p.pre && p.pre_part) ||
                     (im == IN_PLAIN && om == OUT_RESID && !p.in1 && cin == p.Cout && (cin == 64 ? nt == 64 : nt == 128));
-  return mode && !p.small && !p.wscale && !p.a8 && p.Fin == p.Fout && p.Tin == p.Tout && p.Tout <= c1s::TMAX &&
+  return mode && !p.wscale && !p.a8 && p.Fin == p.Fout && p.Tin == p.Tout && p.Tout <= c1s::TMAX &&
          (cin == 64 || cin == 128 || cin == 256 || (cin == 512 && nt == 128)) && p.Cin_pad == cin && p.C0 % 8 == 0 &&
          (p.Cout == 64 || p.Cout % 128 == 0) && p.Cout <= 512 && p.B >= 1 && (long)p.Fout * p.Tout >= 1 &&
          (long)p.B * p.Fout * p.Tout * p.Cout * 2 < (1L << 31);   // (the output's raw buffer range is 32-bit)

@@ -106,11 +106,19 @@ def test_conv1s_fractional_mask(monkeypatch):
         report(f"conv1s vs conv_kernel {name}, fractional mask (C ABI)", rel_err(outs[1][i], outs[0][i]), 2e-2)
 
 
-def test_small_plan_keeps_conv_kernel(monkeypatch):
-    """The small-batch plan's 1-row tiles stay on conv_kernel (conv1s is the throughput plan's)."""
-    mu, z, mask, _ = synthetic_inputs(64, 1, 96)
-    args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(np.array([0.5], np.float32)), None)
-    dec = _decoder(monkeypatch, 1, torch.bfloat16, small=16)
-    _, names = _launches(dec, lambda: dec.estimator(*args))
-    assert not any(n.startswith("conv1s_kernel<") for n in names)
-    assert any(n.startswith("conv_kernel<bf16,2,") for n in names)
+@pytest.mark.parametrize("B,T", [(1, 96), (2, 512)])
+def test_conv1s_small_plan(monkeypatch, B, T):
+    """The small-batch plan takes conv1s too (one stage per workgroup at B = 1): same bits as its conv_kernel 1-row
+    tiles, so the small plan stays batch-invariant."""
+    mu, z, mask, _ = synthetic_inputs(64, B, T)
+    args = (_cuda(z), _cuda(mask), _cuda(mu), _cuda(np.linspace(0.5, 0.3, B).astype(np.float32)), None)
+    outs = {}
+    for c1s in (1, 0):
+        dec = _decoder(monkeypatch, c1s, torch.bfloat16, small=16)
+        est, names = _launches(dec, lambda: dec.estimator(*args))
+        assert any(n.startswith("conv1s_kernel<") for n in names) == bool(c1s)
+        assert any(n.startswith("conv_kernel<bf16,2,") for n in names) == (not c1s)
+        outs[c1s] = (est.cpu().numpy(), dec(args[0], args[1], args[2], 2).cpu().numpy())
+    for i, name in enumerate(("estimator", "sampler N=2")):
+        report(f"conv1s vs conv_kernel {name}, small plan B={B} T={T}: fraction of elements not bit-identical",
+               float(np.mean(outs[1][i] != outs[0][i])), 0.0)
