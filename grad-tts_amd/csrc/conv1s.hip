@@ -124,7 +124,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
   const char* base[3] = {reinterpret_cast<const char*>(p.in0), reinterpret_cast<const char*>(p.in1 ? p.in1 : p.in0),
                          reinterpret_cast<const char*>(OUT == OUT_RBOUT ? p.pre : p.in0) + cout0 * 2};
   const int rowb[3] = {p.C0 * 2, (p.in1 ? p.C1 : p.C0) * 2, p.Cout * 2};
-  int scode[C::DPW], spos[C::DPW], soff[C::DPW];
+  // per slot: its source address in this workgroup's first stage, the row stride of its tensor, and how far (in
+  // positions) it may advance before passing the utterance's last position (later stages clamp there)
+  const char* sp[C::DPW];
+  int srow[C::DPW], slim[C::DPW];
 #pragma unroll
   for (int j = 0; j < C::DPW; ++j) {
     const int s = 64 * (wv + 4 * j) + lane;
@@ -143,19 +146,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
       code = 2;
       off = ch < NT ? ch * 2 : 0;
     }
-    scode[j] = code; spos[j] = pos; soff[j] = off;
+    const long lim = glast - g0 - pos;                        // >= 0 unless the first stage already passes the end
+    const long g = lim < 0 ? glast : g0 + pos;
+    srow[j] = code == 0 ? rowb[0] : code == 1 ? rowb[1] : rowb[2];
+    sp[j] = (code == 0 ? base[0] : code == 1 ? base[1] : base[2]) + g * srow[j] + off;
+    slim[j] = lim < 0 ? 0 : (int)lim;
   }
   // Stage k of this workgroup -> LDS stage k % NSTAGE. Stages past the end load clamped addresses (valid, never used): every
   // stage issues the same DPW DMAs, so the counted wait below holds on every path.
   auto dma_stage = [&](int k) {
     char* st = smem + (k % NSTAGE) * C::STAGE;
-    const long gk = g0 + (long)k * C::PB;
 #pragma unroll
     for (int j = 0; j < C::DPW; ++j) {
-      long gp = gk + spos[j];
-      gp = gp < glast ? gp : glast;
-      const int c = scode[j];
-      const char* src = (c == 0 ? base[0] : c == 1 ? base[1] : base[2]) + gp * (c == 0 ? rowb[0] : c == 1 ? rowb[1] : rowb[2]) + soff[j];
+      const int d = k * C::PB < slim[j] ? k * C::PB : slim[j];
+      const char* src = sp[j] + (long)d * srow[j];
       __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(st + (wv + 4 * j) * 1024),
                                        16, 0, GT_C1S_AUX);
     }
@@ -185,7 +189,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
       s_sc[tid] = sc; s_sh[tid] = sh;
     }
   }
-  if (tid < NT) s_bias[tid] = c_bias;   // visible after the first stage barrier
+  if (tid < NT) s_bias[tid] = c_bias;
+  lds_barrier();
+  // this lane's 16 output channels' bias (and h2 GroupNorm coefficients) in registers for the workgroup's life
+  float rbias[2][8], rsc[2][8], rsh[2][8];
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int cl = wc * 32 + pr * 16 + 8 * h + q;
+      rbias[pr][q] = s_bias[cl];
+      rsc[pr][q] = OUT == OUT_RBOUT ? s_sc[cl] : 0.f;
+      rsh[pr][q] = OUT == OUT_RBOUT ? s_sh[cl] : 0.f;
+    }
 
   const int prow = wp * 32 + r;                 // this lane's position within a stage
   for (int k = 0; k < nst; ++k) {
@@ -252,8 +268,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       const int cl = wc * 32 + pr * 16 + 8 * h;   // channel within the tile
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(s_bias + cl);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(s_bias + cl + 4);
+      const float* b0 = rbias[pr];
+      const float* b1 = rbias[pr] + 4;
       float o[8], e[8];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -268,7 +284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
       item_to_f(eu[pr], e, bf16());
       if (OUT == OUT_RBOUT) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) o[q] = gn_mish_add<bf16>(e[q], s_sc[cl + q], s_sh[cl + q], o[q], m);
+        for (int q = 0; q < 8; ++q) o[q] = gn_mish_add<bf16>(e[q], rsc[pr][q], rsh[pr][q], o[q], m);
       } else {   // residual: the staged input (Cin == Cout)
 #pragma unroll
         for (int q = 0; q < 8; ++q) o[q] += e[q];
