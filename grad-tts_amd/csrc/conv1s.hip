@@ -49,7 +49,10 @@ struct Cfg {
   // The ring fills the LDS: two workgroups per CU when that leaves >= 3 stages each (same-box A/B: two workgroups with
   // three stages beat one with seven), else one with up to 8.
   static constexpr int S2 = (80 * 1024 - EXTRA) / STAGE;
-  static constexpr int WGCU = S2 >= 3 ? 2 : 1;            // workgroups per CU
+#ifndef GT_C1S_ONE_WG
+#define GT_C1S_ONE_WG 0   // experiment builds: 1 = one workgroup per CU with the deepest ring everywhere
+#endif
+  static constexpr int WGCU = S2 >= 3 && !GT_C1S_ONE_WG ? 2 : 1;   // workgroups per CU
   static constexpr int S1 = (160 * 1024 - EXTRA) / STAGE;
   static constexpr int NSTAGE = WGCU == 2 ? (S2 > 8 ? 8 : S2) : (S1 > 8 ? 8 : S1);
   static constexpr int SMEM = NSTAGE * STAGE + EXTRA;
