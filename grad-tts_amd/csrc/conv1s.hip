@@ -49,6 +49,12 @@ struct Cfg {
   // The ring fills the LDS: two workgroups per CU when that leaves >= 3 stages each (same-box A/B: two workgroups with
   // three stages beat one with seven), else one with up to 8.
   static constexpr int S2 = (80 * 1024 - EXTRA) / STAGE;
+#ifndef GT_C1S_STORE_AUX
+#define GT_C1S_STORE_AUX 0   // cache policy of the output stores (experiment builds: 2 = nt)
+#endif
+#ifndef GT_C1S_NOSTORE
+#define GT_C1S_NOSTORE 0
+#endif
 #ifndef GT_C1S_ONE_WG
 #define GT_C1S_ONE_WG 0   // experiment builds: 1 = one workgroup per CU with the deepest ring everywhere
 #endif
@@ -172,7 +178,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(c1s::Cfg<OU
       __builtin_amdgcn_make_buffer_rsrc(p.out, (short)0, (int)((long)p.B * n * p.Cout * 2), 0x00020000);
   auto store2 = [&](const u32x4* v, const unsigned* off) {
 #pragma unroll
-    for (int pr = 0; pr < 2; ++pr) __builtin_amdgcn_raw_buffer_store_b128(v[pr], rso, off[pr], 0, 0);
+    for (int pr = 0; pr < 2; ++pr) {
+#if GT_C1S_NOSTORE   // timing-only experiment build: outputs dropped (wrong results)
+      __builtin_amdgcn_raw_buffer_store_b128(v[pr], rso, 0x80000000u, 0, 0);
+#else
+      __builtin_amdgcn_raw_buffer_store_b128(v[pr], rso, off[pr], 0, GT_C1S_STORE_AUX);
+#endif
+    }
   };
 #pragma unroll
   for (int k = 0; k < NSTAGE - 1; ++k) dma_stage(k);
